@@ -1,0 +1,198 @@
+#!/usr/bin/env python
+"""Headline benchmark: MNISTClassifier data-parallel training throughput.
+
+Metric / config come from BASELINE.json: whole-node samples/sec for
+MNISTClassifier (MLP 784->32->64->10, Adam, per-worker batch 32 -- the
+reference's default config, examples/ray_ddp_example.py:167) at 1/2/4/8
+workers, one process per MI355X (torchrun / RayAccelerator worker), RCCL
+allreduce over xGMI between ranks.  Weak scaling: per-GPU batch is fixed.
+
+Data: synthetic MNIST-shaped uint8 images + labels (55,000 train samples, the
+reference's train split), random-init weights; each rank trains on its
+DistributedSampler shard.  Every timed step is a full optimizer step:
+forward, NLL loss, backward, gradient allreduce (N > 1), Adam update.
+
+Implementations (``--impl``):
+  native  the framework's engine: fused gfx950 HIP step kernel (bf16 MFMA,
+          fp32 master weights/Adam), flat-arena allreduce, fused Adam,
+          hipGraph replay of the per-step device work.
+  torch   stock PyTorch-ROCm baseline: nn.Linear MLP under bf16 autocast,
+          torch.optim.Adam, DistributedDataParallel over RCCL (N > 1).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N > 1 is launched by torch.distributed.run, one rank per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+METRIC = "samples/sec (whole node) + DDP scaling eff, MNISTClassifier at 1/2/4/8 workers"
+# Our measured stock-PyTorch numbers on MI355X (BASELINE.md "Our MI355X measurements");
+# the reference itself publishes none.  None => vs_baseline is null.
+STOCK_BASELINE = {}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--impl", choices=["native", "torch"], default="native")
+    ap.add_argument("--batch-size", type=int, default=32)
+    ap.add_argument("--layer-1", type=int, default=32)
+    ap.add_argument("--layer-2", type=int, default=64)
+    ap.add_argument("--lr", type=float, default=1e-1)
+    ap.add_argument("--graph-steps", type=int, default=8,
+                    help="optimizer steps per captured hipGraph (native); 0 = eager launches")
+    ap.add_argument("--n-data", type=int, default=55000)
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+
+
+def make_native(args, world, rank, dev, x, y):
+    from ray_lightning_accelerators_amd.parallel.mlp_engine import FusedMLPEngine
+
+    def allreduce(t):
+        dist.all_reduce(t)
+
+    eng = FusedMLPEngine(args.layer_1, args.layer_2, args.batch_size, lr=args.lr, device=dev,
+                         world_size=world, rank=rank, allreduce=allreduce if world > 1 else None, seed=0)
+    eng.set_data(x, y, shuffle=True)
+    eng.broadcast_from(0)
+    if args.graph_steps > 0:
+        ok = eng.capture(args.graph_steps)
+        if not ok and rank == 0:
+            print("hipGraph capture failed; running eager", file=sys.stderr)
+    return eng.run, (lambda: float(eng.recent_stats(20)[:, 0].mean()))
+
+
+def make_torch(args, world, rank, dev, x, y):
+    import torch.nn as nn
+    import torch.nn.functional as F
+    from ray_lightning_accelerators_amd.parallel.mlp_engine import shard_indices
+
+    torch.manual_seed(0)
+    model = nn.Sequential(nn.Linear(784, args.layer_1), nn.ReLU(), nn.Linear(args.layer_1, args.layer_2),
+                          nn.ReLU(), nn.Linear(args.layer_2, 10)).to(dev)
+    if world > 1:
+        model = nn.parallel.DistributedDataParallel(model, device_ids=[dev.index])
+    opt = torch.optim.Adam(model.parameters(), lr=args.lr)
+    xd, yd = x.to(dev), y.to(dev)
+    B = args.batch_size
+    state = {"epoch": 0, "i": 0, "last": 0.0}
+    per_rank = -(-x.size(0) // world)
+    nb = per_rank // B
+
+    def load(epoch):
+        state["order"] = shard_indices(x.size(0), world, rank, epoch, 0, True, device=dev)[: nb * B]
+        state["i"] = 0
+
+    load(0)
+
+    def run(n):
+        for _ in range(n):
+            if state["i"] >= nb:
+                state["epoch"] += 1
+                load(state["epoch"])
+            idx = state["order"][state["i"] * B:(state["i"] + 1) * B]
+            state["i"] += 1
+            xb = xd.index_select(0, idx).float().div_(255.0)
+            yb = yd.index_select(0, idx)
+            opt.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                logits = model(xb)
+            loss = F.nll_loss(F.log_softmax(logits.float(), dim=1), yb)
+            loss.backward()
+            opt.step()
+            state["loss"] = loss
+
+    return run, (lambda: float(state["loss"].item()))
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args)
+    dev = torch.device("cuda", local)
+    from ray_lightning_accelerators_amd.models.data import synthetic_mnist
+
+    x, y = synthetic_mnist(args.n_data, seed=0)
+    maker = make_native if args.impl == "native" else make_torch
+    run, last_loss = maker(args, world, rank, dev, x, y)
+
+    run(args.warmup)
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    samples = args.steps * args.batch_size * world
+    value = samples / elapsed
+    loss = last_loss()
+    if rank == 0:
+        base = STOCK_BASELINE.get(world)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (round(value / base, 3) if base else None),
+            "dtype": "bf16",
+            "data": "synthetic",
+            "config": {
+                "model": f"MNISTClassifier(784-{args.layer_1}-{args.layer_2}-10)",
+                "global_batch": args.batch_size * world,
+                "per_gpu_batch": args.batch_size,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "impl": args.impl,
+                "optimizer": "Adam",
+                "final_train_loss": round(loss, 4),
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

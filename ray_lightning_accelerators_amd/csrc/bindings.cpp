@@ -1,0 +1,209 @@
+// torch bindings for the gfx950 kernels (module `ray_lightning_accelerators_amd._C`).
+//
+// Every entry point validates device / dtype / contiguity / sizes on the host
+// before launching: a hand-written kernel must never see a shape it was not
+// built for (an out-of-bounds access can reset every GPU of the host).
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+
+#include "kernels.h"
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+hipStream_t cur_stream(const Tensor& t) {
+  return at::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.get_device()).stream();
+}
+
+void check_dev(const Tensor& t, const char* name, at::ScalarType dt) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+}
+
+template <class T>
+T* ptr_or_null(const optional<Tensor>& t, const char* name, at::ScalarType dt, int64_t min_numel = 0) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  check_dev(*t, name, dt);
+  TORCH_CHECK(t->numel() >= min_numel, name, " has ", t->numel(), " elements, need >= ", min_numel);
+  return reinterpret_cast<T*>(t->data_ptr());
+}
+
+void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, optional<Tensor> p_bf16, double lr,
+               double beta1, double beta2, double eps, double weight_decay, double grad_scale,
+               bool adamw, bool maximize, optional<Tensor> step, int64_t host_step,
+               optional<Tensor> lr_t) {
+  check_dev(p, "param", at::kFloat);
+  check_dev(g, "grad", at::kFloat);
+  check_dev(m, "exp_avg", at::kFloat);
+  check_dev(v, "exp_avg_sq", at::kFloat);
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adam arena size mismatch");
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
+  rla::AdamArgs a{};
+  a.p = p.data_ptr<float>();
+  a.g = g.data_ptr<float>();
+  a.m = m.data_ptr<float>();
+  a.v = v.data_ptr<float>();
+  a.p_bf16 = ptr_or_null<uint16_t>(p_bf16, "param_bf16", at::kBFloat16, n);
+  a.n = n;
+  a.lr = (float)lr; a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.eps = (float)eps;
+  a.weight_decay = (float)weight_decay; a.grad_scale = (float)grad_scale;
+  a.adamw = adamw; a.maximize = maximize;
+  a.step_ptr = ptr_or_null<const int64_t>(step, "step", at::kLong, 1);
+  a.host_step = host_step;
+  a.lr_ptr = ptr_or_null<const float>(lr_t, "lr", at::kFloat, 1);
+  TORCH_CHECK(a.step_ptr || host_step >= 1, "adam: step must be >= 1");
+  rla::launch_adam(a, cur_stream(p));
+}
+
+void sgd_step(Tensor p, Tensor g, optional<Tensor> buf, optional<Tensor> p_bf16, double lr,
+              double momentum, double dampening, double weight_decay, double grad_scale,
+              bool nesterov, bool maximize, optional<Tensor> step, int64_t host_step,
+              optional<Tensor> lr_t) {
+  check_dev(p, "param", at::kFloat);
+  check_dev(g, "grad", at::kFloat);
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n, "sgd arena size mismatch");
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
+  rla::SGDArgs a{};
+  a.p = p.data_ptr<float>();
+  a.g = g.data_ptr<float>();
+  a.buf = ptr_or_null<float>(buf, "momentum_buffer", at::kFloat, n);
+  TORCH_CHECK(momentum == 0.0 || a.buf != nullptr, "sgd: momentum needs a buffer");
+  a.p_bf16 = ptr_or_null<uint16_t>(p_bf16, "param_bf16", at::kBFloat16, n);
+  a.n = n;
+  a.lr = (float)lr; a.momentum = (float)momentum; a.dampening = (float)dampening;
+  a.weight_decay = (float)weight_decay; a.grad_scale = (float)grad_scale;
+  a.nesterov = nesterov; a.maximize = maximize;
+  a.step_ptr = ptr_or_null<const int64_t>(step, "step", at::kLong, 1);
+  a.host_step = host_step;
+  a.lr_ptr = ptr_or_null<const float>(lr_t, "lr", at::kFloat, 1);
+  rla::launch_sgd(a, cur_stream(p));
+}
+
+void multi_copy(Tensor table, double scale, bool accumulate) {
+  check_dev(table, "table", at::kLong);
+  TORCH_CHECK(table.dim() == 2 && table.size(1) == 4, "table must be [nchunks, 4]");
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
+  rla::launch_multi_copy(table.data_ptr<int64_t>(), table.size(0), (float)scale, accumulate,
+                         cur_stream(table));
+}
+
+void scale_(Tensor x, double s) {
+  check_dev(x, "x", at::kFloat);
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  rla::launch_scale(x.data_ptr<float>(), x.numel(), (float)s, cur_stream(x));
+}
+
+Tensor sumsq(Tensor x) {
+  check_dev(x, "x", at::kFloat);
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor out = at::empty({1}, x.options());
+  rla::launch_sumsq(x.data_ptr<float>(), x.numel(), out.data_ptr<float>(), cur_stream(x));
+  return out;
+}
+
+int64_t mlp_param_count(int64_t L1, int64_t L2) {
+  return L1 * 784 + L1 + L2 * L1 + L2 + 10 * L2 + 10;
+}
+
+void mlp_train_step(optional<Tensor> x_u8, optional<Tensor> x_f32, Tensor labels,
+                    optional<Tensor> order, optional<Tensor> counters, int64_t n_batches, int64_t B,
+                    int64_t L1, int64_t L2, Tensor params, Tensor grads, optional<Tensor> exp_avg,
+                    optional<Tensor> exp_avg_sq, optional<Tensor> stats, bool accumulate_grad,
+                    bool apply_adam, bool advance_step, double lr, double beta1, double beta2,
+                    double eps, double weight_decay, optional<Tensor> lr_t, bool adamw) {
+  TORCH_CHECK(rla::mlp_supported((int)L1, (int)L2), "no fused MLP kernel for layer sizes ", L1, "/", L2);
+  TORCH_CHECK(B >= 1, "batch size must be >= 1");
+  const int64_t np = mlp_param_count(L1, L2);
+  check_dev(params, "params", at::kFloat);
+  check_dev(grads, "grads", at::kFloat);
+  TORCH_CHECK(params.numel() == np && grads.numel() == np, "param arena must hold ", np, " floats");
+  check_dev(labels, "labels", at::kLong);
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(params.device());
+  rla::MLPStepArgs a{};
+  a.x_u8 = ptr_or_null<const uint8_t>(x_u8, "x_u8", at::kByte);
+  a.x_f32 = ptr_or_null<const float>(x_f32, "x_f32", at::kFloat);
+  TORCH_CHECK((a.x_u8 != nullptr) != (a.x_f32 != nullptr), "pass exactly one of x_u8 / x_f32");
+  if (a.x_u8) {
+    TORCH_CHECK(x_u8->dim() == 2 && x_u8->size(1) == 784, "x_u8 must be [N, 784]");
+    TORCH_CHECK(labels.numel() == x_u8->size(0), "labels must match the dataset");
+    a.order = ptr_or_null<const int64_t>(order, "order", at::kLong, n_batches * B);
+    TORCH_CHECK(a.order != nullptr && n_batches >= 1, "u8 mode needs order[n_batches * B]");
+    a.counters = ptr_or_null<int64_t>(counters, "counters", at::kLong, 2);
+    TORCH_CHECK(a.counters != nullptr, "u8 mode needs device counters");
+    // Indices are range-checked on the host by the caller when `order` is
+    // built (see ops.fused_mlp.MLPDataset); the kernel trusts them.
+  } else {
+    TORCH_CHECK(x_f32->numel() == B * 784, "x_f32 must be [B, 784]");
+    TORCH_CHECK(labels.numel() == B, "labels must be [B]");
+    a.counters = ptr_or_null<int64_t>(counters, "counters", at::kLong, 2);
+  }
+  a.labels = labels.data_ptr<int64_t>();
+  a.n_batches = n_batches;
+  a.B = (int)B; a.L1 = (int)L1; a.L2 = (int)L2;
+  a.params = params.data_ptr<float>();
+  a.grads = grads.data_ptr<float>();
+  a.exp_avg = ptr_or_null<float>(exp_avg, "exp_avg", at::kFloat, np);
+  a.exp_avg_sq = ptr_or_null<float>(exp_avg_sq, "exp_avg_sq", at::kFloat, np);
+  TORCH_CHECK(!apply_adam || (a.exp_avg && a.exp_avg_sq), "apply_adam needs optimizer state");
+  a.stats = ptr_or_null<float>(stats, "stats", at::kFloat, 4);
+  a.stats_ring = a.stats ? (int)(stats->numel() / 4) : 0;
+  a.accumulate_grad = accumulate_grad;
+  a.apply_adam = apply_adam;
+  a.advance_step = advance_step;
+  a.lr = (float)lr; a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.eps = (float)eps;
+  a.weight_decay = (float)weight_decay;
+  a.lr_ptr = ptr_or_null<const float>(lr_t, "lr", at::kFloat, 1);
+  a.adamw = adamw;
+  TORCH_CHECK(rla::launch_mlp_train_step(a, cur_stream(params)) == 0, "fused MLP launch failed");
+}
+
+void mlp_eval(optional<Tensor> x_u8, optional<Tensor> x_f32, Tensor labels, optional<Tensor> index,
+              int64_t B, int64_t L1, int64_t L2, Tensor params, optional<Tensor> logits, Tensor out) {
+  TORCH_CHECK(rla::mlp_supported((int)L1, (int)L2), "no fused MLP kernel for layer sizes ", L1, "/", L2);
+  check_dev(params, "params", at::kFloat);
+  TORCH_CHECK(params.numel() == mlp_param_count(L1, L2), "param arena size mismatch");
+  check_dev(labels, "labels", at::kLong);
+  check_dev(out, "out", at::kFloat);
+  TORCH_CHECK(out.numel() >= 2, "out must hold 2 floats");
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(params.device());
+  rla::MLPEvalArgs a{};
+  a.x_u8 = ptr_or_null<const uint8_t>(x_u8, "x_u8", at::kByte);
+  a.x_f32 = ptr_or_null<const float>(x_f32, "x_f32", at::kFloat);
+  TORCH_CHECK((a.x_u8 != nullptr) != (a.x_f32 != nullptr), "pass exactly one of x_u8 / x_f32");
+  if (a.x_u8) {
+    TORCH_CHECK(x_u8->dim() == 2 && x_u8->size(1) == 784, "x_u8 must be [N, 784]");
+    a.index = ptr_or_null<const int64_t>(index, "index", at::kLong, B);
+    TORCH_CHECK(a.index != nullptr, "u8 mode needs index[B]");
+  } else {
+    TORCH_CHECK(x_f32->numel() == B * 784, "x_f32 must be [B, 784]");
+    TORCH_CHECK(labels.numel() == B, "labels must be [B]");
+  }
+  a.labels = labels.data_ptr<int64_t>();
+  a.B = (int)B; a.L1 = (int)L1; a.L2 = (int)L2;
+  a.params = params.data_ptr<float>();
+  a.logits = ptr_or_null<float>(logits, "logits", at::kFloat, B * 10);
+  a.out = out.data_ptr<float>();
+  TORCH_CHECK(rla::launch_mlp_eval(a, cur_stream(params)) == 0, "fused MLP eval launch failed");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gfx950 HIP kernels of ray_lightning_accelerators_amd";
+  m.def("adam_step", &adam_step, "fused Adam over a flat fp32 arena");
+  m.def("sgd_step", &sgd_step, "fused SGD (momentum/nesterov/wd) over a flat fp32 arena");
+  m.def("multi_copy", &multi_copy, "multi-tensor copy/scale/cast via a chunk table");
+  m.def("scale_", &scale_, "in-place scale of an fp32 arena");
+  m.def("sumsq", &sumsq, "sum of squares of an fp32 arena");
+  m.def("mlp_train_step", &mlp_train_step, "fused MNIST-MLP forward+backward(+Adam) step");
+  m.def("mlp_eval", &mlp_eval, "fused MNIST-MLP forward + NLL/accuracy");
+  m.def("mlp_supported", [](int64_t a, int64_t b) { return rla::mlp_supported((int)a, (int)b); });
+  m.def("mlp_param_count", &mlp_param_count);
+  m.attr("ARCH") = "gfx950";
+}

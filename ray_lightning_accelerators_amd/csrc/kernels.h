@@ -1,0 +1,88 @@
+// Host-callable launch API of the HIP kernels (plain pointers + hipStream_t).
+// The torch bindings (bindings.cpp) are the only caller; keeping this header
+// free of torch types lets the .hip files compile with hipcc alone.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rla {
+
+struct AdamArgs {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  uint16_t* p_bf16;        // optional bf16 copy-out of the updated params
+  int64_t n;
+  float lr, beta1, beta2, eps, weight_decay, grad_scale;
+  int adamw, maximize;
+  const int64_t* step_ptr;  // device step counter (already incremented) or null
+  int64_t host_step;        // used when step_ptr is null
+  const float* lr_ptr;      // device learning rate (graph-replay friendly) or null
+};
+
+struct SGDArgs {
+  float* p;
+  const float* g;
+  float* buf;
+  uint16_t* p_bf16;
+  int64_t n;
+  float lr, momentum, dampening, weight_decay, grad_scale;
+  int nesterov, maximize;
+  const int64_t* step_ptr;
+  int64_t host_step;
+  const float* lr_ptr;
+};
+
+void launch_adam(const AdamArgs& a, hipStream_t stream);
+void launch_sgd(const SGDArgs& a, hipStream_t stream);
+void launch_multi_copy(const int64_t* table, int64_t nchunks, float scale, int accumulate,
+                       hipStream_t stream);
+void launch_scale(float* x, int64_t n, float s, hipStream_t stream);
+void launch_sumsq(const float* x, int64_t n, float* out, hipStream_t stream);
+
+// ---------------------------------------------------------------------------
+// Fused MNIST-MLP training step (784 -> L1 -> L2 -> 10, ReLU, log_softmax+NLL).
+// ---------------------------------------------------------------------------
+struct MLPStepArgs {
+  // input: either a uint8 dataset gathered through `order` (GPU-resident data,
+  // pixels scaled by 1/255 in-kernel) or a dense fp32 batch [B, 784].
+  const uint8_t* x_u8;      // [N_data, 784] or null
+  const float* x_f32;       // [B, 784] or null
+  const int64_t* labels;    // [N_data] (u8 mode) or [B] (f32 mode)
+  const int64_t* order;     // [n_batches * B] sample indices for the epoch (u8 mode)
+  int64_t* counters;        // [0] optimizer step t, [1] batch cursor (u8 mode)
+  int64_t n_batches;        // cursor wraps modulo this (u8 mode)
+  int B;                    // full batch size (loss is a mean over B)
+  int L1, L2;
+  float* params;            // arena: W1[L1,784] b1[L1] W2[L2,L1] b2[L2] W3[10,L2] b3[10]
+  float* grads;             // same layout
+  float* exp_avg;           // Adam state (same layout) when apply_adam
+  float* exp_avg_sq;
+  float* stats;             // ring [ring, 4]: loss, correct, count, step
+  int stats_ring;
+  int accumulate_grad;      // add existing grads (gradient accumulation)
+  int apply_adam;           // fuse Adam into the gradient epilogues (world size 1)
+  int advance_step;         // increment counters[0] (this call completes an optimizer step)
+  float lr, beta1, beta2, eps, weight_decay;
+  const float* lr_ptr;
+  int adamw;
+};
+
+struct MLPEvalArgs {
+  const uint8_t* x_u8;
+  const float* x_f32;
+  const int64_t* labels;
+  const int64_t* index;     // [B] sample indices (u8 mode) or null
+  int B, L1, L2;
+  const float* params;
+  float* logits;            // optional [B, 10] output (log-probabilities)
+  float* out;               // [2]: += sum of NLL, += correct count
+};
+
+// returns 0 on success, -1 if (L1, L2) has no compiled instantiation
+int launch_mlp_train_step(const MLPStepArgs& a, hipStream_t stream);
+int launch_mlp_eval(const MLPEvalArgs& a, hipStream_t stream);
+bool mlp_supported(int L1, int L2);
+
+}  // namespace rla

@@ -1,0 +1,75 @@
+"""Synthetic, MNIST-shaped data (no downloads are possible on this platform).
+
+``synthetic_mnist`` produces uint8 28x28 images of a *learnable* 10-class task
+(class-conditional stroke prototypes + per-sample jitter and noise), so the
+reference's accuracy gates (>= 0.5 after 10 train batches,
+ray_lightning/tests/utils.py:137-152 of the reference) remain meaningful.
+Images are uint8 like real MNIST; the ``ToTensor`` scaling (x / 255) happens
+in the dataset's ``__getitem__`` on CPU or inside the fused kernel on GPU.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+from torch.utils.data import Dataset
+
+IMG = 28
+
+
+def _prototypes(seed: int) -> torch.Tensor:
+    g = torch.Generator().manual_seed(10_000 + seed)
+    yy, xx = torch.meshgrid(torch.arange(IMG).float(), torch.arange(IMG).float(), indexing="ij")
+    protos = torch.zeros(10, IMG, IMG)
+    for c in range(10):
+        for _ in range(3):  # three gaussian "strokes" per class
+            cy, cx = torch.rand(2, generator=g) * 16 + 6
+            sy, sx = torch.rand(2, generator=g) * 4 + 1.5
+            protos[c] += torch.exp(-((yy - cy) ** 2 / (2 * sy ** 2) + (xx - cx) ** 2 / (2 * sx ** 2)))
+        protos[c] /= protos[c].max()
+    return protos
+
+
+def synthetic_mnist(n: int, seed: int = 0, noise: float = 0.25) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Return (images uint8 [n, 784], labels int64 [n])."""
+    g = torch.Generator().manual_seed(seed)
+    protos = _prototypes(0)  # class definitions are shared by every split
+    labels = torch.randint(0, 10, (n,), generator=g)
+    shifts = torch.randint(-2, 3, (n, 2), generator=g)
+    imgs = protos[labels]
+    # per-sample translation jitter (rolled in blocks of equal shift for speed)
+    out = torch.empty(n, IMG, IMG)
+    for dy in range(-2, 3):
+        for dx in range(-2, 3):
+            m = (shifts[:, 0] == dy) & (shifts[:, 1] == dx)
+            if m.any():
+                out[m] = torch.roll(imgs[m], shifts=(dy, dx), dims=(1, 2))
+    out = out * (0.7 + 0.6 * torch.rand(n, 1, 1, generator=g)) + noise * torch.rand(n, IMG, IMG, generator=g)
+    return (out.clamp(0, 1) * 255).round().to(torch.uint8).reshape(n, IMG * IMG), labels
+
+
+class SyntheticMNIST(Dataset):
+    """Map-style dataset yielding (float [1,28,28] in [0,1], label) like torchvision MNIST+ToTensor."""
+
+    def __init__(self, n: int = 60000, seed: int = 0, train: bool = True):
+        self.images, self.targets = synthetic_mnist(n, seed=seed if train else seed + 1)
+
+    def __len__(self) -> int:
+        return self.targets.numel()
+
+    def __getitem__(self, i):
+        return self.images[i].view(1, IMG, IMG).float() / 255.0, int(self.targets[i])
+
+
+class RandomDataset(Dataset):
+    """Gaussian vectors (reference tests/utils.py:12-21)."""
+
+    def __init__(self, size: int, length: int, generator: Optional[torch.Generator] = None):
+        self.len = length
+        self.data = torch.randn(length, size, generator=generator)
+
+    def __getitem__(self, index: int):
+        return self.data[index]
+
+    def __len__(self) -> int:
+        return self.len

@@ -1,0 +1,179 @@
+"""Fused MNIST-classifier MLP step (784 -> L1 -> L2 -> 10).
+
+GPU: one HIP launch per training step (``csrc/mlp_kernels.hip``): forward,
+log_softmax + NLL + accuracy, backward and -- at world size 1 -- the Adam
+update fused into the weight-gradient epilogues.  CPU: an fp32 PyTorch
+reference with identical semantics (also the oracle for the GPU tests).
+
+Parameter arena layout (== ``nn.Linear`` state_dict order of
+``layer_1``/``layer_2``/``layer_3``):  W1[L1,784] b1[L1] W2[L2,L1] b2[L2] W3[10,L2] b3[10].
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import require, use_native
+
+IN_FEATURES = 784
+NUM_CLASSES = 10
+SUPPORTED = {(32, 32), (32, 64), (32, 128), (32, 256), (64, 64), (64, 128), (64, 256),
+             (128, 64), (128, 128), (128, 256)}
+
+
+def mlp_param_count(L1: int, L2: int) -> int:
+    return L1 * IN_FEATURES + L1 + L2 * L1 + L2 + NUM_CLASSES * L2 + NUM_CLASSES
+
+
+def mlp_supported(L1: int, L2: int) -> bool:
+    return (int(L1), int(L2)) in SUPPORTED
+
+
+def mlp_unpack(flat: torch.Tensor, L1: int, L2: int) -> Dict[str, torch.Tensor]:
+    """Views of the arena as nn.Linear tensors (state_dict key order)."""
+    shapes = [
+        ("layer_1.weight", (L1, IN_FEATURES)), ("layer_1.bias", (L1,)),
+        ("layer_2.weight", (L2, L1)), ("layer_2.bias", (L2,)),
+        ("layer_3.weight", (NUM_CLASSES, L2)), ("layer_3.bias", (NUM_CLASSES,)),
+    ]
+    out, off = {}, 0
+    for name, shp in shapes:
+        n = math.prod(shp)
+        out[name] = flat[off:off + n].view(shp)
+        off += n
+    assert off == flat.numel(), "arena size mismatch"
+    return out
+
+
+def _gather_batch(x_u8, x_f32, labels, order, cursor, B, index=None):
+    if x_u8 is not None:
+        if index is None:
+            index = order[cursor * B:(cursor + 1) * B]
+        x = x_u8.index_select(0, index).float() / 255.0
+        y = labels.index_select(0, index)
+    else:
+        x = x_f32.reshape(B, IN_FEATURES).float()
+        y = labels
+    return x, y
+
+
+def _reference_forward(p: Dict[str, torch.Tensor], x: torch.Tensor) -> torch.Tensor:
+    h1 = F.relu(F.linear(x, p["layer_1.weight"], p["layer_1.bias"]))
+    h2 = F.relu(F.linear(h1, p["layer_2.weight"], p["layer_2.bias"]))
+    return F.linear(h2, p["layer_3.weight"], p["layer_3.bias"])
+
+
+def mlp_train_step(
+    params: torch.Tensor,
+    grads: torch.Tensor,
+    *,
+    L1: int,
+    L2: int,
+    B: int,
+    labels: torch.Tensor,
+    x_u8: Optional[torch.Tensor] = None,
+    x_f32: Optional[torch.Tensor] = None,
+    order: Optional[torch.Tensor] = None,
+    counters: Optional[torch.Tensor] = None,
+    n_batches: int = 0,
+    exp_avg: Optional[torch.Tensor] = None,
+    exp_avg_sq: Optional[torch.Tensor] = None,
+    stats: Optional[torch.Tensor] = None,
+    accumulate_grad: bool = False,
+    apply_adam: bool = False,
+    advance_step: bool = True,
+    lr: float = 1e-3,
+    betas: Tuple[float, float] = (0.9, 0.999),
+    eps: float = 1e-8,
+    weight_decay: float = 0.0,
+    lr_tensor: Optional[torch.Tensor] = None,
+    adamw: bool = False,
+) -> None:
+    """One training micro-step of the MNIST MLP over a flat parameter arena.
+
+    u8 mode (``x_u8`` = GPU-resident uint8 dataset [N, 784]): the batch is
+    ``order[cursor*B:(cursor+1)*B]`` with ``cursor = counters[1]``, which the
+    step advances (mod ``n_batches``) -- so a captured hipGraph replays
+    successive batches.  ``counters[0]`` is the optimizer step t.
+    """
+    if use_native(params):
+        require().mlp_train_step(
+            x_u8, x_f32, labels, order, counters, int(n_batches), int(B), int(L1), int(L2),
+            params, grads, exp_avg, exp_avg_sq, stats, bool(accumulate_grad), bool(apply_adam),
+            bool(advance_step), float(lr), float(betas[0]), float(betas[1]), float(eps),
+            float(weight_decay), lr_tensor, bool(adamw),
+        )
+        return
+    # ---- fp32 reference ----
+    cursor = int(counters[1].item()) if (counters is not None and x_u8 is not None) else 0
+    x, y = _gather_batch(x_u8, x_f32, labels, order, cursor, B)
+    with torch.enable_grad():
+        leaf = params.detach().clone().requires_grad_(True)
+        p = mlp_unpack(leaf, L1, L2)
+        logits = _reference_forward(p, x)
+        logp = F.log_softmax(logits, dim=1)
+        loss = F.nll_loss(logp, y)
+        (g,) = torch.autograd.grad(loss, [leaf])
+    with torch.no_grad():
+        if accumulate_grad:
+            g = g + grads
+        t = (int(counters[0].item()) if counters is not None else 0) + 1
+        if apply_adam:
+            from .optim import fused_adam_
+
+            gbuf = g.clone()
+            fused_adam_(params, gbuf, exp_avg, exp_avg_sq, lr=lr, betas=betas, eps=eps,
+                        weight_decay=weight_decay, adamw=adamw, step=t, lr_tensor=lr_tensor)
+        else:
+            grads.copy_(g)
+        if counters is not None:
+            if advance_step:
+                counters[0] = t
+            if x_u8 is not None:
+                counters[1] = (cursor + 1) % n_batches if n_batches > 0 else cursor + 1
+        if stats is not None:
+            ring = stats.numel() // 4
+            slot = (t - 1) % max(ring, 1)
+            correct = (logp.argmax(dim=1) == y).sum().float()
+            stats.view(-1, 4)[slot] = torch.stack(
+                [loss.detach(), correct, torch.tensor(float(B)), torch.tensor(float(t))])
+
+
+def mlp_eval(
+    params: torch.Tensor,
+    *,
+    L1: int,
+    L2: int,
+    B: int,
+    labels: torch.Tensor,
+    out: torch.Tensor,
+    x_u8: Optional[torch.Tensor] = None,
+    x_f32: Optional[torch.Tensor] = None,
+    index: Optional[torch.Tensor] = None,
+    logits: Optional[torch.Tensor] = None,
+) -> None:
+    """Forward only: out[0] += sum NLL, out[1] += #correct; optional log-probs."""
+    if use_native(params):
+        require().mlp_eval(x_u8, x_f32, labels, index, int(B), int(L1), int(L2), params, logits, out)
+        return
+    x, y = _gather_batch(x_u8, x_f32, labels, None, 0, B, index=index)
+    with torch.no_grad():
+        logp = F.log_softmax(_reference_forward(mlp_unpack(params, L1, L2), x), dim=1)
+        out[0] += F.nll_loss(logp, y, reduction="sum")
+        out[1] += (logp.argmax(dim=1) == y).sum().float()
+        if logits is not None:
+            logits.view(B, NUM_CLASSES).copy_(logp)
+
+
+def init_mlp_params(L1: int, L2: int, generator: Optional[torch.Generator] = None) -> torch.Tensor:
+    """nn.Linear default init (kaiming_uniform(a=sqrt(5)) == U(+-1/sqrt(fan_in))) into a flat arena."""
+    flat = torch.empty(mlp_param_count(L1, L2), dtype=torch.float32)
+    views = mlp_unpack(flat, L1, L2)
+    fans = {"layer_1": IN_FEATURES, "layer_2": L1, "layer_3": L2}
+    for name, t in views.items():
+        bound = 1.0 / math.sqrt(fans[name.split(".")[0]])
+        t.uniform_(-bound, bound, generator=generator)
+    return flat

@@ -1,0 +1,181 @@
+"""Flat-arena optimizer steps and bucket copy kernels (HIP on GPU, torch on CPU).
+
+Replaces the upstream ``torch.optim.Adam``/``SGD`` steps and DDP bucket
+flatten/unflatten the reference relies on.
+"""
+from __future__ import annotations
+
+import math
+from typing import Iterable, List, Optional, Sequence, Tuple, Union
+
+import torch
+
+from . import require, use_native
+
+StepLike = Union[int, torch.Tensor]
+
+
+def _step_args(step: StepLike) -> Tuple[Optional[torch.Tensor], int]:
+    if isinstance(step, torch.Tensor):
+        return step, 0
+    return None, int(step)
+
+
+def fused_adam_(
+    p: torch.Tensor,
+    g: torch.Tensor,
+    m: torch.Tensor,
+    v: torch.Tensor,
+    *,
+    lr: float,
+    betas: Tuple[float, float] = (0.9, 0.999),
+    eps: float = 1e-8,
+    weight_decay: float = 0.0,
+    grad_scale: float = 1.0,
+    adamw: bool = False,
+    maximize: bool = False,
+    step: StepLike = 1,
+    lr_tensor: Optional[torch.Tensor] = None,
+    p_bf16: Optional[torch.Tensor] = None,
+) -> None:
+    """One Adam/AdamW step over flat fp32 arenas, in place.
+
+    ``step`` is the 1-based step number AFTER this update (torch semantics), a
+    Python int or a device int64 tensor (graph-replay friendly).
+    """
+    if use_native(p):
+        step_t, host_step = _step_args(step)
+        require().adam_step(
+            p, g, m, v, p_bf16, float(lr), float(betas[0]), float(betas[1]), float(eps),
+            float(weight_decay), float(grad_scale), bool(adamw), bool(maximize), step_t,
+            host_step, lr_tensor,
+        )
+        return
+    t = int(step.item()) if isinstance(step, torch.Tensor) else int(step)
+    lr_v = float(lr_tensor.item()) if lr_tensor is not None else float(lr)
+    b1, b2 = betas
+    with torch.no_grad():
+        grad = g * grad_scale if grad_scale != 1.0 else g.clone()
+        if maximize:
+            grad = -grad
+        if weight_decay != 0:
+            if adamw:
+                p.mul_(1 - lr_v * weight_decay)
+            else:
+                grad = grad.add(p, alpha=weight_decay)
+        m.lerp_(grad, 1 - b1)
+        v.mul_(b2).addcmul_(grad, grad, value=1 - b2)
+        bc1 = 1 - b1 ** t
+        bc2 = 1 - b2 ** t
+        denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+        p.addcdiv_(m, denom, value=-(lr_v / bc1))
+        if p_bf16 is not None:
+            p_bf16.copy_(p)
+
+
+def fused_sgd_(
+    p: torch.Tensor,
+    g: torch.Tensor,
+    buf: Optional[torch.Tensor],
+    *,
+    lr: float,
+    momentum: float = 0.0,
+    dampening: float = 0.0,
+    weight_decay: float = 0.0,
+    nesterov: bool = False,
+    maximize: bool = False,
+    grad_scale: float = 1.0,
+    step: StepLike = 1,
+    lr_tensor: Optional[torch.Tensor] = None,
+    p_bf16: Optional[torch.Tensor] = None,
+) -> None:
+    """One SGD step (torch.optim.SGD semantics) over flat fp32 arenas."""
+    if use_native(p):
+        step_t, host_step = _step_args(step)
+        require().sgd_step(
+            p, g, buf, p_bf16, float(lr), float(momentum), float(dampening), float(weight_decay),
+            float(grad_scale), bool(nesterov), bool(maximize), step_t, host_step, lr_tensor,
+        )
+        return
+    t = int(step.item()) if isinstance(step, torch.Tensor) else int(step)
+    lr_v = float(lr_tensor.item()) if lr_tensor is not None else float(lr)
+    with torch.no_grad():
+        d = g * grad_scale if grad_scale != 1.0 else g.clone()
+        if maximize:
+            d = -d
+        if weight_decay != 0:
+            d = d.add(p, alpha=weight_decay)
+        if momentum != 0:
+            assert buf is not None
+            if t <= 1:
+                buf.copy_(d)
+            else:
+                buf.mul_(momentum).add_(d, alpha=1 - dampening)
+            d = d.add(buf, alpha=momentum) if nesterov else buf
+        p.add_(d, alpha=-lr_v)
+        if p_bf16 is not None:
+            p_bf16.copy_(p)
+
+
+_DT = {torch.float32: 0, torch.bfloat16: 1}
+CHUNK_ELEMS = 16384
+
+
+def build_copy_table(pairs: Sequence[Tuple[torch.Tensor, torch.Tensor]], device=None) -> torch.Tensor:
+    """Chunk table for :func:`multi_copy`: one row per <=16K-element chunk.
+
+    ``pairs`` are (src, dst) tensors of equal numel (fp32 or bf16, contiguous).
+    The table is built once per bucket layout and reused every step.
+    """
+    rows: List[List[int]] = []
+    for src, dst in pairs:
+        assert src.numel() == dst.numel(), "copy pair size mismatch"
+        assert src.is_contiguous() and dst.is_contiguous()
+        sd, dd = _DT[src.dtype], _DT[dst.dtype]
+        ss, ds = src.element_size(), dst.element_size()
+        n = src.numel()
+        for off in range(0, n, CHUNK_ELEMS):
+            cnt = min(CHUNK_ELEMS, n - off)
+            rows.append([src.data_ptr() + off * ss, dst.data_ptr() + off * ds, cnt, sd | (dd << 8)])
+    dev = device if device is not None else (pairs[0][0].device if pairs else "cpu")
+    return torch.tensor(rows, dtype=torch.int64, device=dev).reshape(-1, 4)
+
+
+def multi_copy(
+    pairs: Sequence[Tuple[torch.Tensor, torch.Tensor]],
+    scale: float = 1.0,
+    accumulate: bool = False,
+    table: Optional[torch.Tensor] = None,
+) -> None:
+    """dst (+)= src * scale for every pair, casting fp32<->bf16, in ONE launch on GPU."""
+    if not pairs:
+        return
+    if use_native(pairs[0][0]):
+        if table is None:
+            table = build_copy_table(pairs)
+        require().multi_copy(table, float(scale), bool(accumulate))
+        return
+    with torch.no_grad():
+        for src, dst in pairs:
+            val = src.float() * scale
+            if accumulate:
+                val = val + dst.float()
+            dst.copy_(val.view_as(dst))
+
+
+def scale_(x: torch.Tensor, s: float) -> None:
+    if use_native(x):
+        require().scale_(x, float(s))
+    else:
+        x.mul_(s)
+
+
+def sumsq(x: torch.Tensor) -> torch.Tensor:
+    if use_native(x):
+        return require().sumsq(x)
+    return (x.float() * x.float()).sum().reshape(1)
+
+
+def iter_chunks(n: int, chunk: int) -> Iterable[Tuple[int, int]]:
+    for off in range(0, n, chunk):
+        yield off, min(chunk, n - off)
