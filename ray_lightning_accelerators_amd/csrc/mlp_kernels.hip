@@ -93,12 +93,14 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 
 __device__ __forceinline__ bf16x8 lds8(const __bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
-typedef __attribute__((address_space(3))) short4v lds_short4;
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 // Transposed 4x16 read (ds_read_b64_tr_b16): lane i of each 16-lane group gets
 // column i of the 4 rows whose addresses lanes 4q+p supply (row q, cols 4p..4p+3).
-__device__ __forceinline__ short4v tr_read(const __bf16* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(p));
+// (The v4bf16 form is used directly: element-wise bit casts out of the v4i16 form
+// were mis-lowered by hipcc 7.2 into duplicated dwords.)
+__device__ __forceinline__ bf16x4 tr_read(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p));
 }
 
 // -------------------------------------------------------------------------
@@ -440,14 +442,9 @@ __device__ __forceinline__ void backward(const Smem& s, const GradSink& sink, fl
 #pragma unroll
       for (int ks = 0; ks < BC / 32; ++ks) {
         const int b0 = ks * 32 + 8 * g;
-        const short4v lo = tr_read(s.X + (b0 + q) * kXS + kt * 16 + 4 * p);
-        const short4v hi = tr_read(s.X + (b0 + 4 + q) * kXS + kt * 16 + 4 * p);
-        bf16x8 afrag;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          afrag[j] = __builtin_bit_cast(__bf16, lo[j]);
-          afrag[4 + j] = __builtin_bit_cast(__bf16, hi[j]);
-        }
+        const bf16x4 lo = tr_read(s.X + (b0 + q) * kXS + kt * 16 + 4 * p);
+        const bf16x4 hi = tr_read(s.X + (b0 + 4 + q) * kXS + kt * 16 + 4 * p);
+        const bf16x8 afrag = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
         const bf16x8 bfrag = lds8(s.dH1T + (ct * 16 + r16) * C::TS + b0);
         acc = mfma16(afrag, bfrag, acc);
       }

@@ -1,0 +1,318 @@
+"""Node daemon ("head") of the actor runtime -- the stand-in for Ray's GCS + raylet.
+
+Responsibilities (reference call sites in SURVEY.md §2.2 U17):
+  * resource accounting per (possibly simulated) node: CPUs, GPUs (with GPU
+    ids), custom resources; actors wait until their request fits;
+  * spawning worker processes with ``HIP_VISIBLE_DEVICES`` / ``CUDA_VISIBLE_DEVICES``
+    set to the allocated GPU (one whole GPU per training worker, reference
+    ray_ddp.py:94-96) and ``RLA_NODE_IP`` set to the node's address;
+  * the actor table (ALIVE / DEAD) behind ``runtime.actors()``;
+  * killing actors and noticing workers that die (fail-fast).
+
+The head never imports torch and never touches a GPU, so it can fork workers
+safely even when the driver process has already initialised HIP.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import signal
+import subprocess
+import sys
+import threading
+import time
+from typing import Dict, List, Optional
+
+from . import protocol as P
+
+
+class Node:
+    def __init__(self, ip: str, num_cpus: float, num_gpus: int, gpu_ids: List[str], resources: Dict[str, float]):
+        self.ip = ip
+        self.total = {"CPU": float(num_cpus), "GPU": float(num_gpus), **{k: float(v) for k, v in resources.items()}}
+        self.avail = dict(self.total)
+        self.free_gpus = list(gpu_ids)  # visible-device tokens in allocation order
+
+    def fits(self, req: Dict[str, float]) -> bool:
+        return all(self.avail.get(k, 0.0) + 1e-9 >= v for k, v in req.items() if v > 0)
+
+    def take(self, req: Dict[str, float]) -> List[str]:
+        for k, v in req.items():
+            if v > 0:
+                self.avail[k] = self.avail.get(k, 0.0) - v
+        n = int(round(req.get("GPU", 0)))
+        ids, self.free_gpus = self.free_gpus[:n], self.free_gpus[n:]
+        return ids
+
+    def give(self, req: Dict[str, float], gpu_ids: List[str]) -> None:
+        for k, v in req.items():
+            if v > 0:
+                self.avail[k] = self.avail.get(k, 0.0) + v
+        # keep GPU hand-out order stable (lowest id first), as Ray does per node
+        self.free_gpus = sorted(self.free_gpus + list(gpu_ids), key=lambda s: (len(s), s))
+
+
+class ActorRecord:
+    def __init__(self, actor_id: str, name: Optional[str], req: Dict[str, float], node: Node, gpu_ids: List[str]):
+        self.actor_id = actor_id
+        self.name = name
+        self.req = req
+        self.node = node
+        self.gpu_ids = gpu_ids
+        self.state = "PENDING_CREATION"
+        self.address: Optional[str] = None
+        self.proc: Optional[subprocess.Popen] = None
+        self.pid: Optional[int] = None
+        self.registered = threading.Event()
+        self.death_cause: Optional[str] = None
+        self.class_name = ""
+
+
+class Head:
+    def __init__(self, session_dir: str, authkey: bytes, nodes: List[Node], sys_path: str, log_dir: str):
+        self.session_dir = session_dir
+        self.authkey = authkey
+        self.nodes = nodes
+        self.sys_path = sys_path
+        self.log_dir = log_dir
+        self.lock = threading.Condition()
+        self.actors: Dict[str, ActorRecord] = {}
+        self.listener, self.address = P.make_listener(session_dir, authkey, "head")
+        self.stopping = False
+
+    # ---------------------------------------------------------- scheduling
+    def _place(self, req: Dict[str, float], node_ip: Optional[str]) -> Optional[Node]:
+        for n in self.nodes:
+            if node_ip is not None and n.ip != node_ip:
+                continue
+            if n.fits(req):
+                return n
+        return None
+
+    def _feasible(self, req: Dict[str, float], node_ip: Optional[str]) -> bool:
+        for n in self.nodes:
+            if node_ip is not None and n.ip != node_ip:
+                continue
+            if all(n.total.get(k, 0.0) + 1e-9 >= v for k, v in req.items() if v > 0):
+                return True
+        return False
+
+    def create_actor(self, msg: dict) -> dict:
+        req = {k: float(v) for k, v in msg["resources"].items() if v}
+        node_ip = msg.get("node_ip")
+        if not self._feasible(req, node_ip):
+            return {"ok": False, "error": f"infeasible resource request {req} (cluster: "
+                                         f"{[n.total for n in self.nodes]})"}
+        actor_id = P.new_id()
+        deadline = time.time() + float(msg.get("timeout", 3600))
+        with self.lock:
+            while True:
+                node = self._place(req, node_ip)
+                if node is not None:
+                    gpu_ids = node.take(req)
+                    break
+                if time.time() > deadline:
+                    return {"ok": False, "error": f"timed out waiting for resources {req}"}
+                self.lock.wait(timeout=0.5)
+            rec = ActorRecord(actor_id, msg.get("name"), req, node, gpu_ids)
+            rec.class_name = msg.get("class_name", "")
+            self.actors[actor_id] = rec
+        env = dict(os.environ)
+        env.update(msg.get("env") or {})
+        env[P.ENV_HEAD] = self.address
+        env[P.ENV_AUTH] = self.authkey.hex()
+        env[P.ENV_SESSION_DIR] = self.session_dir
+        env[P.ENV_NODE_IP] = node.ip
+        env[P.ENV_ACTOR_ID] = actor_id
+        env[P.ENV_SYS_PATH] = msg.get("sys_path") or self.sys_path
+        if "GPU" in req:
+            vis = ",".join(gpu_ids)
+            env["HIP_VISIBLE_DEVICES"] = vis
+            env["CUDA_VISIBLE_DEVICES"] = vis
+            env.pop("ROCR_VISIBLE_DEVICES", None) if msg.get("reset_rocr") else None
+        elif msg.get("hide_gpus", True):
+            env["HIP_VISIBLE_DEVICES"] = ""
+            env["CUDA_VISIBLE_DEVICES"] = ""
+        env["RLA_GPU_IDS"] = ",".join(gpu_ids)
+        env["PYTHONUNBUFFERED"] = "1"
+        log = open(os.path.join(self.log_dir, f"worker-{actor_id[:8]}.log"), "ab")
+        cmd = [sys.executable, "-m", "ray_lightning_accelerators_amd.runtime.worker"]
+        proc = subprocess.Popen(cmd, env=env, stdout=log if msg.get("capture_output", True) else None,
+                                stderr=subprocess.STDOUT if msg.get("capture_output", True) else None,
+                                cwd=msg.get("cwd") or os.getcwd(), start_new_session=True)
+        log.close()
+        rec.proc = proc
+        rec.pid = proc.pid
+        # wait for the worker to register its listener
+        while not rec.registered.wait(timeout=0.2):
+            if proc.poll() is not None:
+                self._mark_dead(rec, f"worker exited during startup (code {proc.returncode})")
+                return {"ok": False, "error": rec.death_cause, "log": self._tail_log(actor_id)}
+            if time.time() > deadline:
+                self._kill(rec, "startup timeout")
+                return {"ok": False, "error": "worker startup timed out"}
+        return {"ok": True, "actor_id": actor_id, "address": rec.address, "node_ip": node.ip,
+                "gpu_ids": gpu_ids, "pid": rec.pid}
+
+    def _tail_log(self, actor_id: str, n: int = 4000) -> str:
+        try:
+            with open(os.path.join(self.log_dir, f"worker-{actor_id[:8]}.log"), "rb") as f:
+                return f.read()[-n:].decode(errors="replace")
+        except OSError:
+            return ""
+
+    def _mark_dead(self, rec: ActorRecord, cause: str) -> None:
+        with self.lock:
+            if rec.state == "DEAD":
+                return
+            rec.state = "DEAD"
+            rec.death_cause = cause
+            rec.node.give(rec.req, rec.gpu_ids)
+            self.lock.notify_all()
+
+    def _kill(self, rec: ActorRecord, cause: str) -> None:
+        proc = rec.proc
+        if proc is not None and proc.poll() is None:
+            try:
+                os.killpg(proc.pid, signal.SIGTERM)
+            except (ProcessLookupError, PermissionError):
+                pass
+            try:
+                proc.wait(timeout=5)
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(proc.pid, signal.SIGKILL)
+                except (ProcessLookupError, PermissionError):
+                    pass
+                proc.wait(timeout=5)
+        self._mark_dead(rec, cause)
+
+    # ----------------------------------------------------------- handlers
+    def handle(self, conn: P.SafeConn) -> None:
+        while True:
+            try:
+                msg = conn.recv()
+            except (EOFError, OSError):
+                return
+            op = msg.get("op")
+            try:
+                if op == "create_actor":
+                    reply = self.create_actor(msg)
+                elif op == "register":
+                    rec = self.actors.get(msg["actor_id"])
+                    if rec is not None:
+                        rec.address = msg["address"]
+                        rec.state = "ALIVE"
+                        rec.registered.set()
+                    reply = {"ok": True}
+                elif op == "kill":
+                    rec = self.actors.get(msg["actor_id"])
+                    if rec is not None:
+                        self._kill(rec, msg.get("cause", "killed"))
+                    reply = {"ok": True}
+                elif op == "actors":
+                    with self.lock:
+                        reply = {"ok": True, "actors": {
+                            a.actor_id: {"ActorID": a.actor_id, "State": a.state, "Name": a.name,
+                                         "Pid": a.pid, "NodeIP": a.node.ip, "GPUIds": a.gpu_ids,
+                                         "ClassName": a.class_name, "DeathCause": a.death_cause,
+                                         "Address": a.address}
+                            for a in self.actors.values()}}
+                elif op == "resources":
+                    with self.lock:
+                        tot, av = {}, {}
+                        for n in self.nodes:
+                            for k, v in n.total.items():
+                                tot[k] = tot.get(k, 0.0) + v
+                            for k, v in n.avail.items():
+                                av[k] = av.get(k, 0.0) + v
+                        reply = {"ok": True, "total": tot, "available": av,
+                                 "nodes": [{"ip": n.ip, "total": dict(n.total), "available": dict(n.avail)}
+                                           for n in self.nodes]}
+                elif op == "ping":
+                    reply = {"ok": True, "pid": os.getpid()}
+                elif op == "shutdown":
+                    conn.send({"ok": True})
+                    self.shutdown()
+                    return
+                else:
+                    reply = {"ok": False, "error": f"unknown op {op}"}
+            except Exception as e:  # noqa: BLE001
+                reply = {"ok": False, "error": repr(e)}
+            try:
+                conn.send(reply)
+            except (OSError, EOFError):
+                return
+
+    def monitor(self) -> None:
+        while not self.stopping:
+            time.sleep(0.2)
+            with self.lock:
+                recs = list(self.actors.values())
+            for rec in recs:
+                if rec.state != "DEAD" and rec.proc is not None and rec.proc.poll() is not None:
+                    self._mark_dead(rec, f"worker process exited with code {rec.proc.returncode}")
+
+    def shutdown(self) -> None:
+        self.stopping = True
+        for rec in list(self.actors.values()):
+            if rec.state != "DEAD":
+                self._kill(rec, "runtime shutdown")
+        try:
+            self.listener.close()
+        except OSError:
+            pass
+        os._exit(0)
+
+    def serve(self, ready_fd: Optional[int]) -> None:
+        threading.Thread(target=self.monitor, daemon=True).start()
+        if ready_fd is not None:
+            os.write(ready_fd, (self.address + "\n").encode())
+            os.close(ready_fd)
+        while not self.stopping:
+            try:
+                c = self.listener.accept()
+            except (OSError, EOFError):
+                if self.stopping:
+                    break
+                continue
+            threading.Thread(target=self.handle, args=(P.SafeConn(c),), daemon=True).start()
+
+
+def parse_nodes(spec: str) -> List[Node]:
+    """spec: JSON list of {ip, num_cpus, num_gpus, gpu_ids, resources}."""
+    import json
+
+    nodes = []
+    for d in json.loads(spec):
+        nodes.append(Node(d["ip"], d.get("num_cpus", 1), int(d.get("num_gpus", 0)),
+                          [str(x) for x in d.get("gpu_ids", [])], d.get("resources", {})))
+    return nodes
+
+
+def main(argv=None) -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--session-dir", required=True)
+    ap.add_argument("--nodes", required=True)
+    ap.add_argument("--ready-fd", type=int, default=None)
+    ap.add_argument("--parent-pid", type=int, default=None)
+    args = ap.parse_args(argv)
+    authkey = bytes.fromhex(os.environ[P.ENV_AUTH])
+    log_dir = os.path.join(args.session_dir, "logs")
+    os.makedirs(log_dir, exist_ok=True)
+    head = Head(args.session_dir, authkey, parse_nodes(args.nodes), os.environ.get(P.ENV_SYS_PATH, ""), log_dir)
+    if args.parent_pid:
+        def watch_parent():
+            while True:
+                time.sleep(1.0)
+                try:
+                    os.kill(args.parent_pid, 0)
+                except ProcessLookupError:
+                    head.shutdown()
+        threading.Thread(target=watch_parent, daemon=True).start()
+    signal.signal(signal.SIGTERM, lambda *a: head.shutdown())
+    head.serve(args.ready_fd)
+
+
+if __name__ == "__main__":
+    main()

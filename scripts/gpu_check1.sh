@@ -6,7 +6,7 @@ cd "$R"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 echo "== host: $(hostname) gpus: $(python -c 'import torch;print(torch.cuda.device_count())')"
-timeout -k 10 900 python -m pytest tests/test_kernels.py -x -q -m gpu > gpurun_out/pytest_kernels.log 2>&1
+timeout -k 10 900 python -m pytest tests/test_kernels.py -q -m gpu > gpurun_out/pytest_kernels.log 2>&1
 rc=$?; tail -5 gpurun_out/pytest_kernels.log; echo "pytest rc=$rc"
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --steps 2000 --warmup 200 > gpurun_out/bench_native.log 2>&1; rc=$?; cat gpurun_out/bench_native.log; [ $rc -eq 0 ] || exit $rc
