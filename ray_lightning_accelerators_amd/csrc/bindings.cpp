@@ -116,7 +116,8 @@ void mlp_train_step(optional<Tensor> x_u8, optional<Tensor> x_f32, Tensor labels
                     int64_t L1, int64_t L2, Tensor params, Tensor grads, optional<Tensor> exp_avg,
                     optional<Tensor> exp_avg_sq, optional<Tensor> stats, bool accumulate_grad,
                     bool apply_adam, bool advance_step, double lr, double beta1, double beta2,
-                    double eps, double weight_decay, optional<Tensor> lr_t, bool adamw) {
+                    double eps, double weight_decay, optional<Tensor> lr_t, bool adamw,
+                    optional<Tensor> stamps) {
   TORCH_CHECK(rla::mlp_supported((int)L1, (int)L2), "no fused MLP kernel for layer sizes ", L1, "/", L2);
   TORCH_CHECK(B >= 1, "batch size must be >= 1");
   const int64_t np = mlp_param_count(L1, L2);
@@ -160,6 +161,7 @@ void mlp_train_step(optional<Tensor> x_u8, optional<Tensor> x_f32, Tensor labels
   a.weight_decay = (float)weight_decay;
   a.lr_ptr = ptr_or_null<const float>(lr_t, "lr", at::kFloat, 1);
   a.adamw = adamw;
+  a.stamps = ptr_or_null<int64_t>(stamps, "stamps", at::kLong, 16);
   TORCH_CHECK(rla::launch_mlp_train_step(a, cur_stream(params)) == 0, "fused MLP launch failed");
 }
 
@@ -201,7 +203,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("multi_copy", &multi_copy, "multi-tensor copy/scale/cast via a chunk table");
   m.def("scale_", &scale_, "in-place scale of an fp32 arena");
   m.def("sumsq", &sumsq, "sum of squares of an fp32 arena");
-  m.def("mlp_train_step", &mlp_train_step, "fused MNIST-MLP forward+backward(+Adam) step");
+  m.def("mlp_train_step", &mlp_train_step, "fused MNIST-MLP forward+backward(+Adam) step",
+        py::arg("x_u8"), py::arg("x_f32"), py::arg("labels"), py::arg("order"), py::arg("counters"),
+        py::arg("n_batches"), py::arg("B"), py::arg("L1"), py::arg("L2"), py::arg("params"),
+        py::arg("grads"), py::arg("exp_avg"), py::arg("exp_avg_sq"), py::arg("stats"),
+        py::arg("accumulate_grad"), py::arg("apply_adam"), py::arg("advance_step"), py::arg("lr"),
+        py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"), py::arg("lr_t"),
+        py::arg("adamw"), py::arg("stamps") = py::none());
   m.def("mlp_eval", &mlp_eval, "fused MNIST-MLP forward + NLL/accuracy");
   m.def("mlp_supported", [](int64_t a, int64_t b) { return rla::mlp_supported((int)a, (int)b); });
   m.def("mlp_param_count", &mlp_param_count);

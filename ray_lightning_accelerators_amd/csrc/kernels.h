@@ -67,6 +67,7 @@ struct MLPStepArgs {
   float lr, beta1, beta2, eps, weight_decay;
   const float* lr_ptr;
   int adamw;
+  int64_t* stamps;          // optional [16] phase timestamps (diagnostics)
 };
 
 struct MLPEvalArgs {

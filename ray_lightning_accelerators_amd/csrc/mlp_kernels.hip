@@ -68,7 +68,14 @@ struct Smem {
   __bf16 *X, *H1, *H1T, *H2, *H2T, *dH2T, *dH1T, *dZ, *dZT;
   float *acc1, *Z, *misc;
   int* ys;
+  int64_t* stamps;  // diagnostic phase timestamps (s_memrealtime, 100 MHz) or null
 };
+
+// Phase stamps for the diagnostic build path: thread 0, right after a barrier.
+#define RLA_STAMP(s, k)                                                        \
+  do {                                                                         \
+    if ((s).stamps && threadIdx.x == 0) (s).stamps[k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 
 template <class C>
 __device__ __forceinline__ Smem carve(char* smem) {
@@ -86,6 +93,7 @@ __device__ __forceinline__ Smem carve(char* smem) {
   s.dZT = (__bf16*)(smem + C::odZT);
   s.ys = (int*)(smem + C::oY);
   s.misc = (float*)(smem + C::oMisc);
+  s.stamps = nullptr;
   return s;
 }
 
@@ -211,6 +219,7 @@ __device__ __forceinline__ void forward(const Smem& s, const float* P) {
       }
   }
   __syncthreads();
+  RLA_STAMP(s, 2);
   for (int e = tid; e < BC * L1; e += kThreads) {
     const int b = e / L1, j = e - b * L1;
     const __bf16 h = (__bf16)fmaxf(s.acc1[e] + b1[j], 0.f);
@@ -218,6 +227,7 @@ __device__ __forceinline__ void forward(const Smem& s, const float* P) {
     s.H1T[j * C::TS + b] = h;
   }
   __syncthreads();
+  RLA_STAMP(s, 3);
 
   // ---- layer 2 ----
   for (int tile = w; tile < C::MT * C::TN2; tile += kWaves) {
@@ -243,6 +253,7 @@ __device__ __forceinline__ void forward(const Smem& s, const float* P) {
     *reinterpret_cast<bf16x4*>(s.H2T + n * C::TS + mt * 16 + 4 * g) = t4;
   }
   __syncthreads();
+  RLA_STAMP(s, 4);
 
   // ---- layer 3 (logits, classes padded to 16) ----
   if (w < C::MT) {
@@ -263,6 +274,7 @@ __device__ __forceinline__ void forward(const Smem& s, const float* P) {
     }
   }
   __syncthreads();
+  RLA_STAMP(s, 5);
 }
 
 // log_softmax + NLL + argmax for one row; returns false for padded rows.
@@ -382,6 +394,7 @@ __device__ __forceinline__ void backward(const Smem& s, const GradSink& sink, fl
     for (int j = 0; j < 16; ++j) s.dZT[j * C::TS + r] = (j < kNC) ? d8[j >> 3][j & 7] : (__bf16)0.f;
   }
   __syncthreads();
+  RLA_STAMP(s, 6);
 
   // ---- dH2 = (dZ W3) * (H2 > 0); written in place of H2 and transposed ----
   for (int tile = w; tile < C::MT * C::TN2; tile += kWaves) {
@@ -405,6 +418,7 @@ __device__ __forceinline__ void backward(const Smem& s, const GradSink& sink, fl
     *reinterpret_cast<bf16x4*>(s.dH2T + n * C::TS + mt * 16 + 4 * g) = t4;
   }
   __syncthreads();
+  RLA_STAMP(s, 7);
 
   // ---- dH1 = (dH2 W2) * (H1 > 0), stored transposed ----
   for (int tile = w; tile < C::MT * C::TN1; tile += kWaves) {
@@ -428,6 +442,7 @@ __device__ __forceinline__ void backward(const Smem& s, const GradSink& sink, fl
     *reinterpret_cast<bf16x4*>(s.dH1T + m * C::TS + mt * 16 + 4 * g) = t4;
   }
   __syncthreads();
+  RLA_STAMP(s, 8);
 
   // ---- weight gradients (+ fused Adam): dW1 tiles, dW2 tiles, dW3 tiles ----
   constexpr int NT_W1 = (kD / 16) * C::TN1;
@@ -495,13 +510,15 @@ __device__ __forceinline__ void backward(const Smem& s, const GradSink& sink, fl
     sink.put1(gi, sum);
   }
   __syncthreads();
+  RLA_STAMP(s, 9);
 }
 
 template <int BC, int L1, int L2, bool U8>
 __global__ __launch_bounds__(kThreads) void mlp_train_kernel(MLPStepArgs a) {
   using C = Cfg<BC, L1, L2>;
   __shared__ __attribute__((aligned(16))) char smem[C::total];
-  const Smem s = carve<C>(smem);
+  Smem s = carve<C>(smem);
+  s.stamps = a.stamps;
   __shared__ int64_t sh_t, sh_cursor;
   __shared__ AdamScal sh_o;
   if (threadIdx.x == 0) {
@@ -519,6 +536,7 @@ __global__ __launch_bounds__(kThreads) void mlp_train_kernel(MLPStepArgs a) {
     s.misc[0] = 0.f; s.misc[1] = 0.f; s.misc[2] = 0.f;
   }
   __syncthreads();
+  RLA_STAMP(s, 0);
   const int64_t* idx = U8 ? a.order + sh_cursor * a.B : nullptr;
   const float invB = 1.f / (float)a.B;
   const int nchunks = (a.B + BC - 1) / BC;
@@ -527,6 +545,7 @@ __global__ __launch_bounds__(kThreads) void mlp_train_kernel(MLPStepArgs a) {
     const int nvalid = min(BC, a.B - row0);
     stage_inputs<BC, L1, U8>(s, a.x_u8, a.x_f32, a.labels, idx, row0, nvalid);
     __syncthreads();
+    RLA_STAMP(s, 1);
     forward<BC, L1, L2>(s, a.params);
     GradSink sink;
     sink.P = a.params; sink.G = a.grads; sink.M = a.exp_avg; sink.V = a.exp_avg_sq;
@@ -535,6 +554,7 @@ __global__ __launch_bounds__(kThreads) void mlp_train_kernel(MLPStepArgs a) {
     sink.o = sh_o;
     backward<BC, L1, L2>(s, sink, invB);
   }
+  RLA_STAMP(s, 10);
   if (threadIdx.x == 0) {
     const int64_t t = sh_t;
     if (a.counters) {

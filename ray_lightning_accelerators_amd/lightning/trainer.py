@@ -1,0 +1,812 @@
+"""Lightning-compatible ``Trainer``.
+
+Re-implements the PyTorch Lightning 1.1 training-loop contract that the
+reference inherits: ``fit`` returns 1, the sanity
+validation run (``running_sanity_check``), train/val/test loops with
+``limit_*_batches``, ``DistributedSampler`` injection when the accelerator
+requires it (reference ray_ddp.py:280-295), hook ordering (validation before
+``on_epoch_end``), ``ModelCheckpoint``/``EarlyStopping``, LR schedulers,
+gradient accumulation/clipping, ``self.log`` metrics in ``callback_metrics``,
+and the Lightning checkpoint format.
+
+Distribution is delegated to the accelerator object: the driver calls
+``accelerator.setup(model) -> train() -> teardown()``; every worker then runs
+``Trainer._run(model)`` (via the accelerator's ``ddp_train``-style entry).
+"""
+from __future__ import annotations
+
+import math
+import os
+from collections import defaultdict
+from typing import Any, Dict, List, Optional, Sequence, Union
+
+import torch
+from torch.utils.data import DataLoader, DistributedSampler, RandomSampler, SequentialSampler
+
+from .callbacks import Callback, EarlyStopping, ModelCheckpoint
+from .core import LightningDataModule, LightningModule, _normalize_optimizers
+from .loggers import CSVLogger, LightningLoggerBase
+from .utilities import atomic_save, load_checkpoint, log, move_to_device, rank_zero_warn
+
+PL_COMPAT_VERSION = "1.1.7"
+
+
+class _CheckpointConnector:
+    def __init__(self, trainer: "Trainer"):
+        self.trainer = trainer
+
+    def dump_checkpoint(self, weights_only: bool = False) -> dict:
+        """The Lightning checkpoint dict (PL 1.1 layout; callback keys are class names)."""
+        t = self.trainer
+        model = t.get_model()
+        ckpt: Dict[str, Any] = {
+            "epoch": t.current_epoch + 1,
+            "global_step": t.global_step + 1,
+            "pytorch-lightning_version": PL_COMPAT_VERSION,
+        }
+        if not weights_only:
+            cb_states = {}
+            for cb in t.callbacks:
+                st = cb.on_save_checkpoint(t, model, ckpt)
+                if st is not None:
+                    cb_states[cb.state_key] = st
+            ckpt["callbacks"] = cb_states
+            ckpt["optimizer_states"] = [t._optimizer_state_dict(o) for o in t.optimizers]
+            ckpt["lr_schedulers"] = [s["scheduler"].state_dict() for s in t.lr_schedulers]
+        ckpt["state_dict"] = t._model_state_dict(model)
+        hp = dict(model.hparams) if getattr(model, "hparams", None) else {}
+        if hp:
+            ckpt[LightningModule.CHECKPOINT_HYPER_PARAMS_NAME] = "hparams"
+            ckpt[LightningModule.CHECKPOINT_HYPER_PARAMS_KEY] = hp
+        model.on_save_checkpoint(ckpt)
+        return ckpt
+
+    def restore(self, checkpoint_path: str, on_gpu: bool = False) -> None:
+        t = self.trainer
+        ckpt = load_checkpoint(checkpoint_path, map_location="cpu")
+        model = t.get_model()
+        model.on_load_checkpoint(ckpt)
+        model.load_state_dict(ckpt["state_dict"])
+        if t._fused is not None:
+            t._fused.load_params_from_module()
+        for cb in t.callbacks:
+            st = ckpt.get("callbacks", {}).get(cb.state_key)
+            if st is not None:
+                cb.on_load_checkpoint(st)
+        for opt, st in zip(t.optimizers, ckpt.get("optimizer_states", [])):
+            opt.load_state_dict(st)
+        for s, st in zip(t.lr_schedulers, ckpt.get("lr_schedulers", [])):
+            s["scheduler"].load_state_dict(st)
+        t.current_epoch = ckpt.get("epoch", 0)
+        t.global_step = ckpt.get("global_step", 0)
+
+
+class Trainer:
+    def __init__(
+        self,
+        default_root_dir: Optional[str] = None,
+        gpus: Optional[Union[int, List[int]]] = None,
+        max_epochs: Optional[int] = None,
+        min_epochs: Optional[int] = None,
+        max_steps: Optional[int] = None,
+        limit_train_batches: Union[int, float] = 1.0,
+        limit_val_batches: Union[int, float] = 1.0,
+        limit_test_batches: Union[int, float] = 1.0,
+        val_check_interval: Union[int, float] = 1.0,
+        check_val_every_n_epoch: int = 1,
+        num_sanity_val_steps: int = 2,
+        progress_bar_refresh_rate: int = 1,
+        checkpoint_callback: bool = True,
+        callbacks: Optional[List[Callback]] = None,
+        accelerator: Any = None,
+        precision: Union[int, str] = 32,
+        gradient_clip_val: float = 0.0,
+        accumulate_grad_batches: int = 1,
+        logger: Union[bool, LightningLoggerBase] = True,
+        log_every_n_steps: int = 50,
+        resume_from_checkpoint: Optional[str] = None,
+        deterministic: bool = False,
+        benchmark: bool = False,
+        weights_summary: Optional[str] = "top",
+        fast_dev_run: Union[bool, int] = False,
+        num_nodes: int = 1,
+        sync_batchnorm: bool = False,
+        replace_sampler_ddp: bool = True,
+        reload_dataloaders_every_epoch: bool = False,
+        fused_step: Optional[bool] = None,
+        **kwargs,
+    ):
+        for k in kwargs:
+            rank_zero_warn(f"Trainer argument {k!r} is accepted for compatibility and ignored")
+        self.default_root_dir = default_root_dir or os.getcwd()
+        if isinstance(gpus, (list, tuple)):
+            gpus = len(gpus)
+        elif isinstance(gpus, str):
+            gpus = len([g for g in gpus.split(",") if g.strip()])
+        self.gpus = int(gpus or 0)
+        self.fast_dev_run = int(fast_dev_run) if fast_dev_run else 0
+        if self.fast_dev_run:
+            max_epochs = 1
+            limit_train_batches = limit_val_batches = limit_test_batches = self.fast_dev_run
+            num_sanity_val_steps = 0
+        self.max_epochs = 1000 if max_epochs is None else int(max_epochs)
+        self.min_epochs = 1 if min_epochs is None else int(min_epochs)
+        self.max_steps = max_steps
+        self.limit_train_batches = limit_train_batches
+        self.limit_val_batches = limit_val_batches
+        self.limit_test_batches = limit_test_batches
+        self.val_check_interval = val_check_interval
+        self.check_val_every_n_epoch = check_val_every_n_epoch
+        self.num_sanity_val_steps = num_sanity_val_steps
+        self.progress_bar_refresh_rate = progress_bar_refresh_rate
+        self.precision = precision
+        self.gradient_clip_val = gradient_clip_val
+        self.accumulate_grad_batches = int(accumulate_grad_batches)
+        self.log_every_n_steps = log_every_n_steps
+        self.resume_from_checkpoint = resume_from_checkpoint
+        self.deterministic = deterministic
+        self.num_nodes = num_nodes
+        self.sync_batchnorm = sync_batchnorm
+        self.replace_sampler_ddp = replace_sampler_ddp
+        self.reload_dataloaders_every_epoch = reload_dataloaders_every_epoch
+        self.weights_summary = weights_summary
+        self.fused_step = fused_step
+        if deterministic:
+            torch.use_deterministic_algorithms(True, warn_only=True)
+        # callbacks
+        self.callbacks: List[Callback] = list(callbacks or [])
+        self._checkpoint_enabled = bool(checkpoint_callback)
+        if isinstance(checkpoint_callback, ModelCheckpoint):
+            self.callbacks.append(checkpoint_callback)
+        elif checkpoint_callback and not any(isinstance(c, ModelCheckpoint) for c in self.callbacks):
+            self.callbacks.append(ModelCheckpoint())
+        # logger
+        if logger is True:
+            self.logger: Optional[LightningLoggerBase] = CSVLogger(self.default_root_dir)
+        elif logger is False or logger is None:
+            self.logger = None
+        else:
+            self.logger = logger
+        self.accelerator = accelerator
+        self.accelerator_backend = None
+        self.distributed_backend = None
+        # state
+        self.global_rank = 0
+        self.local_rank = 0
+        self.node_rank = 0
+        self.world_size = 1
+        self.root_gpu: Optional[int] = None
+        self.use_ddp = False
+        self.use_horovod = False
+        self.use_dp = False
+        self.use_single_gpu = False
+        self.model: Optional[LightningModule] = None
+        self.datamodule: Optional[LightningDataModule] = None
+        self.train_dataloader: Optional[DataLoader] = None
+        self.val_dataloaders: Optional[List[DataLoader]] = None
+        self.test_dataloaders: Optional[List[DataLoader]] = None
+        self.num_training_batches = 0
+        self.num_val_batches: List[int] = []
+        self.num_test_batches: List[int] = []
+        self.callback_metrics: Dict[str, Any] = {}
+        self.logged_metrics: Dict[str, Any] = {}
+        self.progress_bar_metrics: Dict[str, Any] = {}
+        self.running_sanity_check = False
+        self.testing = False
+        self.training = False
+        self.current_epoch = 0
+        self.global_step = 0
+        self.should_stop = False
+        self.optimizers: List[torch.optim.Optimizer] = []
+        self.lr_schedulers: List[dict] = []
+        self.optimizer_frequencies: List[int] = []
+        self.checkpoint_connector = _CheckpointConnector(self)
+        self.interrupted = False
+        self._has_val_loop = False
+        self._fused = None
+        self._log_dir: Optional[str] = None
+        self._train_dl_src = self._val_dl_src = self._test_dl_src = None
+        self._results: Dict[str, Dict[str, list]] = {}
+        self._current_fx: Optional[str] = None
+        self.test_results = None
+
+    # ------------------------------------------------------------ properties
+    @property
+    def on_gpu(self) -> bool:
+        acc = self.accelerator
+        if acc is not None and hasattr(acc, "use_gpu"):
+            return bool(acc.use_gpu) or self.gpus > 0 and bool(getattr(acc, "use_gpu", True))
+        return self.gpus > 0
+
+    @property
+    def is_global_zero(self) -> bool:
+        return self.global_rank == 0
+
+    @property
+    def checkpoint_callback(self) -> Optional[ModelCheckpoint]:
+        for c in self.callbacks:
+            if isinstance(c, ModelCheckpoint):
+                return c
+        return None
+
+    @property
+    def checkpoint_callbacks(self) -> List[ModelCheckpoint]:
+        return [c for c in self.callbacks if isinstance(c, ModelCheckpoint)]
+
+    @property
+    def early_stopping_callback(self) -> Optional[EarlyStopping]:
+        for c in self.callbacks:
+            if isinstance(c, EarlyStopping):
+                return c
+        return None
+
+    @property
+    def log_dir(self) -> Optional[str]:
+        if self._log_dir is not None:
+            return self._log_dir
+        if self.logger is not None and getattr(self.logger, "log_dir", None):
+            return self.logger.log_dir
+        return self.default_root_dir
+
+    @property
+    def lightning_module(self) -> Optional[LightningModule]:
+        return self.get_model()
+
+    def get_model(self) -> Optional[LightningModule]:
+        m = self.model
+        while m is not None and hasattr(m, "module") and not isinstance(m, LightningModule):
+            m = m.module
+        return m
+
+    # ---------------------------------------------------------------- public
+    def fit(self, model: LightningModule, train_dataloader: Optional[DataLoader] = None,
+            val_dataloaders: Optional[Union[DataLoader, List[DataLoader]]] = None,
+            datamodule: Optional[LightningDataModule] = None):
+        self._attach(model, train_dataloader, val_dataloaders, None, datamodule)
+        self.testing = False
+        self._prepare_data_on_driver(model)
+        results = self._launch(model)
+        return results if results not in (None, 0) else 1
+
+    def test(self, model: Optional[LightningModule] = None, test_dataloaders=None, ckpt_path: Optional[str] = "best",
+             verbose: bool = True, datamodule: Optional[LightningDataModule] = None):
+        if model is None:
+            model = self.get_model()
+            if ckpt_path == "best" and self.checkpoint_callback and self.checkpoint_callback.best_model_path:
+                ckpt = load_checkpoint(self.checkpoint_callback.best_model_path)
+                model.load_state_dict(ckpt["state_dict"])
+            elif ckpt_path not in (None, "best"):
+                ckpt = load_checkpoint(ckpt_path)
+                model.load_state_dict(ckpt["state_dict"])
+        self._attach(model, None, None, test_dataloaders, datamodule)
+        self.testing = True
+        self._prepare_data_on_driver(model)
+        try:
+            results = self._launch(model)
+        finally:
+            self.testing = False
+        if verbose and results and self.is_global_zero:
+            for i, r in enumerate(results):
+                print(f"TEST RESULTS (dataloader {i}): {r}")
+        return results
+
+    def validate(self, model: Optional[LightningModule] = None, val_dataloaders=None,
+                 datamodule: Optional[LightningDataModule] = None):
+        model = model or self.get_model()
+        self._attach(model, None, val_dataloaders, None, datamodule)
+        model.trainer = self
+        self._setup_stage(model, "validate")
+        self._prepare_dataloaders(model)
+        return self.run_evaluation(test_mode=False)
+
+    def save_checkpoint(self, filepath: str, weights_only: bool = False) -> None:
+        ckpt = self.checkpoint_connector.dump_checkpoint(weights_only)
+        if self.is_global_zero:
+            atomic_save(ckpt, filepath)
+
+    # ------------------------------------------------------------- driving
+    def _attach(self, model, train_dl, val_dls, test_dls, datamodule) -> None:
+        model.trainer = self
+        self.model = model
+        if train_dl is not None:
+            self._train_dl_src = train_dl
+        if val_dls is not None:
+            self._val_dl_src = val_dls
+        if test_dls is not None:
+            self._test_dl_src = test_dls
+        if datamodule is not None:
+            self.datamodule = datamodule
+            datamodule.trainer = self
+
+    def _prepare_data_on_driver(self, model: LightningModule) -> None:
+        # PL data_connector.prepare_data: on the DRIVER (reference examples rely on it,
+        # ray_ddp_example.py:23-28: the dataset is pickled to the workers with the model)
+        dm = self.datamodule
+        if dm is not None and not getattr(dm, "has_prepared_data", False):
+            dm.prepare_data()
+            dm.has_prepared_data = True
+        model.prepare_data()
+        if self._log_dir is None and self.logger is not None:
+            self._log_dir = self.logger.log_dir
+
+    def _launch(self, model: LightningModule):
+        from .accelerators import resolve_accelerator
+
+        acc = resolve_accelerator(self)
+        acc.trainer = self
+        acc.setup(model)
+        try:
+            results = acc.train()
+        finally:
+            acc.teardown()
+        return results
+
+    # -------------------------------------------------- worker-side entry
+    def _setup_stage(self, model: LightningModule, stage: str) -> None:
+        dm = self.datamodule
+        if dm is not None:
+            flag = "has_setup_test" if stage == "test" else "has_setup_fit"
+            if not getattr(dm, flag, False):
+                dm.setup(stage)
+                setattr(dm, flag, True)
+        model.setup(stage)
+        for cb in self.callbacks:
+            cb.setup(self, model, stage)
+
+    def call_setup_hook(self, model: LightningModule) -> None:
+        self._setup_stage(model, "test" if self.testing else "fit")
+
+    def _run(self, model: LightningModule):
+        """Everything after process-group bring-up and device placement (runs on every worker)."""
+        model.trainer = self
+        self.model = model
+        self.call_setup_hook(model)
+        self._prepare_dataloaders(model)
+        if self.testing:
+            self.optimizers, self.lr_schedulers = [], []
+            results = self.run_test()
+            model.teardown("test")
+            return results
+        opts, scheds = _normalize_optimizers(model.configure_optimizers())
+        self.optimizers, self.lr_schedulers = self.accelerator_backend.setup_optimizers(model, opts, scheds)
+        self.accelerator_backend.configure_ddp(model)
+        self._fused = self._maybe_fused(model)
+        if self.resume_from_checkpoint and os.path.exists(self.resume_from_checkpoint):
+            self.checkpoint_connector.restore(self.resume_from_checkpoint, on_gpu=self.on_gpu)
+        self.run_train()
+        model.teardown("fit")
+        return None
+
+    def _maybe_fused(self, model: LightningModule):
+        """Model-provided fused training step (e.g. MNISTClassifier's single HIP launch)."""
+        want = self.fused_step
+        if want is False or not hasattr(model, "configure_fused_step"):
+            return None
+        if self.accumulate_grad_batches != 1 or self.gradient_clip_val:
+            return None
+        try:
+            return model.configure_fused_step(self)
+        except Exception as e:  # noqa: BLE001
+            if want:
+                raise
+            log.info(f"fused step unavailable ({e!r}); using the autograd path")
+            return None
+
+    # ----------------------------------------------------------- dataloaders
+    def _resolve_loader(self, name: str, model: LightningModule):
+        src = {"train": self._train_dl_src, "val": self._val_dl_src, "test": self._test_dl_src}[name]
+        if src is None and self.datamodule is not None:
+            src = getattr(self.datamodule, f"{name}_dataloader")()
+        if src is None:
+            src = getattr(model, f"{name}_dataloader")()
+        return src
+
+    def _maybe_replace_sampler(self, dl: DataLoader, shuffle: bool) -> DataLoader:
+        acc = self.accelerator_backend
+        if dl is None or acc is None or not acc.require_distributed_sampler or not self.replace_sampler_ddp:
+            return dl
+        if isinstance(dl.sampler, DistributedSampler):
+            return dl
+        kw = dict(acc.distributed_sampler_kwargs)
+        sampler = DistributedSampler(dl.dataset, shuffle=shuffle, **kw)
+        return DataLoader(
+            dl.dataset, batch_size=dl.batch_size, sampler=sampler, num_workers=dl.num_workers,
+            collate_fn=dl.collate_fn, pin_memory=dl.pin_memory, drop_last=dl.drop_last,
+            timeout=dl.timeout, worker_init_fn=dl.worker_init_fn,
+            persistent_workers=getattr(dl, "persistent_workers", False) and dl.num_workers > 0,
+        )
+
+    @staticmethod
+    def _num_batches(dl, limit) -> int:
+        try:
+            n = len(dl)
+        except TypeError:
+            n = math.inf
+        if isinstance(limit, float):
+            if limit >= 1.0:
+                return n if n != math.inf else int(1e18)
+            return int(n * limit) if n != math.inf else int(1e18)
+        return min(int(limit), n) if n != math.inf else int(limit)
+
+    def _prepare_dataloaders(self, model: LightningModule) -> None:
+        if not self.testing:
+            dl = self._resolve_loader("train", model)
+            self.train_dataloader = self._maybe_replace_sampler(dl, shuffle=True) if dl is not None else None
+            self.num_training_batches = self._num_batches(self.train_dataloader, self.limit_train_batches) \
+                if self.train_dataloader is not None else 0
+            vdl = self._resolve_loader("val", model)
+            self.val_dataloaders = self._as_list(vdl, shuffle=False)
+            self.num_val_batches = [self._num_batches(d, self.limit_val_batches) for d in self.val_dataloaders]
+            has_val_step = type(model).validation_step is not LightningModule.validation_step
+            self._has_val_loop = bool(self.val_dataloaders) and has_val_step and \
+                sum(self.num_val_batches) > 0
+        else:
+            tdl = self._resolve_loader("test", model)
+            self.test_dataloaders = self._as_list(tdl, shuffle=False)
+            self.num_test_batches = [self._num_batches(d, self.limit_test_batches) for d in self.test_dataloaders]
+
+    def _as_list(self, dls, shuffle: bool) -> List[DataLoader]:
+        if dls is None:
+            return []
+        if not isinstance(dls, (list, tuple)):
+            dls = [dls]
+        return [self._maybe_replace_sampler(d, shuffle=shuffle) for d in dls]
+
+    # ---------------------------------------------------------------- hooks
+    def call_hook(self, name: str, *args, **kwargs):
+        model = self.get_model()
+        for cb in self.callbacks:
+            fn = getattr(cb, name, None)
+            if fn is not None:
+                fn(self, model, *args, **kwargs)
+        mfn = getattr(model, name, None)
+        if mfn is not None and callable(mfn):
+            return mfn(*args, **kwargs) if name != "on_train_epoch_end" else mfn(*args, **kwargs)
+        return None
+
+    # -------------------------------------------------------------- metrics
+    def _log_metric(self, module, name, value, prog_bar=False, logger=True, on_step=None, on_epoch=None,
+                    sync_dist=False, sync_dist_op="mean") -> None:
+        fx = self._current_fx or "training_step"
+        training = fx.startswith("training")
+        if on_step is None:
+            on_step = training
+        if on_epoch is None:
+            on_epoch = not training
+        if not isinstance(value, torch.Tensor):
+            value = torch.tensor(float(value))
+        value = value.detach()
+        if sync_dist and self.accelerator_backend is not None:
+            value = self.accelerator_backend.sync_tensor(value.float(), reduce_op=sync_dist_op)
+        store = self._results.setdefault(fx, defaultdict(list))
+        if on_epoch:
+            store[name].append(value)
+        if on_step:
+            key = name if not on_epoch else f"{name}_step"
+            self.callback_metrics[key] = value
+            if logger:
+                self.logged_metrics[key] = value
+            if prog_bar:
+                self.progress_bar_metrics[key] = value
+        self._results.setdefault("_meta", {})[name] = (prog_bar, logger, on_step, on_epoch)
+
+    def _reduce_epoch_metrics(self, fx: str) -> Dict[str, torch.Tensor]:
+        store = self._results.pop(fx, None) or {}
+        meta = self._results.get("_meta", {})
+        out = {}
+        for name, vals in store.items():
+            v = torch.stack([x.float().mean().cpu() for x in vals]).mean()
+            prog_bar, logger, on_step, on_epoch = meta.get(name, (False, True, False, True))
+            key = f"{name}_epoch" if on_step else name
+            out[key] = v
+            self.callback_metrics[key] = v
+            if logger:
+                self.logged_metrics[key] = v
+            if prog_bar:
+                self.progress_bar_metrics[key] = v
+        return out
+
+    def _absorb_legacy(self, out: Any) -> None:
+        """PL <1.0 style dict returns ({'val_loss':..., 'log': {...}, 'progress_bar': {...}})."""
+        if not isinstance(out, dict):
+            return
+        for k, v in out.items():
+            if k in ("log", "progress_bar") and isinstance(v, dict):
+                for kk, vv in v.items():
+                    t = vv.detach() if isinstance(vv, torch.Tensor) else torch.tensor(float(vv))
+                    self.callback_metrics[kk] = t
+                    (self.logged_metrics if k == "log" else self.progress_bar_metrics)[kk] = t
+            elif isinstance(v, torch.Tensor) and v.numel() == 1:
+                self.callback_metrics[k] = v.detach()
+
+    def _flush_logger(self) -> None:
+        if self.logger is not None and self.logged_metrics and self.is_global_zero:
+            self.logger.log_metrics({k: v for k, v in self.logged_metrics.items()}, step=self.global_step)
+
+    # ---------------------------------------------------------- evaluation
+    def run_sanity_check(self, model: LightningModule) -> None:
+        if not self._has_val_loop or self.num_sanity_val_steps == 0:
+            return
+        self.running_sanity_check = True
+        self.call_hook("on_sanity_check_start")
+        n = self.num_sanity_val_steps if self.num_sanity_val_steps > 0 else None
+        self.run_evaluation(test_mode=False, max_batches=n)
+        self.call_hook("on_sanity_check_end")
+        # PL resets metrics logged during the sanity check
+        self.callback_metrics = {}
+        self.logged_metrics = {}
+        self.progress_bar_metrics = {}
+        self.running_sanity_check = False
+
+    def run_evaluation(self, test_mode: bool = False, max_batches: Optional[int] = None):
+        model = self.get_model()
+        stage = "test" if test_mode else "validation"
+        dls = self.test_dataloaders if test_mode else self.val_dataloaders
+        nbs = self.num_test_batches if test_mode else self.num_val_batches
+        if not dls:
+            return []
+        was_training = model.training
+        model.eval()
+        self.call_hook(f"on_{stage}_start")
+        self.call_hook(f"on_{stage}_epoch_start")
+        fused_eval = (self._fused is not None and not test_mode and hasattr(self._fused, "eval_batch"))
+        all_outputs = []
+        with torch.no_grad():
+            for dl_idx, dl in enumerate(dls):
+                limit = nbs[dl_idx] if max_batches is None else min(max_batches, nbs[dl_idx])
+                outputs = []
+                if fused_eval:
+                    self._fused.sync_params_to_module()
+                for batch_idx, batch in enumerate(dl):
+                    if batch_idx >= limit:
+                        break
+                    batch = self.accelerator_backend.batch_to_device(batch)
+                    self.call_hook(f"on_{stage}_batch_start", batch, batch_idx, dl_idx)
+                    self._current_fx = f"{stage}_step"
+                    args = [batch, batch_idx] + ([dl_idx] if len(dls) > 1 else [])
+                    with self.accelerator_backend.autocast():
+                        out = getattr(model, f"{stage}_step")(*args)
+                    self._current_fx = f"{stage}_step_end"
+                    out = getattr(model, f"{stage}_step_end")(out)
+                    self._current_fx = None
+                    self.call_hook(f"on_{stage}_batch_end", out, batch, batch_idx, dl_idx)
+                    if out is not None:
+                        outputs.append(out)
+                all_outputs.append(outputs)
+        self._current_fx = f"{stage}_epoch_end"
+        epoch_out = getattr(model, f"{stage}_epoch_end")(all_outputs[0] if len(dls) == 1 else all_outputs)
+        self._absorb_legacy(epoch_out)
+        self._current_fx = None
+        metrics = {}
+        metrics.update(self._reduce_epoch_metrics(f"{stage}_step"))
+        metrics.update(self._reduce_epoch_metrics(f"{stage}_step_end"))
+        metrics.update(self._reduce_epoch_metrics(f"{stage}_epoch_end"))
+        self.call_hook(f"on_{stage}_epoch_end")
+        self.call_hook(f"on_{stage}_end")
+        if was_training:
+            model.train()
+        if not self.running_sanity_check:
+            self._flush_logger()
+        return [{k: float(v) for k, v in metrics.items()}]
+
+    def run_test(self):
+        model = self.get_model()
+        self.call_hook("on_test_start") if False else None
+        results = self.run_evaluation(test_mode=True)
+        self.test_results = results
+        return results
+
+    # -------------------------------------------------------------- training
+    def _should_validate(self, batch_idx: int, is_last: bool) -> bool:
+        if not self._has_val_loop or (self.current_epoch + 1) % self.check_val_every_n_epoch != 0:
+            return False
+        vci = self.val_check_interval
+        if isinstance(vci, float):
+            if vci >= 1.0:
+                return is_last
+            every = max(1, int(self.num_training_batches * vci))
+        else:
+            every = int(vci)
+        return (batch_idx + 1) % every == 0 or is_last
+
+    def run_train(self) -> None:
+        model = self.get_model()
+        self.training = True
+        self.call_hook("on_fit_start")
+        for cb in self.callbacks:
+            if hasattr(cb, "on_pretrain_routine_start"):
+                cb.on_pretrain_routine_start(self, model)
+        if self.logger is not None:
+            self.logger.rank = self.global_rank
+            if self.is_global_zero and model.hparams:
+                self.logger.log_hyperparams(model.hparams)
+        self.run_sanity_check(model)
+        self.call_hook("on_train_start")
+        try:
+            while self.current_epoch < self.max_epochs:
+                self._run_epoch(model)
+                if self.max_steps is not None and self.global_step >= self.max_steps:
+                    break
+                if self.should_stop and self.current_epoch + 1 >= self.min_epochs:
+                    break
+                self.current_epoch += 1
+                self.should_stop = False if self.current_epoch < self.min_epochs else self.should_stop
+        except KeyboardInterrupt:
+            self.interrupted = True
+            self.call_hook("on_keyboard_interrupt")
+        self.call_hook("on_train_end")
+        self.call_hook("on_fit_end")
+        if self.logger is not None:
+            self.logger.finalize("success")
+        self.training = False
+
+    def _run_epoch(self, model: LightningModule) -> None:
+        dl = self.train_dataloader
+        sampler = getattr(dl, "sampler", None)
+        if hasattr(sampler, "set_epoch"):
+            sampler.set_epoch(self.current_epoch)
+        self.call_hook("on_epoch_start")
+        self.call_hook("on_train_epoch_start")
+        epoch_outputs: List[Any] = []
+        n = self.num_training_batches
+        validated = False
+        batches = None
+        if self._fused is not None and hasattr(self._fused, "make_epoch_batches") and \
+                not self._batch_hooks_overridden(model) and dl is not None and n > 0:
+            batches = self._fused.make_epoch_batches(dl, n)  # data stays resident on the device
+            if batches is not None:
+                n = min(n, len(batches))
+        if dl is not None and n > 0:
+            for batch_idx, batch in enumerate(batches if batches is not None else dl):
+                if batch_idx >= n:
+                    break
+                is_last = batch_idx + 1 >= n
+                out = self._train_batch(model, batch, batch_idx, is_last)
+                if out is not None:
+                    epoch_outputs.append(out)
+                if self.max_steps is not None and self.global_step >= self.max_steps:
+                    is_last = True
+                if self._should_validate(batch_idx, is_last):
+                    self.run_evaluation(test_mode=False)
+                    validated = True
+                if is_last and self.max_steps is not None and self.global_step >= self.max_steps:
+                    break
+                if self.should_stop:
+                    break
+        self._current_fx = "training_epoch_end"
+        res = model.training_epoch_end(epoch_outputs)
+        self._absorb_legacy(res)
+        self._current_fx = None
+        self._reduce_epoch_metrics("training_step")
+        self._reduce_epoch_metrics("training_step_end")
+        self._reduce_epoch_metrics("training_epoch_end")
+        # PL 1.1: on_epoch_end, then on_train_epoch_end
+        self.call_hook("on_epoch_end")
+        for cb in self.callbacks:
+            cb.on_train_epoch_end(self, model, epoch_outputs)
+        model.on_train_epoch_end(epoch_outputs)
+        self._update_lr_schedulers("epoch")
+        if not validated:
+            self._flush_logger()
+
+    def _batch_hooks_overridden(self, model: LightningModule) -> bool:
+        names = ("on_train_batch_start", "on_train_batch_end", "on_batch_start", "on_batch_end")
+        for cb in self.callbacks:
+            for nm in names:
+                if getattr(type(cb), nm, None) is not getattr(Callback, nm):
+                    return True
+        for nm in ("on_train_batch_start", "on_train_batch_end"):
+            if getattr(type(model), nm) is not getattr(LightningModule, nm) or nm in model.__dict__:
+                return True
+        return False
+
+    def _train_batch(self, model: LightningModule, batch, batch_idx: int, is_last: bool):
+        acc = self.accelerator_backend
+        self.call_hook("on_batch_start")
+        r = model.on_train_batch_start(batch, batch_idx, 0)
+        for cb in self.callbacks:
+            cb.on_train_batch_start(self, model, batch, batch_idx, 0)
+        if r == -1:
+            return None
+        if self._fused is not None:
+            out = self._fused.train_batch(batch, batch_idx)
+            self.global_step += 1
+        else:
+            batch = acc.batch_to_device(batch)
+            out = None
+            for opt_idx, opt in enumerate(self.optimizers or [None]):
+                out = self._optimizer_step_for(model, batch, batch_idx, opt_idx, opt, is_last)
+            accumulate_done = ((batch_idx + 1) % self.accumulate_grad_batches == 0) or is_last
+            if accumulate_done:
+                self.global_step += 1
+                self._update_lr_schedulers("step")
+        for cb in self.callbacks:
+            cb.on_train_batch_end(self, model, out, batch, batch_idx, 0)
+        model.on_train_batch_end(out, batch, batch_idx, 0)
+        self.call_hook("on_batch_end")
+        if self.global_step % max(1, self.log_every_n_steps) == 0:
+            self._flush_logger()
+        return out
+
+    def _optimizer_step_for(self, model, batch, batch_idx, opt_idx, opt, is_last):
+        acc = self.accelerator_backend
+        n_opt = len(self.optimizers)
+        accumulate_done = ((batch_idx + 1) % self.accumulate_grad_batches == 0) or is_last
+        self._current_fx = "training_step"
+        args = [batch, batch_idx] + ([opt_idx] if n_opt > 1 else [])
+        acc.before_forward(sync=accumulate_done)
+        with acc.autocast():
+            out = model.training_step(*args)
+        self._current_fx = "training_step_end"
+        out = model.training_step_end(out)
+        self._current_fx = None
+        if out is None:
+            return None
+        loss = out if isinstance(out, torch.Tensor) else out["loss"]
+        if isinstance(out, dict):
+            self._absorb_legacy({k: v for k, v in out.items() if k in ("log", "progress_bar")})
+        if opt is not None:
+            scaled = loss / self.accumulate_grad_batches if self.accumulate_grad_batches > 1 else loss
+            acc.backward(model, scaled, opt, opt_idx)
+            model.on_after_backward()
+            for cb in self.callbacks:
+                cb.on_after_backward(self, model)
+            if accumulate_done:
+                acc.before_optimizer_step(opt)
+                if self.gradient_clip_val:
+                    acc.clip_gradients(opt, self.gradient_clip_val)
+                model.optimizer_step(self.current_epoch, batch_idx, opt, opt_idx, None)
+                model.on_before_zero_grad(opt)
+                for cb in self.callbacks:
+                    cb.on_before_zero_grad(self, model, opt)
+                model.optimizer_zero_grad(self.current_epoch, batch_idx, opt, opt_idx)
+        self.callback_metrics.setdefault("loss", loss.detach())
+        self.callback_metrics["loss"] = loss.detach()
+        if isinstance(out, dict):
+            return {k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in out.items()}
+        return {"loss": loss.detach()}
+
+    def _update_lr_schedulers(self, interval: str) -> None:
+        for s in self.lr_schedulers:
+            if s.get("interval", "epoch") != interval:
+                continue
+            freq = s.get("frequency", 1)
+            counter = self.current_epoch + 1 if interval == "epoch" else self.global_step
+            if counter % freq != 0:
+                continue
+            sch = s["scheduler"]
+            if s.get("reduce_on_plateau"):
+                key = s.get("monitor") or "val_loss"
+                if key in self.callback_metrics:
+                    sch.step(float(self.callback_metrics[key]))
+            else:
+                sch.step()
+            if self._fused is not None and hasattr(self._fused, "on_lr_change"):
+                self._fused.on_lr_change()
+
+    # ---------------------------------------------------------------- state
+    def _model_state_dict(self, model: LightningModule) -> Dict[str, torch.Tensor]:
+        if self._fused is not None:
+            self._fused.sync_params_to_module()
+        return {k: v.detach().cpu() for k, v in model.state_dict().items()}
+
+    def _optimizer_state_dict(self, opt) -> dict:
+        if self._fused is not None and hasattr(self._fused, "optimizer_state_dict"):
+            return self._fused.optimizer_state_dict()
+        return _to_cpu(opt.state_dict())
+
+    def __getstate__(self):
+        d = self.__dict__.copy()
+        d["_fused"] = None
+        d["accelerator_backend"] = None
+        return d
+
+
+def _to_cpu(obj):
+    if isinstance(obj, torch.Tensor):
+        return obj.detach().cpu()
+    if isinstance(obj, dict):
+        return {k: _to_cpu(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_cpu(v) for v in obj)
+    return obj

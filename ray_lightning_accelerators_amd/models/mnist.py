@@ -1,0 +1,237 @@
+"""MNIST classifier workloads.
+
+``LightningMNISTClassifier`` is the upstream ``ray.tune.examples.mnist_ptl_mini``
+model the reference imports (examples/ray_ddp_example.py:13,
+tests/test_ddp.py:11): MLP 784 -> layer_1 -> layer_2 -> 10 with ReLU and
+log_softmax, NLL loss, Adam(lr), metrics ``ptl/train_loss``,
+``ptl/train_accuracy``, ``ptl/val_loss``, ``ptl/val_accuracy``.
+
+On an MI355X the training step of this module runs as ONE fused HIP kernel
+(``configure_fused_step``): the trainer hands it the epoch's sampler indices
+once, the images stay resident in HBM as uint8, and each step is a single
+launch (world size 1) or launch + flat-bucket allreduce + fused Adam (world
+size > 1).  CPU / unsupported shapes use the ordinary autograd path.
+"""
+from __future__ import annotations
+
+import os
+from typing import Any, Dict, Optional
+
+import torch
+import torch.nn.functional as F
+from torch.utils.data import DataLoader, Subset, random_split
+
+from ..lightning import LightningModule
+from ..lightning.metrics import Accuracy
+from ..ops import fused_mlp
+from .data import SyntheticMNIST
+
+
+class LightningMNISTClassifier(LightningModule):
+    def __init__(self, config: Dict[str, Any], data_dir: Optional[str] = None):
+        super().__init__()
+        self.data_dir = data_dir or os.getcwd()
+        self.lr = config["lr"]
+        layer_1, layer_2 = config["layer_1"], config["layer_2"]
+        self.batch_size = config["batch_size"]
+        self.layer_1 = torch.nn.Linear(28 * 28, layer_1)
+        self.layer_2 = torch.nn.Linear(layer_1, layer_2)
+        self.layer_3 = torch.nn.Linear(layer_2, 10)
+        self.accuracy = Accuracy()
+        self.config = dict(config)
+
+    def forward(self, x):
+        b = x.size(0)
+        x = x.reshape(b, -1)
+        x = torch.relu(self.layer_1(x))
+        x = torch.relu(self.layer_2(x))
+        return torch.log_softmax(self.layer_3(x), dim=1)
+
+    def configure_optimizers(self):
+        return torch.optim.Adam(self.parameters(), lr=self.lr)
+
+    def training_step(self, train_batch, batch_idx):
+        x, y = train_batch
+        logits = self.forward(x)
+        loss = F.nll_loss(logits, y)
+        acc = self.accuracy(logits, y)
+        self.log("ptl/train_loss", loss)
+        self.log("ptl/train_accuracy", acc)
+        return loss
+
+    def validation_step(self, val_batch, batch_idx):
+        x, y = val_batch
+        logits = self.forward(x)
+        loss = F.nll_loss(logits, y)
+        acc = self.accuracy(logits, y)
+        return {"val_loss": loss, "val_accuracy": acc}
+
+    def validation_epoch_end(self, outputs):
+        if not outputs:
+            return
+        avg_loss = torch.stack([x["val_loss"] for x in outputs]).mean()
+        avg_acc = torch.stack([x["val_accuracy"] for x in outputs]).mean()
+        self.log("ptl/val_loss", avg_loss)
+        self.log("ptl/val_accuracy", avg_acc)
+
+    # default synthetic data (the upstream module downloads MNIST; no network here)
+    def prepare_data(self):
+        if not hasattr(self, "_train_set"):
+            full = SyntheticMNIST(60000, seed=0)
+            self._train_set, self._val_set = random_split(
+                full, [55000, 5000], generator=torch.Generator().manual_seed(0))
+
+    def train_dataloader(self):
+        self.prepare_data()
+        return DataLoader(self._train_set, batch_size=self.batch_size, drop_last=True)
+
+    def val_dataloader(self):
+        self.prepare_data()
+        return DataLoader(self._val_set, batch_size=self.batch_size, drop_last=True)
+
+    # ------------------------------------------------------------ fast path
+    def configure_fused_step(self, trainer):
+        if type(self).training_step is not LightningMNISTClassifier.training_step or \
+                type(self).forward is not LightningMNISTClassifier.forward:
+            raise RuntimeError("training_step/forward overridden: fused step not applicable")
+        return FusedMNISTStep(self, trainer)
+
+    def __getstate__(self):
+        d = super().__getstate__()
+        return d
+
+
+def _u8_source(dataset):
+    """Find (images_u8 [N,784], targets, index_map) behind a dataset (Subset chains allowed)."""
+    idx_map = None
+    ds = dataset
+    while isinstance(ds, Subset):
+        ind = torch.as_tensor(ds.indices, dtype=torch.int64)
+        idx_map = ind if idx_map is None else ind[idx_map]
+        ds = ds.dataset
+    images = getattr(ds, "images", None)
+    targets = getattr(ds, "targets", None)
+    if isinstance(images, torch.Tensor) and images.dtype == torch.uint8 and images.dim() == 2 \
+            and images.size(1) == 784 and isinstance(targets, torch.Tensor):
+        return images, targets, idx_map
+    return None
+
+
+class FusedMNISTStep:
+    """Drives the fused HIP step from the Trainer's loop (replaces autograd + optimizer)."""
+
+    def __init__(self, model: LightningMNISTClassifier, trainer):
+        dev = model.device
+        if dev.type != "cuda":
+            raise RuntimeError("fused step needs a GPU")
+        L1, L2 = model.layer_1.out_features, model.layer_2.out_features
+        if not fused_mlp.mlp_supported(L1, L2):
+            raise RuntimeError(f"no fused kernel for {L1}/{L2}")
+        if len(trainer.optimizers) != 1:
+            raise RuntimeError("fused step expects one optimizer")
+        opt = trainer.optimizers[0]
+        if type(opt) is not torch.optim.Adam or len(opt.param_groups) != 1 or \
+                not getattr(opt, "_rla_fused", False) or opt.param_groups[0].get("amsgrad"):
+            raise RuntimeError("fused step expects a fused single-group torch.optim.Adam")
+        acc = trainer.accelerator_backend
+        arena = acc.arena
+        self.np = fused_mlp.mlp_param_count(L1, L2)
+        if arena is None or arena.numel < self.np or arena.params[0] is not model.layer_1.weight:
+            raise RuntimeError("parameters are not in the expected arena layout")
+        self.model, self.trainer, self.opt, self.acc, self.arena = model, trainer, opt, acc, arena
+        self.L1, self.L2 = L1, L2
+        self.gs = opt._rla_groups[0]
+        self.dev = dev
+        self.world = trainer.world_size
+        self.counters = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.counters[0] = self.gs.step
+        self.lr_val = float(opt.param_groups[0]["lr"])
+        self.lr_tensor = torch.full((1,), self.lr_val, device=dev)
+        self.stats = torch.zeros(64, 4, device=dev)
+        self._u8 = None
+        self._order = None
+        self._epoch_key = None
+
+    # ---------------------------------------------------------- data plane
+    def make_epoch_batches(self, dl, n_batches: int):
+        """Resident-data mode: upload this epoch's sampler order once; yield batch indices."""
+        src = _u8_source(dl.dataset)
+        if src is None or dl.batch_size is None:
+            return None
+        images, targets, idx_map = src
+        if self._u8 is None:
+            self._u8 = images.to(self.dev).contiguous()
+            self._labels = targets.to(self.dev, torch.int64).contiguous()
+        order = torch.as_tensor(list(iter(dl.sampler)), dtype=torch.int64)
+        if idx_map is not None:
+            order = idx_map[order]
+        B = dl.batch_size
+        nb = min(n_batches, order.numel() // B if dl.drop_last else -(-order.numel() // B))
+        nb = min(nb, order.numel() // B)
+        if nb <= 0:
+            return None
+        assert int(order.max()) < self._u8.size(0)
+        self._order = order[: nb * B].to(self.dev)
+        self._B = B
+        self._nb = nb
+        self.counters[1] = 0
+        return [("__rla_resident__", i) for i in range(nb)]
+
+    def _sync_lr(self) -> None:
+        lr = float(self.opt.param_groups[0]["lr"])
+        if lr != self.lr_val:
+            self.lr_val = lr
+            self.lr_tensor.fill_(lr)
+
+    def on_lr_change(self) -> None:
+        self._sync_lr()
+
+    def train_batch(self, batch, batch_idx: int):
+        self._sync_lr()
+        g = self.opt.param_groups[0]
+        b1, b2 = g["betas"]
+        p = self.arena.data[: self.np]
+        gr = self.arena.grad[: self.np]
+        m, v = self.gs.m[: self.np], self.gs.v[: self.np]
+        fused = self.world == 1
+        kw = dict(L1=self.L1, L2=self.L2, exp_avg=m, exp_avg_sq=v, stats=self.stats, apply_adam=fused,
+                  advance_step=True, lr=self.lr_val, betas=(b1, b2), eps=g["eps"], weight_decay=g["weight_decay"],
+                  lr_tensor=self.lr_tensor, counters=self.counters)
+        if isinstance(batch, tuple) and len(batch) == 2 and batch[0] == "__rla_resident__":
+            fused_mlp.mlp_train_step(p, gr, B=self._B, labels=self._labels, x_u8=self._u8, order=self._order,
+                                     n_batches=self._nb, **kw)
+        else:
+            x, y = batch
+            x = x.to(self.dev, non_blocking=True).reshape(x.size(0), -1).float().contiguous()
+            y = y.to(self.dev, non_blocking=True).long().contiguous()
+            fused_mlp.mlp_train_step(p, gr, B=x.size(0), labels=y, x_f32=x, **kw)
+        if not fused:
+            sync = self.acc.sync
+            if sync is not None:
+                import torch.distributed as dist
+
+                dist.all_reduce(self.arena.grad[: self.np])
+            from ..ops.optim import fused_adam_
+
+            fused_adam_(p, gr, m, v, lr=self.lr_val, betas=(b1, b2), eps=g["eps"], weight_decay=g["weight_decay"],
+                        grad_scale=1.0 / self.world, step=self.counters[0:1], lr_tensor=self.lr_tensor)
+        self.gs.step += 1
+        for q in g["params"]:
+            st = self.opt.state.get(q)
+            if st is not None and "step" in st:
+                st["step"].fill_(float(self.gs.step))
+        slot = (self.gs.step - 1) % self.stats.size(0)
+        loss = self.stats[slot, 0]
+        # metrics (device tensors; no host sync here)
+        self.model.log("ptl/train_loss", loss)
+        self.model.log("ptl/train_accuracy", self.stats[slot, 1] / self.stats[slot, 2].clamp(min=1))
+        self.trainer.callback_metrics["loss"] = loss
+        return {"loss": loss}
+
+    # --------------------------------------------------------------- state
+    def sync_params_to_module(self) -> None:
+        pass  # module parameters ARE arena views
+
+    def load_params_from_module(self) -> None:
+        self.arena.rebind_all()
+        self.counters[0] = self.gs.step

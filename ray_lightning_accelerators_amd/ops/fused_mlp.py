@@ -91,6 +91,7 @@ def mlp_train_step(
     weight_decay: float = 0.0,
     lr_tensor: Optional[torch.Tensor] = None,
     adamw: bool = False,
+    stamps: Optional[torch.Tensor] = None,
 ) -> None:
     """One training micro-step of the MNIST MLP over a flat parameter arena.
 
@@ -104,7 +105,7 @@ def mlp_train_step(
             x_u8, x_f32, labels, order, counters, int(n_batches), int(B), int(L1), int(L2),
             params, grads, exp_avg, exp_avg_sq, stats, bool(accumulate_grad), bool(apply_adam),
             bool(advance_step), float(lr), float(betas[0]), float(betas[1]), float(eps),
-            float(weight_decay), lr_tensor, bool(adamw),
+            float(weight_decay), lr_tensor, bool(adamw), stamps,
         )
         return
     # ---- fp32 reference ----

@@ -1,0 +1,111 @@
+"""Flat parameter / gradient arenas (SURVEY.md §7 decision D3).
+
+Every floating-point parameter of a module becomes a view into ONE contiguous
+fp32 buffer per device, and its ``.grad`` a view into a parallel gradient
+buffer.  Consequences on MI355X:
+  * the optimizer step is one fused HIP launch over the arena
+    (``ops.fused_adam_`` / ``ops.fused_sgd_``) instead of a multi-tensor apply;
+  * DDP buckets are contiguous arena slices, so the allreduce runs in place
+    with no flatten/unflatten copies (the reference's DDP reducer copies every
+    grad into a bucket and back);
+  * checkpoints still see ordinary per-parameter tensors (views).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import torch
+from torch import nn
+
+
+class ParamArena:
+    def __init__(self, module: nn.Module, params: Optional[List[nn.Parameter]] = None, align: int = 4):
+        if params is None:
+            params = [p for p in module.parameters() if p.requires_grad]
+        if not params:
+            raise ValueError("module has no trainable parameters")
+        dev = params[0].device
+        for p in params:
+            if p.device != dev:
+                raise ValueError("all parameters of an arena must live on one device")
+            if p.dtype != torch.float32:
+                raise ValueError(f"arena parameters must be fp32 master weights, got {p.dtype}")
+        self.device = dev
+        self.params = params
+        # offsets aligned to 4 elements (16 B) so every view is float4-aligned
+        self.offsets: List[Tuple[int, int]] = []
+        off = 0
+        for p in params:
+            n = p.numel()
+            self.offsets.append((off, n))
+            off += (n + align - 1) // align * align
+        self.numel = off
+        self.data = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(off, dtype=torch.float32, device=dev)
+        with torch.no_grad():
+            for p, (o, n) in zip(params, self.offsets):
+                view = self.data[o:o + n].view_as(p)
+                view.copy_(p.data)
+                p.data = view
+                p.grad = self.grad[o:o + n].view_as(p)
+        self._index: Dict[int, int] = {id(p): i for i, p in enumerate(params)}
+
+    def param_view(self, i: int) -> torch.Tensor:
+        o, n = self.offsets[i]
+        return self.data[o:o + n].view_as(self.params[i])
+
+    def grad_view(self, i: int) -> torch.Tensor:
+        o, n = self.offsets[i]
+        return self.grad[o:o + n].view_as(self.params[i])
+
+    def index_of(self, p: torch.Tensor) -> Optional[int]:
+        return self._index.get(id(p))
+
+    def owns_grad(self, i: int) -> bool:
+        p = self.params[i]
+        g = p.grad
+        o, n = self.offsets[i]
+        return g is not None and g.data_ptr() == self.grad.data_ptr() + o * 4 and g.numel() == n
+
+    def rebind_grad(self, i: int) -> None:
+        """Move a freshly allocated .grad (e.g. after zero_grad(set_to_none=True)) into the arena."""
+        p = self.params[i]
+        view = self.grad_view(i)
+        if p.grad is None:
+            view.zero_()
+        elif not self.owns_grad(i):
+            view.copy_(p.grad)
+        p.grad = view
+
+    def rebind_all(self) -> None:
+        for i, p in enumerate(self.params):
+            o, n = self.offsets[i]
+            if p.data.data_ptr() != self.data.data_ptr() + o * 4:
+                with torch.no_grad():
+                    self.data[o:o + n].view_as(p).copy_(p.data)
+                p.data = self.data[o:o + n].view_as(p)
+            if not self.owns_grad(i):
+                self.rebind_grad(i)
+
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+        for i, p in enumerate(self.params):
+            if not self.owns_grad(i):
+                p.grad = self.grad_view(i)
+
+    def is_arena_group(self, params: List[torch.Tensor]) -> bool:
+        return len(params) == len(self.params) and all(a is b for a, b in zip(params, self.params))
+
+    def contiguous_range(self, params: List[torch.Tensor]) -> Optional[Tuple[int, int]]:
+        """(start, end) in the arena if ``params`` are consecutive arena members, else None."""
+        idx = [self.index_of(p) for p in params]
+        if any(i is None for i in idx) or not idx:
+            return None
+        idx_sorted = sorted(idx)
+        if idx_sorted != list(range(idx_sorted[0], idx_sorted[-1] + 1)):
+            return None
+        start = self.offsets[idx_sorted[0]][0]
+        last_o, last_n = self.offsets[idx_sorted[-1]]
+        end = last_o + last_n
+        end = min(self.numel, (end + 3) // 4 * 4)
+        return start, end

@@ -1,0 +1,156 @@
+"""Data-parallel gradient synchronisation over a flat arena (replaces torch DDP's
+Reducer).
+
+Design for MI355X + RCCL over xGMI:
+  * buckets are contiguous slices of the gradient arena, formed in REVERSE
+    parameter order (grads become ready back-to-front during backward);
+  * ``register_post_accumulate_grad_hook`` counts ready parameters per bucket;
+    a full bucket's allreduce is launched immediately (async, on the process
+    group's comm stream) so communication overlaps the rest of backward;
+  * default bucket cap 8 MiB: on 7 point-to-point xGMI links a ring/tree step
+    is per-link bound (~153 GB/s) and RCCL's small-message latency is a few
+    microseconds, so buckets far below ~1 MiB pay latency while buckets far
+    above ~16 MiB delay the first launch; 8 MiB keeps ~4 buckets in flight on
+    ResNet-50 (97.5 MiB fp32) and ONE bucket for the MNIST MLP (109 KiB);
+  * optional bf16 gradient compression (``grad_dtype="bf16"``) packs a bucket
+    with the multi-tensor cast kernel before the collective;
+  * the 1/world average is NOT applied here when the optimizer is fused
+    (``grad_scale`` of the fused Adam/SGD kernel) -- one less pass over HBM;
+  * unused parameters (no grad this step) simply leave their bucket
+    incomplete; ``finish()`` launches such buckets synchronously, so no
+    autograd-graph walk (PL 1.1's find_unused_parameters=True) is needed.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+from torch import nn
+
+from .. import ops
+from .arena import ParamArena
+
+
+class Bucket:
+    def __init__(self, index: int, start: int, end: int, param_ids: List[int]):
+        self.index = index
+        self.start, self.end = start, end
+        self.param_ids = param_ids
+        self.pending = len(param_ids)
+        self.work = None
+        self.comm_buf: Optional[torch.Tensor] = None
+
+
+class GradSynchronizer:
+    def __init__(self, module: nn.Module, arena: ParamArena, process_group=None, bucket_cap_mb: float = 8.0,
+                 grad_dtype: str = "fp32", average_in_optimizer: bool = True, broadcast_buffers: bool = True):
+        self.module = module
+        self.arena = arena
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.grad_dtype = grad_dtype
+        self.average_in_optimizer = average_in_optimizer
+        self.broadcast_buffers = broadcast_buffers and any(True for _ in module.buffers())
+        self.enabled = True
+        cap = int(bucket_cap_mb * 1024 * 1024 / 4)
+        self.buckets: List[Bucket] = []
+        self.param_bucket: List[int] = [0] * len(arena.params)
+        # reverse order: the last layers' grads are ready first
+        order = list(range(len(arena.params)))[::-1]
+        cur: List[int] = []
+        cur_elems = 0
+        for i in order:
+            cur.append(i)
+            cur_elems += arena.offsets[i][1]
+            if cur_elems >= cap:
+                self._close_bucket(cur)
+                cur, cur_elems = [], 0
+        if cur:
+            self._close_bucket(cur)
+        self._hooks = []
+        for i, p in enumerate(arena.params):
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+        self._started = False
+
+    def _close_bucket(self, ids: List[int]) -> None:
+        starts = [self.arena.offsets[i][0] for i in ids]
+        ends = [self.arena.offsets[i][0] + self.arena.offsets[i][1] for i in ids]
+        s, e = min(starts), max(ends)
+        e = min(self.arena.numel, (e + 3) // 4 * 4)
+        b = Bucket(len(self.buckets), s, e, ids)
+        for i in ids:
+            self.param_bucket[i] = b.index
+        self.buckets.append(b)
+
+    # ------------------------------------------------------------- lifecycle
+    def broadcast_parameters(self, src: int = 0) -> None:
+        if self.world > 1:
+            dist.broadcast(self.arena.data, src, group=self.pg)
+            for b in self.module.buffers():
+                dist.broadcast(b, src, group=self.pg)
+
+    def prepare_for_backward(self, sync: bool = True) -> None:
+        """Reset bucket counters before a backward pass (``sync=False``: no_sync accumulation)."""
+        self.enabled = sync and self.world > 1
+        for b in self.buckets:
+            b.pending = len(b.param_ids)
+            b.work = None
+        self._started = True
+        if self.broadcast_buffers and self.world > 1 and sync:
+            for buf in self.module.buffers():
+                dist.broadcast(buf, 0, group=self.pg)
+
+    def _make_hook(self, i: int):
+        def hook(p: torch.Tensor) -> None:
+            if not self.arena.owns_grad(i):
+                self.arena.rebind_grad(i)
+            if not self.enabled or not self._started:
+                return
+            b = self.buckets[self.param_bucket[i]]
+            b.pending -= 1
+            if b.pending == 0:
+                self._launch(b)
+
+        return hook
+
+    def _launch(self, b: Bucket) -> None:
+        grad = self.arena.grad[b.start:b.end]
+        if self.grad_dtype == "bf16" and grad.is_cuda:
+            if b.comm_buf is None or b.comm_buf.numel() != grad.numel():
+                b.comm_buf = torch.empty(grad.numel(), dtype=torch.bfloat16, device=grad.device)
+            ops.multi_copy([(grad, b.comm_buf)])
+            b.work = dist.all_reduce(b.comm_buf, group=self.pg, async_op=True)
+        else:
+            b.work = dist.all_reduce(grad, group=self.pg, async_op=True)
+
+    def finish(self) -> None:
+        """Wait for every bucket; launch the ones unused parameters left incomplete."""
+        if not self.enabled:
+            self._started = False
+            return
+        for b in self.buckets:
+            if b.work is None:
+                self._launch(b)
+        for b in self.buckets:
+            b.work.wait()
+            if b.comm_buf is not None and self.grad_dtype == "bf16":
+                ops.multi_copy([(b.comm_buf, self.arena.grad[b.start:b.end])])
+            b.work = None
+        if not self.average_in_optimizer:
+            ops.scale_(self.arena.grad, 1.0 / self.world)
+        self._started = False
+
+    @property
+    def grad_scale(self) -> float:
+        return (1.0 / self.world) if (self.average_in_optimizer and self.world > 1) else 1.0
+
+    def remove(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+
+def default_bucket_cap_mb() -> float:
+    return float(os.environ.get("RLA_BUCKET_CAP_MB", "8"))

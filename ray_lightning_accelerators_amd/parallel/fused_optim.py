@@ -1,0 +1,132 @@
+"""Fuse a user's torch optimizer onto the flat arena without replacing it.
+
+``configure_optimizers`` returns a stock ``torch.optim.Adam``/``AdamW``/``SGD``
+(reference workloads).  Rather than swapping the object (LR
+schedulers keep a reference to it), :func:`fuse_optimizer` rebinds its
+``step``/``zero_grad`` to ONE gfx950 launch per param group over the arena
+slice the group covers.  Optimizer state lives in arena-shaped buffers and is
+exposed through ``optimizer.state[p]`` as per-parameter views, so
+``optimizer.state_dict()`` keeps torch's exact format (Lightning checkpoint
+``optimizer_states``).
+"""
+from __future__ import annotations
+
+import types
+from typing import Callable, List, Optional
+
+import torch
+
+from ..ops.optim import fused_adam_, fused_sgd_
+from .arena import ParamArena
+
+SUPPORTED = (torch.optim.Adam, torch.optim.AdamW, torch.optim.SGD)
+
+
+def can_fuse(opt: torch.optim.Optimizer, arena: ParamArena) -> bool:
+    if type(opt) not in SUPPORTED:
+        return False
+    for g in opt.param_groups:
+        if g.get("amsgrad") or g.get("differentiable"):
+            return False
+        if arena.contiguous_range(g["params"]) is None:
+            return False
+        if isinstance(opt, torch.optim.SGD) and g.get("momentum", 0) == 0 and g.get("dampening", 0) != 0:
+            return False
+    return True
+
+
+class _GroupState:
+    def __init__(self, arena: ParamArena, start: int, end: int, kind: str):
+        self.start, self.end = start, end
+        self.kind = kind
+        n = end - start
+        dev = arena.device
+        if kind == "adam":
+            self.m = torch.zeros(n, device=dev)
+            self.v = torch.zeros(n, device=dev)
+        else:
+            self.buf = torch.zeros(n, device=dev)
+        self.step = 0
+
+
+def fuse_optimizer(opt: torch.optim.Optimizer, arena: ParamArena,
+                   grad_scale_fn: Optional[Callable[[], float]] = None) -> torch.optim.Optimizer:
+    """Rebind ``opt.step`` / ``opt.zero_grad`` to fused arena kernels (in place)."""
+    if not can_fuse(opt, arena):
+        return opt
+    kind = "sgd" if isinstance(opt, torch.optim.SGD) else "adam"
+    adamw = isinstance(opt, torch.optim.AdamW)
+    groups: List[_GroupState] = []
+    for g in opt.param_groups:
+        s, e = arena.contiguous_range(g["params"])
+        gs = _GroupState(arena, s, e, kind)
+        groups.append(gs)
+        # expose per-param views in torch's state layout
+        for p in g["params"]:
+            i = arena.index_of(p)
+            o, n = arena.offsets[i]
+            if kind == "adam":
+                opt.state[p] = {"step": torch.tensor(0.0),
+                                "exp_avg": gs.m[o - s:o - s + n].view_as(p),
+                                "exp_avg_sq": gs.v[o - s:o - s + n].view_as(p)}
+            elif g.get("momentum", 0) != 0:
+                opt.state[p] = {"momentum_buffer": gs.buf[o - s:o - s + n].view_as(p)}
+
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        scale = grad_scale_fn() if grad_scale_fn is not None else 1.0
+        arena.rebind_all()
+        for g, gs in zip(self.param_groups, groups):
+            p = arena.data[gs.start:gs.end]
+            gr = arena.grad[gs.start:gs.end]
+            gs.step += 1
+            if gs.kind == "adam":
+                b1, b2 = g["betas"]
+                fused_adam_(p, gr, gs.m, gs.v, lr=float(g["lr"]), betas=(b1, b2), eps=g["eps"],
+                            weight_decay=g["weight_decay"], grad_scale=scale, adamw=adamw,
+                            maximize=g.get("maximize", False), step=gs.step)
+                for q in g["params"]:
+                    st = self.state.get(q)
+                    if st is not None and "step" in st:
+                        st["step"].fill_(float(gs.step))
+            else:
+                fused_sgd_(p, gr, gs.buf if g.get("momentum", 0) != 0 else None, lr=float(g["lr"]),
+                           momentum=g.get("momentum", 0.0), dampening=g.get("dampening", 0.0),
+                           weight_decay=g.get("weight_decay", 0.0), nesterov=g.get("nesterov", False),
+                           maximize=g.get("maximize", False), grad_scale=scale, step=gs.step)
+        return loss
+
+    def zero_grad(self, set_to_none: bool = True):
+        arena.zero_grad()
+
+    orig_load = opt.load_state_dict
+
+    def load_state_dict(self, state_dict):
+        orig_load(state_dict)
+        # torch replaced the state tensors: copy them back into the arena buffers
+        for g, gs in zip(self.param_groups, groups):
+            for p in g["params"]:
+                st = self.state.get(p, {})
+                i = arena.index_of(p)
+                o, n = arena.offsets[i]
+                sl = slice(o - gs.start, o - gs.start + n)
+                if gs.kind == "adam" and "exp_avg" in st:
+                    gs.m[sl].copy_(st["exp_avg"].reshape(-1))
+                    gs.v[sl].copy_(st["exp_avg_sq"].reshape(-1))
+                    gs.step = int(float(st.get("step", 0)))
+                    self.state[p] = {"step": torch.tensor(float(gs.step)),
+                                     "exp_avg": gs.m[sl].view_as(p), "exp_avg_sq": gs.v[sl].view_as(p)}
+                elif gs.kind == "sgd" and "momentum_buffer" in st and st["momentum_buffer"] is not None:
+                    gs.buf[sl].copy_(st["momentum_buffer"].reshape(-1))
+                    gs.step = max(gs.step, 1)
+                    self.state[p] = {"momentum_buffer": gs.buf[sl].view_as(p)}
+
+    opt.step = types.MethodType(step, opt)
+    opt.zero_grad = types.MethodType(zero_grad, opt)
+    opt.load_state_dict = types.MethodType(load_state_dict, opt)
+    opt._rla_fused = True
+    opt._rla_groups = groups
+    return opt

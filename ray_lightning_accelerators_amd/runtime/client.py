@@ -358,6 +358,7 @@ class ActorClass:
             "env": opts.get("runtime_env_vars") or {},
             "sys_path": os.pathsep.join(p for p in sys.path if p),
             "cwd": os.getcwd(), "timeout": float(opts.get("_creation_timeout", 3600)),
+            "owner": os.environ.get(P.ENV_ACTOR_ID),
         }
         cls_payload = P.dumps(self._cls)
         init_payload = P.dumps(_deref_args(args, kwargs))

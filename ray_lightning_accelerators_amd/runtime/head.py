@@ -66,6 +66,7 @@ class ActorRecord:
         self.registered = threading.Event()
         self.death_cause: Optional[str] = None
         self.class_name = ""
+        self.owner: Optional[str] = None
 
 
 class Head:
@@ -116,6 +117,7 @@ class Head:
                 self.lock.wait(timeout=0.5)
             rec = ActorRecord(actor_id, msg.get("name"), req, node, gpu_ids)
             rec.class_name = msg.get("class_name", "")
+            rec.owner = msg.get("owner")
             self.actors[actor_id] = rec
         env = dict(os.environ)
         env.update(msg.get("env") or {})
@@ -169,6 +171,10 @@ class Head:
             rec.death_cause = cause
             rec.node.give(rec.req, rec.gpu_ids)
             self.lock.notify_all()
+            orphans = [a for a in self.actors.values() if a.owner == rec.actor_id and a.state != "DEAD"]
+        # actors created BY a dead actor (e.g. a Tune trial's training workers) die with it
+        for o in orphans:
+            threading.Thread(target=self._kill, args=(o, f"owner {rec.actor_id[:8]} died"), daemon=True).start()
 
     def _kill(self, rec: ActorRecord, cause: str) -> None:
         proc = rec.proc

@@ -117,10 +117,20 @@ def pack_exception(e: BaseException) -> dict:
 
 
 def unpack_exception(d: dict) -> BaseException:
+    """RemoteError that is ALSO an instance of the original exception type
+    (``except ValueError`` keeps working across the process boundary)."""
     cause = None
     if d.get("exc") is not None:
         try:
             cause = loads(d["exc"])
         except Exception:
             cause = None
+    if isinstance(cause, Exception) and not isinstance(cause, RemoteError):
+        try:
+            cls = type(f"RemoteError[{type(cause).__name__}]", (RemoteError, type(cause)), {})
+            err = cls.__new__(cls)
+            RemoteError.__init__(err, d["repr"], d["tb"], cause)
+            return err
+        except TypeError:
+            pass
     return RemoteError(d["repr"], d["tb"], cause)
