@@ -181,7 +181,10 @@ def DistributedOptimizer(optimizer: torch.optim.Optimizer, named_parameters=None
         if not st.skip and not st.synchronized:
             st.synchronize()
         st.synchronized = False
+        self._opt_called = True
         return inner_step(closure) if closure is not None else inner_step()
+
+    step._wrapped_by_lr_sched = True
 
     def synchronize(self):
         st.synchronize()

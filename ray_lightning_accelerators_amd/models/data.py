@@ -9,6 +9,7 @@ in the dataset's ``__getitem__`` on CPU or inside the fused kernel on GPU.
 """
 from __future__ import annotations
 
+import math
 from typing import Optional, Tuple
 
 import torch
@@ -17,30 +18,30 @@ from torch.utils.data import Dataset
 IMG = 28
 
 
-def _prototypes(seed: int) -> torch.Tensor:
-    g = torch.Generator().manual_seed(10_000 + seed)
+def _prototypes(seed: int = 0) -> torch.Tensor:
+    """Ten class prototypes: two gaussian blobs per class on distinct ring angles."""
     yy, xx = torch.meshgrid(torch.arange(IMG).float(), torch.arange(IMG).float(), indexing="ij")
     protos = torch.zeros(10, IMG, IMG)
     for c in range(10):
-        for _ in range(3):  # three gaussian "strokes" per class
-            cy, cx = torch.rand(2, generator=g) * 16 + 6
-            sy, sx = torch.rand(2, generator=g) * 4 + 1.5
-            protos[c] += torch.exp(-((yy - cy) ** 2 / (2 * sy ** 2) + (xx - cx) ** 2 / (2 * sx ** 2)))
+        for k, r, s in ((c, 8.0, 2.5), ((3 * c + 1) % 10, 4.0, 2.0)):
+            a = 2 * math.pi * k / 10
+            cy, cx = 13.5 + r * math.sin(a), 13.5 + r * math.cos(a)
+            protos[c] += torch.exp(-((yy - cy) ** 2 + (xx - cx) ** 2) / (2 * s * s))
         protos[c] /= protos[c].max()
     return protos
 
 
-def synthetic_mnist(n: int, seed: int = 0, noise: float = 0.25) -> Tuple[torch.Tensor, torch.Tensor]:
+def synthetic_mnist(n: int, seed: int = 0, noise: float = 0.1, jitter: int = 1) -> Tuple[torch.Tensor, torch.Tensor]:
     """Return (images uint8 [n, 784], labels int64 [n])."""
     g = torch.Generator().manual_seed(seed)
     protos = _prototypes(0)  # class definitions are shared by every split
     labels = torch.randint(0, 10, (n,), generator=g)
-    shifts = torch.randint(-2, 3, (n, 2), generator=g)
+    shifts = torch.randint(-jitter, jitter + 1, (n, 2), generator=g)
     imgs = protos[labels]
     # per-sample translation jitter (rolled in blocks of equal shift for speed)
     out = torch.empty(n, IMG, IMG)
-    for dy in range(-2, 3):
-        for dx in range(-2, 3):
+    for dy in range(-jitter, jitter + 1):
+        for dx in range(-jitter, jitter + 1):
             m = (shifts[:, 0] == dy) & (shifts[:, 1] == dx)
             if m.any():
                 out[m] = torch.roll(imgs[m], shifts=(dy, dx), dims=(1, 2))

@@ -124,7 +124,16 @@ def fuse_optimizer(opt: torch.optim.Optimizer, arena: ParamArena,
                     gs.step = max(gs.step, 1)
                     self.state[p] = {"momentum_buffer": gs.buf[sl].view_as(p)}
 
-    opt.step = types.MethodType(step, opt)
+    # keep torch's LR-scheduler bookkeeping happy (it wraps optimizer.step)
+    step._wrapped_by_lr_sched = True
+    orig_step_fn = step
+
+    def counted_step(self, closure=None):
+        self._opt_called = True
+        return orig_step_fn(self, closure)
+
+    counted_step._wrapped_by_lr_sched = True
+    opt.step = types.MethodType(counted_step, opt)
     opt.zero_grad = types.MethodType(zero_grad, opt)
     opt.load_state_dict = types.MethodType(load_state_dict, opt)
     opt._rla_fused = True

@@ -228,10 +228,14 @@ class ObjectRef:
                 f.write(P.dumps(value))
             os.replace(path + ".tmp", path)
             self._path = path
-        return (ObjectRef, (None, _MISSING, self._path, self.id))
+        return (_ref_from_path, (self._path, self.id))
 
     def __repr__(self) -> str:
         return f"ObjectRef({self.id[:12]})"
+
+
+def _ref_from_path(path: str, ref_id: str) -> ObjectRef:
+    return ObjectRef(None, _MISSING, path, ref_id)
 
 
 def _deref_args(args: Sequence[Any], kwargs: Dict[str, Any]) -> Tuple[tuple, dict]:

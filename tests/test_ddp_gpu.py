@@ -1,0 +1,147 @@
+"""GPU integration (MI355X): port of the reference's test_ddp_gpu.py plus 1-GPU variants.
+
+The reference's tests need >= 2 GPUs (skipped on a 1-GPU box, exactly like the
+reference); the 1-GPU variants exercise the same paths -- actor pinning,
+device placement, RCCL process group, the fused HIP step and fused optimizers.
+"""
+import os
+
+import pytest
+import torch
+
+import ray_lightning_accelerators_amd.lightning as pl
+from ray_lightning_accelerators_amd import HorovodRayAccelerator, RayAccelerator
+from ray_lightning_accelerators_amd import runtime as ray
+from ray_lightning_accelerators_amd.lightning import Callback
+from ray_lightning_accelerators_amd.models.datamodules import MNISTDataModule
+from ray_lightning_accelerators_amd.models.mnist import LightningMNISTClassifier
+
+from helpers import BoringModel, get_trainer, predict_test, train_test
+
+pytestmark = pytest.mark.gpu
+
+multi_gpu = pytest.mark.skipif(torch.cuda.device_count() < 2, reason="test requires multi-GPU machine")
+
+
+@pytest.fixture
+def ray_start_gpus():
+    n = max(1, torch.cuda.device_count())
+    info = ray.init(num_cpus=2 * n, num_gpus=n)
+    yield info
+    ray.shutdown()
+
+
+@pytest.fixture
+def seed():
+    pl.seed_everything(0)
+
+
+class CheckDevicesCallback(Callback):
+    def on_epoch_end(self, trainer, pl_module):
+        assert trainer.root_gpu == 0
+        assert int(os.environ["CUDA_VISIBLE_DEVICES"]) == trainer.local_rank
+        assert int(os.environ["HIP_VISIBLE_DEVICES"]) == trainer.local_rank
+        assert trainer.root_gpu == pl_module.device.index
+        assert torch.cuda.current_device() == trainer.root_gpu
+
+
+class CheckGPUCallback(Callback):
+    def on_epoch_end(self, trainer, pl_module):
+        assert next(pl_module.parameters()).is_cuda
+
+
+class CheckFusedCallback(Callback):
+    def on_train_end(self, trainer, pl_module):
+        assert trainer._fused is not None, "fused HIP step was not used"
+        from ray_lightning_accelerators_amd import ops
+
+        ops.require()
+
+
+# ---------------------------------------------------------------- 1 GPU
+def test_train_1gpu(tmpdir, ray_start_gpus):
+    model = BoringModel()
+    trainer = get_trainer(tmpdir, accelerator=RayAccelerator(num_workers=1, use_gpu=True), use_gpu=True)
+    train_test(trainer, model)
+
+
+def test_model_to_gpu_and_devices_1gpu(tmpdir, ray_start_gpus):
+    trainer = get_trainer(tmpdir, accelerator=RayAccelerator(num_workers=1, use_gpu=True), use_gpu=True,
+                          callbacks=[CheckGPUCallback(), CheckDevicesCallback()])
+    assert trainer.fit(BoringModel()) == 1
+
+
+def test_predict_fused_mnist_1gpu(tmpdir, ray_start_gpus, seed):
+    config = {"layer_1": 32, "layer_2": 32, "lr": 1e-2, "batch_size": 32}
+    model = LightningMNISTClassifier(config, str(tmpdir))
+    dm = MNISTDataModule(data_dir=str(tmpdir), num_workers=1, batch_size=config["batch_size"])
+    trainer = get_trainer(tmpdir, limit_train_batches=10, max_epochs=1, use_gpu=True,
+                          accelerator=RayAccelerator(num_workers=1, use_gpu=True), callbacks=[CheckFusedCallback()])
+    predict_test(trainer, model, dm)
+
+
+def test_horovod_train_1gpu(tmpdir, ray_start_gpus, seed):
+    trainer = get_trainer(tmpdir, accelerator=HorovodRayAccelerator(num_slots=1, use_gpu=True), use_gpu=True,
+                          callbacks=[CheckGPUCallback()])
+    train_test(trainer, BoringModel())
+
+
+def test_single_process_gpu_trainer_fused(tmpdir, seed):
+    """Default accelerator with gpus=1: fused MNIST step + resident data, in-process."""
+    config = {"layer_1": 64, "layer_2": 128, "lr": 1e-3, "batch_size": 64}
+    model = LightningMNISTClassifier(config)
+    trainer = pl.Trainer(default_root_dir=str(tmpdir), gpus=1, max_epochs=2, limit_train_batches=50,
+                         limit_val_batches=5, callbacks=[CheckFusedCallback()])
+    assert trainer.fit(model) == 1
+    assert float(trainer.callback_metrics["ptl/val_accuracy"]) > 0.8
+    ckpt = trainer.checkpoint_connector.dump_checkpoint()
+    assert float(ckpt["optimizer_states"][0]["state"][0]["step"]) == 100
+
+
+# ------------------------------------------------- reference (>= 2 GPUs)
+@multi_gpu
+@pytest.mark.parametrize("num_workers", [1, 2])
+def test_train(tmpdir, ray_start_gpus, num_workers):
+    model = BoringModel()
+    trainer = get_trainer(tmpdir, accelerator=RayAccelerator(num_workers=num_workers, use_gpu=True), use_gpu=True)
+    train_test(trainer, model)
+
+
+@multi_gpu
+@pytest.mark.parametrize("num_workers", [1, 2])
+def test_predict(tmpdir, ray_start_gpus, seed, num_workers):
+    config = {"layer_1": 32, "layer_2": 32, "lr": 1e-2, "batch_size": 32}
+    model = LightningMNISTClassifier(config, str(tmpdir))
+    dm = MNISTDataModule(data_dir=str(tmpdir), num_workers=1, batch_size=config["batch_size"])
+    trainer = get_trainer(tmpdir, limit_train_batches=10, max_epochs=1, use_gpu=True,
+                          accelerator=RayAccelerator(num_workers=num_workers, use_gpu=True))
+    predict_test(trainer, model, dm)
+
+
+@multi_gpu
+def test_model_to_gpu(tmpdir, ray_start_gpus):
+    trainer = get_trainer(tmpdir, accelerator=RayAccelerator(num_workers=2, use_gpu=True), use_gpu=True,
+                          callbacks=[CheckGPUCallback()])
+    trainer.fit(BoringModel())
+
+
+@multi_gpu
+def test_correct_devices(tmpdir, ray_start_gpus):
+    trainer = get_trainer(tmpdir, accelerator=RayAccelerator(num_workers=2, use_gpu=True), use_gpu=True,
+                          callbacks=[CheckDevicesCallback()])
+    trainer.fit(BoringModel())
+
+
+@multi_gpu
+@pytest.mark.parametrize("num_slots", [1, 2])
+def test_horovod_train_gpu(tmpdir, ray_start_gpus, seed, num_slots):
+    trainer = get_trainer(tmpdir, accelerator=HorovodRayAccelerator(num_slots=num_slots, use_gpu=True), use_gpu=True)
+    train_test(trainer, BoringModel())
+
+
+@pytest.mark.skipif(os.environ.get("CLUSTER", "0") != "1", reason="needs a multi-node cluster")
+def test_multi_node(tmpdir):
+    ray.init(address="auto")
+    num_gpus = int(ray.available_resources()["GPU"])
+    trainer = get_trainer(tmpdir, accelerator=RayAccelerator(num_workers=num_gpus, use_gpu=True), use_gpu=True)
+    train_test(trainer, BoringModel())

@@ -1,0 +1,115 @@
+"""HorovodRayAccelerator + Horovod-compatible API -- port of the reference's test_horovod.py (CPU/gloo)."""
+import pytest
+import torch
+
+import ray_lightning_accelerators_amd.lightning as pl
+from ray_lightning_accelerators_amd import HorovodRayAccelerator
+from ray_lightning_accelerators_amd import horovod as hvd
+from ray_lightning_accelerators_amd import runtime as ray
+from ray_lightning_accelerators_amd.accelerators.ray_horovod import HorovodRayExecutor
+from ray_lightning_accelerators_amd.models.datamodules import MNISTDataModule
+from ray_lightning_accelerators_amd.models.mnist import LightningMNISTClassifier
+
+from helpers import BoringModel, get_trainer, load_test, predict_test, train_test
+
+
+@pytest.fixture
+def ray_start_2_cpus():
+    info = ray.init(num_cpus=2, num_gpus=0)
+    yield info
+    ray.shutdown()
+
+
+@pytest.fixture
+def seed():
+    pl.seed_everything(0)
+
+
+@pytest.mark.parametrize("num_slots", [1, 2])
+def test_train(tmpdir, ray_start_2_cpus, seed, num_slots):
+    model = BoringModel()
+    accelerator = HorovodRayAccelerator(num_slots=num_slots, use_gpu=False)
+    trainer = get_trainer(tmpdir, accelerator=accelerator)
+    train_test(trainer, model)
+
+
+@pytest.mark.parametrize("num_slots", [1, 2])
+def test_load(tmpdir, ray_start_2_cpus, seed, num_slots):
+    model = BoringModel()
+    accelerator = HorovodRayAccelerator(num_slots=num_slots, use_gpu=False)
+    trainer = get_trainer(tmpdir, accelerator=accelerator)
+    load_test(trainer, model)
+
+
+@pytest.mark.parametrize("num_slots", [1, 2])
+def test_predict(tmpdir, ray_start_2_cpus, seed, num_slots):
+    config = {"layer_1": 32, "layer_2": 32, "lr": 1e-2, "batch_size": 32}
+    model = LightningMNISTClassifier(config, tmpdir)
+    dm = MNISTDataModule(data_dir=tmpdir, num_workers=1, batch_size=config["batch_size"])
+    accelerator = HorovodRayAccelerator(num_slots=num_slots, use_gpu=False)
+    trainer = get_trainer(tmpdir, limit_train_batches=10, max_epochs=1, accelerator=accelerator)
+    predict_test(trainer, model, dm)
+
+
+def _collectives():
+    hvd.init()
+    r, n = hvd.rank(), hvd.size()
+    out = {}
+    t = torch.full((5,), float(r + 1))
+    out["avg"] = hvd.allreduce(t).tolist()
+    out["sum"] = hvd.allreduce(t, op=hvd.Sum).tolist()
+    out["gather"] = hvd.allgather(torch.full((r + 1, 2), float(r))).tolist()
+    out["bcast"] = hvd.broadcast(torch.tensor([float(r)]), root_rank=1).tolist()
+    out["obj"] = hvd.broadcast_object({"rank": r}, root_rank=0)
+    grouped = hvd.grouped_allreduce([torch.ones(3) * r, torch.ones(2) * (r + 10)])
+    out["grouped"] = [g.tolist() for g in grouped]
+    # DistributedOptimizer: fused grad averaging across ranks
+    lin = torch.nn.Linear(4, 3)
+    hvd.broadcast_parameters(lin.state_dict(), root_rank=0)
+    opt = hvd.DistributedOptimizer(torch.optim.SGD(lin.parameters(), lr=0.1),
+                                   named_parameters=lin.named_parameters())
+    x = torch.full((2, 4), float(r + 1))
+    lin(x).sum().backward()
+    opt.synchronize()
+    out["grad"] = lin.weight.grad.clone().tolist()
+    with opt.skip_synchronize():
+        opt.step()
+    out["w"] = lin.weight.detach().tolist()
+    out["rank"], out["size"], out["local_rank"] = r, n, hvd.local_rank()
+    out["join"] = hvd.join()
+    hvd.shutdown()
+    return out
+
+
+def test_horovod_api_collectives(ray_start_2_cpus):
+    ex = HorovodRayExecutor(num_hosts=1, num_slots=2, use_gpu=False)
+    ex.start()
+    try:
+        res = ex.execute(_collectives)
+    finally:
+        ex.shutdown()
+    r0, r1 = res
+    assert r0["rank"] == 0 and r1["rank"] == 1 and r0["size"] == 2
+    assert r0["local_rank"] == 0 and r1["local_rank"] == 1
+    assert r0["avg"] == [1.5] * 5 and r1["sum"] == [3.0] * 5
+    assert r0["gather"] == [[0.0, 0.0], [1.0, 1.0], [1.0, 1.0]]
+    assert r0["bcast"] == [1.0] and r1["obj"] == {"rank": 0}
+    assert r0["grouped"] == [[0.5] * 3, [10.5] * 2]
+    # grad of sum(W x) wrt W = sum over batch of x = 2 * (r+1) per element -> averaged: 3.0
+    assert all(abs(v - 3.0) < 1e-6 for row in r0["grad"] for v in row)
+    assert r0["w"] == r1["w"]
+
+
+def test_multi_host_topology():
+    """Simulated 2-host x 2-slot cluster: Horovod local/cross ranks follow node IPs."""
+    ray.init(_nodes=[{"ip": "10.0.0.1", "num_cpus": 2}, {"ip": "10.0.0.2", "num_cpus": 2}])
+    try:
+        ex = HorovodRayExecutor(num_hosts=2, num_slots=2, use_gpu=False)
+        ex.start()
+        envs = ex.envs
+        ex.shutdown()
+    finally:
+        ray.shutdown()
+    assert [e["HOROVOD_LOCAL_RANK"] for e in envs] == [0, 1, 0, 1]
+    assert [e["HOROVOD_CROSS_RANK"] for e in envs] == [0, 0, 1, 1]
+    assert all(e["HOROVOD_SIZE"] == 4 and e["HOROVOD_LOCAL_SIZE"] == 2 for e in envs)

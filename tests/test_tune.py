@@ -1,0 +1,87 @@
+"""Tune integration -- port of the reference's ray_lightning/tests/test_tune.py."""
+import os
+
+import pytest
+
+from ray_lightning_accelerators_amd import HorovodRayAccelerator, RayAccelerator
+from ray_lightning_accelerators_amd import runtime as ray
+from ray_lightning_accelerators_amd import tune
+from ray_lightning_accelerators_amd.tune import TuneReportCallback, TuneReportCheckpointCallback
+
+from helpers import BoringModel, get_trainer
+
+
+@pytest.fixture
+def ray_start_4_cpus():
+    info = ray.init(num_cpus=4, num_gpus=0)
+    yield info
+    ray.shutdown()
+
+
+def train_func(dir, accelerator, use_gpu=False, callbacks=None):
+    def _inner_train(config):
+        model = BoringModel()
+        trainer = get_trainer(dir, use_gpu=use_gpu, callbacks=callbacks, accelerator=accelerator, **config)
+        trainer.fit(model)
+
+    return _inner_train
+
+
+def tune_test(dir, accelerator):
+    callbacks = [TuneReportCallback(on="validation_end")]
+    analysis = tune.run(train_func(dir, accelerator, callbacks=callbacks),
+                        config={"max_epochs": tune.choice([1, 2, 3])},
+                        resources_per_trial={"cpu": 0, "extra_cpu": 2}, num_samples=2,
+                        local_dir=str(dir))
+    assert all(analysis.results_df["training_iteration"] == analysis.results_df["config.max_epochs"])
+
+
+def test_tune_iteration_ddp(tmpdir, ray_start_4_cpus):
+    accelerator = RayAccelerator(num_workers=2, use_gpu=False)
+    tune_test(tmpdir, accelerator)
+
+
+def test_tune_iteration_horovod(tmpdir, ray_start_4_cpus):
+    accelerator = HorovodRayAccelerator(num_hosts=1, num_slots=2, use_gpu=False)
+    tune_test(tmpdir, accelerator)
+
+
+def checkpoint_test(dir, accelerator):
+    callbacks = [TuneReportCheckpointCallback(on="validation_end")]
+    analysis = tune.run(train_func(dir, accelerator, callbacks=callbacks), config={"max_epochs": 2},
+                        resources_per_trial={"cpu": 0, "extra_cpu": 2}, num_samples=1, local_dir=str(dir),
+                        log_to_file=True, metric="val_loss", mode="min")
+    assert analysis.best_checkpoint is not None
+    assert os.path.exists(analysis.best_checkpoint)
+    assert os.path.exists(os.path.join(analysis.best_checkpoint, "checkpoint"))
+
+
+def test_checkpoint_ddp(tmpdir, ray_start_4_cpus):
+    accelerator = RayAccelerator(num_workers=2, use_gpu=False)
+    checkpoint_test(tmpdir, accelerator)
+
+
+def test_checkpoint_horovod(tmpdir, ray_start_4_cpus):
+    accelerator = HorovodRayAccelerator(num_hosts=1, num_slots=2, use_gpu=False)
+    checkpoint_test(tmpdir, accelerator)
+
+
+def test_report_metric_mapping(tmpdir, ray_start_4_cpus):
+    """dict metrics map tune names -> Lightning names; best_config uses them."""
+    callbacks = [TuneReportCallback({"loss": "val_loss"}, on="validation_end")]
+    analysis = tune.run(train_func(tmpdir, RayAccelerator(num_workers=1), callbacks=callbacks),
+                        config={"max_epochs": tune.grid_search([1, 2])}, resources_per_trial={"cpu": 0, "extra_cpu": 1},
+                        num_samples=1, local_dir=str(tmpdir), metric="loss", mode="min")
+    df = analysis.results_df
+    assert len(df) == 2 and set(df["config.max_epochs"]) == {1, 2}
+    assert "loss" in df.columns and (df["loss"] == 1.0).all()
+    assert analysis.best_config["max_epochs"] in (1, 2)
+
+
+def test_sample_space():
+    cfgs = tune.sample.generate_variants(
+        {"a": tune.choice([32, 64]), "lr": tune.loguniform(1e-4, 1e-1), "g": tune.grid_search([1, 2, 3])},
+        num_samples=4, seed=0)
+    assert len(cfgs) == 12
+    assert all(c["a"] in (32, 64) and 1e-4 <= c["lr"] <= 1e-1 for c in cfgs)
+    assert sorted({c["g"] for c in cfgs}) == [1, 2, 3]
