@@ -59,8 +59,14 @@ class HorovodRayExecutor:
         return self.num_hosts * self.num_slots
 
     def start(self, executable_cls=None, executable_args=None, executable_kwargs=None, extra_env_vars=None):
-        self.workers = [RayExecutor.options(num_cpus=self.cpus_per_slot, num_gpus=self.gpus_per_slot).remote()
-                        for _ in range(self.num_workers)]
+        # colocate each host's slots on one node (horovod.ray's colocator semantics)
+        node_ips = [n["NodeManagerAddress"] for n in ray.nodes()]
+        placement = None
+        if self.num_hosts > 1 and len(node_ips) >= self.num_hosts:
+            placement = [node_ips[h] for h in range(self.num_hosts) for _ in range(self.num_slots)]
+        self.workers = [RayExecutor.options(num_cpus=self.cpus_per_slot, num_gpus=self.gpus_per_slot,
+                                            _node_ip=(placement[i] if placement else None)).remote()
+                        for i in range(self.num_workers)]
         ips = ray.get([w.get_node_ip.remote() for w in self.workers])
         gpu_ids = ray.get([w.get_gpu_ids.remote() for w in self.workers]) if self.use_gpu else [[]] * len(ips)
         hosts: List[str] = []
