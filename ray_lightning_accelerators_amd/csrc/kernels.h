@@ -68,6 +68,31 @@ struct MLPStepArgs {
   const float* lr_ptr;
   int adamw;
   int64_t* stamps;          // optional [16] phase timestamps (diagnostics)
+  // v2 (two-kernel) step only:
+  uint16_t* shadow;         // bf16 weight shadows (row-major copy + W2^T + W3^T), see mlp_shadow_layout
+  uint16_t* dh1t;           // scratch [L1, round_up(B, 32)] bf16: dH1^T handed from head to W1 kernel
+};
+
+// bf16 shadow layout (elements): [0, np) row-major copy of the fp32 arena,
+// [w2t, w2t + L1*L2) W2^T [L1][L2], [w3t, w3t + 16*L2) W3^T [L2][16] (classes
+// zero-padded to 16).  The forward/backward read 16-byte bf16 fragments from it.
+struct MLPShadowLayout {
+  int64_t np, w2t, w3t, total;
+};
+MLPShadowLayout mlp_shadow_layout(int L1, int L2);
+
+struct MLPAdamArgs {
+  float* params;
+  const float* grads;
+  float* exp_avg;
+  float* exp_avg_sq;
+  uint16_t* shadow;
+  int L1, L2;
+  float lr, beta1, beta2, eps, weight_decay, grad_scale;
+  int adamw;
+  int update;               // 0: only refresh the shadows from params
+  const int64_t* step_ptr;  // already-incremented step
+  const float* lr_ptr;
 };
 
 struct MLPEvalArgs {
@@ -85,5 +110,9 @@ struct MLPEvalArgs {
 int launch_mlp_train_step(const MLPStepArgs& a, hipStream_t stream);
 int launch_mlp_eval(const MLPEvalArgs& a, hipStream_t stream);
 bool mlp_supported(int L1, int L2);
+// v2: head kernel (1 WG: forward, loss, dH, small-param grads/Adam) + W1 kernel
+// (49 WGs: dW1 tile + Adam, bf16 shadow write).  counters needs 3 slots.
+int launch_mlp_train_step2(const MLPStepArgs& a, hipStream_t stream);
+int launch_mlp_adam(const MLPAdamArgs& a, hipStream_t stream);
 
 }  // namespace rla

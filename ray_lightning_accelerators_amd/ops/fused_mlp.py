@@ -143,6 +143,96 @@ def mlp_train_step(
                 [loss.detach(), correct, torch.tensor(float(B)), torch.tensor(float(t))])
 
 
+def mlp_shadow_layout(L1: int, L2: int) -> Dict[str, int]:
+    """bf16 shadow layout: row-major copy [0, np), W2^T at w2t, W3^T (classes padded to 16) at w3t."""
+    np_ = mlp_param_count(L1, L2)
+    w2t = (np_ + 7) // 8 * 8
+    w3t = w2t + L1 * L2
+    return {"np": np_, "w2t": w2t, "w3t": w3t, "total": w3t + 16 * L2}
+
+
+def mlp_refresh_shadow(params: torch.Tensor, shadow: torch.Tensor, L1: int, L2: int) -> None:
+    """Recompute every bf16 shadow from the fp32 master weights."""
+    if use_native(params):
+        require().mlp_adam(params, params, params, params, shadow, int(L1), int(L2), 0.0, 0.9, 0.999, 1e-8, 0.0,
+                           1.0, False, False, None, None)
+        return
+    lay = mlp_shadow_layout(L1, L2)
+    v = mlp_unpack(params, L1, L2)
+    with torch.no_grad():
+        shadow[: lay["np"]].copy_(params)
+        shadow[lay["w2t"]: lay["w3t"]].copy_(v["layer_2.weight"].t().reshape(-1))
+        w3t = torch.zeros(L2, 16, dtype=params.dtype, device=params.device)
+        w3t[:, :NUM_CLASSES] = v["layer_3.weight"].t()
+        shadow[lay["w3t"]: lay["total"]].copy_(w3t.reshape(-1))
+
+
+def mlp_train_step2(
+    params: torch.Tensor,
+    grads: torch.Tensor,
+    *,
+    shadow: torch.Tensor,
+    dh1t: torch.Tensor,
+    counters: torch.Tensor,
+    L1: int,
+    L2: int,
+    B: int,
+    labels: torch.Tensor,
+    x_u8: Optional[torch.Tensor] = None,
+    x_f32: Optional[torch.Tensor] = None,
+    order: Optional[torch.Tensor] = None,
+    n_batches: int = 0,
+    exp_avg: Optional[torch.Tensor] = None,
+    exp_avg_sq: Optional[torch.Tensor] = None,
+    stats: Optional[torch.Tensor] = None,
+    accumulate_grad: bool = False,
+    apply_adam: bool = False,
+    advance_step: bool = True,
+    lr: float = 1e-3,
+    betas: Tuple[float, float] = (0.9, 0.999),
+    eps: float = 1e-8,
+    weight_decay: float = 0.0,
+    lr_tensor: Optional[torch.Tensor] = None,
+    adamw: bool = False,
+    stamps: Optional[torch.Tensor] = None,
+) -> None:
+    """v2 fused step: head kernel + 49-workgroup W1 kernel, weights read from the
+    bf16 ``shadow`` (kept current by the Adam epilogues).  Same semantics as
+    :func:`mlp_train_step`; ``counters`` has 3 slots (step, cursor, last cursor)."""
+    if use_native(params):
+        require().mlp_train_step2(
+            x_u8, x_f32, labels, order, counters, int(n_batches), int(B), int(L1), int(L2), params, grads,
+            exp_avg, exp_avg_sq, shadow, dh1t, stats, bool(accumulate_grad), bool(apply_adam), bool(advance_step),
+            float(lr), float(betas[0]), float(betas[1]), float(eps), float(weight_decay), lr_tensor, bool(adamw),
+            stamps,
+        )
+        return
+    if x_u8 is not None:
+        counters[2] = counters[1]
+    mlp_train_step(params, grads, L1=L1, L2=L2, B=B, labels=labels, x_u8=x_u8, x_f32=x_f32, order=order,
+                   counters=counters[:2], n_batches=n_batches, exp_avg=exp_avg, exp_avg_sq=exp_avg_sq, stats=stats,
+                   accumulate_grad=accumulate_grad, apply_adam=apply_adam, advance_step=advance_step, lr=lr,
+                   betas=betas, eps=eps, weight_decay=weight_decay, lr_tensor=lr_tensor, adamw=adamw)
+    if apply_adam:
+        mlp_refresh_shadow(params, shadow, L1, L2)
+
+
+def mlp_adam_(params, grads, exp_avg, exp_avg_sq, shadow, *, L1: int, L2: int, lr: float, step: torch.Tensor,
+              betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, grad_scale: float = 1.0,
+              adamw: bool = False, lr_tensor: Optional[torch.Tensor] = None) -> None:
+    """Adam over the MLP arena (world size > 1, after the allreduce) + shadow refresh."""
+    if use_native(params):
+        require().mlp_adam(params, grads, exp_avg, exp_avg_sq, shadow, int(L1), int(L2), float(lr), float(betas[0]),
+                           float(betas[1]), float(eps), float(weight_decay), float(grad_scale), bool(adamw), True,
+                           step, lr_tensor)
+        return
+    from .optim import fused_adam_
+
+    fused_adam_(params, grads, exp_avg, exp_avg_sq, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
+                grad_scale=grad_scale, adamw=adamw, step=step, lr_tensor=lr_tensor)
+    mlp_refresh_shadow(params, shadow, L1, L2)
+
+
 def mlp_eval(
     params: torch.Tensor,
     *,

@@ -76,8 +76,13 @@ class FusedMLPEngine:
         self.grads = torch.zeros(n, device=self.device)
         self.exp_avg = torch.zeros(n, device=self.device)
         self.exp_avg_sq = torch.zeros(n, device=self.device)
-        self.counters = torch.zeros(2, dtype=torch.int64, device=self.device)
+        self.counters = torch.zeros(3, dtype=torch.int64, device=self.device)
         self.lr_tensor = torch.full((1,), self.lr, device=self.device)
+        lay = fused_mlp.mlp_shadow_layout(self.L1, self.L2)
+        self.shadow = torch.zeros(lay["total"], dtype=torch.bfloat16, device=self.device)
+        self.dh1t = torch.zeros(self.L1 * ((self.B + 31) // 32 * 32), dtype=torch.bfloat16, device=self.device)
+        self.kernel_version = 2
+        self.refresh_shadow()
         self.stats = torch.zeros(stats_ring, 4, device=self.device)
         self.seed = seed
         self.epoch = 0
@@ -115,6 +120,11 @@ class FusedMLPEngine:
     def broadcast_from(self, src: int = 0) -> None:
         if self.world_size > 1 and dist.is_initialized():
             dist.broadcast(self.params, src)
+        self.refresh_shadow()
+
+    def refresh_shadow(self) -> None:
+        """Rebuild the bf16 weight shadows after the fp32 params changed outside a step."""
+        fused_mlp.mlp_refresh_shadow(self.params, self.shadow, self.L1, self.L2)
 
     def set_lr(self, lr: float) -> None:
         self.lr = float(lr)
@@ -123,20 +133,35 @@ class FusedMLPEngine:
     # ----------------------------------------------------------------- step
     def _device_step(self) -> None:
         fused = self.world_size == 1
-        fused_mlp.mlp_train_step(
-            self.params, self.grads, L1=self.L1, L2=self.L2, B=self.B, labels=self.labels,
-            x_u8=self.x_u8, order=self.order, counters=self.counters, n_batches=self.n_batches,
-            exp_avg=self.exp_avg, exp_avg_sq=self.exp_avg_sq, stats=self.stats,
-            apply_adam=fused, advance_step=True, lr=self.lr, betas=self.betas, eps=self.eps,
-            weight_decay=self.wd, lr_tensor=self.lr_tensor,
-        )
+        if self.kernel_version == 1:
+            fused_mlp.mlp_train_step(
+                self.params, self.grads, L1=self.L1, L2=self.L2, B=self.B, labels=self.labels,
+                x_u8=self.x_u8, order=self.order, counters=self.counters[:2], n_batches=self.n_batches,
+                exp_avg=self.exp_avg, exp_avg_sq=self.exp_avg_sq, stats=self.stats,
+                apply_adam=fused, advance_step=True, lr=self.lr, betas=self.betas, eps=self.eps,
+                weight_decay=self.wd, lr_tensor=self.lr_tensor,
+            )
+        else:
+            fused_mlp.mlp_train_step2(
+                self.params, self.grads, shadow=self.shadow, dh1t=self.dh1t, counters=self.counters, L1=self.L1,
+                L2=self.L2, B=self.B, labels=self.labels, x_u8=self.x_u8, order=self.order,
+                n_batches=self.n_batches, exp_avg=self.exp_avg, exp_avg_sq=self.exp_avg_sq, stats=self.stats,
+                apply_adam=fused, advance_step=True, lr=self.lr, betas=self.betas, eps=self.eps,
+                weight_decay=self.wd, lr_tensor=self.lr_tensor,
+            )
         if not fused:
             if self.allreduce is not None:
                 self.allreduce(self.grads)
-            fused_adam_(self.params, self.grads, self.exp_avg, self.exp_avg_sq, lr=self.lr,
-                        betas=self.betas, eps=self.eps, weight_decay=self.wd,
-                        grad_scale=1.0 / self.world_size, step=self.counters[0:1],
-                        lr_tensor=self.lr_tensor)
+            if self.kernel_version == 1:
+                fused_adam_(self.params, self.grads, self.exp_avg, self.exp_avg_sq, lr=self.lr,
+                            betas=self.betas, eps=self.eps, weight_decay=self.wd,
+                            grad_scale=1.0 / self.world_size, step=self.counters[0:1],
+                            lr_tensor=self.lr_tensor)
+            else:
+                fused_mlp.mlp_adam_(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.shadow, L1=self.L1,
+                                    L2=self.L2, lr=self.lr, step=self.counters[0:1], betas=self.betas, eps=self.eps,
+                                    weight_decay=self.wd, grad_scale=1.0 / self.world_size,
+                                    lr_tensor=self.lr_tensor)
 
     def _advance_host(self, n: int) -> None:
         self.global_step += n
