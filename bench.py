@@ -40,7 +40,7 @@ if ROOT not in sys.path:
 METRIC = "samples/sec (whole node) + DDP scaling eff, MNISTClassifier at 1/2/4/8 workers"
 # Our measured stock-PyTorch numbers on MI355X (BASELINE.md "Our MI355X measurements");
 # the reference itself publishes none.  None => vs_baseline is null.
-STOCK_BASELINE = {}
+STOCK_BASELINE = {1: 53015.0}  # --impl torch, 1x MI355X (profiles/r1_first/bench_torch.jsonl)
 
 
 def parse():

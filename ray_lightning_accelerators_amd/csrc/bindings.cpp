@@ -224,6 +224,74 @@ void mlp_train_step2(optional<Tensor> x_u8, optional<Tensor> x_f32, Tensor label
   TORCH_CHECK(rla::launch_mlp_train_step2(a, cur_stream(params)) == 0, "fused MLP v2 launch failed");
 }
 
+// v3 pipelined step.  kind: 0 step (head + fused tail), 1 head only (grads),
+// 2 tail GRAD, 3 tail ADAM (after the allreduce), 4 PRIME (H1pre of the pending batch).
+void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counters, int64_t n_batches, int64_t B,
+          int64_t L1, int64_t L2, Tensor params, Tensor grads, Tensor exp_avg, Tensor exp_avg_sq, Tensor shadow,
+          Tensor dh1t, Tensor xring, Tensor h1pre, Tensor act, optional<Tensor> stats, bool advance_step, double lr,
+          double beta1, double beta2, double eps, double weight_decay, double grad_scale, optional<Tensor> lr_t,
+          bool adamw, optional<Tensor> stamps) {
+  TORCH_CHECK(kind >= 0 && kind <= 4, "mlp3: bad kind ", kind);
+  TORCH_CHECK(rla::mlp_supported((int)L1, (int)L2), "no fused MLP kernel for layer sizes ", L1, "/", L2);
+  TORCH_CHECK(B >= 1 && B <= 256, "fused MLP step supports 1 <= batch <= 256");
+  const int64_t np = mlp_param_count(L1, L2);
+  const int64_t Bp = (B + 31) / 32 * 32;
+  const rla::MLPShadowLayout lay = rla::mlp_shadow_layout((int)L1, (int)L2);
+  check_dev(params, "params", at::kFloat);
+  check_dev(grads, "grads", at::kFloat);
+  check_dev(exp_avg, "exp_avg", at::kFloat);
+  check_dev(exp_avg_sq, "exp_avg_sq", at::kFloat);
+  TORCH_CHECK(params.numel() == np && grads.numel() == np && exp_avg.numel() == np && exp_avg_sq.numel() == np,
+              "param / grad / Adam arenas must hold ", np, " floats");
+  check_dev(shadow, "shadow", at::kBFloat16);
+  TORCH_CHECK(shadow.numel() >= lay.total, "shadow must hold ", lay.total, " bf16");
+  check_dev(dh1t, "dh1t", at::kBFloat16);
+  TORCH_CHECK(dh1t.numel() >= L1 * Bp, "dh1t must hold L1 * round_up(B, 32)");
+  check_dev(xring, "xring", at::kBFloat16);
+  TORCH_CHECK(xring.numel() >= 2 * 49 * Bp * 16, "xring must hold 2 * 49 * round_up(B, 32) * 16");
+  check_dev(h1pre, "h1pre", at::kLong);
+  TORCH_CHECK(h1pre.numel() >= 2 * Bp * L1, "h1pre must hold 2 * round_up(B, 32) * L1");
+  check_dev(act, "act", at::kBFloat16);
+  TORCH_CHECK(act.numel() >= rla::mlp3_act_rows((int)L1, (int)L2) * Bp, "act must hold (L1 + 2 L2 + 16) * Bp");
+  check_dev(counters, "counters", at::kLong);
+  TORCH_CHECK(counters.numel() >= 5, "counters must hold 5 int64");
+  check_dev(x_u8, "x_u8", at::kByte);
+  TORCH_CHECK(x_u8.dim() == 2 && x_u8.size(1) == 784, "x_u8 must be [N, 784]");
+  check_dev(labels, "labels", at::kLong);
+  TORCH_CHECK(labels.numel() == x_u8.size(0), "labels must match the dataset");
+  check_dev(order, "order", at::kLong);
+  TORCH_CHECK(n_batches >= 1 && order.numel() >= 2 * n_batches * B, "order must be [2, n_batches * B]");
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(params.device());
+  rla::MLP3Args a{};
+  a.x_u8 = x_u8.data_ptr<uint8_t>();
+  a.labels = labels.data_ptr<int64_t>();
+  a.order = order.data_ptr<int64_t>();
+  a.order_stride = order.numel() / 2;
+  a.counters = counters.data_ptr<int64_t>();
+  a.n_batches = n_batches;
+  a.B = (int)B; a.L1 = (int)L1; a.L2 = (int)L2;
+  a.params = params.data_ptr<float>();
+  a.grads = grads.data_ptr<float>();
+  a.exp_avg = exp_avg.data_ptr<float>();
+  a.exp_avg_sq = exp_avg_sq.data_ptr<float>();
+  a.shadow = reinterpret_cast<uint16_t*>(shadow.data_ptr());
+  a.dh1t = reinterpret_cast<uint16_t*>(dh1t.data_ptr());
+  a.xring = reinterpret_cast<uint16_t*>(xring.data_ptr());
+  a.h1pre = h1pre.data_ptr<int64_t>();
+  a.act = reinterpret_cast<uint16_t*>(act.data_ptr());
+  a.stats = ptr_or_null<float>(stats, "stats", at::kFloat, 4);
+  a.stats_ring = a.stats ? (int)(stats->numel() / 4) : 0;
+  a.apply_adam = kind == rla::kMLP3Step;
+  a.advance_step = advance_step;
+  a.lr = (float)lr; a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.eps = (float)eps;
+  a.weight_decay = (float)weight_decay;
+  a.grad_scale = (float)grad_scale;
+  a.lr_ptr = ptr_or_null<const float>(lr_t, "lr", at::kFloat, 1);
+  a.adamw = adamw;
+  a.stamps = ptr_or_null<int64_t>(stamps, "stamps", at::kLong, 16);
+  TORCH_CHECK(rla::launch_mlp3(a, (int)kind, cur_stream(params)) == 0, "fused MLP v3 launch failed");
+}
+
 void mlp_adam(Tensor params, Tensor grads, Tensor exp_avg, Tensor exp_avg_sq, Tensor shadow, int64_t L1,
               int64_t L2, double lr, double beta1, double beta2, double eps, double weight_decay,
               double grad_scale, bool adamw, bool update, optional<Tensor> step, optional<Tensor> lr_t) {
@@ -304,6 +372,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("adamw"), py::arg("stamps") = py::none());
   m.def("mlp_eval", &mlp_eval, "fused MNIST-MLP forward + NLL/accuracy");
   m.def("mlp_train_step2", &mlp_train_step2, "fused MNIST-MLP step v2 (head + W1 kernels, bf16 shadows)");
+  m.def("mlp3", &mlp3, "fused MNIST-MLP step v3 (pipelined layer 1): kind 0 step, 1 head, 2 tail-grad, "
+        "3 tail-adam, 4 prime");
   m.def("mlp_adam", &mlp_adam, "MLP arena Adam + bf16 shadow refresh (update=False: refresh only)");
   m.def("mlp_shadow_size", [](int64_t l1, int64_t l2) { return rla::mlp_shadow_layout((int)l1, (int)l2).total; });
   m.def("mlp_supported", [](int64_t a, int64_t b) { return rla::mlp_supported((int)a, (int)b); });

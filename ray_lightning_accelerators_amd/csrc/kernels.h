@@ -106,6 +106,37 @@ struct MLPEvalArgs {
   float* out;               // [2]: += sum of NLL, += correct count
 };
 
+// v3 (cross-step pipelined layer 1, resident uint8 dataset only); see mlp_step3.hip.
+struct MLP3Args {
+  const uint8_t* x_u8;      // [N_data, 784]
+  const int64_t* labels;    // [N_data]
+  const int64_t* order;     // [2][order_stride]: two epochs' sample orders
+  int64_t order_stride;     // n_batches * B
+  int64_t* counters;        // [5]: step, next cursor, consumed cursor, ring slot, order buffer
+  int64_t n_batches;
+  int B, L1, L2;
+  float* params;
+  float* grads;
+  float* exp_avg;
+  float* exp_avg_sq;
+  uint16_t* shadow;         // bf16 weight shadows (mlp_shadow_layout)
+  uint16_t* dh1t;           // [L1][Bp] bf16
+  uint16_t* xring;          // [2][49][Bp][16] bf16 X tiles
+  int64_t* h1pre;           // [2][Bp * L1] layer-1 pre-activations, 32.32 fixed point (fragment order)
+  uint16_t* act;            // [L1 + 2*L2 + 16][Bp] bf16 head -> tail: H1^T, H2^T, dH2^T, dZ^T
+  float* stats;
+  int stats_ring;
+  int apply_adam;           // head: Adam on the small parameters (world size 1)
+  int advance_step;
+  float lr, beta1, beta2, eps, weight_decay, grad_scale;
+  const float* lr_ptr;
+  int adamw;
+  int64_t* stamps;
+};
+enum MLP3Kind { kMLP3Step = 0, kMLP3Head = 1, kMLP3TailGrad = 2, kMLP3TailAdam = 3, kMLP3Prime = 4 };
+int launch_mlp3(const MLP3Args& a, int kind, hipStream_t stream);
+int mlp3_act_rows(int L1, int L2);
+
 // returns 0 on success, -1 if (L1, L2) has no compiled instantiation
 int launch_mlp_train_step(const MLPStepArgs& a, hipStream_t stream);
 int launch_mlp_eval(const MLPEvalArgs& a, hipStream_t stream);

@@ -22,7 +22,7 @@
 // state stay authoritative.
 #include "common.h"
 #include "kernels.h"
-#include <math.h>
+#include "mlp_common.h"
 
 namespace rla {
 
@@ -37,23 +37,15 @@ MLPShadowLayout mlp_shadow_layout(int L1, int L2) {
 
 namespace {
 
-constexpr int kD = 784;
+using namespace mlp;
+
 constexpr int kKS1 = 25;
 constexpr int kXS = 808;
-constexpr int kNC = 10;
 constexpr int kThreads = 512;
 constexpr int kWaves = 8;
 constexpr int kDZS = 40;
 
 constexpr size_t cmax(size_t a, size_t b) { return a > b ? a : b; }
-
-template <int L1, int L2>
-struct Off {
-  // fp32 arena == bf16 shadow row-major copy
-  static constexpr int64_t W1 = 0, B1 = (int64_t)L1 * kD, W2 = B1 + L1, B2 = W2 + (int64_t)L2 * L1,
-                           W3 = B2 + L2, B3 = W3 + kNC * L2, NP = B3 + kNC;
-  static constexpr int64_t W2T = (NP + 7) / 8 * 8, W3T = W2T + (int64_t)L1 * L2;
-};
 
 template <int BC, int L1, int L2>
 struct Cfg {
@@ -75,39 +67,6 @@ struct Cfg {
   static constexpr size_t oMisc = oY + (size_t)BC * 4;
   static constexpr size_t total = oMisc + 64;
 };
-
-typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
-__device__ __forceinline__ bf16x4 tr_read(const __bf16* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p));
-}
-__device__ __forceinline__ bf16x8 ld8(const __bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
-__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-
-struct AdamScal {
-  float lr, step_size, bc2_sqrt, beta1, beta2, eps, wd;
-  int adamw;
-};
-
-__device__ __forceinline__ void adam_scalars(AdamScal& o, int64_t t, float lr, float b1, float b2, float eps,
-                                             float wd, int adamw) {
-  const double bc1 = 1.0 - pow((double)b1, (double)t);
-  const double bc2 = 1.0 - pow((double)b2, (double)t);
-  o.lr = lr;
-  o.step_size = (float)((double)lr / bc1);
-  o.bc2_sqrt = (float)sqrt(bc2);
-  o.beta1 = b1; o.beta2 = b2; o.eps = eps; o.wd = wd; o.adamw = adamw;
-}
-
-__device__ __forceinline__ float adam1(float p, float g, float& m, float& v, const AdamScal& o) {
-  if (o.wd != 0.f) {
-    if (o.adamw) p = p * (1.f - o.lr * o.wd);
-    else g = g + o.wd * p;
-  }
-  m = m + (1.f - o.beta1) * (g - m);
-  v = v * o.beta2 + (1.f - o.beta2) * (g * g);
-  const float denom = sqrtf(v) / o.bc2_sqrt + o.eps;
-  return p + (-o.step_size) * (m / denom);
-}
 
 // ---------------------------------------------------------------------------
 // Head kernel

@@ -1,0 +1,682 @@
+// Fused MNIST-MLP training step, v3: layer 1 pipelined across steps, every
+// weight-gradient epilogue spread over many CUs.
+//
+// v2 (mlp_step2.hip) measured 25 us/step on MI355X; 10 of its head kernel's
+// 17 us went to staging the X batch (50 KB gathered through the sample index)
+// plus the 784-deep layer-1 GEMM on ONE CU, and 4.4 us to the small-parameter
+// gradient/Adam epilogue on that same CU (profiles/r1_first/mlp_phases_v2.json).
+// v3 keeps only the inherently serial chain on the one-workgroup head and moves
+// everything else to a wide tail launch:
+//
+//   head(t)   1 workgroup: H1 = relu(H1pre[t] + b1) (4 KB read instead of X + W1),
+//             layers 2/3, log_softmax/NLL/accuracy, dH2, dH1.  Hands the
+//             transposed activations / deltas (H1^T, H2^T, dH2^T, dZ^T, dH1^T;
+//             bf16, [rows][Bp]) to the tail through HBM and zeroes the other
+//             H1pre slot.
+//   tail(t)   blocks [0, 49): one 16-pixel W1 column tile each: dW1 tile =
+//             X[t]_tile^T dH1 (MFMA; X^T by ds_read_b64_tr_b16), Adam on the
+//             tile, then gather X[t+1]'s tile (u8 -> bf16) and add
+//             X[t+1]_tile . W1_tile^T into H1pre[t+1] (fp32 agent-scope atomics,
+//             49 adders per element) -- layer 1 is linear in W1 and this block
+//             holds the freshly updated tile in registers.  The X tile is parked
+//             in `xring` for tail(t+1)'s dW1.
+//             blocks [49, ...): one wave per 16x16 dW2 / dW3 tile or 64 biases:
+//             MFMA over the batch from the head's transposes, Adam, bf16 shadow
+//             (row-major + transposed) refresh.
+//
+// World size > 1 splits the tail: GRAD (all gradients -> `grads`, gather
+// X[t+1]) before the allreduce, ADAM (W1 tiles: Adam + the next-step partial;
+// extra blocks: flat Adam over every other parameter) after it.  PRIME computes
+// H1pre for the pending batch from the current weights (after init / load /
+// broadcast).
+//
+// Device state (graph-replay safe): counters[0] optimizer step, [1] cursor of
+// the NEXT batch, [2] cursor the last head consumed, [3] ring slot the next head
+// reads, [4] which of the two `order` epoch buffers counters[1] indexes.
+// H1pre is stored in MFMA-fragment order (element (b, m) at
+// (((b/16 * L1/16 + m/16) * 4 + b%4) * 64 + (b%16/4) * 16 + m%16) so every atomic
+// wave-instruction covers 256 contiguous bytes.  The fp32 atomics make H1pre's
+// last bits depend on arrival order (run-to-run drift at rounding level).
+#include "common.h"
+#include "kernels.h"
+#include "mlp_common.h"
+
+namespace rla {
+namespace {
+
+using namespace mlp;
+
+constexpr int kThreads = 512;
+constexpr int kWaves = 8;
+constexpr int kDZS = 40;
+constexpr int kXSS = 24;   // LDS row stride of a 16-pixel X slice (bf16)
+constexpr int kBMax = 256;
+
+enum TailMode { kFused = 0, kGrad = 1, kAdam = 2, kPrime = 3 };
+
+// rows of the `act` hand-off buffer ([rows][Bp] bf16)
+template <int L1, int L2>
+struct Act {
+  static constexpr int H1T = 0, H2T = L1, DH2T = L1 + L2, DZT = L1 + 2 * L2, ROWS = L1 + 2 * L2 + 16;
+};
+
+template <int BC, int L1, int L2>
+struct Cfg3 {
+  static constexpr int H1S = L1 + 8, H2S = L2 + 8, TS = BC + 8;
+  static constexpr int MT = BC / 16, TN1 = L1 / 16, TN2 = L2 / 16;
+  static constexpr size_t oH1 = 0;
+  static constexpr size_t oH1T = oH1 + (size_t)BC * H1S * 2;
+  static constexpr size_t oH2 = oH1T + (size_t)L1 * TS * 2;
+  static constexpr size_t oZ = oH2 + (size_t)BC * H2S * 2;
+  static constexpr size_t odZ = oZ + (size_t)BC * 16 * 4;
+  static constexpr size_t odZT = odZ + (size_t)BC * kDZS * 2;
+  static constexpr size_t oY = odZT + (size_t)16 * TS * 2;
+  static constexpr size_t oMisc = oY + (size_t)BC * 4;
+  static constexpr size_t oBias = oMisc + 64;
+  static constexpr size_t total = oBias + (((size_t)(L1 + L2 + 16) * 4 + 15) / 16) * 16;
+};
+
+template <int BC, int L1, int L2>
+constexpr bool fits3() {
+  return Cfg3<BC, L1, L2>::total + 256 <= 160 * 1024;
+}
+
+__device__ __forceinline__ __bf16 relu_bf(float x) { return (__bf16)fmaxf(x, 0.f); }
+
+// H1pre partial sums travel as 32.32 fixed point: the 49 tile contributions are
+// added with integer atomics, which are associative, so the sum (and the whole
+// step) is bitwise reproducible whatever order the atomics land in.  Scaling by
+// 2^32 is exact in fp32; |partial| < 2^31 holds for any sane weights.
+constexpr float kFix = 4294967296.0f;  // 2^32
+__device__ __forceinline__ unsigned long long f32_to_fixed(float x) {
+  return (unsigned long long)__float2ll_rn(x * kFix);
+}
+__device__ __forceinline__ float fixed_to_f32(int64_t q) { return (float)((double)q * (1.0 / 4294967296.0)); }
+
+// ---------------------------------------------------------------------------
+// Head kernel (one workgroup, 8 waves)
+// ---------------------------------------------------------------------------
+template <int BC, int L1, int L2>
+__global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
+  using C = Cfg3<BC, L1, L2>;
+  using O = Off<L1, L2>;
+  using A = Act<L1, L2>;
+  __shared__ __attribute__((aligned(16))) char smem[C::total];
+  __bf16* sH1 = (__bf16*)(smem + C::oH1);
+  __bf16* sH1T = (__bf16*)(smem + C::oH1T);
+  __bf16* sH2 = (__bf16*)(smem + C::oH2);
+  float* sZ = (float*)(smem + C::oZ);
+  __bf16* sdZ = (__bf16*)(smem + C::odZ);
+  __bf16* sdZT = (__bf16*)(smem + C::odZT);
+  int* sY = (int*)(smem + C::oY);
+  float* misc = (float*)(smem + C::oMisc);
+  float* sBias = (float*)(smem + C::oBias);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r16 = lane & 15, g = lane >> 4;
+  const __bf16* SH = reinterpret_cast<const __bf16*>(a.shadow);
+  const float* P = a.params;
+
+  // device counters: uniform scalar loads, no LDS broadcast round trip
+  const int64_t t = a.counters[0] + 1;
+  const int64_t cursor = a.counters[1];
+  const int64_t slot = a.counters[3];
+  const int64_t ob = a.counters[4];
+  const int Bp = (a.B + 31) / 32 * 32;
+  const int64_t* h1p = a.h1pre + slot * (int64_t)Bp * L1;
+  const int64_t* idx = a.order + ob * a.order_stride + cursor * a.B;
+  __bf16* ACT = reinterpret_cast<__bf16*>(a.act);
+  __bf16* DH1T = reinterpret_cast<__bf16*>(a.dh1t);
+
+  constexpr int NBIAS = L1 + L2 + kNC;
+  if (tid < NBIAS) {
+    const int64_t bgi = tid < L1 ? O::B1 + tid : (tid < L1 + L2 ? O::B2 + (tid - L1) : O::B3 + (tid - L1 - L2));
+    sBias[tid] = P[bgi];
+  }
+  if (tid == 0) {
+    misc[0] = 0.f; misc[1] = 0.f; misc[2] = 0.f;
+    if (a.stamps) a.stamps[0] = __builtin_amdgcn_s_memrealtime();
+  }
+  // the tail of this step accumulates the next step's H1pre into the other slot
+  {
+    uint4* z = reinterpret_cast<uint4*>(a.h1pre + (slot ^ 1) * (int64_t)Bp * L1);
+    for (int i = tid; i < Bp * L1 / 2; i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  const float invB = 1.f / (float)a.B;
+  const int nchunks = (a.B + BC - 1) / BC;
+  constexpr int KS2 = L1 / 32, KS3 = L2 / 32, KSH = L2 / 32;
+  constexpr int P3 = KS3 < 4 ? KS3 : 4;
+  constexpr int PH = KSH < 4 ? KSH : 4;
+
+  // LDS [rows][TS] -> act rows [dst_row][Bp] at columns [row0, row0 + BC) (< Bp)
+  auto copy_rows = [&](const __bf16* src, int nrows, int dst_row, int row0) {
+    constexpr int CPR = BC / 8;
+    for (int e = tid; e < nrows * CPR; e += kThreads) {
+      const int r = e / CPR, col = (e - r * CPR) * 8;
+      if (row0 + col < Bp)
+        *reinterpret_cast<bf16x8*>(ACT + (int64_t)(dst_row + r) * Bp + row0 + col) = ld8(src + r * C::TS + col);
+    }
+  };
+
+  for (int c = 0; c < nchunks; ++c) {
+    const int row0 = c * BC;
+    const int nvalid = min(BC, a.B - row0);
+
+    // ---- batch-independent weight fragments, issued first ----
+    bf16x8 w2f[KS2];
+    {
+      const int nt = w / C::MT;
+#pragma unroll
+      for (int ks = 0; ks < KS2; ++ks)
+        w2f[ks] = (w < C::MT * C::TN2) ? ld8(SH + O::W2 + (int64_t)(nt * 16 + r16) * L1 + ks * 32 + 8 * g) : zero8();
+    }
+    bf16x8 w3f[P3];
+#pragma unroll
+    for (int ks = 0; ks < P3; ++ks)
+      w3f[ks] = (w < C::MT && r16 < kNC) ? ld8(SH + O::W3 + (int64_t)r16 * L2 + ks * 32 + 8 * g) : zero8();
+    bf16x8 w3tf;
+    {
+      const int nt = w / C::MT;
+      w3tf = (w < C::MT * C::TN2 && g < 2) ? ld8(SH + O::W3T + (int64_t)(nt * 16 + r16) * 16 + 8 * g) : zero8();
+    }
+    bf16x8 w2tf[PH];
+    {
+      const int ct = w / C::MT;
+#pragma unroll
+      for (int ks = 0; ks < PH; ++ks)
+        w2tf[ks] = (w < C::MT * C::TN1) ? ld8(SH + O::W2T + (int64_t)(ct * 16 + r16) * L2 + ks * 32 + 8 * g) : zero8();
+    }
+    if (tid < BC) {
+      int y = -1;
+      if (tid < nvalid) y = (int)a.labels[idx[row0 + tid]];
+      sY[tid] = y;
+    }
+    __syncthreads();  // sBias ready
+
+    // ---- H1 = relu(H1pre + b1); H1pre chunk is contiguous in fragment order ----
+    {
+      const int64_t* src = h1p + (int64_t)row0 * L1;
+      for (int f4 = tid; f4 < BC * L1 / 4; f4 += kThreads) {
+        const int f = f4 * 4;
+        const int ln = f & 63, i = (f >> 6) & 3, blk = f >> 8;
+        const int ct = blk % C::TN1, mtl = blk / C::TN1;
+        const int b = mtl * 16 + 4 * (ln >> 4) + i, m = ct * 16 + (ln & 15);
+        // rows past round_up(B, 32) exist only in the last chunk's LDS image
+        int64_t q[4] = {0, 0, 0, 0};
+        if (row0 + mtl * 16 < Bp) {
+          const longlong2 q01 = *reinterpret_cast<const longlong2*>(src + f);
+          const longlong2 q23 = *reinterpret_cast<const longlong2*>(src + f + 2);
+          q[0] = q01.x; q[1] = q01.y; q[2] = q23.x; q[3] = q23.y;
+        }
+        bf16x4 h;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) h[k] = relu_bf(fixed_to_f32(q[k]) + sBias[m + k]);
+        *reinterpret_cast<bf16x4*>(sH1 + b * C::H1S + m) = h;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sH1T[(m + k) * C::TS + b] = h[k];
+      }
+    }
+    __syncthreads();
+    if (a.stamps && tid == 0 && c == 0) a.stamps[1] = __builtin_amdgcn_s_memrealtime();
+    copy_rows(sH1T, L1, A::H1T, row0);
+
+    // ---------------- layer 2 ----------------
+    for (int tile = w; tile < C::MT * C::TN2; tile += kWaves) {
+      const int mt = tile % C::MT, nt = tile / C::MT;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS2; ++ks) {
+        const bf16x8 bfrag = (tile == w) ? w2f[ks] : ld8(SH + O::W2 + (int64_t)(nt * 16 + r16) * L1 + ks * 32 + 8 * g);
+        acc = mfma16(ld8(sH1 + (mt * 16 + r16) * C::H1S + ks * 32 + 8 * g), bfrag, acc);
+      }
+      const int n = nt * 16 + r16;
+      const float bias = sBias[L1 + n];
+      bf16x4 t4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const __bf16 h = relu_bf(acc[i] + bias);
+        sH2[(mt * 16 + 4 * g + i) * C::H2S + n] = h;
+        t4[i] = h;
+      }
+      if (row0 + mt * 16 < Bp)
+        *reinterpret_cast<bf16x4*>(ACT + (int64_t)(A::H2T + n) * Bp + row0 + mt * 16 + 4 * g) = t4;
+    }
+    __syncthreads();
+
+    // ---------------- layer 3 (logits) ----------------
+    if (w < C::MT) {
+      const int mt = w;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS3; ++ks) {
+        bf16x8 bfrag;
+        if (ks < P3) bfrag = w3f[ks < P3 ? ks : 0];
+        else bfrag = (r16 < kNC) ? ld8(SH + O::W3 + (int64_t)r16 * L2 + ks * 32 + 8 * g) : zero8();
+        acc = mfma16(ld8(sH2 + (mt * 16 + r16) * C::H2S + ks * 32 + 8 * g), bfrag, acc);
+      }
+      if (r16 < kNC) {
+        const float bias = sBias[L1 + L2 + r16];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sZ[(mt * 16 + 4 * g + i) * 16 + r16] = acc[i] + bias;
+      }
+    }
+    __syncthreads();
+    if (a.stamps && tid == 0 && c == 0) a.stamps[2] = __builtin_amdgcn_s_memrealtime();
+
+    // ---------------- log_softmax / NLL / accuracy / dZ (one row per lane) -------------
+    if (w < (BC + 63) / 64) {
+      const int r = w * 64 + lane;
+      float loss = 0.f, correct = 0.f, cnt = 0.f;
+      bf16x8 d8[2];
+      d8[0] = zero8();
+      d8[1] = zero8();
+      const int y = (r < BC) ? sY[r] : -1;
+      if (y >= 0) {
+        float z[kNC];
+        float m = -INFINITY;
+        int arg = 0;
+#pragma unroll
+        for (int j = 0; j < kNC; ++j) {
+          z[j] = sZ[r * 16 + j];
+          if (z[j] > m) { m = z[j]; arg = j; }
+        }
+        float sum = 0.f, pr[kNC], zy = 0.f;
+#pragma unroll
+        for (int j = 0; j < kNC; ++j) {
+          pr[j] = __expf(z[j] - m);
+          sum += pr[j];
+          zy = (j == y) ? z[j] : zy;
+        }
+        const float inv = 1.f / sum;
+        loss = m + __logf(sum) - zy;
+        correct = (arg == y) ? 1.f : 0.f;
+        cnt = 1.f;
+#pragma unroll
+        for (int j = 0; j < kNC; ++j) d8[j >> 3][j & 7] = (__bf16)((pr[j] * inv - (j == y ? 1.f : 0.f)) * invB);
+      }
+      if (r < BC) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) *reinterpret_cast<bf16x8*>(sdZ + r * kDZS + 8 * q) = d8[q];
+        *reinterpret_cast<bf16x8*>(sdZ + r * kDZS + 16) = zero8();
+        *reinterpret_cast<bf16x8*>(sdZ + r * kDZS + 24) = zero8();
+#pragma unroll
+        for (int j = 0; j < 16; ++j) sdZT[j * C::TS + r] = (j < kNC) ? d8[j >> 3][j & 7] : (__bf16)0.f;
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        loss += __shfl_xor(loss, off, 64);
+        correct += __shfl_xor(correct, off, 64);
+        cnt += __shfl_xor(cnt, off, 64);
+      }
+      if (lane == 0) {
+        atomicAdd(&misc[0], loss);
+        atomicAdd(&misc[1], correct);
+        atomicAdd(&misc[2], cnt);
+      }
+    }
+    __syncthreads();
+    copy_rows(sdZT, 16, A::DZT, row0);
+
+    // ---------------- dH2 = (dZ W3) * (H2 > 0) ----------------
+    for (int tile = w; tile < C::MT * C::TN2; tile += kWaves) {
+      const int mt = tile % C::MT, nt = tile / C::MT, n = nt * 16 + r16;
+      const bf16x8 bfrag = (tile == w) ? w3tf : ((g < 2) ? ld8(SH + O::W3T + (int64_t)n * 16 + 8 * g) : zero8());
+      const f32x4 acc = mfma16(ld8(sdZ + (mt * 16 + r16) * kDZS + 8 * g), bfrag, f32x4{0.f, 0.f, 0.f, 0.f});
+      bf16x4 t4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        __bf16* hp = sH2 + (mt * 16 + 4 * g + i) * C::H2S + n;
+        const __bf16 d = ((float)(*hp) > 0.f) ? (__bf16)acc[i] : (__bf16)0.f;
+        *hp = d;
+        t4[i] = d;
+      }
+      if (row0 + mt * 16 < Bp)
+        *reinterpret_cast<bf16x4*>(ACT + (int64_t)(A::DH2T + n) * Bp + row0 + mt * 16 + 4 * g) = t4;
+    }
+    __syncthreads();
+
+    // ---------------- dH1 = (dH2 W2) * (H1 > 0) -> dh1t ----------------
+    for (int tile = w; tile < C::MT * C::TN1; tile += kWaves) {
+      const int mt = tile % C::MT, ct = tile / C::MT, m = ct * 16 + r16;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KSH; ++ks) {
+        bf16x8 bfrag;
+        if (tile == w && ks < PH) bfrag = w2tf[ks < PH ? ks : 0];
+        else bfrag = ld8(SH + O::W2T + (int64_t)m * L2 + ks * 32 + 8 * g);
+        acc = mfma16(ld8(sH2 + (mt * 16 + r16) * C::H2S + ks * 32 + 8 * g), bfrag, acc);
+      }
+      bf16x4 t4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const __bf16 hv = sH1[(mt * 16 + 4 * g + i) * C::H1S + m];
+        t4[i] = ((float)hv > 0.f) ? (__bf16)acc[i] : (__bf16)0.f;
+      }
+      if (row0 + mt * 16 < Bp) *reinterpret_cast<bf16x4*>(DH1T + (int64_t)m * Bp + row0 + mt * 16 + 4 * g) = t4;
+    }
+    __syncthreads();
+    if (a.stamps && tid == 0 && c == 0) a.stamps[3] = __builtin_amdgcn_s_memrealtime();
+  }
+  if (tid == 0) {
+    if (a.advance_step) a.counters[0] = t;
+    a.counters[2] = cursor;
+    int64_t nc = cursor + 1, nob = ob;
+    if (nc >= a.n_batches) { nc = 0; nob ^= 1; }
+    a.counters[1] = nc;
+    a.counters[4] = nob;
+    a.counters[3] = slot ^ 1;
+    if (a.stats) {
+      const int s = (int)((t - 1) % (a.stats_ring > 0 ? a.stats_ring : 1));
+      float* st = a.stats + s * 4;
+      st[0] = misc[0] * invB;
+      st[1] = misc[1];
+      st[2] = misc[2];
+      st[3] = (float)t;
+    }
+    if (a.stamps) a.stamps[4] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Tail kernel pieces
+// ---------------------------------------------------------------------------
+template <int L1, int L2>
+struct SmallTasks {
+  static constexpr int TN1 = L1 / 16, TN2 = L2 / 16;
+  static constexpr int NT_W2 = TN1 * TN2, NT_W3 = TN2, NTILE = NT_W2 + NT_W3;
+  static constexpr int NBIAS = L1 + L2 + kNC, NBW = (NBIAS + 63) / 64;
+  static constexpr int NTASK = NTILE + NBW;
+  static constexpr int NBLK = (NTASK + TN1 - 1) / TN1;  // tail blocks have TN1 waves
+};
+
+// One wave: a 16x16 tile of dW2 or dW3, or 64 biases: gradient from the head's
+// transposes, then Adam (FUSED) or a plain gradient store (GRAD).
+template <int L1, int L2>
+__device__ __forceinline__ void small_task(const MLP3Args& a, int mode, int task, const AdamScal& o) {
+  using O = Off<L1, L2>;
+  using A = Act<L1, L2>;
+  using S = SmallTasks<L1, L2>;
+  const int lane = threadIdx.x & 63, r16 = lane & 15, g = lane >> 4;
+  const int Bp = (a.B + 31) / 32 * 32;
+  const __bf16* ACT = reinterpret_cast<const __bf16*>(a.act);
+  __bf16* SHW = reinterpret_cast<__bf16*>(a.shadow);
+  const bool fused = mode == kFused;
+  if (task < S::NTILE) {
+    int64_t gi[4];
+    bool valid[4];
+    int rowv, colv;
+    const __bf16 *arow, *brow;
+    if (task < S::NT_W2) {  // dW2[n][m] = sum_b dH2[b][n] H1[b][m]
+      const int nt = task % S::TN2, ct = task / S::TN2;
+      rowv = nt * 16 + 4 * g;
+      colv = ct * 16 + r16;
+      arow = ACT + (int64_t)(A::DH2T + nt * 16 + r16) * Bp;
+      brow = ACT + (int64_t)(A::H1T + ct * 16 + r16) * Bp;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { gi[i] = O::W2 + (int64_t)(rowv + i) * L1 + colv; valid[i] = true; }
+    } else {  // dW3[j][n] = sum_b dZ[b][j] H2[b][n]
+      const int nt = task - S::NT_W2;
+      rowv = 4 * g;
+      colv = nt * 16 + r16;
+      arow = ACT + (int64_t)(A::DZT + r16) * Bp;
+      brow = ACT + (int64_t)(A::H2T + nt * 16 + r16) * Bp;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        valid[i] = (rowv + i) < kNC;
+        gi[i] = O::W3 + (int64_t)(valid[i] ? rowv + i : 0) * L2 + colv;
+      }
+    }
+    float pv[4], mv[4], vv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      pv[i] = mv[i] = vv[i] = 0.f;
+      if (fused && valid[i]) { pv[i] = a.params[gi[i]]; mv[i] = a.exp_avg[gi[i]]; vv[i] = a.exp_avg_sq[gi[i]]; }
+    }
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < Bp / 32; ++ks) {
+      const int b0 = ks * 32 + 8 * g;
+      acc = mfma16(ld8(arow + b0), ld8(brow + b0), acc);
+    }
+    bf16x4 sh4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      sh4[i] = (__bf16)0.f;
+      if (!valid[i]) continue;
+      if (fused) {
+        const float p_ = adam1(pv[i], acc[i], mv[i], vv[i], o);
+        a.params[gi[i]] = p_;
+        a.exp_avg[gi[i]] = mv[i];
+        a.exp_avg_sq[gi[i]] = vv[i];
+        SHW[gi[i]] = (__bf16)p_;
+        sh4[i] = (__bf16)p_;
+      } else {
+        a.grads[gi[i]] = acc[i];
+      }
+    }
+    if (fused) {
+      if (task < S::NT_W2) *reinterpret_cast<bf16x4*>(SHW + O::W2T + (int64_t)colv * L2 + rowv) = sh4;
+      else *reinterpret_cast<bf16x4*>(SHW + O::W3T + (int64_t)colv * 16 + rowv) = sh4;
+    }
+  } else {  // 64 biases per wave: row sums of dH1^T / dH2^T / dZ^T
+    const int e = (task - S::NTILE) * 64 + lane;
+    if (e >= S::NBIAS) return;
+    const __bf16* row;
+    int64_t gidx;
+    if (e < L1) { row = reinterpret_cast<const __bf16*>(a.dh1t) + (int64_t)e * Bp; gidx = O::B1 + e; }
+    else if (e < L1 + L2) { row = ACT + (int64_t)(A::DH2T + e - L1) * Bp; gidx = O::B2 + (e - L1); }
+    else { row = ACT + (int64_t)(A::DZT + e - L1 - L2) * Bp; gidx = O::B3 + (e - L1 - L2); }
+    float pv = 0.f, mv = 0.f, vv = 0.f;
+    if (fused) { pv = a.params[gidx]; mv = a.exp_avg[gidx]; vv = a.exp_avg_sq[gidx]; }
+    float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < Bp; b += 8) {
+      const bf16x8 v = ld8(row + b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s8[j] += (float)v[j];
+    }
+    const float sum = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
+    if (fused) {
+      const float p_ = adam1(pv, sum, mv, vv, o);
+      a.params[gidx] = p_;
+      a.exp_avg[gidx] = mv;
+      a.exp_avg_sq[gidx] = vv;
+      SHW[gidx] = (__bf16)p_;
+    } else {
+      a.grads[gidx] = sum;
+    }
+  }
+}
+
+// ADAM mode: flat Adam over every non-W1 parameter (after the allreduce).
+template <int L1, int L2>
+__device__ __forceinline__ void small_adam_flat(const MLP3Args& a, const AdamScal& o, int blk, int nblk) {
+  using O = Off<L1, L2>;
+  __bf16* SHW = reinterpret_cast<__bf16*>(a.shadow);
+  for (int64_t i = O::B1 + (int64_t)blk * blockDim.x + threadIdx.x; i < O::NP; i += (int64_t)nblk * blockDim.x) {
+    float m = a.exp_avg[i], v = a.exp_avg_sq[i];
+    const float p = adam1(a.params[i], a.grads[i] * a.grad_scale, m, v, o);
+    a.params[i] = p;
+    a.exp_avg[i] = m;
+    a.exp_avg_sq[i] = v;
+    const __bf16 pb = (__bf16)p;
+    SHW[i] = pb;
+    if (i >= O::W2 && i < O::B2) {
+      const int64_t r = i - O::W2;
+      const int n = (int)(r / L1), mm = (int)(r - (int64_t)n * L1);
+      SHW[O::W2T + (int64_t)mm * L2 + n] = pb;
+    } else if (i >= O::W3 && i < O::B3) {
+      const int64_t r = i - O::W3;
+      const int j = (int)(r / L2), n = (int)(r - (int64_t)j * L2);
+      SHW[O::W3T + (int64_t)n * 16 + j] = pb;
+    }
+  }
+}
+
+template <int L1, int L2>
+__global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, int mode) {
+  constexpr int TN1 = L1 / 16;
+  constexpr int NT = 64 * TN1;
+  __shared__ __attribute__((aligned(16))) __bf16 sX[kBMax * kXSS];
+  __shared__ __attribute__((aligned(16))) __bf16 sXn[kBMax * kXSS];
+  __shared__ __attribute__((aligned(16))) __bf16 sW[L1 * kXSS];
+  __shared__ AdamScal sh_o;
+  const int tid = threadIdx.x, lane = tid & 63, ct = tid >> 6, r16 = lane & 15, g = lane >> 4;
+  const bool do_grad = mode == kFused || mode == kGrad;
+  const bool do_adam = mode == kFused || mode == kAdam;
+  const bool do_fwd = mode != kGrad;
+  if (a.stamps && blockIdx.x == 0 && tid == 0) a.stamps[8] = __builtin_amdgcn_s_memrealtime();
+  if (tid == 0 && do_adam) {
+    const int64_t t = a.counters[0];  // already advanced by the head kernel
+    adam_scalars(sh_o, t, a.lr_ptr ? a.lr_ptr[0] : a.lr, a.beta1, a.beta2, a.eps, a.weight_decay, a.adamw);
+  }
+  if ((int)blockIdx.x >= kTiles) {  // small parameters (block-uniform branch)
+    __syncthreads();
+    const int sblk = (int)blockIdx.x - kTiles;
+    if (mode == kAdam) small_adam_flat<L1, L2>(a, sh_o, sblk, (int)gridDim.x - kTiles);
+    else small_task<L1, L2>(a, mode, sblk * TN1 + ct, sh_o);
+    return;
+  }
+  const int kt = blockIdx.x;
+  const int B = a.B;
+  const int Bp = (B + 31) / 32 * 32;
+  const int m = ct * 16 + r16, pix = kt * 16 + 4 * g;
+  const int64_t gidx = (int64_t)m * kD + pix;
+
+  // ---- loads that need no device state: Adam state, allreduced grads, current W1 ----
+  F4 p4{}, m4{}, v4{}, g4{};
+  if (do_adam) {
+    p4 = *reinterpret_cast<const F4*>(a.params + gidx);
+    m4 = *reinterpret_cast<const F4*>(a.exp_avg + gidx);
+    v4 = *reinterpret_cast<const F4*>(a.exp_avg_sq + gidx);
+  }
+  if (mode == kAdam) g4 = *reinterpret_cast<const F4*>(a.grads + gidx);
+  bf16x4 w4;
+  if (mode == kPrime) w4 = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(a.shadow) + gidx);
+
+  const int64_t slot = a.counters[3];
+  const int64_t tile_elems = (int64_t)Bp * 16;
+  __bf16* XR = reinterpret_cast<__bf16*>(a.xring);
+  __bf16* xr_next = XR + (slot * kTiles + kt) * tile_elems;
+  const __bf16* xr_cur = XR + ((slot ^ 1) * kTiles + kt) * tile_elems;
+
+  // ---- X slices: this step's (parked by the previous tail) and the next step's ----
+  if (do_grad) {
+    for (int b = tid; b < Bp; b += NT) {
+      *reinterpret_cast<bf16x8*>(sX + b * kXSS) = ld8(xr_cur + b * 16);
+      *reinterpret_cast<bf16x8*>(sX + b * kXSS + 8) = ld8(xr_cur + b * 16 + 8);
+    }
+  }
+  if (mode == kAdam) {
+    for (int b = tid; b < Bp; b += NT) {
+      *reinterpret_cast<bf16x8*>(sXn + b * kXSS) = ld8(xr_next + b * 16);
+      *reinterpret_cast<bf16x8*>(sXn + b * kXSS + 8) = ld8(xr_next + b * 16 + 8);
+    }
+  } else {
+    const int64_t* idx = a.order + a.counters[4] * a.order_stride + a.counters[1] * B;
+    for (int b = tid; b < Bp; b += NT) {
+      bf16x8 lo = zero8(), hi = zero8();
+      if (b < B) u8x16_to_bf16(*reinterpret_cast<const uint4*>(a.x_u8 + idx[b] * kD + kt * 16), lo, hi);
+      *reinterpret_cast<bf16x8*>(sXn + b * kXSS) = lo;
+      *reinterpret_cast<bf16x8*>(sXn + b * kXSS + 8) = hi;
+      *reinterpret_cast<bf16x8*>(xr_next + b * 16) = lo;
+      *reinterpret_cast<bf16x8*>(xr_next + b * 16 + 8) = hi;
+    }
+  }
+  __syncthreads();
+  if (a.stamps && kt == 0 && tid == 0) a.stamps[9] = __builtin_amdgcn_s_memrealtime();
+
+  // ---- dW1 tile: D[pixel pix+i][neuron m] = sum_b X[b][pix+i] dH1[b][m] ----
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (do_grad) {
+    const __bf16* dh = reinterpret_cast<const __bf16*>(a.dh1t) + (int64_t)m * Bp;
+    const int q = r16 >> 2, pp = r16 & 3;
+    for (int ks = 0; ks < Bp / 32; ++ks) {
+      const int b0 = ks * 32 + 8 * g;
+      const bf16x4 lo = tr_read(sX + (b0 + q) * kXSS + 4 * pp);
+      const bf16x4 hi = tr_read(sX + (b0 + 4 + q) * kXSS + 4 * pp);
+      const bf16x8 afrag = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      acc = mfma16(afrag, ld8(dh + b0), acc);
+    }
+  }
+  if (mode == kGrad) {
+    F4 gg{{acc[0], acc[1], acc[2], acc[3]}};
+    *reinterpret_cast<F4*>(a.grads + gidx) = gg;
+    return;
+  }
+  if (do_adam) {
+    const AdamScal o = sh_o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float gr = (mode == kAdam) ? g4.v[i] * a.grad_scale : acc[i];
+      p4.v[i] = adam1(p4.v[i], gr, m4.v[i], v4.v[i], o);
+      w4[i] = (__bf16)p4.v[i];
+    }
+    *reinterpret_cast<F4*>(a.params + gidx) = p4;
+    *reinterpret_cast<F4*>(a.exp_avg + gidx) = m4;
+    *reinterpret_cast<F4*>(a.exp_avg_sq + gidx) = v4;
+    *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.shadow) + gidx) = w4;
+  }
+  // ---- next step's layer-1 partial: H1pre[b][m] += sum_{16 px} X'[b][px] W1[m][px] ----
+  *reinterpret_cast<bf16x4*>(sW + m * kXSS + 4 * g) = w4;
+  __syncthreads();
+  if (do_fwd) {
+    unsigned long long* h1 = reinterpret_cast<unsigned long long*>(a.h1pre + slot * (int64_t)Bp * L1);
+    const bf16x8 bfrag = (g < 2) ? ld8(sW + (ct * 16 + r16) * kXSS + 8 * g) : zero8();
+    for (int mt = 0; mt < Bp / 16; ++mt) {
+      const bf16x8 afrag = (g < 2) ? ld8(sXn + (mt * 16 + r16) * kXSS + 8 * g) : zero8();
+      const f32x4 d = mfma16(afrag, bfrag, f32x4{0.f, 0.f, 0.f, 0.f});
+      unsigned long long* dst = h1 + (int64_t)((mt * TN1 + ct) * 4) * 64 + lane;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) atomicAdd(dst + i * 64, f32_to_fixed(d[i]));
+    }
+  }
+  if (a.stamps && kt == 0 && tid == 0) a.stamps[10] = __builtin_amdgcn_s_memrealtime();
+}
+
+template <int L1, int L2>
+int dispatch3(const MLP3Args& a, int kind, hipStream_t stream) {
+  constexpr int NT = 64 * (L1 / 16);
+  if (kind == kMLP3Step || kind == kMLP3Head) {
+    // the smallest chunk that covers the batch, as LDS allows
+    bool launched = false;
+    if constexpr (fits3<128, L1, L2>()) {
+      if (a.B > 64) {
+        hipLaunchKernelGGL((mlp3_head_kernel<128, L1, L2>), dim3(1), dim3(kThreads), 0, stream, a);
+        launched = true;
+      }
+    }
+    if (!launched && a.B > 32) {
+      hipLaunchKernelGGL((mlp3_head_kernel<64, L1, L2>), dim3(1), dim3(kThreads), 0, stream, a);
+      launched = true;
+    }
+    if (!launched) hipLaunchKernelGGL((mlp3_head_kernel<32, L1, L2>), dim3(1), dim3(kThreads), 0, stream, a);
+  }
+  int mode = -1, grid = kTiles;
+  if (kind == kMLP3Step) { mode = kFused; grid += SmallTasks<L1, L2>::NBLK; }
+  else if (kind == kMLP3TailGrad) { mode = kGrad; grid += SmallTasks<L1, L2>::NBLK; }
+  else if (kind == kMLP3Prime) mode = kPrime;
+  else if (kind == kMLP3TailAdam) {
+    mode = kAdam;
+    const int64_t nsmall = Off<L1, L2>::NP - Off<L1, L2>::B1;
+    int extra = (int)((nsmall + NT - 1) / NT);
+    grid += extra < 64 ? extra : 64;
+  }
+  if (mode >= 0) hipLaunchKernelGGL((mlp3_tail_kernel<L1, L2>), dim3(grid), dim3(NT), 0, stream, a, mode);
+  return 0;
+}
+
+static_assert(fits3<64, 128, 256>(), "v3 head LDS budget");
+
+}  // namespace
+
+int mlp3_act_rows(int L1, int L2) { return L1 + 2 * L2 + 16; }
+
+int launch_mlp3(const MLP3Args& a, int kind, hipStream_t stream) {
+  if (a.B > kBMax || a.B < 1) return -2;
+#define RLA_CASE(a1, a2) if (a.L1 == a1 && a.L2 == a2) return dispatch3<a1, a2>(a, kind, stream);
+  RLA_CASE(32, 32) RLA_CASE(32, 64) RLA_CASE(32, 128) RLA_CASE(32, 256)
+  RLA_CASE(64, 64) RLA_CASE(64, 128) RLA_CASE(64, 256)
+  RLA_CASE(128, 64) RLA_CASE(128, 128) RLA_CASE(128, 256)
+#undef RLA_CASE
+  return -1;
+}
+
+}  // namespace rla

@@ -217,6 +217,67 @@ def mlp_train_step2(
         mlp_refresh_shadow(params, shadow, L1, L2)
 
 
+MLP3_STEP, MLP3_HEAD, MLP3_TAIL_GRAD, MLP3_TAIL_ADAM, MLP3_PRIME = range(5)
+W1_TILES = IN_FEATURES // 16
+
+
+def mlp3_buffers(L1: int, L2: int, B: int, device) -> Dict[str, torch.Tensor]:
+    """Device scratch of the v3 pipelined step (see csrc/mlp_step3.hip)."""
+    bp = (B + 31) // 32 * 32
+    return {
+        "dh1t": torch.zeros(L1 * bp, dtype=torch.bfloat16, device=device),
+        "xring": torch.zeros(2 * W1_TILES * bp * 16, dtype=torch.bfloat16, device=device),
+        # 32.32 fixed point: integer atomics make the 49-way split-K sum order-independent
+        "h1pre": torch.zeros(2 * bp * L1, dtype=torch.int64, device=device),
+        "act": torch.zeros((L1 + 2 * L2 + 16) * bp, dtype=torch.bfloat16, device=device),
+        "counters": torch.zeros(5, dtype=torch.int64, device=device),
+    }
+
+
+def mlp3_launch(
+    kind: int,
+    *,
+    x_u8: torch.Tensor,
+    labels: torch.Tensor,
+    order: torch.Tensor,
+    counters: torch.Tensor,
+    n_batches: int,
+    B: int,
+    L1: int,
+    L2: int,
+    params: torch.Tensor,
+    grads: torch.Tensor,
+    exp_avg: torch.Tensor,
+    exp_avg_sq: torch.Tensor,
+    shadow: torch.Tensor,
+    dh1t: torch.Tensor,
+    xring: torch.Tensor,
+    h1pre: torch.Tensor,
+    act: torch.Tensor,
+    stats: Optional[torch.Tensor] = None,
+    advance_step: bool = True,
+    lr: float = 1e-3,
+    betas: Tuple[float, float] = (0.9, 0.999),
+    eps: float = 1e-8,
+    weight_decay: float = 0.0,
+    grad_scale: float = 1.0,
+    lr_tensor: Optional[torch.Tensor] = None,
+    adamw: bool = False,
+    stamps: Optional[torch.Tensor] = None,
+) -> None:
+    """One v3 launch (GPU only).  ``kind``: MLP3_STEP (head + fused tail, world size 1),
+    MLP3_HEAD / MLP3_TAIL_GRAD (gradients, before the allreduce), MLP3_TAIL_ADAM
+    (Adam with ``grad_scale`` + next-step layer-1 partial, after it), MLP3_PRIME
+    (layer-1 pre-activations of the pending batch from the current weights; the
+    caller zeroes ``h1pre`` first).  ``order`` is [2, n_batches * B]: the current
+    and the next epoch's sample order (counters[4] selects)."""
+    require().mlp3(
+        int(kind), x_u8, labels, order, counters, int(n_batches), int(B), int(L1), int(L2), params, grads, exp_avg,
+        exp_avg_sq, shadow, dh1t, xring, h1pre, act, stats, bool(advance_step), float(lr), float(betas[0]),
+        float(betas[1]), float(eps), float(weight_decay), float(grad_scale), lr_tensor, bool(adamw), stamps,
+    )
+
+
 def mlp_adam_(params, grads, exp_avg, exp_avg_sq, shadow, *, L1: int, L2: int, lr: float, step: torch.Tensor,
               betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, grad_scale: float = 1.0,
               adamw: bool = False, lr_tensor: Optional[torch.Tensor] = None) -> None:

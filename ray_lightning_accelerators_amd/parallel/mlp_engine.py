@@ -1,21 +1,27 @@
 """Data-parallel training engine for the MNIST classifier on the fused HIP step.
 
 This is the worker-side hot loop that ``RayAccelerator`` / ``HorovodRayAccelerator``
-run for ``MNISTClassifier`` (SURVEY.md §3.5 "one training step"), re-designed
-for MI355X instead of translating PL's DDP loop:
+run for ``MNISTClassifier`` (SURVEY.md §3.5 "one training step"; reference
+``ray_lightning/tests/utils.py`` / ``examples/ray_ddp_example.py`` model),
+re-designed for MI355X instead of translating PL's DDP loop:
 
 * the dataset is resident in HBM as uint8 (MNIST is uint8; ToTensor's /255 is
   fused into the kernel), and each rank's DistributedSampler shard for the
-  epoch is an index list on the device, so a step needs NO host->device copy;
+  current AND the next epoch is an index list on the device, so a step needs
+  NO host->device copy and no host sync at epoch boundaries;
 * parameters, gradients and Adam state are flat fp32 arenas; the whole model's
   gradient is ONE allreduce bucket (27,882 floats = 109 KiB at the default
   32/64 config -- far below the ~1 MiB where splitting pays on 7 xGMI links);
-* world size 1: ONE kernel launch per step (Adam fused into the gradient
-  epilogues); world size > 1: fused fwd/bwd kernel -> allreduce(SUM) -> fused
-  Adam with the 1/world average folded into ``grad_scale``;
-* the step's device work can be captured into a hipGraph (``use_graph``): the
-  batch cursor and step counter live on the device, so replays advance by
-  themselves and the host only re-shuffles ``order`` at epoch boundaries.
+* world size 1: TWO launches per step (csrc/mlp_step3.hip: head + 49-workgroup
+  tail; Adam fused into both, the next step's layer 1 computed by the tail);
+  world size > 1: head -> tail(grad) -> allreduce(SUM) -> tail(adam) with the
+  1/world average folded into ``grad_scale``;
+* the step's device work can be captured into a hipGraph (``capture``): batch
+  cursor, step counter, ring slot and epoch buffer live on the device, so
+  replays advance by themselves.
+
+On a CPU device the same engine runs the fp32 PyTorch reference step (the
+oracle of the GPU tests) with identical batch order and optimizer semantics.
 """
 from __future__ import annotations
 
@@ -61,14 +67,19 @@ class FusedMLPEngine:
         init_params: Optional[torch.Tensor] = None,
         stats_ring: int = 1024,
         seed: int = 0,
+        kernel_version: int = 3,
     ):
         if not fused_mlp.mlp_supported(layer_1, layer_2):
             raise ValueError(f"no fused kernel for layer sizes {layer_1}/{layer_2}")
+        if not 1 <= batch_size <= 256:
+            raise ValueError("fused MLP engine supports batch sizes 1..256")
         self.L1, self.L2, self.B = int(layer_1), int(layer_2), int(batch_size)
         self.lr, self.betas, self.eps, self.wd = float(lr), tuple(betas), float(eps), float(weight_decay)
         self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.native = self.device.type == "cuda"
         self.world_size, self.rank = int(world_size), int(rank)
         self.allreduce = allreduce
+        self.kernel_version = int(kernel_version)
         n = fused_mlp.mlp_param_count(self.L1, self.L2)
         if init_params is None:
             init_params = fused_mlp.init_mlp_params(self.L1, self.L2, torch.Generator().manual_seed(seed))
@@ -76,13 +87,14 @@ class FusedMLPEngine:
         self.grads = torch.zeros(n, device=self.device)
         self.exp_avg = torch.zeros(n, device=self.device)
         self.exp_avg_sq = torch.zeros(n, device=self.device)
-        self.counters = torch.zeros(3, dtype=torch.int64, device=self.device)
         self.lr_tensor = torch.full((1,), self.lr, device=self.device)
         lay = fused_mlp.mlp_shadow_layout(self.L1, self.L2)
         self.shadow = torch.zeros(lay["total"], dtype=torch.bfloat16, device=self.device)
-        self.dh1t = torch.zeros(self.L1 * ((self.B + 31) // 32 * 32), dtype=torch.bfloat16, device=self.device)
-        self.kernel_version = 2
-        self.refresh_shadow()
+        bufs = fused_mlp.mlp3_buffers(self.L1, self.L2, self.B, self.device)
+        # counters: [0] optimizer step, [1] next batch cursor, [2] last consumed cursor,
+        # [3] H1pre/X ring slot, [4] epoch buffer of `order` that [1] indexes
+        self.counters = bufs["counters"]
+        self.dh1t, self.xring, self.h1pre, self.act = bufs["dh1t"], bufs["xring"], bufs["h1pre"], bufs["act"]
         self.stats = torch.zeros(stats_ring, 4, device=self.device)
         self.seed = seed
         self.epoch = 0
@@ -90,8 +102,10 @@ class FusedMLPEngine:
         self.global_step = 0
         self._graph = None
         self._graph_steps = 0
+        self._primed = False
         self.x_u8 = self.labels = self.order = None
         self.n_batches = 0
+        self.refresh_shadow()
 
     # ------------------------------------------------------------------ data
     def set_data(self, images_u8: torch.Tensor, labels: torch.Tensor, shuffle: bool = True) -> None:
@@ -105,16 +119,21 @@ class FusedMLPEngine:
         self.n_batches = per_rank // self.B
         if self.n_batches < 1:
             raise ValueError("dataset shard smaller than one batch")
-        self.order = torch.empty(self.n_batches * self.B, dtype=torch.int64, device=self.device)
-        self._load_epoch(0)
+        self.order = torch.empty(2, self.n_batches * self.B, dtype=torch.int64, device=self.device)
+        self._fill_order(0)
+        self._fill_order(1)
+        self.counters[1:].zero_()
+        self.epoch = 0
+        self.step_in_epoch = 0
+        self._graph = None
+        self._primed = False
 
-    def _load_epoch(self, epoch: int) -> None:
+    def _fill_order(self, epoch: int) -> None:
+        """Write ``epoch``'s shard order into buffer ``epoch % 2`` (stream-ordered)."""
         idx = shard_indices(self.n_data, self.world_size, self.rank, epoch, self.seed, self.shuffle)
         idx = idx[: self.n_batches * self.B]
-        assert int(idx.max()) < self.n_data and int(idx.min()) >= 0  # kernel trusts indices
-        self.order.copy_(idx.to(self.device), non_blocking=True)
-        self.epoch = epoch
-        self.step_in_epoch = 0
+        assert int(idx.max()) < self.n_data and int(idx.min()) >= 0  # the kernels trust indices
+        self.order[epoch % 2].copy_(idx.to(self.device), non_blocking=True)
 
     # ------------------------------------------------------------ broadcast
     def broadcast_from(self, src: int = 0) -> None:
@@ -125,61 +144,115 @@ class FusedMLPEngine:
     def refresh_shadow(self) -> None:
         """Rebuild the bf16 weight shadows after the fp32 params changed outside a step."""
         fused_mlp.mlp_refresh_shadow(self.params, self.shadow, self.L1, self.L2)
+        self._primed = False
+
+    def load_params(self, flat: torch.Tensor) -> None:
+        with torch.no_grad():
+            self.params.copy_(flat.reshape(-1).to(self.params))
+        self.refresh_shadow()
 
     def set_lr(self, lr: float) -> None:
         self.lr = float(lr)
         self.lr_tensor.fill_(self.lr)
 
     # ----------------------------------------------------------------- step
+    def _kw3(self) -> dict:
+        return dict(x_u8=self.x_u8, labels=self.labels, order=self.order, counters=self.counters,
+                    n_batches=self.n_batches, B=self.B, L1=self.L1, L2=self.L2, params=self.params,
+                    grads=self.grads, exp_avg=self.exp_avg, exp_avg_sq=self.exp_avg_sq, shadow=self.shadow,
+                    dh1t=self.dh1t, xring=self.xring, h1pre=self.h1pre, act=self.act, lr=self.lr, betas=self.betas,
+                    eps=self.eps, weight_decay=self.wd, lr_tensor=self.lr_tensor)
+
+    def prime(self) -> None:
+        """Layer-1 pre-activations of the pending batch from the current weights."""
+        if self.native and self.kernel_version == 3:
+            self.h1pre.zero_()
+            fused_mlp.mlp3_launch(fused_mlp.MLP3_PRIME, **self._kw3())
+        self._primed = True
+
     def _device_step(self) -> None:
-        fused = self.world_size == 1
-        if self.kernel_version == 1:
-            fused_mlp.mlp_train_step(
-                self.params, self.grads, L1=self.L1, L2=self.L2, B=self.B, labels=self.labels,
-                x_u8=self.x_u8, order=self.order, counters=self.counters[:2], n_batches=self.n_batches,
-                exp_avg=self.exp_avg, exp_avg_sq=self.exp_avg_sq, stats=self.stats,
-                apply_adam=fused, advance_step=True, lr=self.lr, betas=self.betas, eps=self.eps,
-                weight_decay=self.wd, lr_tensor=self.lr_tensor,
-            )
+        if self.x_u8 is None:
+            raise RuntimeError("set_data() first")
+        if not self._primed:
+            self.prime()
+        if not self.native:
+            self._reference_step()
+        elif self.kernel_version == 3:
+            kw = self._kw3()
+            if self.world_size == 1:
+                fused_mlp.mlp3_launch(fused_mlp.MLP3_STEP, stats=self.stats, **kw)
+            else:
+                fused_mlp.mlp3_launch(fused_mlp.MLP3_HEAD, stats=self.stats, **kw)
+                fused_mlp.mlp3_launch(fused_mlp.MLP3_TAIL_GRAD, **kw)
+                if self.allreduce is not None:
+                    self.allreduce(self.grads)
+                fused_mlp.mlp3_launch(fused_mlp.MLP3_TAIL_ADAM, grad_scale=1.0 / self.world_size, **kw)
         else:
-            fused_mlp.mlp_train_step2(
-                self.params, self.grads, shadow=self.shadow, dh1t=self.dh1t, counters=self.counters, L1=self.L1,
-                L2=self.L2, B=self.B, labels=self.labels, x_u8=self.x_u8, order=self.order,
-                n_batches=self.n_batches, exp_avg=self.exp_avg, exp_avg_sq=self.exp_avg_sq, stats=self.stats,
-                apply_adam=fused, advance_step=True, lr=self.lr, betas=self.betas, eps=self.eps,
-                weight_decay=self.wd, lr_tensor=self.lr_tensor,
-            )
+            self._v2_step()
+
+    def _v2_step(self) -> None:
+        """Previous two-kernel step (kept for A/B comparisons); reads order buffer 0 only."""
+        fused = self.world_size == 1
+        fused_mlp.mlp_train_step2(
+            self.params, self.grads, shadow=self.shadow, dh1t=self.dh1t, counters=self.counters, L1=self.L1,
+            L2=self.L2, B=self.B, labels=self.labels, x_u8=self.x_u8, order=self.order[0],
+            n_batches=self.n_batches, exp_avg=self.exp_avg, exp_avg_sq=self.exp_avg_sq, stats=self.stats,
+            apply_adam=fused, advance_step=True, lr=self.lr, betas=self.betas, eps=self.eps,
+            weight_decay=self.wd, lr_tensor=self.lr_tensor,
+        )
         if not fused:
             if self.allreduce is not None:
                 self.allreduce(self.grads)
-            if self.kernel_version == 1:
-                fused_adam_(self.params, self.grads, self.exp_avg, self.exp_avg_sq, lr=self.lr,
-                            betas=self.betas, eps=self.eps, weight_decay=self.wd,
-                            grad_scale=1.0 / self.world_size, step=self.counters[0:1],
-                            lr_tensor=self.lr_tensor)
-            else:
-                fused_mlp.mlp_adam_(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.shadow, L1=self.L1,
-                                    L2=self.L2, lr=self.lr, step=self.counters[0:1], betas=self.betas, eps=self.eps,
-                                    weight_decay=self.wd, grad_scale=1.0 / self.world_size,
-                                    lr_tensor=self.lr_tensor)
+            fused_mlp.mlp_adam_(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.shadow, L1=self.L1,
+                                L2=self.L2, lr=self.lr, step=self.counters[0:1], betas=self.betas, eps=self.eps,
+                                weight_decay=self.wd, grad_scale=1.0 / self.world_size, lr_tensor=self.lr_tensor)
+
+    def _reference_step(self) -> None:
+        """fp32 PyTorch step with the device kernels' batch / counter semantics."""
+        c = self.counters
+        cursor, ob = int(c[1]), int(c[4])
+        fused = self.world_size == 1
+        fused_mlp.mlp_train_step(
+            self.params, self.grads, L1=self.L1, L2=self.L2, B=self.B, labels=self.labels, x_u8=self.x_u8,
+            order=self.order[ob], counters=c[:2], n_batches=self.n_batches, exp_avg=self.exp_avg,
+            exp_avg_sq=self.exp_avg_sq, stats=self.stats, apply_adam=fused, advance_step=True, lr=self.lr,
+            betas=self.betas, eps=self.eps, weight_decay=self.wd, lr_tensor=self.lr_tensor,
+        )
+        c[2] = cursor
+        c[3] = int(c[3]) ^ 1
+        if cursor + 1 >= self.n_batches:
+            c[4] = ob ^ 1
+        if not fused:
+            if self.allreduce is not None:
+                self.allreduce(self.grads)
+            fused_adam_(self.params, self.grads, self.exp_avg, self.exp_avg_sq, lr=self.lr, betas=self.betas,
+                        eps=self.eps, weight_decay=self.wd, grad_scale=1.0 / self.world_size,
+                        step=self.counters[0:1], lr_tensor=self.lr_tensor)
 
     def _advance_host(self, n: int) -> None:
         self.global_step += n
         self.step_in_epoch += n
         if self.step_in_epoch >= self.n_batches:
-            # the device cursor wrapped to 0 in the same step; load the next shuffle
-            self._load_epoch(self.epoch + 1)
+            # the device switched to the other order buffer in the same step
+            self.epoch += 1
+            self.step_in_epoch = 0
+            if self.kernel_version == 3 or not self.native:
+                # buffer (epoch + 1) % 2 was last read by the step just enqueued
+                self._fill_order(self.epoch + 1)
+            else:
+                idx = shard_indices(self.n_data, self.world_size, self.rank, self.epoch, self.seed, self.shuffle)
+                self.order[0].copy_(idx[: self.n_batches * self.B].to(self.device), non_blocking=True)
 
     def steps_to_epoch_end(self) -> int:
         return self.n_batches - self.step_in_epoch
 
     def capture(self, steps_per_graph: int = 1) -> bool:
         """Capture ``steps_per_graph`` consecutive steps into one hipGraph."""
-        if self.device.type != "cuda":
+        if not self.native:
             return False
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        # warm the allocator / RCCL outside capture (does a real step; keep counters consistent)
+        # warm the allocator / RCCL outside capture (a real step; keeps counters consistent)
         with torch.cuda.stream(s):
             self._device_step()
         torch.cuda.current_stream().wait_stream(s)
@@ -196,9 +269,14 @@ class FusedMLPEngine:
         self._graph_steps = steps_per_graph
         return True
 
+    def _graph_ok(self, remaining: int) -> bool:
+        k = self._graph_steps
+        return (self._graph is not None and self._primed and remaining >= k
+                and self.step_in_epoch + k <= self.n_batches)
+
     def step(self) -> None:
         """Run one (or ``steps_per_graph`` when captured) optimizer step(s)."""
-        if self._graph is not None and self.step_in_epoch + self._graph_steps <= self.n_batches:
+        if self._graph_ok(self._graph_steps):
             self._graph.replay()
             self._advance_host(self._graph_steps)
             return
@@ -208,14 +286,14 @@ class FusedMLPEngine:
     def run(self, n_steps: int) -> None:
         done = 0
         while done < n_steps:
-            k = self._graph_steps if self._graph is not None else 1
-            if self._graph is not None and (n_steps - done < k or self.step_in_epoch + k > self.n_batches):
+            if self._graph_ok(n_steps - done):
+                self._graph.replay()
+                self._advance_host(self._graph_steps)
+                done += self._graph_steps
+            else:
                 self._device_step()
                 self._advance_host(1)
                 done += 1
-                continue
-            self.step()
-            done += k
 
     # --------------------------------------------------------------- export
     def recent_stats(self, n: int = 1) -> torch.Tensor:
