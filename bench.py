@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--graph-steps", type=int, default=8,
                     help="optimizer steps per captured hipGraph (native); 0 = eager launches")
     ap.add_argument("--n-data", type=int, default=55000)
+    ap.add_argument("--comm", choices=["auto", "xgmi", "rccl", "torch"], default="auto",
+                    help="N>1 gradient allreduce: native xGMI one-shot (auto/xgmi), native RCCL, or c10d")
     return ap.parse_args()
 
 
@@ -81,11 +83,25 @@ def barrier(world):
 def make_native(args, world, rank, dev, x, y):
     from ray_lightning_accelerators_amd.parallel.mlp_engine import FusedMLPEngine
 
-    def allreduce(t):
-        dist.all_reduce(t)
+    allreduce = None
+    if world > 1:
+        # native data plane: xGMI one-shot push allreduce for the gradient bucket
+        # (validated at setup, RCCL fallback), enqueued on the step's stream so
+        # the hipGraph captures it with the step kernels
+        from ray_lightning_accelerators_amd.parallel.comm import get_native_comm
+
+        comm = None
+        if args.comm != "torch":
+            comm = get_native_comm(use_xgmi=args.comm in ("auto", "xgmi"), use_rccl=True)
+        if comm is not None:
+            if rank == 0:
+                print(comm.describe(), file=sys.stderr, flush=True)
+            allreduce = comm.allreduce_
+        else:
+            allreduce = dist.all_reduce
 
     eng = FusedMLPEngine(args.layer_1, args.layer_2, args.batch_size, lr=args.lr, device=dev,
-                         world_size=world, rank=rank, allreduce=allreduce if world > 1 else None, seed=0)
+                         world_size=world, rank=rank, allreduce=allreduce, seed=0)
     eng.set_data(x, y, shuffle=True)
     eng.broadcast_from(0)
     if args.graph_steps > 0:
@@ -160,6 +176,11 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        from ray_lightning_accelerators_amd.parallel.comm import get_native_comm
+
+        comm = get_native_comm(create=False)
+        if comm is not None:
+            comm.check()  # a timed-out xGMI poll or RCCL async error invalidates the run
     samples = args.steps * args.batch_size * world
     value = samples / elapsed
     loss = last_loss()

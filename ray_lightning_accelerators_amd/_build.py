@@ -51,7 +51,7 @@ EXTENSIONS = {
         "libs": [],
     },
     "_comm": {
-        "hip": ["comm/ipc_allreduce.hip"],
+        "hip": ["comm/xgmi_allreduce.hip", "comm/pack.hip"],
         "cpp": ["comm/comm_bindings.cpp", "comm/communicator.cpp", "comm/fusion_engine.cpp"],
         "torch": True,
         "libs": ["rccl"],

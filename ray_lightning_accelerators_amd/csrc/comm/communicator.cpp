@@ -1,0 +1,207 @@
+#include "comm/communicator.h"
+
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+
+namespace rla {
+namespace comm {
+namespace {
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+ncclDataType_t to_nccl(DType d) {
+  switch (d) {
+    case DType::kF32: return ncclFloat32;
+    case DType::kBF16: return ncclBfloat16;
+    case DType::kF16: return ncclFloat16;
+    case DType::kI32: return ncclInt32;
+    case DType::kI64: return ncclInt64;
+    case DType::kU8: return ncclUint8;
+    case DType::kF64: return ncclFloat64;
+  }
+  throw std::runtime_error("unsupported dtype");
+}
+
+ncclRedOp_t to_nccl(RedOp o) {
+  switch (o) {
+    case RedOp::kSum: return ncclSum;
+    case RedOp::kMax: return ncclMax;
+    case RedOp::kMin: return ncclMin;
+    case RedOp::kProd: return ncclProd;
+  }
+  throw std::runtime_error("unsupported reduction");
+}
+
+}  // namespace
+
+Communicator::Communicator(int rank, int world, int device) : rank_(rank), world_(world), device_(device) {
+  if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("bad rank / world size");
+}
+
+Communicator::~Communicator() {
+  stop_ = true;
+  if (watchdog_.joinable()) watchdog_.join();
+  hipSetDevice(device_);
+  if (comm_ && !aborted_.exchange(true)) {
+    if (state_.load() != 0) ncclCommAbort(comm_);
+    else ncclCommDestroy(comm_);
+  }
+  comm_ = nullptr;
+  for (int r = 0; r < world_ && r < kXgmiMaxRanks; ++r)
+    if (peers_[r] && peers_[r] != region_) hipIpcCloseMemHandle(peers_[r]);
+  if (region_) hipFree(region_);
+  if (gen_) hipFree(gen_);
+  if (err_host_) hipHostFree(err_host_);
+}
+
+std::string Communicator::unique_id() {
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) throw std::runtime_error("ncclGetUniqueId failed");
+  return std::string(id.internal, NCCL_UNIQUE_ID_BYTES);
+}
+
+void Communicator::check_rccl(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) {
+    state_ = 2;
+    std::lock_guard<std::mutex> g(mu_);
+    message_ = std::string(what) + ": " + ncclGetErrorString(r);
+    throw std::runtime_error(message_);
+  }
+}
+
+void Communicator::init_rccl(const std::string& uid) {
+  if (uid.size() != NCCL_UNIQUE_ID_BYTES) throw std::runtime_error("bad RCCL unique id");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  ncclUniqueId id;
+  std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
+  check_rccl(ncclCommInitRank(&comm_, world_, id, rank_), "ncclCommInitRank");
+}
+
+void Communicator::allreduce(void* buf, int64_t count, DType dt, RedOp op, hipStream_t s) {
+  if (!comm_ || aborted_.load()) throw std::runtime_error("RCCL communicator not initialised or aborted");
+  check_rccl(ncclAllReduce(buf, buf, (size_t)count, to_nccl(dt), to_nccl(op), comm_, s), "ncclAllReduce");
+}
+
+void Communicator::broadcast(void* buf, int64_t count, DType dt, int root, hipStream_t s) {
+  if (!comm_ || aborted_.load()) throw std::runtime_error("RCCL communicator not initialised or aborted");
+  check_rccl(ncclBroadcast(buf, buf, (size_t)count, to_nccl(dt), root, comm_, s), "ncclBroadcast");
+}
+
+void Communicator::allgather(const void* in, void* out, int64_t count, DType dt, hipStream_t s) {
+  if (!comm_ || aborted_.load()) throw std::runtime_error("RCCL communicator not initialised or aborted");
+  check_rccl(ncclAllGather(in, out, (size_t)count, to_nccl(dt), comm_, s), "ncclAllGather");
+}
+
+void Communicator::reduce_scatter(const void* in, void* out, int64_t count, DType dt, RedOp op, hipStream_t s) {
+  if (!comm_ || aborted_.load()) throw std::runtime_error("RCCL communicator not initialised or aborted");
+  check_rccl(ncclReduceScatter(in, out, (size_t)count, to_nccl(dt), to_nccl(op), comm_, s), "ncclReduceScatter");
+}
+
+std::string Communicator::xgmi_handle(int64_t capacity_floats) {
+  if (world_ > kXgmiMaxRanks) throw std::runtime_error("xGMI one-shot supports at most 8 ranks");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  if (!region_) {
+    slot_stride_ = (capacity_floats + 63) / 64 * 64;
+    const int64_t bytes = xgmi_region_bytes(slot_stride_);
+    hip_check(hipExtMallocWithFlags(reinterpret_cast<void**>(&region_), (size_t)bytes, hipDeviceMallocUncached),
+              "hipExtMallocWithFlags(uncached)");
+    hip_check(hipMemset(region_, 0, (size_t)bytes), "hipMemset(region)");
+    hip_check(hipMalloc(reinterpret_cast<void**>(&gen_), kXgmiMaxBlocks * sizeof(uint32_t)), "hipMalloc(gen)");
+    hip_check(hipMemset(gen_, 0, kXgmiMaxBlocks * sizeof(uint32_t)), "hipMemset(gen)");
+    hip_check(hipHostMalloc(reinterpret_cast<void**>(&err_host_), sizeof(int), hipHostMallocMapped),
+              "hipHostMalloc(error)");
+    *err_host_ = 0;
+    hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_dev_), err_host_, 0), "hipHostGetDevicePointer");
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  }
+  hipIpcMemHandle_t h;
+  hip_check(hipIpcGetMemHandle(&h, region_), "hipIpcGetMemHandle");
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void Communicator::xgmi_open(const std::vector<std::string>& handles) {
+  if ((int)handles.size() != world_) throw std::runtime_error("need one IPC handle per rank");
+  if (!region_) throw std::runtime_error("xgmi_handle() first");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  for (int r = 0; r < world_; ++r) {
+    if (r == rank_) {
+      peers_[r] = region_;
+      continue;
+    }
+    if (handles[r].size() != sizeof(hipIpcMemHandle_t)) throw std::runtime_error("bad IPC handle size");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handles[r].data(), sizeof(h));
+    void* p = nullptr;
+    hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    peers_[r] = static_cast<char*>(p);
+  }
+  xgmi_ready_ = true;
+}
+
+void Communicator::allreduce_xgmi(float* buf, int64_t count, hipStream_t s) {
+  if (!xgmi_ready_) throw std::runtime_error("xGMI peers not open");
+  if (count > slot_stride_ || count % 4 != 0) throw std::runtime_error("xGMI one-shot: count exceeds capacity or % 4");
+  XgmiLaunch l{};
+  l.x = buf;
+  l.n = count;
+  for (int r = 0; r < world_; ++r) l.regions[r] = peers_[r];
+  l.rank = rank_;
+  l.world = world_;
+  l.gen = gen_;
+  l.error = err_dev_;
+  l.slot_stride = slot_stride_;
+  l.spin_limit = spin_limit_;
+  if (launch_xgmi_oneshot(l, s) != 0) throw std::runtime_error("xGMI one-shot launch failed");
+}
+
+int Communicator::error_state() {
+  if (state_.load() == 0 && err_host_ && __atomic_load_n(err_host_, __ATOMIC_ACQUIRE) != 0) {
+    state_ = 1;
+    std::lock_guard<std::mutex> g(mu_);
+    message_ = "xGMI allreduce: peer flag poll timed out (a rank is dead or desynchronised)";
+  }
+  if (state_.load() == 0 && comm_) {
+    ncclResult_t async = ncclSuccess;
+    if (ncclCommGetAsyncError(comm_, &async) == ncclSuccess && async != ncclSuccess && async != ncclInProgress) {
+      state_ = 2;
+      std::lock_guard<std::mutex> g(mu_);
+      message_ = std::string("RCCL async error: ") + ncclGetErrorString(async);
+    }
+  }
+  return state_.load();
+}
+
+std::string Communicator::error_message() {
+  std::lock_guard<std::mutex> g(mu_);
+  return message_;
+}
+
+void Communicator::watchdog_loop(int period_ms) {
+  while (!stop_.load()) {
+    if (error_state() != 0) {
+      // a dead peer must not hang the job: abort RCCL so pending collectives return
+      if (comm_ && state_.load() == 2 && !aborted_.exchange(true)) ncclCommAbort(comm_);
+      return;
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(period_ms));
+  }
+}
+
+void Communicator::start_watchdog(int period_ms) {
+  if (watchdog_.joinable()) return;
+  stop_ = false;
+  watchdog_ = std::thread([this, period_ms] { watchdog_loop(period_ms); });
+}
+
+void Communicator::abort() {
+  stop_ = true;
+  if (watchdog_.joinable() && watchdog_.get_id() != std::this_thread::get_id()) watchdog_.join();
+  if (comm_ && !aborted_.exchange(true)) ncclCommAbort(comm_);
+  state_ = 3;
+}
+
+}  // namespace comm
+}  // namespace rla

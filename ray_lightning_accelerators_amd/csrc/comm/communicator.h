@@ -1,0 +1,93 @@
+// Native communicator of one rank: an RCCL communicator (bootstrapped from a
+// unique id the Python side exchanges over the rendezvous store) plus the xGMI
+// peer map used by the one-shot allreduce, and a watchdog thread.
+//
+// MI355X-first split of the data plane:
+//   * small buckets (<= xgmi capacity, e.g. the 110-530 KiB MNIST gradient):
+//     one-shot push allreduce through IPC-mapped peer memory -- latency is two
+//     xGMI crossings instead of RCCL's protocol rounds;
+//   * everything else: RCCL (ring/tree over the same links).
+// Every collective is enqueued on the caller's stream, so it can be captured
+// into a hipGraph together with the step's compute kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdint.h>
+
+#include <atomic>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "comm/xgmi.h"
+
+namespace rla {
+namespace comm {
+
+enum class RedOp : int { kSum = 0, kMax = 1, kMin = 2, kProd = 3 };
+enum class DType : int { kF32 = 0, kBF16 = 1, kF16 = 2, kI32 = 3, kI64 = 4, kU8 = 5, kF64 = 6 };
+
+class Communicator {
+ public:
+  Communicator(int rank, int world, int device);
+  ~Communicator();
+  Communicator(const Communicator&) = delete;
+  Communicator& operator=(const Communicator&) = delete;
+
+  static std::string unique_id();  // rank 0 creates, everyone passes it to init_rccl
+
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+
+  // ---- RCCL ----
+  void init_rccl(const std::string& uid);
+  bool has_rccl() const { return comm_ != nullptr; }
+  void allreduce(void* buf, int64_t count, DType dt, RedOp op, hipStream_t s);
+  void broadcast(void* buf, int64_t count, DType dt, int root, hipStream_t s);
+  void allgather(const void* in, void* out, int64_t count, DType dt, hipStream_t s);
+  void reduce_scatter(const void* in, void* out, int64_t count, DType dt, RedOp op, hipStream_t s);
+
+  // ---- xGMI one-shot ----
+  // Allocates this rank's uncached region (capacity floats per peer slot) and
+  // returns its IPC handle bytes; open_peers maps every other rank's region.
+  std::string xgmi_handle(int64_t capacity_floats);
+  void xgmi_open(const std::vector<std::string>& handles);
+  bool has_xgmi() const { return xgmi_ready_; }
+  int64_t xgmi_capacity() const { return slot_stride_; }
+  void allreduce_xgmi(float* buf, int64_t count, hipStream_t s);
+  void set_spin_limit(int64_t n) { spin_limit_ = n; }
+
+  // ---- health ----
+  // 0 healthy; 1 xGMI poll timed out; 2 RCCL async error; 3 aborted
+  int error_state();
+  std::string error_message();
+  void start_watchdog(int period_ms);
+  void abort();
+
+ private:
+  void check_rccl(ncclResult_t r, const char* what);
+  void watchdog_loop(int period_ms);
+
+  int rank_, world_, device_;
+  ncclComm_t comm_ = nullptr;
+  // xGMI
+  char* region_ = nullptr;                 // own region (uncached device memory)
+  char* peers_[kXgmiMaxRanks] = {};        // mapped regions (own included)
+  bool xgmi_ready_ = false;
+  int64_t slot_stride_ = 0;
+  uint32_t* gen_ = nullptr;                // device: per-block generations
+  int* err_host_ = nullptr;                // host-mapped error word
+  int* err_dev_ = nullptr;
+  int64_t spin_limit_ = int64_t(1) << 24;  // ~2-4 s of s_sleep polling
+  // health
+  std::atomic<int> state_{0};
+  std::string message_;
+  std::mutex mu_;
+  std::thread watchdog_;
+  std::atomic<bool> stop_{false};
+  std::atomic<bool> aborted_{false};
+};
+
+}  // namespace comm
+}  // namespace rla

@@ -1,0 +1,222 @@
+"""Per-rank native communicator (C++ ``_comm`` extension) on top of torch.distributed.
+
+``torch.distributed`` (gloo or RCCL process group) is only the bootstrap and
+the CPU data plane here.  On MI355X the data plane is the C++ engine
+(csrc/comm/): an RCCL communicator created from a unique id that rank 0
+broadcasts over the existing group, plus the xGMI one-shot allreduce over
+IPC-mapped peer memory for buckets up to ``xgmi_bytes`` (the MNIST gradient is
+one 110-530 KiB bucket -- RCCL's ring protocol latency, not link bandwidth,
+dominates there).  Reference behaviour being replaced: c10d ProcessGroupNCCL
+(``ray_ddp.py:227-237`` init_ddp_connection) and the DDP/Horovod allreduce
+(SURVEY.md §2.7 X3/X11).
+
+Safety rules (a wrong collective can hang 8 GPUs):
+* the xGMI path is enabled only if EVERY rank set it up and a validation
+  allreduce produced the exact expected sum on every rank (agreed with a
+  MIN-allreduce over the bootstrap group) -- otherwise all ranks use RCCL;
+* the device-side flag polls are bounded: a dead peer sets an error word
+  instead of hanging the GPU; ``check()`` raises it, a watchdog thread aborts
+  RCCL on async errors.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+
+_mod = None
+_mod_err: Optional[BaseException] = None
+
+
+def native_comm_module():
+    global _mod, _mod_err
+    if _mod is None and _mod_err is None:
+        try:
+            _mod = importlib.import_module("ray_lightning_accelerators_amd._comm")
+        except BaseException as e:  # noqa: BLE001
+            _mod_err = e
+    return _mod
+
+
+def _agree(flag: bool, group=None) -> bool:
+    """True only if every rank passes True (MIN over the bootstrap group)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return bool(flag)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
+        else torch.device("cpu")
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
+
+
+class NativeCommunicator:
+    """RCCL + xGMI communicator of this rank.  ``allreduce_(t)`` sums in place on
+    the current stream (graph-capturable); ``average=True`` divides by world."""
+
+    def __init__(self, group=None, device: Optional[int] = None, use_rccl: bool = True,
+                 use_xgmi: bool = True, xgmi_bytes: int = 2 << 20, validate: bool = True,
+                 spin_limit: Optional[int] = None, watchdog_ms: int = 100):
+        mod = native_comm_module()
+        if mod is None:
+            raise RuntimeError(f"native comm extension (_comm) unavailable: {_mod_err!r}")
+        self.group = group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        self._c = mod.Communicator(self.rank, self.world, self.device)
+        self.rccl = False
+        self.xgmi = False
+        if use_rccl and os.environ.get("RLA_DISABLE_RCCL", "0") != "1":
+            uid = [mod.Communicator.unique_id() if self.rank == 0 else None]
+            if self.world > 1:
+                dist.broadcast_object_list(uid, src=0, group=group)
+            ok = True
+            try:
+                self._c.init_rccl(uid[0])
+            except RuntimeError:
+                ok = False
+            self.rccl = _agree(ok, group)
+        if use_xgmi and 1 < self.world <= mod.XGMI_MAX_RANKS and os.environ.get("RLA_DISABLE_XGMI", "0") != "1":
+            self._setup_xgmi(xgmi_bytes, validate, spin_limit, group)
+        if watchdog_ms > 0:
+            self._c.start_watchdog(watchdog_ms)
+
+    # ------------------------------------------------------------- xGMI
+    def _setup_xgmi(self, xgmi_bytes, validate, spin_limit, group):
+        ok = True
+        handle = b""
+        try:
+            handle = self._c.xgmi_handle(max(4, xgmi_bytes // 4))
+        except RuntimeError:
+            ok = False
+        handles = [None] * self.world
+        dist.all_gather_object(handles, handle if ok else b"", group=group)
+        ok = ok and all(h for h in handles)
+        if ok:
+            try:
+                self._c.xgmi_open(handles)
+            except RuntimeError:
+                ok = False
+        if not _agree(ok, group):
+            return
+        if spin_limit is not None:
+            self._c.set_spin_limit(int(spin_limit))
+        if validate:
+            ok = self._validate_xgmi(group)
+            if not _agree(ok, group):
+                return
+        self.xgmi = True
+
+    def _validate_xgmi(self, group) -> bool:
+        n = 4096 + 4
+        dev = torch.device("cuda", self.device)
+        ok = True
+        for it in range(3):  # both receive-area parities + one reuse
+            x = (torch.arange(n, device=dev, dtype=torch.float32) % 97) * (self.rank + 1) + it
+            want = (torch.arange(n, device=dev, dtype=torch.float32) % 97) * (self.world * (self.world + 1) / 2) \
+                + it * self.world
+            torch.cuda.synchronize(dev)
+            dist.barrier(group=group)
+            try:
+                self._c.allreduce_xgmi(x)
+                torch.cuda.synchronize(dev)
+            except RuntimeError:
+                return False
+            ok = ok and self._c.error_state() == 0 and bool(torch.equal(x, want))
+        return ok
+
+    @property
+    def xgmi_capacity(self) -> int:
+        return int(self._c.xgmi_capacity) if self.xgmi else 0
+
+    # ------------------------------------------------------- collectives
+    def allreduce_(self, t: torch.Tensor, average: bool = False) -> torch.Tensor:
+        if self.world == 1:
+            return t
+        if (self.xgmi and t.dtype == torch.float32 and t.is_contiguous() and t.numel() % 4 == 0
+                and t.numel() <= self.xgmi_capacity):
+            self._c.allreduce_xgmi(t)
+        elif self.rccl:
+            self._c.allreduce(t, 0)
+        else:
+            dist.all_reduce(t, group=self.group)
+        if average:
+            t.div_(self.world)
+        return t
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.world == 1:
+            return t
+        if self.rccl:
+            self._c.broadcast(t, src)
+        else:
+            dist.broadcast(t, src, group=self.group)
+        return t
+
+    def allgather(self, t: torch.Tensor) -> torch.Tensor:
+        out = torch.empty(self.world * t.numel(), dtype=t.dtype, device=t.device)
+        if self.rccl:
+            self._c.allgather(t.contiguous(), out)
+        else:
+            dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        return out.view(self.world, *t.shape)
+
+    def reduce_scatter(self, t: torch.Tensor) -> torch.Tensor:
+        assert t.numel() % self.world == 0
+        out = torch.empty(t.numel() // self.world, dtype=t.dtype, device=t.device)
+        if self.rccl:
+            self._c.reduce_scatter(t.contiguous(), out, 0)
+        else:
+            dist.reduce_scatter_tensor(out, t.contiguous(), group=self.group)
+        return out
+
+    def fusion_engine(self, fusion_bytes: int = 8 << 20):
+        return native_comm_module().FusionEngine(self._c, int(fusion_bytes), self.device)
+
+    # ------------------------------------------------------------ health
+    def check(self) -> None:
+        st = self._c.error_state()
+        if st != 0:
+            raise RuntimeError(f"collective failure on rank {self.rank}: {self._c.error_message()}")
+
+    def abort(self) -> None:
+        self._c.abort()
+
+    def describe(self) -> str:
+        return (f"NativeCommunicator(rank={self.rank}, world={self.world}, rccl={self.rccl}, "
+                f"xgmi={self.xgmi}, xgmi_capacity={self.xgmi_capacity})")
+
+
+_default: Optional[NativeCommunicator] = None
+
+
+def get_native_comm(create: bool = True, **kw) -> Optional[NativeCommunicator]:
+    """Process-wide communicator for the default group (GPU ranks only)."""
+    global _default
+    if _default is None and create and torch.cuda.is_available() and dist.is_initialized() \
+            and native_comm_module() is not None:
+        _default = NativeCommunicator(**kw)
+    return _default
+
+
+def reset_native_comm() -> None:
+    global _default
+    _default = None
+
+
+def make_allreduce(average: bool = False, prefer_native: bool = True) -> Callable[[torch.Tensor], torch.Tensor]:
+    """Best available in-place SUM (or mean) allreduce for this process."""
+    comm = get_native_comm() if prefer_native else None
+    if comm is not None:
+        return lambda t: comm.allreduce_(t, average=average)
+
+    def _f(t):
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(t)
+            if average:
+                t.div_(dist.get_world_size())
+        return t
+    return _f
