@@ -68,6 +68,15 @@ def setup_dist(args):
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    if os.environ.get("RLA_BENCH_SHARE_GPU") == "1":
+        # rehearsal of the N>1 path on a 1-GPU box: every rank on device 0, gloo
+        # bootstrap, native xGMI-protocol allreduce through same-device IPC
+        # (throughput is meaningless in this mode; correctness is the point)
+        local = 0
+        torch.cuda.set_device(0)
+        if world > 1:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        return world, rank, local
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", rank=rank, world_size=world,
@@ -92,7 +101,8 @@ def make_native(args, world, rank, dev, x, y):
 
         comm = None
         if args.comm != "torch":
-            comm = get_native_comm(use_xgmi=args.comm in ("auto", "xgmi"), use_rccl=True)
+            comm = get_native_comm(use_xgmi=args.comm in ("auto", "xgmi"),
+                                   use_rccl=dist.get_backend() == "nccl")
         if comm is not None:
             if rank == 0:
                 print(comm.describe(), file=sys.stderr, flush=True)
@@ -173,7 +183,8 @@ def main():
     barrier(world)
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         from ray_lightning_accelerators_amd.parallel.comm import get_native_comm

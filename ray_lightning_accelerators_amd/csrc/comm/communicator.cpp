@@ -143,7 +143,8 @@ void Communicator::xgmi_open(const std::vector<std::string>& handles) {
 
 void Communicator::allreduce_xgmi(float* buf, int64_t count, hipStream_t s) {
   if (!xgmi_ready_) throw std::runtime_error("xGMI peers not open");
-  if (count > slot_stride_ || count % 4 != 0) throw std::runtime_error("xGMI one-shot: count exceeds capacity or % 4");
+  if (count > slot_stride_ || (reinterpret_cast<uintptr_t>(buf) & 15))
+    throw std::runtime_error("xGMI one-shot: count exceeds capacity or buffer not 16-byte aligned");
   XgmiLaunch l{};
   l.x = buf;
   l.n = count;

@@ -112,7 +112,8 @@ void FusionEngine::execute(Batch& b) {
   for (auto& r : b.reqs) hip_check(hipStreamWaitEvent(stream_, r.ready, 0), "hipStreamWaitEvent(ready)");
   const bool xgmi = comm_->has_xgmi();
   auto reduce = [&](float* p, int64_t n) {
-    if (xgmi && n % 4 == 0 && n <= comm_->xgmi_capacity()) comm_->allreduce_xgmi(p, n, stream_);
+    if (xgmi && (reinterpret_cast<uintptr_t>(p) & 15) == 0 && n <= comm_->xgmi_capacity())
+      comm_->allreduce_xgmi(p, n, stream_);
     else comm_->allreduce(p, n, DType::kF32, RedOp::kSum, stream_);
   };
   auto copy = [&](bool in, float scale_override, bool use_req_scale) {

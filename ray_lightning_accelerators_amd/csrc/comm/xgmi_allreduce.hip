@@ -65,10 +65,12 @@ __global__ __launch_bounds__(kThreads) void oneshot_allreduce_kernel(Args a) {
   const uint32_t gen = sh_gen;
   const int slot = gen & 1u;
 
-  // this block's slice, in float4 units (the host guarantees n % 4 == 0)
+  // this block's slice in float4 units; the last block also owns the n % 4 tail
   const int64_t n4 = a.n / 4;
   const int64_t per = (n4 + nblk - 1) / nblk;
   const int64_t lo = blk * per, hi = lo + per < n4 ? lo + per : n4;
+  const bool tail_owner = blk == nblk - 1;
+  const int64_t t0 = n4 * 4;
   const v4f* src = reinterpret_cast<const v4f*>(a.x);
 
   // 1. push my slice into every rank's receive area [slot][my rank]
@@ -78,6 +80,11 @@ __global__ __launch_bounds__(kThreads) void oneshot_allreduce_kernel(Args a) {
       v4f* dst = reinterpret_cast<v4f*>(data_ptr(a.regions[r], slot, a.rank, a.slot_stride));
       __builtin_nontemporal_store(v, dst + i);
     }
+  }
+  if (tail_owner && t0 + tid < a.n) {
+    const float v = a.x[t0 + tid];
+    for (int r = 0; r < a.world; ++r)
+      __builtin_nontemporal_store(v, data_ptr(a.regions[r], slot, a.rank, a.slot_stride) + t0 + tid);
   }
   __threadfence_system();
   __syncthreads();
@@ -115,6 +122,12 @@ __global__ __launch_bounds__(kThreads) void oneshot_allreduce_kernel(Args a) {
     }
     reinterpret_cast<v4f*>(a.x)[i] = s;
   }
+  if (tail_owner && t0 + tid < a.n) {
+    float s = 0.f;
+    for (int r = 0; r < a.world; ++r)
+      s += __builtin_nontemporal_load(data_ptr(a.regions[a.rank], slot, r, a.slot_stride) + t0 + tid);
+    a.x[t0 + tid] = s;
+  }
   if (tid == 0) a.gen[blk] = gen;
 }
 
@@ -129,7 +142,8 @@ int xgmi_blocks_for(int64_t n) {
 }
 
 int launch_xgmi_oneshot(const XgmiLaunch& l, hipStream_t stream) {
-  if (l.world < 1 || l.world > kXgmiMaxRanks || l.n % 4 != 0 || l.n > l.slot_stride) return -1;
+  if (l.world < 1 || l.world > kXgmiMaxRanks || l.n > l.slot_stride || (reinterpret_cast<uintptr_t>(l.x) & 15))
+    return -1;
   Args a{};
   a.x = l.x;
   a.n = l.n;

@@ -136,11 +136,15 @@ class NativeCommunicator:
     def allreduce_(self, t: torch.Tensor, average: bool = False) -> torch.Tensor:
         if self.world == 1:
             return t
-        if (self.xgmi and t.dtype == torch.float32 and t.is_contiguous() and t.numel() % 4 == 0
+        if (self.xgmi and t.dtype == torch.float32 and t.is_contiguous() and t.data_ptr() % 16 == 0
                 and t.numel() <= self.xgmi_capacity):
             self._c.allreduce_xgmi(t)
         elif self.rccl:
             self._c.allreduce(t, 0)
+        elif t.is_cuda and dist.get_backend(self.group) == "gloo":
+            tmp = t.cpu()  # CPU bootstrap group: not graph-capturable, correctness path only
+            dist.all_reduce(tmp, group=self.group)
+            t.copy_(tmp)
         else:
             dist.all_reduce(t, group=self.group)
         if average:

@@ -138,7 +138,12 @@ class FusedMLPEngine:
     # ------------------------------------------------------------ broadcast
     def broadcast_from(self, src: int = 0) -> None:
         if self.world_size > 1 and dist.is_initialized():
-            dist.broadcast(self.params, src)
+            if self.params.is_cuda and dist.get_backend() == "gloo":  # CPU bootstrap group
+                tmp = self.params.cpu()
+                dist.broadcast(tmp, src)
+                self.params.copy_(tmp)
+            else:
+                dist.broadcast(self.params, src)
         self.refresh_shadow()
 
     def refresh_shadow(self) -> None:

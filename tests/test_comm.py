@@ -73,7 +73,7 @@ def _gpu_worker(rank, world, port, q, mode):
         res = {"xgmi": comm.xgmi}
         dev = torch.device("cuda", 0)
         if mode == "allreduce":
-            for n in (4, 1024, 27884, 262144):
+            for n in (1, 3, 4, 1024, 27882, 27884, 262143):  # incl. the 32/64 MLP arena (27,882)
                 x = torch.arange(n, device=dev, dtype=torch.float32) * 0.5 + rank
                 comm.allreduce_(x)
                 torch.cuda.synchronize()
