@@ -151,6 +151,31 @@ class FusedMNISTStep:
         self._u8 = None
         self._order = None
         self._epoch_key = None
+        self.eng = None  # v3 pipelined engine (resident-data mode), bound to the arena
+        self._allreduce = None
+        if self.world > 1:
+            from ..parallel.comm import make_allreduce
+
+            self._allreduce = make_allreduce()
+
+    def _engine(self, B: int):
+        """The v3 engine over the Trainer's arena views (module params stay the masters)."""
+        if self.eng is not None and self.eng.B == B:
+            return self.eng
+        from ..parallel.mlp_engine import FusedMLPEngine
+
+        g = self.opt.param_groups[0]
+        bufs = dict(params=self.arena.data[: self.np], grads=self.arena.grad[: self.np],
+                    exp_avg=self.gs.m[: self.np], exp_avg_sq=self.gs.v[: self.np])
+        eng = FusedMLPEngine(self.L1, self.L2, B, lr=float(g["lr"]), betas=tuple(g["betas"]), eps=g["eps"],
+                             weight_decay=g["weight_decay"], device=self.dev, world_size=self.world,
+                             rank=self.trainer.global_rank, allreduce=self._allreduce, buffers=bufs,
+                             stats_ring=self.stats.size(0))
+        eng.counters[0] = self.gs.step
+        eng.lr_tensor = self.lr_tensor  # LR schedulers update one device scalar
+        eng.attach_dataset(self._u8, self._labels)
+        self.eng = eng
+        return eng
 
     # ---------------------------------------------------------- data plane
     def make_epoch_batches(self, dl, n_batches: int):
@@ -171,10 +196,9 @@ class FusedMNISTStep:
         if nb <= 0:
             return None
         assert int(order.max()) < self._u8.size(0)
-        self._order = order[: nb * B].to(self.dev)
         self._B = B
         self._nb = nb
-        self.counters[1] = 0
+        self._engine(B).begin_epoch(order[: nb * B], nb)
         return [("__rla_resident__", i) for i in range(nb)]
 
     def _sync_lr(self) -> None:
@@ -197,34 +221,40 @@ class FusedMNISTStep:
         kw = dict(L1=self.L1, L2=self.L2, exp_avg=m, exp_avg_sq=v, stats=self.stats, apply_adam=fused,
                   advance_step=True, lr=self.lr_val, betas=(b1, b2), eps=g["eps"], weight_decay=g["weight_decay"],
                   lr_tensor=self.lr_tensor, counters=self.counters)
+        stats = self.stats
         if isinstance(batch, tuple) and len(batch) == 2 and batch[0] == "__rla_resident__":
-            fused_mlp.mlp_train_step(p, gr, B=self._B, labels=self._labels, x_u8=self._u8, order=self._order,
-                                     n_batches=self._nb, **kw)
+            # v3 pipelined step (head + tail [+ allreduce + tail-adam]); Adam is the engine's
+            eng = self.eng
+            eng.lr, eng.betas, eng.eps, eng.wd = self.lr_val, (b1, b2), g["eps"], g["weight_decay"]
+            eng.step()
+            stats = eng.stats
+            fused = True  # optimizer already applied
         else:
+            if self.eng is not None:
+                self.counters[0] = self.gs.step
             x, y = batch
             x = x.to(self.dev, non_blocking=True).reshape(x.size(0), -1).float().contiguous()
             y = y.to(self.dev, non_blocking=True).long().contiguous()
             fused_mlp.mlp_train_step(p, gr, B=x.size(0), labels=y, x_f32=x, **kw)
         if not fused:
-            sync = self.acc.sync
-            if sync is not None:
-                import torch.distributed as dist
-
-                dist.all_reduce(self.arena.grad[: self.np])
+            if self._allreduce is not None and self.acc.sync is not None:
+                self._allreduce(self.arena.grad[: self.np])
             from ..ops.optim import fused_adam_
 
             fused_adam_(p, gr, m, v, lr=self.lr_val, betas=(b1, b2), eps=g["eps"], weight_decay=g["weight_decay"],
                         grad_scale=1.0 / self.world, step=self.counters[0:1], lr_tensor=self.lr_tensor)
+        if self.eng is not None and stats is self.stats:
+            self.eng.refresh_shadow()  # params moved outside the engine
         self.gs.step += 1
         for q in g["params"]:
             st = self.opt.state.get(q)
             if st is not None and "step" in st:
                 st["step"].fill_(float(self.gs.step))
-        slot = (self.gs.step - 1) % self.stats.size(0)
-        loss = self.stats[slot, 0]
+        slot = (self.gs.step - 1) % stats.size(0)
+        loss = stats[slot, 0]
         # metrics (device tensors; no host sync here)
         self.model.log("ptl/train_loss", loss)
-        self.model.log("ptl/train_accuracy", self.stats[slot, 1] / self.stats[slot, 2].clamp(min=1))
+        self.model.log("ptl/train_accuracy", stats[slot, 1] / stats[slot, 2].clamp(min=1))
         self.trainer.callback_metrics["loss"] = loss
         return {"loss": loss}
 
@@ -235,3 +265,6 @@ class FusedMNISTStep:
     def load_params_from_module(self) -> None:
         self.arena.rebind_all()
         self.counters[0] = self.gs.step
+        if self.eng is not None:
+            self.eng.counters[0] = self.gs.step
+            self.eng.refresh_shadow()

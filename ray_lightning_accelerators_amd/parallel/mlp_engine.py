@@ -68,7 +68,11 @@ class FusedMLPEngine:
         stats_ring: int = 1024,
         seed: int = 0,
         kernel_version: int = 3,
+        buffers: Optional[Dict[str, torch.Tensor]] = None,
     ):
+        """``buffers``: optional external fp32 tensors ``params`` / ``grads`` /
+        ``exp_avg`` / ``exp_avg_sq`` (e.g. views of a Trainer's parameter arena,
+        so the nn.Module parameters stay the engine's master weights)."""
         if not fused_mlp.mlp_supported(layer_1, layer_2):
             raise ValueError(f"no fused kernel for layer sizes {layer_1}/{layer_2}")
         if not 1 <= batch_size <= 256:
@@ -81,12 +85,20 @@ class FusedMLPEngine:
         self.allreduce = allreduce
         self.kernel_version = int(kernel_version)
         n = fused_mlp.mlp_param_count(self.L1, self.L2)
-        if init_params is None:
-            init_params = fused_mlp.init_mlp_params(self.L1, self.L2, torch.Generator().manual_seed(seed))
-        self.params = init_params.detach().to(self.device, torch.float32).contiguous().clone()
-        self.grads = torch.zeros(n, device=self.device)
-        self.exp_avg = torch.zeros(n, device=self.device)
-        self.exp_avg_sq = torch.zeros(n, device=self.device)
+        if buffers is not None:
+            for k in ("params", "grads", "exp_avg", "exp_avg_sq"):
+                t = buffers[k]
+                assert t.dtype == torch.float32 and t.is_contiguous() and t.numel() == n and t.device == self.device, k
+                setattr(self, k, t)
+        else:
+            if init_params is None:
+                init_params = fused_mlp.init_mlp_params(self.L1, self.L2, torch.Generator().manual_seed(seed))
+            self.params = init_params.detach().to(self.device, torch.float32).contiguous().clone()
+            # padded to 4 floats: the xGMI one-shot allreduce moves 16-byte vectors
+            self._grads_padded = torch.zeros((n + 3) // 4 * 4, device=self.device)
+            self.grads = self._grads_padded[:n]
+            self.exp_avg = torch.zeros(n, device=self.device)
+            self.exp_avg_sq = torch.zeros(n, device=self.device)
         self.lr_tensor = torch.full((1,), self.lr, device=self.device)
         lay = fused_mlp.mlp_shadow_layout(self.L1, self.L2)
         self.shadow = torch.zeros(lay["total"], dtype=torch.bfloat16, device=self.device)
@@ -103,9 +115,43 @@ class FusedMLPEngine:
         self._graph = None
         self._graph_steps = 0
         self._primed = False
+        self._host_epochs = False
         self.x_u8 = self.labels = self.order = None
         self.n_batches = 0
         self.refresh_shadow()
+
+    @property
+    def comm_buffer(self) -> torch.Tensor:
+        """The gradient bucket handed to the allreduce (16-byte padded when owned)."""
+        return getattr(self, "_grads_padded", self.grads)
+
+    # ------------------------------------------------- host-driven epochs
+    def attach_dataset(self, images_u8: torch.Tensor, labels: torch.Tensor) -> None:
+        """Trainer mode: the dataset is resident, the host supplies each epoch's order."""
+        assert images_u8.dtype == torch.uint8 and images_u8.dim() == 2 and images_u8.size(1) == 784
+        self.x_u8 = images_u8.to(self.device).contiguous()
+        self.labels = labels.to(self.device, torch.int64).contiguous()
+        self.n_data = self.x_u8.size(0)
+        self._host_epochs = True
+
+    def begin_epoch(self, order: torch.Tensor, n_batches: int) -> None:
+        """Load one epoch's sample order ([n_batches * B] indices) and re-prime.
+
+        Both order buffers get the same list, so the last step's look-ahead
+        gather wraps into valid indices; the next ``begin_epoch`` re-primes."""
+        order = order.reshape(-1)[: n_batches * self.B]
+        assert n_batches >= 1 and order.numel() == n_batches * self.B
+        assert int(order.max()) < self.n_data and int(order.min()) >= 0  # the kernels trust indices
+        if self.order is None or self.order.size(1) != order.numel():
+            self.order = torch.empty(2, order.numel(), dtype=torch.int64, device=self.device)
+        dev_order = order.to(self.device)
+        self.order[0].copy_(dev_order)
+        self.order[1].copy_(dev_order)
+        self.n_batches = int(n_batches)
+        self.counters[1:].zero_()
+        self.step_in_epoch = 0
+        self._graph = None
+        self._primed = False
 
     # ------------------------------------------------------------------ data
     def set_data(self, images_u8: torch.Tensor, labels: torch.Tensor, shuffle: bool = True) -> None:
@@ -190,7 +236,7 @@ class FusedMLPEngine:
                 fused_mlp.mlp3_launch(fused_mlp.MLP3_HEAD, stats=self.stats, **kw)
                 fused_mlp.mlp3_launch(fused_mlp.MLP3_TAIL_GRAD, **kw)
                 if self.allreduce is not None:
-                    self.allreduce(self.grads)
+                    self.allreduce(self.comm_buffer)
                 fused_mlp.mlp3_launch(fused_mlp.MLP3_TAIL_ADAM, grad_scale=1.0 / self.world_size, **kw)
         else:
             self._v2_step()
@@ -207,7 +253,7 @@ class FusedMLPEngine:
         )
         if not fused:
             if self.allreduce is not None:
-                self.allreduce(self.grads)
+                self.allreduce(self.comm_buffer)
             fused_mlp.mlp_adam_(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.shadow, L1=self.L1,
                                 L2=self.L2, lr=self.lr, step=self.counters[0:1], betas=self.betas, eps=self.eps,
                                 weight_decay=self.wd, grad_scale=1.0 / self.world_size, lr_tensor=self.lr_tensor)
@@ -229,7 +275,7 @@ class FusedMLPEngine:
             c[4] = ob ^ 1
         if not fused:
             if self.allreduce is not None:
-                self.allreduce(self.grads)
+                self.allreduce(self.comm_buffer)
             fused_adam_(self.params, self.grads, self.exp_avg, self.exp_avg_sq, lr=self.lr, betas=self.betas,
                         eps=self.eps, weight_decay=self.wd, grad_scale=1.0 / self.world_size,
                         step=self.counters[0:1], lr_tensor=self.lr_tensor)
@@ -241,6 +287,8 @@ class FusedMLPEngine:
             # the device switched to the other order buffer in the same step
             self.epoch += 1
             self.step_in_epoch = 0
+            if self._host_epochs:
+                return  # the host calls begin_epoch()
             if self.kernel_version == 3 or not self.native:
                 # buffer (epoch + 1) % 2 was last read by the step just enqueued
                 self._fill_order(self.epoch + 1)

@@ -53,6 +53,7 @@ class CheckGPUCallback(Callback):
 class CheckFusedCallback(Callback):
     def on_train_end(self, trainer, pl_module):
         assert trainer._fused is not None, "fused HIP step was not used"
+        assert trainer._fused.eng is not None, "resident-data v3 engine was not used"
         from ray_lightning_accelerators_amd import ops
 
         ops.require()

@@ -129,7 +129,7 @@ def test_mlp3_pipeline_grads_vs_emulation(L1, L2, B):
         torch.cuda.synchronize()
         idx = shard_indices(n_data, 2, 0, epoch, 0, True)[cur * B:(cur + 1) * B]
         emu = _emulate_bf16_grads(p_before, x[idx].float() / 255.0, y[idx], L1, L2, B)
-        err = _rel(captured[-1], emu)
+        err = _rel(captured[-1][: emu.numel()], emu)  # the comm bucket is padded to 16 B
         assert err < 2e-2, (s, err)
     assert eng.counters[0].item() == steps
 
@@ -217,4 +217,4 @@ def test_mlp3_reload_params_reprimes():
     torch.cuda.synchronize()
     idx = shard_indices(256, 2, 0, epoch, 0, True)[cur * 32:(cur + 1) * 32]
     emu = _emulate_bf16_grads(newp, x[idx].float() / 255.0, y[idx], 32, 64, 32)
-    assert _rel(captured[-1], emu) < 2e-2
+    assert _rel(captured[-1][: emu.numel()], emu) < 2e-2
