@@ -128,6 +128,9 @@ class RayAccelerator(DataParallelAccelerator):
             return
 
         def shutdown_remote():
+            from ..parallel.comm import reset_native_comm
+
+            reset_native_comm()  # RCCL comm destroy + IPC unmap before the group goes
             if dist.is_available() and dist.is_initialized():
                 dist.destroy_process_group()
             if torch.cuda.is_available():

@@ -91,6 +91,9 @@ def init(comm=None, process_sets=None) -> None:
 
 
 def shutdown() -> None:
+    from ..parallel.comm import reset_native_comm
+
+    reset_native_comm()
     if dist.is_initialized():
         dist.destroy_process_group()
     _state.clear()

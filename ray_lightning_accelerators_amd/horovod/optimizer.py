@@ -65,6 +65,17 @@ class _FusionState:
         self.passes = 0
         self.skip = False
         self.synchronized = False
+        # GPU ranks: the C++ fusion engine (csrc/comm/fusion_engine.cpp) packs,
+        # allreduces (xGMI one-shot / RCCL) and unpacks each bucket on its own
+        # thread + comm stream.  Created here, where every rank is in lock-step.
+        self.engine = None
+        if (size() > 1 and compression is Compression.none and params and params[0].is_cuda
+                and os.environ.get("RLA_HVD_NATIVE", "1") == "1"):
+            from ..parallel.comm import get_native_comm
+
+            comm = get_native_comm()
+            if comm is not None:
+                self.engine = comm.fusion_engine(threshold_bytes)
         self.hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
 
     def _add(self, ps):
@@ -110,6 +121,13 @@ class _FusionState:
         for p in b.params:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
+        if self.engine is not None and all(p.grad.dtype == torch.float32 and p.grad.is_contiguous()
+                                           for p in b.params):
+            scale = 1.0 / size() if self.op == Average else 1.0
+            b.handles = [(self.engine.submit(p.grad, scale), p.grad) for p in b.params]
+            self.engine.flush()  # one fusion batch per bucket: identical on every rank
+            b.work = "native"
+            return
         flat = self._contiguous_grads(b) if self.compression is Compression.none else None
         if flat is not None:
             b.buf = flat
@@ -138,6 +156,12 @@ class _FusionState:
         scale = 1.0 / size() if self.op == Average else 1.0
         for b in self.buckets:
             if b.work is None:
+                continue
+            if b.work == "native":  # averaged in the engine's unpack
+                for h, g in b.handles:
+                    self.engine.wait(h, g)
+                b.handles = []
+                b.work = None
                 continue
             b.work.wait()
             b.work = None

@@ -240,6 +240,12 @@ class DataParallelAccelerator(Accelerator):
             self.sync = None
             return
         fused = any(getattr(o, "_rla_fused", False) for o in self.trainer.optimizers)
+        if self.arena.data.is_cuda and os.environ.get("RLA_NATIVE_COMM", "1") == "1":
+            # bring the native data plane (RCCL + validated xGMI one-shot) up on every
+            # rank together, before backward hooks start issuing collectives
+            from ..parallel.comm import get_native_comm
+
+            get_native_comm()
         self.sync = GradSynchronizer(
             model, self.arena, bucket_cap_mb=self.bucket_cap_mb or default_bucket_cap_mb(),
             grad_dtype=self.grad_dtype, average_in_optimizer=fused)

@@ -67,6 +67,7 @@ class NativeCommunicator:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.device = torch.cuda.current_device() if device is None else int(device)
         self._c = mod.Communicator(self.rank, self.world, self.device)
+        self._stream = None
         self.rccl = False
         self.xgmi = False
         if use_rccl and os.environ.get("RLA_DISABLE_RCCL", "0") != "1":
@@ -151,6 +152,21 @@ class NativeCommunicator:
             t.div_(self.world)
         return t
 
+    def allreduce_async(self, t: torch.Tensor, average: bool = False) -> "_StreamWork":
+        """Allreduce on this communicator's high-priority side stream, ordered after
+        the current stream's pending work (the gradient producer); ``wait()``
+        makes the then-current stream wait for it -- DDP bucket overlap."""
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(device=t.device, priority=-1)
+        cur = torch.cuda.current_stream(t.device)
+        self._stream.wait_stream(cur)
+        with torch.cuda.stream(self._stream):
+            self.allreduce_(t, average=average)
+        ev = torch.cuda.Event()
+        ev.record(self._stream)
+        t.record_stream(self._stream)
+        return _StreamWork(ev)
+
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.world == 1:
             return t
@@ -194,6 +210,20 @@ class NativeCommunicator:
                 f"xgmi={self.xgmi}, xgmi_capacity={self.xgmi_capacity})")
 
 
+class _StreamWork:
+    """c10d-Work-like handle of a side-stream collective."""
+
+    def __init__(self, event: "torch.cuda.Event"):
+        self.event = event
+
+    def wait(self) -> bool:
+        torch.cuda.current_stream().wait_event(self.event)
+        return True
+
+    def is_completed(self) -> bool:
+        return self.event.query()
+
+
 _default: Optional[NativeCommunicator] = None
 
 
@@ -201,14 +231,29 @@ def get_native_comm(create: bool = True, **kw) -> Optional[NativeCommunicator]:
     """Process-wide communicator for the default group (GPU ranks only)."""
     global _default
     if _default is None and create and torch.cuda.is_available() and dist.is_initialized() \
-            and native_comm_module() is not None:
+            and os.environ.get("RLA_NATIVE_COMM", "1") == "1" and native_comm_module() is not None:
         _default = NativeCommunicator(**kw)
     return _default
 
 
 def reset_native_comm() -> None:
     global _default
-    _default = None
+    if _default is not None:
+        try:
+            torch.cuda.synchronize(_default.device)
+        except Exception:  # noqa: BLE001 - teardown must not raise
+            pass
+    _default = None  # the C++ destructor destroys the RCCL comm and unmaps peers
+
+
+def allreduce_async(t: torch.Tensor, group=None):
+    """Async SUM allreduce: native side-stream collective for GPU tensors on the
+    default group when the native engine is up, else c10d's async work."""
+    if group is None and t.is_cuda:
+        comm = get_native_comm()
+        if comm is not None:
+            return comm.allreduce_async(t)
+    return dist.all_reduce(t, group=group, async_op=True)
 
 
 def make_allreduce(average: bool = False, prefer_native: bool = True) -> Callable[[torch.Tensor], torch.Tensor]:

@@ -31,6 +31,7 @@ from torch import nn
 
 from .. import ops
 from .arena import ParamArena
+from .comm import allreduce_async
 
 
 class Bucket:
@@ -69,6 +70,7 @@ class GradSynchronizer:
                 cur, cur_elems = [], 0
         if cur:
             self._close_bucket(cur)
+        self._next = 0
         self._hooks = []
         for i, p in enumerate(arena.params):
             self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
@@ -98,6 +100,7 @@ class GradSynchronizer:
             b.pending = len(b.param_ids)
             b.work = None
         self._started = True
+        self._next = 0
         if self.broadcast_buffers and self.world > 1 and sync:
             for buf in self.module.buffers():
                 dist.broadcast(buf, 0, group=self.pg)
@@ -111,9 +114,16 @@ class GradSynchronizer:
             b = self.buckets[self.param_bucket[i]]
             b.pending -= 1
             if b.pending == 0:
-                self._launch(b)
+                self._launch_ready()
 
         return hook
+
+    def _launch_ready(self) -> None:
+        # strictly in bucket order: every rank must issue its collectives in the
+        # same sequence (c10d and the xGMI generation counters both pair calls by order)
+        while self._next < len(self.buckets) and self.buckets[self._next].pending <= 0:
+            self._launch(self.buckets[self._next])
+            self._next += 1
 
     def _launch(self, b: Bucket) -> None:
         grad = self.arena.grad[b.start:b.end]
@@ -123,7 +133,8 @@ class GradSynchronizer:
             ops.multi_copy([(grad, b.comm_buf)])
             b.work = dist.all_reduce(b.comm_buf, group=self.pg, async_op=True)
         else:
-            b.work = dist.all_reduce(grad, group=self.pg, async_op=True)
+            # GPU: the native engine's side stream (xGMI one-shot / RCCL); CPU: gloo
+            b.work = allreduce_async(grad, group=self.pg)
 
     def finish(self) -> None:
         """Wait for every bucket; launch the ones unused parameters left incomplete."""
@@ -131,8 +142,8 @@ class GradSynchronizer:
             self._started = False
             return
         for b in self.buckets:
-            if b.work is None:
-                self._launch(b)
+            b.pending = 0  # unused parameters: their buckets go out now, still in order
+        self._launch_ready()
         for b in self.buckets:
             b.work.wait()
             if b.comm_buf is not None and self.grad_dtype == "bf16":
@@ -141,6 +152,7 @@ class GradSynchronizer:
         if not self.average_in_optimizer:
             ops.scale_(self.arena.grad, 1.0 / self.world)
         self._started = False
+        self._next = 0
 
     @property
     def grad_scale(self) -> float:

@@ -105,6 +105,45 @@ def _gpu_worker(rank, world, port, q, mode):
             res["batches"] = eng.batches_executed
             res["fingerprint"] = eng.fingerprint
             eng.drain()
+        elif mode == "hvd":
+            # Horovod DistributedOptimizer on the C++ fusion engine vs. a local reference
+            os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), HOROVOD_FUSION_THRESHOLD="4096")
+            import ray_lightning_accelerators_amd.horovod as hvd
+            from ray_lightning_accelerators_amd.parallel import comm as comm_mod
+
+            comm_mod._default = comm  # the group is up; reuse this rank's communicator
+            hvd.init()
+
+            def make():
+                torch.manual_seed(0)
+                return torch.nn.Sequential(torch.nn.Linear(64, 33), torch.nn.ReLU(),
+                                           torch.nn.Linear(33, 5)).to(dev)
+
+            def data(r):
+                g = torch.Generator().manual_seed(100 + r)
+                return torch.randn(16, 64, generator=g).to(dev), torch.randn(16, 5, generator=g).to(dev)
+
+            model = make()
+            opt = hvd.DistributedOptimizer(torch.optim.SGD(model.parameters(), lr=0.1),
+                                           named_parameters=model.named_parameters())
+            res["native_engine"] = opt._hvd_state.engine is not None
+            for _ in range(3):
+                x, y = data(rank)
+                opt.zero_grad()
+                torch.nn.functional.mse_loss(model(x), y).backward()
+                opt.step()
+            ref = make()
+            ropt = torch.optim.SGD(ref.parameters(), lr=0.1)
+            for _ in range(3):
+                ropt.zero_grad()
+                for r in range(world):
+                    x, y = data(r)
+                    (torch.nn.functional.mse_loss(ref(x), y) / world).backward()
+                ropt.step()
+            torch.cuda.synchronize()
+            res["match"] = all(bool(torch.allclose(a, b, atol=1e-5)) for a, b in
+                               zip(model.parameters(), ref.parameters()))
+            res["batches"] = opt._hvd_state.engine.batches_executed if res["native_engine"] else 0
         elif mode == "timeout":
             x = torch.ones(1024, device=dev)
             if rank == 0:
@@ -156,6 +195,14 @@ def test_fusion_engine_two_ranks():
     assert out[0]["fused"] and out[1]["fused"], out
     assert out[0]["fingerprint"] == out[1]["fingerprint"]
     assert out[0]["batches"] >= 2  # 64 KiB threshold splits the 6 requests
+
+
+@gpu
+def test_horovod_optimizer_on_native_fusion_engine():
+    out = _run_gpu("hvd")
+    for r, res in out.items():
+        assert res["native_engine"] and res["match"], (r, res)
+        assert res["batches"] >= 6  # 3 steps x >= 2 fusion buckets (4 KiB threshold)
 
 
 @gpu
