@@ -40,25 +40,37 @@ if ROOT not in sys.path:
 METRIC = "samples/sec (whole node) + DDP scaling eff, MNISTClassifier at 1/2/4/8 workers"
 # Our measured stock-PyTorch numbers on MI355X (BASELINE.md "Our MI355X measurements");
 # the reference itself publishes none.  None => vs_baseline is null.
+RESNET_METRIC = "images/sec (whole node), ResNet-50 synthetic ImageNet 224px"
 STOCK_BASELINE = {1: 53015.0}  # --impl torch, 1x MI355X (profiles/r1_first/bench_torch.jsonl)
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2000)
-    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=None, help="default 2000 (mnist) / 20 (resnet50)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 200 (mnist) / 5 (resnet50)")
+    ap.add_argument("--model", choices=["mnist", "resnet50"], default="mnist",
+                    help="mnist: the BASELINE headline (MNISTClassifier); resnet50: config 5 (bucket stress)")
     ap.add_argument("--impl", choices=["native", "torch"], default="native")
-    ap.add_argument("--batch-size", type=int, default=32)
+    ap.add_argument("--batch-size", type=int, default=None, help="per GPU; default 32 (mnist) / 128 (resnet50)")
     ap.add_argument("--layer-1", type=int, default=32)
     ap.add_argument("--layer-2", type=int, default=64)
     ap.add_argument("--lr", type=float, default=1e-1)
     ap.add_argument("--graph-steps", type=int, default=8,
                     help="optimizer steps per captured hipGraph (native); 0 = eager launches")
     ap.add_argument("--n-data", type=int, default=55000)
+    ap.add_argument("--bucket-mb", type=float, default=8.0, help="resnet50 DDP bucket cap (MiB)")
     ap.add_argument("--comm", choices=["auto", "xgmi", "rccl", "torch"], default="auto",
                     help="N>1 gradient allreduce: native xGMI one-shot (auto/xgmi), native RCCL, or c10d")
-    return ap.parse_args()
+    args = ap.parse_args()
+    rn = args.model == "resnet50"
+    if args.steps is None:
+        args.steps = 20 if rn else 2000
+    if args.warmup is None:
+        args.warmup = 5 if rn else 200
+    if args.batch_size is None:
+        args.batch_size = 128 if rn else 32
+    return args
 
 
 def setup_dist(args):
@@ -164,14 +176,82 @@ def make_torch(args, world, rank, dev, x, y):
     return run, (lambda: float(state["loss"].item()))
 
 
+def make_resnet(args, world, rank, dev, x, y):
+    """ResNet-50, synthetic ImageNet batch resident on the GPU, bf16 autocast, NHWC.
+
+    native: flat fp32 arena + ONE fused SGD-momentum launch, bucketed in-place
+    allreduce on the native comm engine's side stream overlapping backward.
+    torch:  torch DDP (RCCL) + torch.optim.SGD(foreach)."""
+    import torch.nn.functional as F
+    from ray_lightning_accelerators_amd.models.resnet import resnet50
+
+    torch.manual_seed(0)
+    model = resnet50().to(dev).to(memory_format=torch.channels_last)
+    B = args.batch_size
+    g = torch.Generator(device=dev).manual_seed(rank)
+    xb = torch.randn(B, 3, 224, 224, device=dev, generator=g).contiguous(memory_format=torch.channels_last)
+    yb = torch.randint(0, 1000, (B,), device=dev, generator=g)
+    state = {}
+    if args.impl == "native":
+        from ray_lightning_accelerators_amd.parallel.arena import ParamArena
+        from ray_lightning_accelerators_amd.parallel.ddp import GradSynchronizer
+        from ray_lightning_accelerators_amd.parallel.fused_optim import fuse_optimizer
+
+        arena = ParamArena(model)
+        sync = None
+        if world > 1:
+            from ray_lightning_accelerators_amd.parallel.comm import get_native_comm
+
+            get_native_comm()
+            sync = GradSynchronizer(model, arena, bucket_cap_mb=args.bucket_mb, average_in_optimizer=True)
+            sync.broadcast_parameters(0)
+        opt = fuse_optimizer(torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5), arena,
+                             grad_scale_fn=(lambda: sync.grad_scale) if sync is not None else None)
+
+        def run(n):
+            for _ in range(n):
+                if sync is not None:
+                    sync.prepare_for_backward()
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    out = model(xb)
+                loss = F.cross_entropy(out.float(), yb)
+                loss.backward()
+                if sync is not None:
+                    sync.finish()
+                opt.step()
+                opt.zero_grad()
+                state["loss"] = loss
+    else:
+        m = model
+        if world > 1:
+            m = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index])
+        opt = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5, foreach=True)
+
+        def run(n):
+            for _ in range(n):
+                opt.zero_grad(set_to_none=True)
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    out = m(xb)
+                loss = F.cross_entropy(out.float(), yb)
+                loss.backward()
+                opt.step()
+                state["loss"] = loss
+
+    return run, (lambda: float(state["loss"].item()))
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist(args)
     dev = torch.device("cuda", local)
     from ray_lightning_accelerators_amd.models.data import synthetic_mnist
 
-    x, y = synthetic_mnist(args.n_data, seed=0)
-    maker = make_native if args.impl == "native" else make_torch
+    if args.model == "resnet50":
+        x = y = None
+        maker = make_resnet
+    else:
+        x, y = synthetic_mnist(args.n_data, seed=0)
+        maker = make_native if args.impl == "native" else make_torch
     run, last_loss = maker(args, world, rank, dev, x, y)
 
     run(args.warmup)
@@ -196,11 +276,12 @@ def main():
     value = samples / elapsed
     loss = last_loss()
     if rank == 0:
-        base = STOCK_BASELINE.get(world)
+        rn = args.model == "resnet50"
+        base = None if rn else STOCK_BASELINE.get(world)
         out = {
-            "metric": METRIC,
+            "metric": RESNET_METRIC if rn else METRIC,
             "value": round(value, 1),
-            "unit": "samples/s",
+            "unit": "images/s" if rn else "samples/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -211,13 +292,13 @@ def main():
             "dtype": "bf16",
             "data": "synthetic",
             "config": {
-                "model": f"MNISTClassifier(784-{args.layer_1}-{args.layer_2}-10)",
+                "model": "ResNet-50" if rn else f"MNISTClassifier(784-{args.layer_1}-{args.layer_2}-10)",
                 "global_batch": args.batch_size * world,
                 "per_gpu_batch": args.batch_size,
                 "seq_len": None,
                 "parallelism": f"dp{world}",
                 "impl": args.impl,
-                "optimizer": "Adam",
+                "optimizer": "SGD-momentum" if rn else "Adam",
                 "final_train_loss": round(loss, 4),
             },
         }

@@ -1,0 +1,149 @@
+"""ResNet-50 on synthetic ImageNet (BASELINE.json config 5: "ResNet-50
+synthetic-ImageNet RayAccelerator num_workers=8 bf16 -- large-grad-bucket xGMI
+allreduce stress").  Not part of the reference tree (SURVEY.md §2.8 last row);
+torchvision is not available in this image, so the architecture is defined
+here (He et al. 2015, v1.5: stride on the 3x3 conv of each bottleneck).
+
+MI355X choices:
+  * channels_last activations + bf16 autocast: MIOpen's NHWC bf16 convolutions
+    run on the MFMA units; BatchNorm statistics stay fp32;
+  * parameters live in a flat fp32 arena (25,557,032 params = 97.5 MiB), the
+    SGD-momentum step is ONE fused HIP launch over it, and DDP buckets are
+    arena slices allreduced in place (no flatten/unflatten copies);
+  * zero-init of the last BN gamma in each residual branch (standard large-batch
+    recipe) is optional (``zero_init_residual``).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+from torch.utils.data import Dataset
+
+from ..lightning import LightningModule
+
+
+def _conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
+    return nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+
+
+def _conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
+    return nn.Conv2d(cin, cout, 1, stride, bias=False)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin: int, width: int, stride: int = 1, downsample: Optional[nn.Module] = None):
+        super().__init__()
+        cout = width * self.expansion
+        self.conv1 = _conv1x1(cin, width)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = _conv3x3(width, width, stride)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = _conv1x1(width, cout)
+        self.bn3 = nn.BatchNorm2d(cout)
+        self.downsample = downsample
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        out = F.relu(self.bn1(self.conv1(x)), inplace=True)
+        out = F.relu(self.bn2(self.conv2(out)), inplace=True)
+        out = self.bn3(self.conv3(out))
+        return F.relu(out + idt, inplace=True)
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers: List[int], num_classes: int = 1000, zero_init_residual: bool = False):
+        super().__init__()
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.maxpool = nn.MaxPool2d(3, 2, 1)
+        self.layer1 = self._make(64, layers[0])
+        self.layer2 = self._make(128, layers[1], 2)
+        self.layer3 = self._make(256, layers[2], 2)
+        self.layer4 = self._make(512, layers[3], 2)
+        self.fc = nn.Linear(512 * Bottleneck.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        if zero_init_residual:
+            for m in self.modules():
+                if isinstance(m, Bottleneck):
+                    nn.init.zeros_(m.bn3.weight)
+
+    def _make(self, width: int, blocks: int, stride: int = 1) -> nn.Sequential:
+        down = None
+        cout = width * Bottleneck.expansion
+        if stride != 1 or self.inplanes != cout:
+            down = nn.Sequential(_conv1x1(self.inplanes, cout, stride), nn.BatchNorm2d(cout))
+        layers = [Bottleneck(self.inplanes, width, stride, down)]
+        self.inplanes = cout
+        layers += [Bottleneck(cout, width) for _ in range(1, blocks)]
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        x = self.maxpool(F.relu(self.bn1(self.conv1(x)), inplace=True))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
+
+
+def resnet50(num_classes: int = 1000, zero_init_residual: bool = False) -> ResNet:
+    return ResNet([3, 4, 6, 3], num_classes, zero_init_residual)
+
+
+RESNET50_PARAMS = 25_557_032
+
+
+class SyntheticImageNet(Dataset):
+    """Random images / labels of ImageNet shape, generated per index (deterministic)."""
+
+    def __init__(self, length: int = 1281, image_size: int = 224, num_classes: int = 1000, seed: int = 0):
+        self.length, self.size, self.nc, self.seed = length, image_size, num_classes, seed
+
+    def __len__(self) -> int:
+        return self.length
+
+    def __getitem__(self, i: int):
+        g = torch.Generator().manual_seed(self.seed * 1_000_003 + i)
+        return torch.randn(3, self.size, self.size, generator=g), int(torch.randint(0, self.nc, (1,), generator=g))
+
+
+class LightningResNet50(LightningModule):
+    """ResNet-50 as a LightningModule (SGD momentum, cross-entropy), for RayAccelerator runs."""
+
+    def __init__(self, config: Optional[dict] = None):
+        super().__init__()
+        cfg = dict(lr=0.1, momentum=0.9, weight_decay=5e-5, batch_size=64, num_classes=1000,
+                   image_size=224, n_train=512)
+        cfg.update(config or {})
+        self.cfg = cfg
+        self.model = resnet50(cfg["num_classes"])
+
+    def forward(self, x):
+        return self.model(x)
+
+    def training_step(self, batch, batch_idx):
+        x, y = batch
+        x = x.contiguous(memory_format=torch.channels_last)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=x.is_cuda):
+            logits = self(x)
+        loss = F.cross_entropy(logits.float(), y)
+        self.log("train_loss", loss)
+        return loss
+
+    def configure_optimizers(self):
+        return torch.optim.SGD(self.parameters(), lr=self.cfg["lr"], momentum=self.cfg["momentum"],
+                               weight_decay=self.cfg["weight_decay"])
+
+    def train_dataloader(self):
+        from torch.utils.data import DataLoader
+
+        ds = SyntheticImageNet(self.cfg["n_train"], self.cfg["image_size"], self.cfg["num_classes"])
+        return DataLoader(ds, batch_size=self.cfg["batch_size"], num_workers=0)
