@@ -262,6 +262,9 @@ class Trainer:
     def fit(self, model: LightningModule, train_dataloader: Optional[DataLoader] = None,
             val_dataloaders: Optional[Union[DataLoader, List[DataLoader]]] = None,
             datamodule: Optional[LightningDataModule] = None):
+        # PL 1.1: a datamodule passed positionally (reference examples/ray_ddp_tune.py:42)
+        if isinstance(train_dataloader, LightningDataModule):
+            datamodule, train_dataloader = train_dataloader, None
         self._attach(model, train_dataloader, val_dataloaders, None, datamodule)
         self.testing = False
         self._prepare_data_on_driver(model)
@@ -270,6 +273,8 @@ class Trainer:
 
     def test(self, model: Optional[LightningModule] = None, test_dataloaders=None, ckpt_path: Optional[str] = "best",
              verbose: bool = True, datamodule: Optional[LightningDataModule] = None):
+        if isinstance(test_dataloaders, LightningDataModule):
+            datamodule, test_dataloaders = test_dataloaders, None
         if model is None:
             model = self.get_model()
             if ckpt_path == "best" and self.checkpoint_callback and self.checkpoint_callback.best_model_path:
