@@ -168,6 +168,10 @@ class RayAccelerator(DataParallelAccelerator):
         if "PL_GLOBAL_SEED" in os.environ:
             seed = os.environ["PL_GLOBAL_SEED"]
             ray.get([w.set_env_var.remote("PL_GLOBAL_SEED", seed) for w in self.workers])
+        from ..utils.faults import fault_env
+
+        for k, v in fault_env().items():  # fault-injection tests
+            ray.get([w.set_env_var.remote(k, v) for w in self.workers])
         self.ddp_address = ray.get(self.workers[0].execute.remote(setup_address))
         self.global_to_local = self.get_local_ranks()
         trainer = self.trainer

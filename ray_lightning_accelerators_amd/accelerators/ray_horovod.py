@@ -166,6 +166,11 @@ class HorovodRayAccelerator(Accelerator):
         if "PL_GLOBAL_SEED" in os.environ:
             seed = os.environ["PL_GLOBAL_SEED"]
             self.executor.execute(lambda: os.environ.__setitem__("PL_GLOBAL_SEED", seed))
+        from ..utils.faults import fault_env
+
+        fenv = fault_env()
+        if fenv:
+            self.executor.execute(lambda: os.environ.update(fenv))
         trainer_ref = ray.put(trainer)
         self.trainer = None
         queue = None

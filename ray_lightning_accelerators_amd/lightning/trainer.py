@@ -27,6 +27,8 @@ from .callbacks import Callback, EarlyStopping, ModelCheckpoint
 from .core import LightningDataModule, LightningModule, _normalize_optimizers
 from .loggers import CSVLogger, LightningLoggerBase
 from .utilities import atomic_save, load_checkpoint, log, move_to_device, rank_zero_warn
+from ..utils.faults import maybe_inject as maybe_inject_fault
+from ..utils.profiling import resolve_profiler
 
 PL_COMPAT_VERSION = "1.1.7"
 
@@ -114,6 +116,7 @@ class Trainer:
         replace_sampler_ddp: bool = True,
         reload_dataloaders_every_epoch: bool = False,
         fused_step: Optional[bool] = None,
+        profiler=None,
         **kwargs,
     ):
         for k in kwargs:
@@ -151,6 +154,8 @@ class Trainer:
         self.reload_dataloaders_every_epoch = reload_dataloaders_every_epoch
         self.weights_summary = weights_summary
         self.fused_step = fused_step
+        self.profiler = resolve_profiler(profiler)
+        self.profiler_summary = ""
         if deterministic:
             torch.use_deterministic_algorithms(True, warn_only=True)
         # callbacks
@@ -644,6 +649,9 @@ class Trainer:
         if self.logger is not None:
             self.logger.finalize("success")
         self.training = False
+        self.profiler_summary = self.profiler.summary()
+        if self.profiler_summary and self.is_global_zero:
+            print(self.profiler_summary, flush=True)
 
     def _run_epoch(self, model: LightningModule) -> None:
         dl = self.train_dataloader
@@ -713,6 +721,8 @@ class Trainer:
             cb.on_train_batch_start(self, model, batch, batch_idx, 0)
         if r == -1:
             return None
+        maybe_inject_fault(self.global_rank, self.global_step)
+        self.profiler.start("run_training_batch")
         if self._fused is not None:
             out = self._fused.train_batch(batch, batch_idx)
             self.global_step += 1
@@ -725,6 +735,7 @@ class Trainer:
             if accumulate_done:
                 self.global_step += 1
                 self._update_lr_schedulers("step")
+        self.profiler.stop("run_training_batch")
         for cb in self.callbacks:
             cb.on_train_batch_end(self, model, out, batch, batch_idx, 0)
         model.on_train_batch_end(out, batch, batch_idx, 0)
