@@ -228,7 +228,8 @@ void mlp_train_step2(optional<Tensor> x_u8, optional<Tensor> x_f32, Tensor label
 // 2 tail GRAD, 3 tail ADAM (after the allreduce), 4 PRIME (H1pre of the pending batch).
 void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counters, int64_t n_batches, int64_t B,
           int64_t L1, int64_t L2, Tensor params, Tensor grads, Tensor exp_avg, Tensor exp_avg_sq, Tensor shadow,
-          Tensor dh1t, Tensor xring, Tensor h1pre, Tensor act, optional<Tensor> stats, bool advance_step, double lr,
+          Tensor dh1t, Tensor xring, Tensor h1pre, Tensor act, Tensor yring, optional<Tensor> stats,
+          bool advance_step, double lr,
           double beta1, double beta2, double eps, double weight_decay, double grad_scale, optional<Tensor> lr_t,
           bool adamw, optional<Tensor> stamps) {
   TORCH_CHECK(kind >= 0 && kind <= 4, "mlp3: bad kind ", kind);
@@ -254,7 +255,9 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
   check_dev(act, "act", at::kBFloat16);
   TORCH_CHECK(act.numel() >= rla::mlp3_act_rows((int)L1, (int)L2) * Bp, "act must hold (L1 + 2 L2 + 16) * Bp");
   check_dev(counters, "counters", at::kLong);
-  TORCH_CHECK(counters.numel() >= 5, "counters must hold 5 int64");
+  TORCH_CHECK(counters.numel() >= 10, "counters must hold 10 int64 (current + advanced state)");
+  check_dev(yring, "yring", at::kInt);
+  TORCH_CHECK(yring.numel() >= 2 * Bp, "yring must hold 2 * round_up(B, 32) int32");
   check_dev(x_u8, "x_u8", at::kByte);
   TORCH_CHECK(x_u8.dim() == 2 && x_u8.size(1) == 784, "x_u8 must be [N, 784]");
   check_dev(labels, "labels", at::kLong);
@@ -279,6 +282,7 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
   a.xring = reinterpret_cast<uint16_t*>(xring.data_ptr());
   a.h1pre = h1pre.data_ptr<int64_t>();
   a.act = reinterpret_cast<uint16_t*>(act.data_ptr());
+  a.yring = yring.data_ptr<int>();
   a.stats = ptr_or_null<float>(stats, "stats", at::kFloat, 4);
   a.stats_ring = a.stats ? (int)(stats->numel() / 4) : 0;
   a.apply_adam = kind == rla::kMLP3Step;

@@ -112,7 +112,7 @@ struct MLP3Args {
   const int64_t* labels;    // [N_data]
   const int64_t* order;     // [2][order_stride]: two epochs' sample orders
   int64_t order_stride;     // n_batches * B
-  int64_t* counters;        // [5]: step, next cursor, consumed cursor, ring slot, order buffer
+  int64_t* counters;        // [10]: (step, next cursor, consumed cursor, ring slot, order buffer) x {current, next}
   int64_t n_batches;
   int B, L1, L2;
   float* params;
@@ -124,6 +124,7 @@ struct MLP3Args {
   uint16_t* xring;          // [2][49][Bp][16] bf16 X tiles
   int64_t* h1pre;           // [2][Bp * L1] layer-1 pre-activations, 32.32 fixed point (fragment order)
   uint16_t* act;            // [L1 + 2*L2 + 16][Bp] bf16 head -> tail: H1^T, H2^T, dH2^T, dZ^T
+  int* yring;               // [2][Bp] int32 staged labels (-1 past B), slot-indexed like xring
   float* stats;
   int stats_ring;
   int apply_adam;           // head: Adam on the small parameters (world size 1)

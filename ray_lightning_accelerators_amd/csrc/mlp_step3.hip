@@ -51,6 +51,7 @@ constexpr int kWaves = 8;
 constexpr int kDZS = 40;
 constexpr int kXSS = 24;   // LDS row stride of a 16-pixel X slice (bf16)
 constexpr int kBMax = 256;
+constexpr int kCnt = 5;  // counters: [0, 5) current state, [5, 10) the head's advanced copy
 
 enum TailMode { kFused = 0, kGrad = 1, kAdam = 2, kPrime = 3 };
 
@@ -93,8 +94,29 @@ __device__ __forceinline__ unsigned long long f32_to_fixed(float x) {
 }
 __device__ __forceinline__ float fixed_to_f32(int64_t q) { return (float)((double)q * (1.0 / 4294967296.0)); }
 
+// Gather one 16-pixel tile of batch (ob, cursor) as bf16 rows into xring slot
+// `dst_slot` (rows >= B zero); block kt == 0 also stages that batch's labels
+// into yring (-1 for padded rows), so no kernel chases the sample index on
+// its critical path.  Runs as extra workgroups of the head launch (for the
+// NEXT batch, concurrently with the head's serial chain) or in PRIME.
+__device__ __forceinline__ void gather_tile(const MLP3Args& a, int kt, int64_t ob, int64_t cursor,
+                                            int64_t dst_slot, int nthreads) {
+  const int tid = threadIdx.x;
+  const int B = a.B, Bp = (B + 31) / 32 * 32;
+  const int64_t* idx = a.order + ob * a.order_stride + cursor * B;
+  __bf16* dst = reinterpret_cast<__bf16*>(a.xring) + (dst_slot * kTiles + kt) * (int64_t)Bp * 16;
+  for (int b = tid; b < Bp; b += nthreads) {
+    bf16x8 lo = zero8(), hi = zero8();
+    if (b < B) u8x16_to_bf16(*reinterpret_cast<const uint4*>(a.x_u8 + idx[b] * kD + kt * 16), lo, hi);
+    *reinterpret_cast<bf16x8*>(dst + b * 16) = lo;
+    *reinterpret_cast<bf16x8*>(dst + b * 16 + 8) = hi;
+  }
+  if (kt == 0)
+    for (int b = tid; b < Bp; b += nthreads) a.yring[dst_slot * Bp + b] = b < B ? (int)a.labels[idx[b]] : -1;
+}
+
 // ---------------------------------------------------------------------------
-// Head kernel (one workgroup, 8 waves)
+// Head kernel (block 0: one workgroup, 8 waves; blocks 1..49: next-batch gather)
 // ---------------------------------------------------------------------------
 template <int BC, int L1, int L2>
 __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
@@ -116,14 +138,19 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
   const __bf16* SH = reinterpret_cast<const __bf16*>(a.shadow);
   const float* P = a.params;
 
+  if (blockIdx.x > 0) {  // the NEXT batch's tiles, for this step's tail (xring / yring slot ^ 1)
+    int64_t nc = a.counters[1] + 1, nob = a.counters[4];
+    if (nc >= a.n_batches) { nc = 0; nob ^= 1; }
+    gather_tile(a, (int)blockIdx.x - 1, nob, nc, a.counters[3] ^ 1, kThreads);
+    return;
+  }
+
   // device counters: uniform scalar loads, no LDS broadcast round trip
   const int64_t t = a.counters[0] + 1;
   const int64_t cursor = a.counters[1];
   const int64_t slot = a.counters[3];
   const int64_t ob = a.counters[4];
   const int Bp = (a.B + 31) / 32 * 32;
-  const int64_t* h1p = a.h1pre + slot * (int64_t)Bp * L1;
-  const int64_t* idx = a.order + ob * a.order_stride + cursor * a.B;
   __bf16* ACT = reinterpret_cast<__bf16*>(a.act);
   __bf16* DH1T = reinterpret_cast<__bf16*>(a.dh1t);
 
@@ -159,7 +186,6 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
 
   for (int c = 0; c < nchunks; ++c) {
     const int row0 = c * BC;
-    const int nvalid = min(BC, a.B - row0);
 
     // ---- batch-independent weight fragments, issued first ----
     bf16x8 w2f[KS2];
@@ -185,28 +211,45 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
       for (int ks = 0; ks < PH; ++ks)
         w2tf[ks] = (w < C::MT * C::TN1) ? ld8(SH + O::W2T + (int64_t)(ct * 16 + r16) * L2 + ks * 32 + 8 * g) : zero8();
     }
+    // Labels and H1pre of BOTH ring slots are loaded before the barrier and
+    // selected after it: none of these loads waits for the counters read.
+    constexpr int NQ = (BC * L1 / 4 + kThreads - 1) / kThreads;
+    longlong2 qs[NQ][2][2];  // [item][slot][half]
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+      const int f4 = tid + k * kThreads;
+      const int mtl = (f4 * 4 >> 8) / C::TN1;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        qs[k][s][0] = qs[k][s][1] = make_longlong2(0, 0);
+        // rows past round_up(B, 32) exist only in the last chunk's LDS image
+        if (f4 < BC * L1 / 4 && row0 + mtl * 16 < Bp) {
+          const int64_t* src = a.h1pre + s * (int64_t)Bp * L1 + (int64_t)row0 * L1 + f4 * 4;
+          qs[k][s][0] = *reinterpret_cast<const longlong2*>(src);
+          qs[k][s][1] = *reinterpret_cast<const longlong2*>(src + 2);
+        }
+      }
+    }
     if (tid < BC) {
-      int y = -1;
-      if (tid < nvalid) y = (int)a.labels[idx[row0 + tid]];
-      sY[tid] = y;
+      const bool ok = row0 + tid < Bp;
+      const int y0 = ok ? a.yring[row0 + tid] : -1, y1 = ok ? a.yring[Bp + row0 + tid] : -1;
+      sY[tid] = slot ? y1 : y0;  // staged by the previous head launch; -1 past B
     }
     __syncthreads();  // sBias ready
 
     // ---- H1 = relu(H1pre + b1); H1pre chunk is contiguous in fragment order ----
     {
-      const int64_t* src = h1p + (int64_t)row0 * L1;
-      for (int f4 = tid; f4 < BC * L1 / 4; f4 += kThreads) {
+#pragma unroll
+      for (int k = 0; k < NQ; ++k) {
+        const int f4 = tid + k * kThreads;
+        if (f4 >= BC * L1 / 4) continue;
         const int f = f4 * 4;
         const int ln = f & 63, i = (f >> 6) & 3, blk = f >> 8;
         const int ct = blk % C::TN1, mtl = blk / C::TN1;
         const int b = mtl * 16 + 4 * (ln >> 4) + i, m = ct * 16 + (ln & 15);
-        // rows past round_up(B, 32) exist only in the last chunk's LDS image
-        int64_t q[4] = {0, 0, 0, 0};
-        if (row0 + mtl * 16 < Bp) {
-          const longlong2 q01 = *reinterpret_cast<const longlong2*>(src + f);
-          const longlong2 q23 = *reinterpret_cast<const longlong2*>(src + f + 2);
-          q[0] = q01.x; q[1] = q01.y; q[2] = q23.x; q[3] = q23.y;
-        }
+        const longlong2 lo = slot ? qs[k][1][0] : qs[k][0][0];
+        const longlong2 hi = slot ? qs[k][1][1] : qs[k][0][1];
+        const int64_t q[4] = {lo.x, lo.y, hi.x, hi.y};
         bf16x4 h;
 #pragma unroll
         for (int k = 0; k < 4; ++k) h[k] = relu_bf(fixed_to_f32(q[k]) + sBias[m + k]);
@@ -357,13 +400,16 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
     if (a.stamps && tid == 0 && c == 0) a.stamps[3] = __builtin_amdgcn_s_memrealtime();
   }
   if (tid == 0) {
-    if (a.advance_step) a.counters[0] = t;
-    a.counters[2] = cursor;
+    // the advanced state goes to the NEXT copy: this launch's gather blocks are
+    // still reading the current one (the tail publishes it, see mlp3_tail_kernel)
+    int64_t* cn = a.counters + kCnt;
+    cn[0] = a.advance_step ? t : t - 1;
+    cn[2] = cursor;
     int64_t nc = cursor + 1, nob = ob;
     if (nc >= a.n_batches) { nc = 0; nob ^= 1; }
-    a.counters[1] = nc;
-    a.counters[4] = nob;
-    a.counters[3] = slot ^ 1;
+    cn[1] = nc;
+    cn[4] = nob;
+    cn[3] = slot ^ 1;
     if (a.stats) {
       const int s = (int)((t - 1) % (a.stats_ring > 0 ? a.stats_ring : 1));
       float* st = a.stats + s * 4;
@@ -467,10 +513,16 @@ __device__ __forceinline__ void small_task(const MLP3Args& a, int mode, int task
     float pv = 0.f, mv = 0.f, vv = 0.f;
     if (fused) { pv = a.params[gidx]; mv = a.exp_avg[gidx]; vv = a.exp_avg_sq[gidx]; }
     float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int b = 0; b < Bp; b += 8) {
-      const bf16x8 v = ld8(row + b);
+    // 32 rows per group: four independent 16-byte loads in flight before any add
+    // (a one-load-per-iteration loop made this wave the tail kernel's straggler)
+    for (int b0 = 0; b0 < Bp; b0 += 32) {
+      bf16x8 v[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s8[j] += (float)v[j];
+      for (int q = 0; q < 4; ++q) v[q] = ld8(row + b0 + 8 * q);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s8[j] += (float)v[q][j];
     }
     const float sum = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
     if (fused) {
@@ -523,8 +575,12 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
   const bool do_adam = mode == kFused || mode == kAdam;
   const bool do_fwd = mode != kGrad;
   if (a.stamps && blockIdx.x == 0 && tid == 0) a.stamps[8] = __builtin_amdgcn_s_memrealtime();
+  // every block reads the head's NEXT copy (never written in this launch);
+  // block 0 publishes it as the current state for the next head
+  const int64_t* cn = a.counters + kCnt;
+  if (blockIdx.x == 0 && tid < kCnt) a.counters[tid] = cn[tid];
   if (tid == 0 && do_adam) {
-    const int64_t t = a.counters[0];  // already advanced by the head kernel
+    const int64_t t = cn[0];  // already advanced by the head kernel
     adam_scalars(sh_o, t, a.lr_ptr ? a.lr_ptr[0] : a.lr, a.beta1, a.beta2, a.eps, a.weight_decay, a.adamw);
   }
   if ((int)blockIdx.x >= kTiles) {  // small parameters (block-uniform branch)
@@ -551,26 +607,36 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
   bf16x4 w4;
   if (mode == kPrime) w4 = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(a.shadow) + gidx);
 
-  const int64_t slot = a.counters[3];
+  const int64_t slot = cn[3];
   const int64_t tile_elems = (int64_t)Bp * 16;
   __bf16* XR = reinterpret_cast<__bf16*>(a.xring);
   __bf16* xr_next = XR + (slot * kTiles + kt) * tile_elems;
-  const __bf16* xr_cur = XR + ((slot ^ 1) * kTiles + kt) * tile_elems;
 
   // ---- X slices: this step's (parked by the previous tail) and the next step's ----
-  if (do_grad) {
+  if (mode != kPrime) {
+    // Both ring slots are loaded unconditionally and selected afterwards, so the
+    // loads do not wait for the counters read (one memory round trip, not two).
+    // cur = X[t] (parked by the previous step), next = X[t+1] (the head launch's
+    // gather blocks); slot = cn[3] is where next lives.
+    const __bf16* t0 = XR + (int64_t)kt * tile_elems;
+    const __bf16* t1 = XR + (int64_t)(kTiles + kt) * tile_elems;
     for (int b = tid; b < Bp; b += NT) {
-      *reinterpret_cast<bf16x8*>(sX + b * kXSS) = ld8(xr_cur + b * 16);
-      *reinterpret_cast<bf16x8*>(sX + b * kXSS + 8) = ld8(xr_cur + b * 16 + 8);
+      const bf16x8 a0 = ld8(t0 + b * 16), a1 = ld8(t0 + b * 16 + 8);
+      const bf16x8 c0 = ld8(t1 + b * 16), c1 = ld8(t1 + b * 16 + 8);
+      const bool next_is_0 = slot == 0;
+      if (do_grad) {
+        *reinterpret_cast<bf16x8*>(sX + b * kXSS) = next_is_0 ? c0 : a0;
+        *reinterpret_cast<bf16x8*>(sX + b * kXSS + 8) = next_is_0 ? c1 : a1;
+      }
+      if (do_fwd) {
+        *reinterpret_cast<bf16x8*>(sXn + b * kXSS) = next_is_0 ? a0 : c0;
+        *reinterpret_cast<bf16x8*>(sXn + b * kXSS + 8) = next_is_0 ? a1 : c1;
+      }
     }
-  }
-  if (mode == kAdam) {
-    for (int b = tid; b < Bp; b += NT) {
-      *reinterpret_cast<bf16x8*>(sXn + b * kXSS) = ld8(xr_next + b * 16);
-      *reinterpret_cast<bf16x8*>(sXn + b * kXSS + 8) = ld8(xr_next + b * 16 + 8);
-    }
-  } else {
-    const int64_t* idx = a.order + a.counters[4] * a.order_stride + a.counters[1] * B;
+  } else {  // PRIME: no head ran, gather the pending batch here
+    const int64_t* idx = a.order + cn[4] * a.order_stride + cn[1] * B;
+    if (kt == 0)
+      for (int b = tid; b < Bp; b += NT) a.yring[slot * Bp + b] = b < B ? (int)a.labels[idx[b]] : -1;
     for (int b = tid; b < Bp; b += NT) {
       bf16x8 lo = zero8(), hi = zero8();
       if (b < B) u8x16_to_bf16(*reinterpret_cast<const uint4*>(a.x_u8 + idx[b] * kD + kt * 16), lo, hi);
@@ -639,15 +705,15 @@ int dispatch3(const MLP3Args& a, int kind, hipStream_t stream) {
     bool launched = false;
     if constexpr (fits3<128, L1, L2>()) {
       if (a.B > 64) {
-        hipLaunchKernelGGL((mlp3_head_kernel<128, L1, L2>), dim3(1), dim3(kThreads), 0, stream, a);
+        hipLaunchKernelGGL((mlp3_head_kernel<128, L1, L2>), dim3(1 + kTiles), dim3(kThreads), 0, stream, a);
         launched = true;
       }
     }
     if (!launched && a.B > 32) {
-      hipLaunchKernelGGL((mlp3_head_kernel<64, L1, L2>), dim3(1), dim3(kThreads), 0, stream, a);
+      hipLaunchKernelGGL((mlp3_head_kernel<64, L1, L2>), dim3(1 + kTiles), dim3(kThreads), 0, stream, a);
       launched = true;
     }
-    if (!launched) hipLaunchKernelGGL((mlp3_head_kernel<32, L1, L2>), dim3(1), dim3(kThreads), 0, stream, a);
+    if (!launched) hipLaunchKernelGGL((mlp3_head_kernel<32, L1, L2>), dim3(1 + kTiles), dim3(kThreads), 0, stream, a);
   }
   int mode = -1, grid = kTiles;
   if (kind == kMLP3Step) { mode = kFused; grid += SmallTasks<L1, L2>::NBLK; }

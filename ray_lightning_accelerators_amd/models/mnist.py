@@ -171,7 +171,7 @@ class FusedMNISTStep:
                              weight_decay=g["weight_decay"], device=self.dev, world_size=self.world,
                              rank=self.trainer.global_rank, allreduce=self._allreduce, buffers=bufs,
                              stats_ring=self.stats.size(0))
-        eng.counters[0] = self.gs.step
+        eng.set_step(self.gs.step)
         eng.lr_tensor = self.lr_tensor  # LR schedulers update one device scalar
         eng.attach_dataset(self._u8, self._labels)
         self.eng = eng
@@ -266,7 +266,7 @@ class FusedMNISTStep:
         self.arena.rebind_all()
         self.counters[0] = self.gs.step
         if self.eng is not None:
-            self.eng.counters[0] = self.gs.step
+            self.eng.set_step(self.gs.step)
             self.eng.refresh_shadow()
 
 

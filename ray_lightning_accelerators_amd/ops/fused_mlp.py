@@ -230,7 +230,9 @@ def mlp3_buffers(L1: int, L2: int, B: int, device) -> Dict[str, torch.Tensor]:
         # 32.32 fixed point: integer atomics make the 49-way split-K sum order-independent
         "h1pre": torch.zeros(2 * bp * L1, dtype=torch.int64, device=device),
         "act": torch.zeros((L1 + 2 * L2 + 16) * bp, dtype=torch.bfloat16, device=device),
-        "counters": torch.zeros(5, dtype=torch.int64, device=device),
+        "yring": torch.full((2 * bp,), -1, dtype=torch.int32, device=device),
+        # [0, 5) current state, [5, 10) the head's advanced copy (published by the tail)
+        "counters": torch.zeros(10, dtype=torch.int64, device=device),
     }
 
 
@@ -254,6 +256,7 @@ def mlp3_launch(
     xring: torch.Tensor,
     h1pre: torch.Tensor,
     act: torch.Tensor,
+    yring: torch.Tensor,
     stats: Optional[torch.Tensor] = None,
     advance_step: bool = True,
     lr: float = 1e-3,
@@ -273,7 +276,7 @@ def mlp3_launch(
     and the next epoch's sample order (counters[4] selects)."""
     require().mlp3(
         int(kind), x_u8, labels, order, counters, int(n_batches), int(B), int(L1), int(L2), params, grads, exp_avg,
-        exp_avg_sq, shadow, dh1t, xring, h1pre, act, stats, bool(advance_step), float(lr), float(betas[0]),
+        exp_avg_sq, shadow, dh1t, xring, h1pre, act, yring, stats, bool(advance_step), float(lr), float(betas[0]),
         float(betas[1]), float(eps), float(weight_decay), float(grad_scale), lr_tensor, bool(adamw), stamps,
     )
 

@@ -107,6 +107,7 @@ class FusedMLPEngine:
         # [3] H1pre/X ring slot, [4] epoch buffer of `order` that [1] indexes
         self.counters = bufs["counters"]
         self.dh1t, self.xring, self.h1pre, self.act = bufs["dh1t"], bufs["xring"], bufs["h1pre"], bufs["act"]
+        self.yring = bufs["yring"]
         self.stats = torch.zeros(stats_ring, 4, device=self.device)
         self.seed = seed
         self.epoch = 0
@@ -119,6 +120,14 @@ class FusedMLPEngine:
         self.x_u8 = self.labels = self.order = None
         self.n_batches = 0
         self.refresh_shadow()
+
+    def _publish_counters(self) -> None:
+        """Host edits of the device state go to both copies (current / advanced)."""
+        self.counters[5:10].copy_(self.counters[0:5])
+
+    def set_step(self, step: int) -> None:
+        self.counters[0] = int(step)
+        self._publish_counters()
 
     @property
     def comm_buffer(self) -> torch.Tensor:
@@ -148,7 +157,8 @@ class FusedMLPEngine:
         self.order[0].copy_(dev_order)
         self.order[1].copy_(dev_order)
         self.n_batches = int(n_batches)
-        self.counters[1:].zero_()
+        self.counters[1:5].zero_()
+        self._publish_counters()
         self.step_in_epoch = 0
         self._graph = None
         self._primed = False
@@ -168,7 +178,8 @@ class FusedMLPEngine:
         self.order = torch.empty(2, self.n_batches * self.B, dtype=torch.int64, device=self.device)
         self._fill_order(0)
         self._fill_order(1)
-        self.counters[1:].zero_()
+        self.counters[1:5].zero_()
+        self._publish_counters()
         self.epoch = 0
         self.step_in_epoch = 0
         self._graph = None
@@ -211,7 +222,7 @@ class FusedMLPEngine:
         return dict(x_u8=self.x_u8, labels=self.labels, order=self.order, counters=self.counters,
                     n_batches=self.n_batches, B=self.B, L1=self.L1, L2=self.L2, params=self.params,
                     grads=self.grads, exp_avg=self.exp_avg, exp_avg_sq=self.exp_avg_sq, shadow=self.shadow,
-                    dh1t=self.dh1t, xring=self.xring, h1pre=self.h1pre, act=self.act, lr=self.lr, betas=self.betas,
+                    dh1t=self.dh1t, xring=self.xring, h1pre=self.h1pre, act=self.act, yring=self.yring, lr=self.lr, betas=self.betas,
                     eps=self.eps, weight_decay=self.wd, lr_tensor=self.lr_tensor)
 
     def prime(self) -> None:
@@ -273,6 +284,7 @@ class FusedMLPEngine:
         c[3] = int(c[3]) ^ 1
         if cursor + 1 >= self.n_batches:
             c[4] = ob ^ 1
+        self._publish_counters()
         if not fused:
             if self.allreduce is not None:
                 self.allreduce(self.comm_buffer)
