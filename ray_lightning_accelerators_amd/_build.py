@@ -52,7 +52,7 @@ EXTENSIONS = {
     },
     "_comm": {
         "hip": ["comm/xgmi_allreduce.hip", "comm/pack.hip"],
-        "cpp": ["comm/comm_bindings.cpp", "comm/communicator.cpp", "comm/fusion_engine.cpp"],
+        "cpp": ["comm/comm_bindings.cpp", "comm/communicator.cpp", "comm/fusion_engine.cpp", "comm/reducer.cpp"],
         "torch": True,
         "libs": ["rccl"],
     },

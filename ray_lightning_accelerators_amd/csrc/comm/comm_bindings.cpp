@@ -5,6 +5,7 @@
 
 #include "comm/communicator.h"
 #include "comm/fusion_engine.h"
+#include "comm/reducer.h"
 
 namespace {
 
@@ -13,6 +14,7 @@ using rla::comm::Communicator;
 using rla::comm::DType;
 using rla::comm::FusionEngine;
 using rla::comm::RedOp;
+using rla::comm::Reducer;
 
 hipStream_t cur_stream(const Tensor& t) {
   return at::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.get_device()).stream();
@@ -120,6 +122,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("fingerprint", &FusionEngine::fingerprint)
       .def_property_readonly("batches_executed", &FusionEngine::batches_executed)
       .def("last_error", &FusionEngine::last_error);
+  py::class_<Reducer>(m, "Reducer")
+      .def(py::init([](Communicator* c, Tensor grad, std::vector<int64_t> bounds, std::vector<int> pb, int dev) {
+             check(grad, "grad arena");
+             TORCH_CHECK(grad.scalar_type() == at::kFloat, "gradient arena must be fp32");
+             return new Reducer(c, grad.data_ptr<float>(), grad.numel(), bounds, pb, dev);
+           }),
+           py::arg("comm"), py::arg("grad"), py::arg("bucket_bounds"), py::arg("param_bucket"), py::arg("device"),
+           py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
+      .def("prepare", &Reducer::prepare)
+      .def("mark_ready", [](Reducer& r, int i, Tensor like) { r.mark_ready(i, cur_stream(like)); })
+      .def("finish", [](Reducer& r, Tensor like) { r.finish(cur_stream(like)); })
+      .def_property_readonly("launched", &Reducer::launched)
+      .def_property_readonly("num_buckets", &Reducer::num_buckets);
   m.attr("XGMI_MAX_RANKS") = rla::comm::kXgmiMaxRanks;
   m.attr("ARCH") = "gfx950";
 }

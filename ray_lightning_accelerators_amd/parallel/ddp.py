@@ -71,6 +71,18 @@ class GradSynchronizer:
         if cur:
             self._close_bucket(cur)
         self._next = 0
+        # GPU ranks on the default group: the C++ reducer (csrc/comm/reducer.cpp)
+        # owns readiness counting, in-order launch on its comm stream, and events
+        self._native = None
+        if (self.world > 1 and process_group is None and grad_dtype == "fp32" and arena.grad.is_cuda
+                and os.environ.get("RLA_NATIVE_REDUCER", "1") == "1"):
+            from .comm import get_native_comm, native_comm_module
+
+            comm = get_native_comm()
+            if comm is not None:
+                bounds = [v for b in self.buckets for v in (b.start, b.end)]
+                self._native = native_comm_module().Reducer(comm._c, arena.grad, bounds, self.param_bucket,
+                                                            comm.device)
         self._hooks = []
         for i, p in enumerate(arena.params):
             self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
@@ -101,6 +113,8 @@ class GradSynchronizer:
             b.work = None
         self._started = True
         self._next = 0
+        if self._native is not None:
+            self._native.prepare()
         if self.broadcast_buffers and self.world > 1 and sync:
             for buf in self.module.buffers():
                 dist.broadcast(buf, 0, group=self.pg)
@@ -110,6 +124,9 @@ class GradSynchronizer:
             if not self.arena.owns_grad(i):
                 self.arena.rebind_grad(i)
             if not self.enabled or not self._started:
+                return
+            if self._native is not None:
+                self._native.mark_ready(i, self.arena.grad)
                 return
             b = self.buckets[self.param_bucket[i]]
             b.pending -= 1
@@ -139,6 +156,12 @@ class GradSynchronizer:
     def finish(self) -> None:
         """Wait for every bucket; launch the ones unused parameters left incomplete."""
         if not self.enabled:
+            self._started = False
+            return
+        if self._native is not None:
+            self._native.finish(self.arena.grad)
+            if not self.average_in_optimizer:
+                ops.scale_(self.arena.grad, 1.0 / self.world)
             self._started = False
             return
         for b in self.buckets:

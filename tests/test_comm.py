@@ -144,6 +144,42 @@ def _gpu_worker(rank, world, port, q, mode):
             res["match"] = all(bool(torch.allclose(a, b, atol=1e-5)) for a, b in
                                zip(model.parameters(), ref.parameters()))
             res["batches"] = opt._hvd_state.engine.batches_executed if res["native_engine"] else 0
+        elif mode == "reducer":
+            # GradSynchronizer on the C++ reducer: several in-order buckets, averaged grads
+            from ray_lightning_accelerators_amd.parallel import comm as comm_mod
+            from ray_lightning_accelerators_amd.parallel.arena import ParamArena
+            from ray_lightning_accelerators_amd.parallel.ddp import GradSynchronizer
+
+            comm_mod._default = comm
+
+            def make():
+                torch.manual_seed(0)
+                return torch.nn.Sequential(torch.nn.Linear(64, 130), torch.nn.ReLU(), torch.nn.Linear(130, 7),
+                                           torch.nn.ReLU(), torch.nn.Linear(7, 3)).to(dev)
+
+            def data(r):
+                g = torch.Generator().manual_seed(200 + r)
+                return torch.randn(16, 64, generator=g).to(dev), torch.randn(16, 3, generator=g).to(dev)
+
+            model = make()
+            arena = ParamArena(model)
+            sync = GradSynchronizer(model, arena, bucket_cap_mb=100 / 2 ** 20, average_in_optimizer=False)
+            res["native_reducer"] = sync._native is not None
+            res["buckets"] = len(sync.buckets)
+            for _ in range(2):
+                arena.zero_grad()
+                sync.prepare_for_backward()
+                x, y = data(rank)
+                torch.nn.functional.mse_loss(model(x), y).backward()
+                sync.finish()
+            ref = make()
+            for r in range(world):
+                x, y = data(r)
+                (torch.nn.functional.mse_loss(ref(x), y) / world).backward()
+            torch.cuda.synchronize()
+            res["match"] = all(bool(torch.allclose(p.grad, q.grad, atol=1e-6)) for p, q in
+                               zip(model.parameters(), ref.parameters()))
+            res["launched"] = sync._native.launched if sync._native is not None else 0
         elif mode == "timeout":
             x = torch.ones(1024, device=dev)
             if rank == 0:
@@ -203,6 +239,14 @@ def test_horovod_optimizer_on_native_fusion_engine():
     for r, res in out.items():
         assert res["native_engine"] and res["match"], (r, res)
         assert res["batches"] >= 6  # 3 steps x >= 2 fusion buckets (4 KiB threshold)
+
+
+@gpu
+def test_ddp_native_reducer_two_ranks():
+    out = _run_gpu("reducer")
+    for r, res in out.items():
+        assert res["native_reducer"] and res["match"], (r, res)
+        assert res["buckets"] >= 3 and res["launched"] == 2 * res["buckets"]
 
 
 @gpu
