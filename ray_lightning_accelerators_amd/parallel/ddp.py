@@ -116,8 +116,31 @@ class GradSynchronizer:
         if self._native is not None:
             self._native.prepare()
         if self.broadcast_buffers and self.world > 1 and sync:
-            for buf in self.module.buffers():
-                dist.broadcast(buf, 0, group=self.pg)
+            self._broadcast_buffers()
+
+    def _broadcast_buffers(self) -> None:
+        """torch DDP's broadcast_buffers=True, coalesced: ONE
+        broadcast per dtype of a flattened copy instead of one per buffer
+        (ResNet-50: 161 BN buffers -> 2 collectives per forward)."""
+        from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
+
+        groups = {}
+        for b in self.module.buffers():
+            groups.setdefault((b.dtype, b.device), []).append(b)
+        for (_, dev), bufs in groups.items():
+            flat = _flatten_dense_tensors([b.data for b in bufs])
+            if dev.type == "cuda" and self.pg is None:
+                from .comm import get_native_comm
+
+                comm = get_native_comm()
+                if comm is not None and comm.rccl:
+                    comm.broadcast_(flat, 0)
+                else:
+                    dist.broadcast(flat, 0, group=self.pg)
+            else:
+                dist.broadcast(flat, 0, group=self.pg)
+            for b, v in zip(bufs, _unflatten_dense_tensors(flat, [b.data for b in bufs])):
+                b.data.copy_(v)
 
     def _make_hook(self, i: int):
         def hook(p: torch.Tensor) -> None:
