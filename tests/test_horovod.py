@@ -113,3 +113,45 @@ def test_multi_host_topology():
     assert [e["HOROVOD_LOCAL_RANK"] for e in envs] == [0, 1, 0, 1]
     assert [e["HOROVOD_CROSS_RANK"] for e in envs] == [0, 0, 1, 1]
     assert all(e["HOROVOD_SIZE"] == 4 and e["HOROVOD_LOCAL_SIZE"] == 2 for e in envs)
+
+
+# ------------------------------------------------------------------ GPU (reference test_horovod.py:85-140)
+@pytest.fixture
+def ray_start_gpus():
+    n = max(1, torch.cuda.device_count())
+    info = ray.init(num_cpus=2 * n, num_gpus=n)
+    yield info
+    ray.shutdown()
+
+
+def _need_gpus(n):
+    return pytest.mark.skipif(torch.cuda.device_count() < n, reason=f"test requires {n} GPU(s)")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("num_slots", [pytest.param(1, marks=_need_gpus(1)), pytest.param(2, marks=_need_gpus(2))])
+def test_train_gpu(tmpdir, ray_start_gpus, seed, num_slots):
+    model = BoringModel()
+    accelerator = HorovodRayAccelerator(num_slots=num_slots, use_gpu=True)
+    trainer = get_trainer(tmpdir, accelerator=accelerator, use_gpu=True)
+    train_test(trainer, model)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("num_slots", [pytest.param(1, marks=_need_gpus(1)), pytest.param(2, marks=_need_gpus(2))])
+def test_load_gpu(tmpdir, ray_start_gpus, seed, num_slots):
+    model = BoringModel()
+    accelerator = HorovodRayAccelerator(num_slots=num_slots, use_gpu=True)
+    trainer = get_trainer(tmpdir, accelerator=accelerator, use_gpu=True)
+    load_test(trainer, model)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("num_slots", [pytest.param(1, marks=_need_gpus(1)), pytest.param(2, marks=_need_gpus(2))])
+def test_predict_gpu(tmpdir, ray_start_gpus, seed, num_slots):
+    config = {"layer_1": 32, "layer_2": 32, "lr": 1e-2, "batch_size": 32}
+    model = LightningMNISTClassifier(config, tmpdir)
+    dm = MNISTDataModule(data_dir=tmpdir, num_workers=1, batch_size=config["batch_size"])
+    accelerator = HorovodRayAccelerator(num_slots=num_slots, use_gpu=True)
+    trainer = get_trainer(tmpdir, limit_train_batches=10, max_epochs=1, accelerator=accelerator, use_gpu=True)
+    predict_test(trainer, model, dm)
