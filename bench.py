@@ -60,6 +60,9 @@ def parse():
                     help="optimizer steps per captured hipGraph (native); 0 = eager launches")
     ap.add_argument("--n-data", type=int, default=55000)
     ap.add_argument("--bucket-mb", type=float, default=8.0, help="resnet50 DDP bucket cap (MiB)")
+    ap.add_argument("--dp", choices=["fused", "split"], default="fused",
+                    help="mnist N>1: 'fused' exchanges gradients inside the tail kernel over xGMI "
+                         "(falls back to 'split' = head/tail/allreduce/tail when xGMI is unavailable)")
     ap.add_argument("--comm", choices=["auto", "xgmi", "rccl", "torch"], default="auto",
                     help="N>1 gradient allreduce: native xGMI one-shot (auto/xgmi), native RCCL, or c10d")
     args = ap.parse_args()
@@ -105,6 +108,7 @@ def make_native(args, world, rank, dev, x, y):
     from ray_lightning_accelerators_amd.parallel.mlp_engine import FusedMLPEngine
 
     allreduce = None
+    dp_ctx = None
     if world > 1:
         # native data plane: xGMI one-shot push allreduce for the gradient bucket
         # (validated at setup, RCCL fallback), enqueued on the step's stream so
@@ -119,11 +123,18 @@ def make_native(args, world, rank, dev, x, y):
             if rank == 0:
                 print(comm.describe(), file=sys.stderr, flush=True)
             allreduce = comm.allreduce_
+            if args.dp == "fused":
+                from ray_lightning_accelerators_amd.ops.fused_mlp import mlp_param_count
+
+                dp_ctx = comm.dp_context(mlp_param_count(args.layer_1, args.layer_2))
+                if rank == 0:
+                    print(f"fused data-parallel tail: {'on' if dp_ctx else 'unavailable (split path)'}",
+                          file=sys.stderr, flush=True)
         else:
             allreduce = dist.all_reduce
 
     eng = FusedMLPEngine(args.layer_1, args.layer_2, args.batch_size, lr=args.lr, device=dev,
-                         world_size=world, rank=rank, allreduce=allreduce, seed=0)
+                         world_size=world, rank=rank, allreduce=allreduce, seed=0, dp_context=dp_ctx)
     eng.set_data(x, y, shuffle=True)
     eng.broadcast_from(0)
     if args.graph_steps > 0:

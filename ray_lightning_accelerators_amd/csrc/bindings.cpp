@@ -231,8 +231,8 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
           Tensor dh1t, Tensor xring, Tensor h1pre, Tensor act, Tensor yring, optional<Tensor> stats,
           bool advance_step, double lr,
           double beta1, double beta2, double eps, double weight_decay, double grad_scale, optional<Tensor> lr_t,
-          bool adamw, optional<Tensor> stamps) {
-  TORCH_CHECK(kind >= 0 && kind <= 4, "mlp3: bad kind ", kind);
+          bool adamw, optional<Tensor> stamps, std::vector<int64_t> dp_ctx) {
+  TORCH_CHECK(kind >= 0 && kind <= 5, "mlp3: bad kind ", kind);
   TORCH_CHECK(rla::mlp_supported((int)L1, (int)L2), "no fused MLP kernel for layer sizes ", L1, "/", L2);
   TORCH_CHECK(B >= 1 && B <= 256, "fused MLP step supports 1 <= batch <= 256");
   const int64_t np = mlp_param_count(L1, L2);
@@ -293,6 +293,20 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
   a.lr_ptr = ptr_or_null<const float>(lr_t, "lr", at::kFloat, 1);
   a.adamw = adamw;
   a.stamps = ptr_or_null<int64_t>(stamps, "stamps", at::kLong, 16);
+  if (kind == rla::kMLP3StepDP) {
+    // [world, rank, stride, spin, gen_ptr, err_ptr, region_ptr x world] from the comm engine
+    TORCH_CHECK(dp_ctx.size() >= 6 && dp_ctx[0] >= 1 && dp_ctx[0] <= 8 && (int64_t)dp_ctx.size() == 6 + dp_ctx[0],
+                "mlp3 StepDP needs the comm engine's aux_context()");
+    a.dp_world = (int)dp_ctx[0];
+    a.dp_rank = (int)dp_ctx[1];
+    TORCH_CHECK(a.dp_rank >= 0 && a.dp_rank < a.dp_world, "bad dp rank");
+    a.dp_stride = dp_ctx[2];
+    TORCH_CHECK(a.dp_stride >= np, "aux receive area smaller than the parameter arena");
+    a.dp_spin = dp_ctx[3];
+    a.dp_gen = reinterpret_cast<uint32_t*>(dp_ctx[4]);
+    a.dp_err = reinterpret_cast<int*>(dp_ctx[5]);
+    for (int r = 0; r < a.dp_world; ++r) a.dp_regions[r] = reinterpret_cast<char*>(dp_ctx[6 + r]);
+  }
   TORCH_CHECK(rla::launch_mlp3(a, (int)kind, cur_stream(params)) == 0, "fused MLP v3 launch failed");
 }
 

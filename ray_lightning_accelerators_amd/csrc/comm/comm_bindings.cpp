@@ -98,6 +98,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              TORCH_CHECK(t.scalar_type() == at::kFloat, "xGMI one-shot allreduce is fp32");
              c.allreduce_xgmi(t.data_ptr<float>(), t.numel(), cur_stream(t));
            })
+      .def("aux_handle", [](Communicator& c, int64_t cap) { return py::bytes(c.aux_handle(cap)); })
+      .def("aux_open",
+           [](Communicator& c, std::vector<py::bytes> hs) {
+             std::vector<std::string> v;
+             for (auto& h : hs) v.emplace_back(std::string(h));
+             c.aux_open(v);
+           })
+      .def_property_readonly("has_aux", &Communicator::has_aux)
+      .def("aux_context", &Communicator::aux_context)
       .def("set_spin_limit", &Communicator::set_spin_limit)
       .def("error_state", &Communicator::error_state)
       .def("error_message", &Communicator::error_message)

@@ -50,9 +50,13 @@ Communicator::~Communicator() {
     else ncclCommDestroy(comm_);
   }
   comm_ = nullptr;
-  for (int r = 0; r < world_ && r < kXgmiMaxRanks; ++r)
+  for (int r = 0; r < world_ && r < kXgmiMaxRanks; ++r) {
     if (peers_[r] && peers_[r] != region_) hipIpcCloseMemHandle(peers_[r]);
+    if (aux_peers_[r] && aux_peers_[r] != aux_region_) hipIpcCloseMemHandle(aux_peers_[r]);
+  }
   if (region_) hipFree(region_);
+  if (aux_region_) hipFree(aux_region_);
+  if (aux_gen_) hipFree(aux_gen_);
   if (gen_) hipFree(gen_);
   if (err_host_) hipHostFree(err_host_);
 }
@@ -111,10 +115,13 @@ std::string Communicator::xgmi_handle(int64_t capacity_floats) {
     hip_check(hipMemset(region_, 0, (size_t)bytes), "hipMemset(region)");
     hip_check(hipMalloc(reinterpret_cast<void**>(&gen_), kXgmiMaxBlocks * sizeof(uint32_t)), "hipMalloc(gen)");
     hip_check(hipMemset(gen_, 0, kXgmiMaxBlocks * sizeof(uint32_t)), "hipMemset(gen)");
-    hip_check(hipHostMalloc(reinterpret_cast<void**>(&err_host_), sizeof(int), hipHostMallocMapped),
-              "hipHostMalloc(error)");
-    *err_host_ = 0;
-    hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_dev_), err_host_, 0), "hipHostGetDevicePointer");
+    if (!err_host_) {
+      hip_check(hipHostMalloc(reinterpret_cast<void**>(&err_host_), sizeof(int), hipHostMallocMapped),
+                "hipHostMalloc(error)");
+      *err_host_ = 0;
+      hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_dev_), err_host_, 0),
+                "hipHostGetDevicePointer");
+    }
     hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
   }
   hipIpcMemHandle_t h;
@@ -156,6 +163,57 @@ void Communicator::allreduce_xgmi(float* buf, int64_t count, hipStream_t s) {
   l.slot_stride = slot_stride_;
   l.spin_limit = spin_limit_;
   if (launch_xgmi_oneshot(l, s) != 0) throw std::runtime_error("xGMI one-shot launch failed");
+}
+
+std::string Communicator::aux_handle(int64_t capacity_floats) {
+  if (world_ > kXgmiMaxRanks) throw std::runtime_error("xGMI exchange supports at most 8 ranks");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  if (!err_host_) {
+    hip_check(hipHostMalloc(reinterpret_cast<void**>(&err_host_), sizeof(int), hipHostMallocMapped),
+              "hipHostMalloc(error)");
+    *err_host_ = 0;
+    hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_dev_), err_host_, 0), "hipHostGetDevicePointer");
+  }
+  if (!aux_region_) {
+    aux_stride_ = (capacity_floats + 63) / 64 * 64;
+    const int64_t bytes = xgmi_region_bytes(aux_stride_);
+    hip_check(hipExtMallocWithFlags(reinterpret_cast<void**>(&aux_region_), (size_t)bytes, hipDeviceMallocUncached),
+              "hipExtMallocWithFlags(uncached aux)");
+    hip_check(hipMemset(aux_region_, 0, (size_t)bytes), "hipMemset(aux)");
+    hip_check(hipMalloc(reinterpret_cast<void**>(&aux_gen_), kDpMaxBlocks * sizeof(uint32_t)), "hipMalloc(aux gen)");
+    hip_check(hipMemset(aux_gen_, 0, kDpMaxBlocks * sizeof(uint32_t)), "hipMemset(aux gen)");
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  }
+  hipIpcMemHandle_t h;
+  hip_check(hipIpcGetMemHandle(&h, aux_region_), "hipIpcGetMemHandle(aux)");
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void Communicator::aux_open(const std::vector<std::string>& handles) {
+  if ((int)handles.size() != world_) throw std::runtime_error("need one IPC handle per rank");
+  if (!aux_region_) throw std::runtime_error("aux_handle() first");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  for (int r = 0; r < world_; ++r) {
+    if (r == rank_) {
+      aux_peers_[r] = aux_region_;
+      continue;
+    }
+    if (handles[r].size() != sizeof(hipIpcMemHandle_t)) throw std::runtime_error("bad IPC handle size");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handles[r].data(), sizeof(h));
+    void* p = nullptr;
+    hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(aux)");
+    aux_peers_[r] = static_cast<char*>(p);
+  }
+  aux_ready_ = true;
+}
+
+std::vector<int64_t> Communicator::aux_context() const {
+  if (!aux_ready_) throw std::runtime_error("aux region not open");
+  std::vector<int64_t> v = {world_, rank_, aux_stride_, spin_limit_, reinterpret_cast<int64_t>(aux_gen_),
+                            reinterpret_cast<int64_t>(err_dev_)};
+  for (int r = 0; r < world_; ++r) v.push_back(reinterpret_cast<int64_t>(aux_peers_[r]));
+  return v;
 }
 
 int Communicator::error_state() {

@@ -58,6 +58,16 @@ class Communicator {
   void allreduce_xgmi(float* buf, int64_t count, hipStream_t s);
   void set_spin_limit(int64_t n) { spin_limit_ = n; }
 
+  // ---- auxiliary peer region for kernels that exchange data themselves ----
+  // (the fused data-parallel MLP tail pushes its gradient tiles straight into the
+  // peers' receive areas; a separate region so it never aliases the one-shot
+  // allreduce's areas or generations)
+  std::string aux_handle(int64_t capacity_floats);
+  void aux_open(const std::vector<std::string>& handles);
+  bool has_aux() const { return aux_ready_; }
+  // [world, rank, slot_stride, spin_limit, gen_ptr, err_ptr, region_ptr x world]
+  std::vector<int64_t> aux_context() const;
+
   // ---- health ----
   // 0 healthy; 1 xGMI poll timed out; 2 RCCL async error; 3 aborted
   int error_state();
@@ -80,6 +90,12 @@ class Communicator {
   int* err_host_ = nullptr;                // host-mapped error word
   int* err_dev_ = nullptr;
   int64_t spin_limit_ = int64_t(1) << 24;  // ~2-4 s of s_sleep polling
+  // auxiliary region
+  char* aux_region_ = nullptr;
+  char* aux_peers_[kXgmiMaxRanks] = {};
+  uint32_t* aux_gen_ = nullptr;
+  int64_t aux_stride_ = 0;
+  bool aux_ready_ = false;
   // health
   std::atomic<int> state_{0};
   std::string message_;

@@ -11,6 +11,10 @@ constexpr int kXgmiMaxBlocks = 64;  // << 256 CUs: all blocks stay resident whil
 // flags: [2 slots][kXgmiMaxBlocks][kXgmiMaxRanks] uint32, padded to 64 KiB
 constexpr int64_t kXgmiFlagBytes = 64 * 1024;
 
+// Auxiliary (kernel-driven exchange) region: flags [2 slots][kDpMaxBlocks][kXgmiMaxRanks]
+// uint32 in the same 64 KiB header, then the same receive-area layout.
+constexpr int kDpMaxBlocks = 128;
+
 // Region of one rank: flags, then receive areas [2 slots][kXgmiMaxRanks][slot_stride] fp32.
 inline int64_t xgmi_region_bytes(int64_t slot_stride_floats) {
   return kXgmiFlagBytes + 2 * (int64_t)kXgmiMaxRanks * slot_stride_floats * 4;

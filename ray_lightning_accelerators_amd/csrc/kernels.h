@@ -133,8 +133,17 @@ struct MLP3Args {
   const float* lr_ptr;
   int adamw;
   int64_t* stamps;
+  // fused data-parallel tail (kMLP3StepDP): the comm engine's auxiliary peer
+  // region (csrc/comm/communicator.h aux_context)
+  char* dp_regions[8];
+  uint32_t* dp_gen;         // [128] per-block generations (local device memory)
+  int* dp_err;              // host-mapped error word
+  int64_t dp_stride;        // floats per (slot, rank) receive area (>= param count)
+  int64_t dp_spin;          // poll bound
+  int dp_rank, dp_world;
 };
-enum MLP3Kind { kMLP3Step = 0, kMLP3Head = 1, kMLP3TailGrad = 2, kMLP3TailAdam = 3, kMLP3Prime = 4 };
+enum MLP3Kind { kMLP3Step = 0, kMLP3Head = 1, kMLP3TailGrad = 2, kMLP3TailAdam = 3, kMLP3Prime = 4,
+                kMLP3StepDP = 5 };
 int launch_mlp3(const MLP3Args& a, int kind, hipStream_t stream);
 int mlp3_act_rows(int L1, int L2);
 

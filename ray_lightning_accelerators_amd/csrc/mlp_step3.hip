@@ -40,11 +40,15 @@
 #include "common.h"
 #include "kernels.h"
 #include "mlp_common.h"
+#include "comm/xgmi.h"
 
 namespace rla {
 namespace {
 
 using namespace mlp;
+using comm::kDpMaxBlocks;
+using comm::kXgmiFlagBytes;
+using comm::kXgmiMaxRanks;
 
 constexpr int kThreads = 512;
 constexpr int kWaves = 8;
@@ -53,7 +57,7 @@ constexpr int kXSS = 24;   // LDS row stride of a 16-pixel X slice (bf16)
 constexpr int kBMax = 256;
 constexpr int kCnt = 5;  // counters: [0, 5) current state, [5, 10) the head's advanced copy
 
-enum TailMode { kFused = 0, kGrad = 1, kAdam = 2, kPrime = 3 };
+enum TailMode { kFused = 0, kGrad = 1, kAdam = 2, kPrime = 3, kFusedDP = 4 };
 
 // rows of the `act` hand-off buffer ([rows][Bp] bf16)
 template <int L1, int L2>
@@ -434,84 +438,80 @@ struct SmallTasks {
   static constexpr int NBLK = (NTASK + TN1 - 1) / TN1;  // tail blocks have TN1 waves
 };
 
-// One wave: a 16x16 tile of dW2 or dW3, or 64 biases: gradient from the head's
-// transposes, then Adam (FUSED) or a plain gradient store (GRAD).
+// One wave's share of the small parameters: a 16x16 tile of dW2 or dW3 (4
+// values per lane), or 64 biases (1 per lane).  small_compute produces the
+// gradient values (+ prefetched Adam state); small_finalize applies Adam (or
+// stores gradients).  The fused data-parallel tail exchanges the values over
+// xGMI between the two halves.
+struct SmallRes {
+  float v[4], pv[4], mv[4], vv[4];
+  int64_t gi[4];
+  bool valid[4];
+  int kind;  // 0 W2 tile, 1 W3 tile, 2 bias, -1 idle lane / wave
+  int rowv, colv;
+};
+
 template <int L1, int L2>
-__device__ __forceinline__ void small_task(const MLP3Args& a, int mode, int task, const AdamScal& o) {
+__device__ __forceinline__ void small_compute(const MLP3Args& a, bool prefetch_adam, int task, SmallRes& r) {
   using O = Off<L1, L2>;
   using A = Act<L1, L2>;
   using S = SmallTasks<L1, L2>;
   const int lane = threadIdx.x & 63, r16 = lane & 15, g = lane >> 4;
   const int Bp = (a.B + 31) / 32 * 32;
   const __bf16* ACT = reinterpret_cast<const __bf16*>(a.act);
-  __bf16* SHW = reinterpret_cast<__bf16*>(a.shadow);
-  const bool fused = mode == kFused;
+  r.kind = -1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    r.v[i] = r.pv[i] = r.mv[i] = r.vv[i] = 0.f;
+    r.gi[i] = 0;
+    r.valid[i] = false;
+  }
   if (task < S::NTILE) {
-    int64_t gi[4];
-    bool valid[4];
-    int rowv, colv;
     const __bf16 *arow, *brow;
     if (task < S::NT_W2) {  // dW2[n][m] = sum_b dH2[b][n] H1[b][m]
       const int nt = task % S::TN2, ct = task / S::TN2;
-      rowv = nt * 16 + 4 * g;
-      colv = ct * 16 + r16;
+      r.kind = 0;
+      r.rowv = nt * 16 + 4 * g;
+      r.colv = ct * 16 + r16;
       arow = ACT + (int64_t)(A::DH2T + nt * 16 + r16) * Bp;
       brow = ACT + (int64_t)(A::H1T + ct * 16 + r16) * Bp;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) { gi[i] = O::W2 + (int64_t)(rowv + i) * L1 + colv; valid[i] = true; }
+      for (int i = 0; i < 4; ++i) { r.gi[i] = O::W2 + (int64_t)(r.rowv + i) * L1 + r.colv; r.valid[i] = true; }
     } else {  // dW3[j][n] = sum_b dZ[b][j] H2[b][n]
       const int nt = task - S::NT_W2;
-      rowv = 4 * g;
-      colv = nt * 16 + r16;
+      r.kind = 1;
+      r.rowv = 4 * g;
+      r.colv = nt * 16 + r16;
       arow = ACT + (int64_t)(A::DZT + r16) * Bp;
       brow = ACT + (int64_t)(A::H2T + nt * 16 + r16) * Bp;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        valid[i] = (rowv + i) < kNC;
-        gi[i] = O::W3 + (int64_t)(valid[i] ? rowv + i : 0) * L2 + colv;
+        r.valid[i] = (r.rowv + i) < kNC;
+        r.gi[i] = O::W3 + (int64_t)(r.valid[i] ? r.rowv + i : 0) * L2 + r.colv;
       }
     }
-    float pv[4], mv[4], vv[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      pv[i] = mv[i] = vv[i] = 0.f;
-      if (fused && valid[i]) { pv[i] = a.params[gi[i]]; mv[i] = a.exp_avg[gi[i]]; vv[i] = a.exp_avg_sq[gi[i]]; }
-    }
+    for (int i = 0; i < 4; ++i)
+      if (prefetch_adam && r.valid[i]) {
+        r.pv[i] = a.params[r.gi[i]]; r.mv[i] = a.exp_avg[r.gi[i]]; r.vv[i] = a.exp_avg_sq[r.gi[i]];
+      }
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int ks = 0; ks < Bp / 32; ++ks) {
       const int b0 = ks * 32 + 8 * g;
       acc = mfma16(ld8(arow + b0), ld8(brow + b0), acc);
     }
-    bf16x4 sh4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      sh4[i] = (__bf16)0.f;
-      if (!valid[i]) continue;
-      if (fused) {
-        const float p_ = adam1(pv[i], acc[i], mv[i], vv[i], o);
-        a.params[gi[i]] = p_;
-        a.exp_avg[gi[i]] = mv[i];
-        a.exp_avg_sq[gi[i]] = vv[i];
-        SHW[gi[i]] = (__bf16)p_;
-        sh4[i] = (__bf16)p_;
-      } else {
-        a.grads[gi[i]] = acc[i];
-      }
-    }
-    if (fused) {
-      if (task < S::NT_W2) *reinterpret_cast<bf16x4*>(SHW + O::W2T + (int64_t)colv * L2 + rowv) = sh4;
-      else *reinterpret_cast<bf16x4*>(SHW + O::W3T + (int64_t)colv * 16 + rowv) = sh4;
-    }
+    for (int i = 0; i < 4; ++i) r.v[i] = acc[i];
   } else {  // 64 biases per wave: row sums of dH1^T / dH2^T / dZ^T
     const int e = (task - S::NTILE) * 64 + lane;
     if (e >= S::NBIAS) return;
     const __bf16* row;
-    int64_t gidx;
-    if (e < L1) { row = reinterpret_cast<const __bf16*>(a.dh1t) + (int64_t)e * Bp; gidx = O::B1 + e; }
-    else if (e < L1 + L2) { row = ACT + (int64_t)(A::DH2T + e - L1) * Bp; gidx = O::B2 + (e - L1); }
-    else { row = ACT + (int64_t)(A::DZT + e - L1 - L2) * Bp; gidx = O::B3 + (e - L1 - L2); }
-    float pv = 0.f, mv = 0.f, vv = 0.f;
-    if (fused) { pv = a.params[gidx]; mv = a.exp_avg[gidx]; vv = a.exp_avg_sq[gidx]; }
+    if (e < L1) { row = reinterpret_cast<const __bf16*>(a.dh1t) + (int64_t)e * Bp; r.gi[0] = O::B1 + e; }
+    else if (e < L1 + L2) { row = ACT + (int64_t)(A::DH2T + e - L1) * Bp; r.gi[0] = O::B2 + (e - L1); }
+    else { row = ACT + (int64_t)(A::DZT + e - L1 - L2) * Bp; r.gi[0] = O::B3 + (e - L1 - L2); }
+    r.kind = 2;
+    r.valid[0] = true;
+    if (prefetch_adam) { r.pv[0] = a.params[r.gi[0]]; r.mv[0] = a.exp_avg[r.gi[0]]; r.vv[0] = a.exp_avg_sq[r.gi[0]]; }
     float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     // 32 rows per group: four independent 16-byte loads in flight before any add
     // (a one-load-per-iteration loop made this wave the tail kernel's straggler)
@@ -524,17 +524,96 @@ __device__ __forceinline__ void small_task(const MLP3Args& a, int mode, int task
 #pragma unroll
         for (int j = 0; j < 8; ++j) s8[j] += (float)v[q][j];
     }
-    const float sum = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
-    if (fused) {
-      const float p_ = adam1(pv, sum, mv, vv, o);
-      a.params[gidx] = p_;
-      a.exp_avg[gidx] = mv;
-      a.exp_avg_sq[gidx] = vv;
-      SHW[gidx] = (__bf16)p_;
+    r.v[0] = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
+  }
+}
+
+template <int L1, int L2>
+__device__ __forceinline__ void small_finalize(const MLP3Args& a, bool adam, const SmallRes& r, const AdamScal& o) {
+  using O = Off<L1, L2>;
+  if (r.kind < 0) return;
+  __bf16* SHW = reinterpret_cast<__bf16*>(a.shadow);
+  bf16x4 sh4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    sh4[i] = (__bf16)0.f;
+    if (!r.valid[i]) continue;
+    if (adam) {
+      float m_ = r.mv[i], v_ = r.vv[i];
+      const float p_ = adam1(r.pv[i], r.v[i], m_, v_, o);
+      a.params[r.gi[i]] = p_;
+      a.exp_avg[r.gi[i]] = m_;
+      a.exp_avg_sq[r.gi[i]] = v_;
+      SHW[r.gi[i]] = (__bf16)p_;
+      sh4[i] = (__bf16)p_;
     } else {
-      a.grads[gidx] = sum;
+      a.grads[r.gi[i]] = r.v[i];
     }
   }
+  if (adam && r.kind == 0) *reinterpret_cast<bf16x4*>(SHW + O::W2T + (int64_t)r.colv * L2 + r.rowv) = sh4;
+  if (adam && r.kind == 1) *reinterpret_cast<bf16x4*>(SHW + O::W3T + (int64_t)r.colv * 16 + r.rowv) = sh4;
+}
+
+// ---------------------------------------------------------------------------
+// In-kernel xGMI exchange of the fused data-parallel tail (kind StepDP): every
+// block pushes its gradient values into the peers' receive areas (at their arena
+// index), raises its per-(slot, block, rank) generation flag on every rank,
+// waits for the same block of every other rank, and sums the W contributions in
+// fixed rank order -- the allreduce happens inside the optimizer epilogue.
+// Protocol and memory rules as in csrc/comm/xgmi_allreduce.hip (aux region).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t* dp_flag(char* region, int slot, int blk, int src) {
+  return reinterpret_cast<uint32_t*>(region) + ((size_t)slot * kDpMaxBlocks + blk) * kXgmiMaxRanks + src;
+}
+__device__ __forceinline__ float* dp_data(char* region, int slot, int src, int64_t stride) {
+  return reinterpret_cast<float*>(region + kXgmiFlagBytes) + ((int64_t)slot * kXgmiMaxRanks + src) * stride;
+}
+
+// all threads of the block; returns the receive slot; *fail set on a poll timeout
+__device__ __forceinline__ int dp_begin(const MLP3Args& a, uint32_t* sh_gen) {
+  if (threadIdx.x == 0) *sh_gen = a.dp_gen[blockIdx.x] + 1u;
+  __syncthreads();
+  return (int)(*sh_gen & 1u);
+}
+
+__device__ __forceinline__ void dp_signal_and_wait(const MLP3Args& a, uint32_t gen, int slot, int* sh_fail) {
+  __threadfence_system();
+  __syncthreads();
+  const int tid = threadIdx.x, blk = blockIdx.x;
+  if (tid == 0) *sh_fail = 0;
+  if (tid < a.dp_world)
+    __hip_atomic_store(dp_flag(a.dp_regions[tid], slot, blk, a.dp_rank), gen, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  __syncthreads();
+  if (tid < a.dp_world) {
+    uint32_t* f = dp_flag(a.dp_regions[a.dp_rank], slot, blk, tid);
+    int64_t spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != gen) {
+      if (++spins > a.dp_spin) {
+        *sh_fail = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (tid == 0) {
+    a.dp_gen[blk] = gen;
+    if (*sh_fail) __hip_atomic_store(a.dp_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+__device__ __forceinline__ void dp_push1(const MLP3Args& a, int slot, int64_t idx, float v) {
+  for (int r = 0; r < a.dp_world; ++r)
+    __builtin_nontemporal_store(v, dp_data(a.dp_regions[r], slot, a.dp_rank, a.dp_stride) + idx);
+}
+
+__device__ __forceinline__ float dp_sum1(const MLP3Args& a, int slot, int64_t idx) {
+  float s = 0.f;
+  for (int r = 0; r < a.dp_world; ++r)
+    s += __builtin_nontemporal_load(dp_data(a.dp_regions[a.dp_rank], slot, r, a.dp_stride) + idx);
+  return s;
 }
 
 // ADAM mode: flat Adam over every non-W1 parameter (after the allreduce).
@@ -571,8 +650,9 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
   __shared__ __attribute__((aligned(16))) __bf16 sW[L1 * kXSS];
   __shared__ AdamScal sh_o;
   const int tid = threadIdx.x, lane = tid & 63, ct = tid >> 6, r16 = lane & 15, g = lane >> 4;
-  const bool do_grad = mode == kFused || mode == kGrad;
-  const bool do_adam = mode == kFused || mode == kAdam;
+  const bool dp = mode == kFusedDP;
+  const bool do_grad = mode == kFused || mode == kGrad || dp;
+  const bool do_adam = mode == kFused || mode == kAdam || dp;
   const bool do_fwd = mode != kGrad;
   if (a.stamps && blockIdx.x == 0 && tid == 0) a.stamps[8] = __builtin_amdgcn_s_memrealtime();
   // every block reads the head's NEXT copy (never written in this launch);
@@ -586,8 +666,26 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
   if ((int)blockIdx.x >= kTiles) {  // small parameters (block-uniform branch)
     __syncthreads();
     const int sblk = (int)blockIdx.x - kTiles;
-    if (mode == kAdam) small_adam_flat<L1, L2>(a, sh_o, sblk, (int)gridDim.x - kTiles);
-    else small_task<L1, L2>(a, mode, sblk * TN1 + ct, sh_o);
+    if (mode == kAdam) {
+      small_adam_flat<L1, L2>(a, sh_o, sblk, (int)gridDim.x - kTiles);
+      return;
+    }
+    SmallRes r;
+    small_compute<L1, L2>(a, mode != kGrad, sblk * TN1 + ct, r);
+    if (mode == kFusedDP) {
+      __shared__ uint32_t sh_dgen;
+      __shared__ int sh_dfail;
+      const int dslot = dp_begin(a, &sh_dgen);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (r.valid[i]) dp_push1(a, dslot, r.gi[i], r.v[i]);
+      dp_signal_and_wait(a, sh_dgen, dslot, &sh_dfail);
+      const float scale = a.grad_scale;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (r.valid[i]) r.v[i] = dp_sum1(a, dslot, r.gi[i]) * scale;
+    }
+    small_finalize<L1, L2>(a, mode != kGrad, r, sh_o);
     return;
   }
   const int kt = blockIdx.x;
@@ -667,6 +765,23 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
     *reinterpret_cast<F4*>(a.grads + gidx) = gg;
     return;
   }
+  if (dp) {  // allreduce of this tile inside the epilogue (xGMI push / flag / fixed-order sum)
+    __shared__ uint32_t sh_dgen;
+    __shared__ int sh_dfail;
+    const int dslot = dp_begin(a, &sh_dgen);
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f mine = {acc[0], acc[1], acc[2], acc[3]};
+    for (int r = 0; r < a.dp_world; ++r)
+      __builtin_nontemporal_store(mine, reinterpret_cast<v4f*>(dp_data(a.dp_regions[r], dslot, a.dp_rank,
+                                                                       a.dp_stride) + gidx));
+    dp_signal_and_wait(a, sh_dgen, dslot, &sh_dfail);
+    v4f s = {0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < a.dp_world; ++r)
+      s += __builtin_nontemporal_load(
+          reinterpret_cast<const v4f*>(dp_data(a.dp_regions[a.dp_rank], dslot, r, a.dp_stride) + gidx));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = s[i] * a.grad_scale;
+  }
   if (do_adam) {
     const AdamScal o = sh_o;
 #pragma unroll
@@ -700,7 +815,10 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
 template <int L1, int L2>
 int dispatch3(const MLP3Args& a, int kind, hipStream_t stream) {
   constexpr int NT = 64 * (L1 / 16);
-  if (kind == kMLP3Step || kind == kMLP3Head) {
+  if (kind == kMLP3StepDP && (a.dp_world < 1 || a.dp_world > kXgmiMaxRanks || !a.dp_gen || !a.dp_err ||
+                              a.dp_stride < Off<L1, L2>::NP || kTiles + SmallTasks<L1, L2>::NBLK > kDpMaxBlocks))
+    return -3;
+  if (kind == kMLP3Step || kind == kMLP3Head || kind == kMLP3StepDP) {
     // the smallest chunk that covers the batch, as LDS allows
     bool launched = false;
     if constexpr (fits3<128, L1, L2>()) {
@@ -717,6 +835,7 @@ int dispatch3(const MLP3Args& a, int kind, hipStream_t stream) {
   }
   int mode = -1, grid = kTiles;
   if (kind == kMLP3Step) { mode = kFused; grid += SmallTasks<L1, L2>::NBLK; }
+  else if (kind == kMLP3StepDP) { mode = kFusedDP; grid += SmallTasks<L1, L2>::NBLK; }
   else if (kind == kMLP3TailGrad) { mode = kGrad; grid += SmallTasks<L1, L2>::NBLK; }
   else if (kind == kMLP3Prime) mode = kPrime;
   else if (kind == kMLP3TailAdam) {

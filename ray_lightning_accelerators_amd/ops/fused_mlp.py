@@ -11,7 +11,7 @@ Parameter arena layout (== ``nn.Linear`` state_dict order of
 from __future__ import annotations
 
 import math
-from typing import Dict, Optional, Tuple
+from typing import Dict, Optional, Sequence, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -217,7 +217,7 @@ def mlp_train_step2(
         mlp_refresh_shadow(params, shadow, L1, L2)
 
 
-MLP3_STEP, MLP3_HEAD, MLP3_TAIL_GRAD, MLP3_TAIL_ADAM, MLP3_PRIME = range(5)
+MLP3_STEP, MLP3_HEAD, MLP3_TAIL_GRAD, MLP3_TAIL_ADAM, MLP3_PRIME, MLP3_STEP_DP = range(6)
 W1_TILES = IN_FEATURES // 16
 
 
@@ -267,17 +267,21 @@ def mlp3_launch(
     lr_tensor: Optional[torch.Tensor] = None,
     adamw: bool = False,
     stamps: Optional[torch.Tensor] = None,
+    dp_ctx: Optional[Sequence[int]] = None,
 ) -> None:
     """One v3 launch (GPU only).  ``kind``: MLP3_STEP (head + fused tail, world size 1),
     MLP3_HEAD / MLP3_TAIL_GRAD (gradients, before the allreduce), MLP3_TAIL_ADAM
     (Adam with ``grad_scale`` + next-step layer-1 partial, after it), MLP3_PRIME
     (layer-1 pre-activations of the pending batch from the current weights; the
-    caller zeroes ``h1pre`` first).  ``order`` is [2, n_batches * B]: the current
+    caller zeroes ``h1pre`` first), MLP3_STEP_DP (head + tail whose Adam epilogue
+    sums the gradient tiles of all ranks over xGMI itself; ``dp_ctx`` is
+    ``NativeCommunicator.dp_context``).  ``order`` is [2, n_batches * B]: the current
     and the next epoch's sample order (counters[4] selects)."""
     require().mlp3(
         int(kind), x_u8, labels, order, counters, int(n_batches), int(B), int(L1), int(L2), params, grads, exp_avg,
         exp_avg_sq, shadow, dh1t, xring, h1pre, act, yring, stats, bool(advance_step), float(lr), float(betas[0]),
         float(betas[1]), float(eps), float(weight_decay), float(grad_scale), lr_tensor, bool(adamw), stamps,
+        [int(v) for v in (dp_ctx or ())],
     )
 
 

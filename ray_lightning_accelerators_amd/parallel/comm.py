@@ -133,6 +133,35 @@ class NativeCommunicator:
     def xgmi_capacity(self) -> int:
         return int(self._c.xgmi_capacity) if self.xgmi else 0
 
+    def dp_context(self, capacity_floats: int) -> Optional[list]:
+        """Open the auxiliary peer region that a compute kernel exchanges through
+        directly (the fused data-parallel MLP tail pushes its gradient tiles into
+        every peer's receive area from its Adam epilogue).  Collective; returns the
+        kernel context ``[world, rank, stride, spin, gen, err, region_0..]`` or None
+        on every rank when any rank could not map the peers (caller falls back to
+        the communicator's allreduce)."""
+        if not self.xgmi or self.world == 1:
+            return None
+        if self._c.has_aux:
+            return list(self._c.aux_context())
+        ok = True
+        handle = b""
+        try:
+            handle = self._c.aux_handle(int(capacity_floats))
+        except RuntimeError:
+            ok = False
+        handles = [None] * self.world
+        dist.all_gather_object(handles, handle if ok else b"", group=self.group)
+        ok = ok and all(h for h in handles)
+        if ok:
+            try:
+                self._c.aux_open(handles)
+            except RuntimeError:
+                ok = False
+        if not _agree(ok, self.group):
+            return None
+        return list(self._c.aux_context())
+
     # ------------------------------------------------------- collectives
     def allreduce_(self, t: torch.Tensor, average: bool = False) -> torch.Tensor:
         if self.world == 1:

@@ -14,8 +14,10 @@ re-designed for MI355X instead of translating PL's DDP loop:
   32/64 config -- far below the ~1 MiB where splitting pays on 7 xGMI links);
 * world size 1: TWO launches per step (csrc/mlp_step3.hip: head + 49-workgroup
   tail; Adam fused into both, the next step's layer 1 computed by the tail);
-  world size > 1: head -> tail(grad) -> allreduce(SUM) -> tail(adam) with the
-  1/world average folded into ``grad_scale``;
+  world size > 1: with a ``dp_context`` the same two launches, the tail
+  exchanging each gradient tile with the peers over xGMI inside its Adam
+  epilogue (kind StepDP); otherwise head -> tail(grad) -> allreduce(SUM) ->
+  tail(adam), the 1/world average folded into ``grad_scale``;
 * the step's device work can be captured into a hipGraph (``capture``): batch
   cursor, step counter, ring slot and epoch buffer live on the device, so
   replays advance by themselves.
@@ -26,7 +28,7 @@ oracle of the GPU tests) with identical batch order and optimizer semantics.
 from __future__ import annotations
 
 import math
-from typing import Callable, Dict, Optional
+from typing import Callable, Dict, Optional, Sequence
 
 import torch
 import torch.distributed as dist
@@ -69,10 +71,15 @@ class FusedMLPEngine:
         seed: int = 0,
         kernel_version: int = 3,
         buffers: Optional[Dict[str, torch.Tensor]] = None,
+        dp_context: Optional[Sequence[int]] = None,
     ):
         """``buffers``: optional external fp32 tensors ``params`` / ``grads`` /
         ``exp_avg`` / ``exp_avg_sq`` (e.g. views of a Trainer's parameter arena,
-        so the nn.Module parameters stay the engine's master weights)."""
+        so the nn.Module parameters stay the engine's master weights).
+        ``dp_context``: ``NativeCommunicator.dp_context(...)`` -- world size > 1
+        then runs the fused data-parallel step (the tail kernel exchanges its
+        gradient tiles with the peers over xGMI inside the Adam epilogue: two
+        launches per step, no separate allreduce)."""
         if not fused_mlp.mlp_supported(layer_1, layer_2):
             raise ValueError(f"no fused kernel for layer sizes {layer_1}/{layer_2}")
         if not 1 <= batch_size <= 256:
@@ -84,6 +91,12 @@ class FusedMLPEngine:
         self.world_size, self.rank = int(world_size), int(rank)
         self.allreduce = allreduce
         self.kernel_version = int(kernel_version)
+        self.dp_ctx = None
+        if dp_context is not None and self.world_size > 1 and self.device.type == "cuda" and self.kernel_version == 3:
+            ctx = [int(v) for v in dp_context]
+            if ctx[0] != self.world_size or ctx[1] != self.rank:
+                raise ValueError("dp_context belongs to a different (world, rank)")
+            self.dp_ctx = ctx
         n = fused_mlp.mlp_param_count(self.L1, self.L2)
         if buffers is not None:
             for k in ("params", "grads", "exp_avg", "exp_avg_sq"):
@@ -243,6 +256,9 @@ class FusedMLPEngine:
             kw = self._kw3()
             if self.world_size == 1:
                 fused_mlp.mlp3_launch(fused_mlp.MLP3_STEP, stats=self.stats, **kw)
+            elif self.dp_ctx is not None:
+                fused_mlp.mlp3_launch(fused_mlp.MLP3_STEP_DP, stats=self.stats, grad_scale=1.0 / self.world_size,
+                                      dp_ctx=self.dp_ctx, **kw)
             else:
                 fused_mlp.mlp3_launch(fused_mlp.MLP3_HEAD, stats=self.stats, **kw)
                 fused_mlp.mlp3_launch(fused_mlp.MLP3_TAIL_GRAD, **kw)
