@@ -141,7 +141,10 @@ def make_native(args, world, rank, dev, x, y):
         ok = eng.capture(args.graph_steps)
         if not ok and rank == 0:
             print("hipGraph capture failed; running eager", file=sys.stderr)
-    return eng.run, (lambda: float(eng.recent_stats(20)[:, 0].mean()))
+    def replica_checksum():
+        return float(eng.params.double().sum()) + 1e-3 * float(eng.params.double().abs().sum())
+
+    return eng.run, (lambda: float(eng.recent_stats(20)[:, 0].mean())), replica_checksum
 
 
 def make_torch(args, world, rank, dev, x, y):
@@ -263,7 +266,8 @@ def main():
     else:
         x, y = synthetic_mnist(args.n_data, seed=0)
         maker = make_native if args.impl == "native" else make_torch
-    run, last_loss = maker(args, world, rank, dev, x, y)
+    run, last_loss, *extra = maker(args, world, rank, dev, x, y)
+    replica_checksum = extra[0] if extra else None
 
     run(args.warmup)
     barrier(world)
@@ -283,6 +287,12 @@ def main():
         comm = get_native_comm(create=False)
         if comm is not None:
             comm.check()  # a timed-out xGMI poll or RCCL async error invalidates the run
+        if replica_checksum is not None:
+            # data-parallel replicas must still hold identical weights after the timed steps
+            sums = [None] * world
+            dist.all_gather_object(sums, replica_checksum())
+            if any(v != sums[0] for v in sums):
+                raise RuntimeError(f"replicas diverged: {sums}")
     samples = args.steps * args.batch_size * world
     value = samples / elapsed
     loss = last_loss()
