@@ -89,16 +89,18 @@ class RayAccelerator(DataParallelAccelerator):
         init_hook: function run on every worker right after creation.
         bucket_cap_mb: DDP gradient bucket size (default 8 MiB, tuned for xGMI).
         grad_dtype: ``"fp32"`` or ``"bf16"`` gradient communication.
+        config / **knobs: :class:`~ray_lightning_accelerators_amd.config.RLAConfig`
+            (or individual fields, e.g. ``allreduce_algo="rccl"``); default env ``RLA_*``.
     """
 
     nickname = "ddp_ray"
 
     def __init__(self, num_workers: int = 1, num_cpus_per_worker: int = 1, use_gpu: bool = False,
                  init_hook: Optional[Callable] = None, cpus_per_worker: Optional[int] = None,
-                 bucket_cap_mb: Optional[float] = None, grad_dtype: str = "fp32",
-                 fused_optimizer: bool = True):
+                 bucket_cap_mb: Optional[float] = None, grad_dtype: Optional[str] = None,
+                 fused_optimizer: bool = True, config=None, **knobs):
         super().__init__(trainer=None, use_gpu=use_gpu, bucket_cap_mb=bucket_cap_mb, grad_dtype=grad_dtype,
-                         fused_optimizer=fused_optimizer)
+                         fused_optimizer=fused_optimizer, config=config, **knobs)
         self.num_workers = int(num_workers)
         self.num_cpus_per_worker = cpus_per_worker if cpus_per_worker is not None else num_cpus_per_worker
         self.use_gpu = use_gpu

@@ -23,6 +23,7 @@ from typing import Callable, List, Optional
 
 import torch
 
+from ..config import RLAConfig, log_config, set_config
 from .. import horovod as hvd
 from .. import runtime as ray
 from ..lightning.accelerators import Accelerator
@@ -133,13 +134,16 @@ CustomRayExecutor = HorovodRayExecutor
 
 
 class HorovodRayAccelerator(Accelerator):
-    """Args: ``num_hosts`` nodes x ``num_slots`` workers per node; ``use_gpu``."""
+    """Args: ``num_hosts`` nodes x ``num_slots`` workers per node; ``use_gpu``;
+    ``config`` / RLAConfig field kwargs (e.g. ``hvd_native=False``), default env ``RLA_*``."""
 
     nickname = "horovod_ray"
 
     def __init__(self, *args, num_hosts: int = 1, num_slots: int = 1, use_gpu: bool = False,
-                 fused_optimizer: bool = True, **kwargs):
+                 fused_optimizer: bool = True, config: Optional[RLAConfig] = None, **kwargs):
         super().__init__(trainer=None, use_gpu=use_gpu, fused_optimizer=fused_optimizer)
+        knobs = {k: kwargs.pop(k) for k in list(kwargs) if k in RLAConfig.__dataclass_fields__}
+        self.config = (config or RLAConfig.from_env()).replace(**knobs)
         self.num_hosts = num_hosts
         self.num_slots = num_slots
         self.executor: Optional[HorovodRayExecutor] = None
@@ -205,6 +209,7 @@ class HorovodRayAccelerator(Accelerator):
         trainer.accelerator = self
         if "PL_GLOBAL_SEED" in os.environ:
             seed_everything(int(os.environ["PL_GLOBAL_SEED"]))
+        set_config(self.config)
         hvd.init()
         if queue is not None:
             init_session(rank=hvd.rank(), queue=queue)
@@ -212,6 +217,7 @@ class HorovodRayAccelerator(Accelerator):
         trainer.local_rank = hvd.local_rank()
         trainer.world_size = hvd.size()
         rank_zero_only_state.rank = hvd.rank()
+        log_config(hvd.rank(), self.config)
         if self.use_gpu:
             trainer.root_gpu = hvd.local_rank()
             torch.cuda.set_device(trainer.root_gpu)

@@ -1,0 +1,169 @@
+"""Typed run-time configuration of the MI355X data plane.
+
+The reference is configured by constructor kwargs only
+(``ray_lightning/ray_ddp.py:79-83``, ``ray_horovod.py:82-87``) plus
+``PL_GLOBAL_SEED`` (``ray_ddp.py:154-159``).  Those kwargs are kept unchanged;
+the knobs that exist only because this framework owns its data plane live in
+ONE dataclass, settable three ways (later wins):
+
+1. defaults below,
+2. environment ``RLA_<FIELD>`` (e.g. ``RLA_BUCKET_CAP_MB=4``),
+3. explicit kwargs (``RayAccelerator(..., allreduce_algo="rccl")`` or
+   ``RLAConfig.resolve(bucket_cap_mb=4)``).
+
+The driver resolves the config once; it travels to the workers with the
+accelerator and is installed there with :func:`set_config`, so every rank uses
+the same values even when the workers' environments differ.  Rank 0 logs it
+once at worker start (``describe``).
+"""
+from __future__ import annotations
+
+import dataclasses
+import logging
+import os
+from dataclasses import dataclass, field, fields
+from typing import Any, Dict, Optional
+
+log = logging.getLogger(__name__)
+
+ENV_PREFIX = "RLA_"
+
+_CHOICES = {
+    "grad_dtype": ("fp32", "bf16"),
+    "allreduce_algo": ("auto", "oneshot", "twoshot", "rccl", "torch"),
+    "precision": ("32", "bf16"),
+}
+
+# legacy env names kept working (first release used these spellings)
+_ALIASES = {"fused_optimizer": "RLA_FUSED_OPTIM"}
+
+
+@dataclass
+class RLAConfig:
+    """Data-plane knobs.  Every field maps to env ``RLA_<FIELD upper-case>``."""
+
+    # DDP gradient bucket cap in MiB: large enough to amortise the ~us xGMI flag
+    # barrier, small enough that the first bucket leaves early in backward
+    bucket_cap_mb: float = 8.0
+    # gradient wire dtype: bf16 halves the bytes on the 7 xGMI links
+    grad_dtype: str = "fp32"
+    # allreduce selection for fp32 buckets: auto = xGMI one-shot up to
+    # ``xgmi_bytes``, xGMI two-shot up to ``twoshot_bytes``, RCCL above
+    allreduce_algo: str = "auto"
+    # one-shot receive area per rank (bytes); the MNIST gradient is 109-532 KiB
+    xgmi_bytes: int = 2 << 20
+    # two-shot scratch per rank (bytes); 0 disables two-shot in "auto"
+    twoshot_bytes: int = 0
+    # native C++ communicator / reducer / Horovod fusion engine (else torch.distributed)
+    native_comm: bool = True
+    native_reducer: bool = True
+    hvd_native: bool = True
+    # fused single-launch HIP optimizers over the parameter arena
+    fused_optimizer: bool = True
+    # MNIST fused step: exchange gradients inside the tail kernel (world > 1)
+    fused_dp: bool = True
+    # capture the resident MNIST step into hipGraphs
+    use_hip_graph: bool = True
+    # generic-model compute precision ("32" or "bf16" autocast)
+    precision: str = "32"
+    # bounded polls of the xGMI kernels (iterations) and the watchdog period (ms)
+    spin_limit: int = 1 << 24
+    watchdog_ms: int = 100
+    # debug: verify that every DDP bucket the comm stream reads equals what the
+    # compute stream produced (stream-ordering race detector)
+    check_streams: bool = False
+    extra: Dict[str, Any] = field(default_factory=dict)
+
+    # --------------------------------------------------------------- build
+    def __post_init__(self) -> None:
+        for k, allowed in _CHOICES.items():
+            v = str(getattr(self, k))
+            if v not in allowed:
+                raise ValueError(f"{k}={v!r}: expected one of {allowed}")
+            setattr(self, k, v)
+        if self.bucket_cap_mb <= 0:
+            raise ValueError("bucket_cap_mb must be > 0")
+
+    @staticmethod
+    def env_name(name: str) -> str:
+        return ENV_PREFIX + name.upper()
+
+    @classmethod
+    def from_env(cls, environ: Optional[Dict[str, str]] = None) -> "RLAConfig":
+        env = os.environ if environ is None else environ
+        kw: Dict[str, Any] = {}
+        for f in fields(cls):
+            if f.name == "extra":
+                continue
+            for key in (cls.env_name(f.name), _ALIASES.get(f.name)):
+                if key and key in env:
+                    kw[f.name] = _parse(f.type, env[key], key)
+                    break
+        return cls(**kw)
+
+    @classmethod
+    def resolve(cls, **overrides) -> "RLAConfig":
+        """defaults < env < explicit (non-None) kwargs."""
+        cfg = cls.from_env()
+        return cfg.replace(**{k: v for k, v in overrides.items() if v is not None})
+
+    def replace(self, **kw) -> "RLAConfig":
+        names = {f.name for f in fields(self)}
+        bad = set(kw) - names
+        if bad:
+            raise TypeError(f"unknown config field(s): {sorted(bad)}")
+        return dataclasses.replace(self, **kw)
+
+    def to_env(self) -> Dict[str, str]:
+        out = {}
+        for f in fields(self):
+            if f.name == "extra":
+                continue
+            v = getattr(self, f.name)
+            out[self.env_name(f.name)] = ("1" if v else "0") if isinstance(v, bool) else str(v)
+        return out
+
+    def describe(self) -> str:
+        items = ", ".join(f"{f.name}={getattr(self, f.name)!r}" for f in fields(self) if f.name != "extra")
+        return f"RLAConfig({items})"
+
+
+def _parse(typ, raw: str, key: str):
+    t = typ if isinstance(typ, str) else getattr(typ, "__name__", str(typ))
+    try:
+        if t == "bool":
+            low = raw.strip().lower()
+            if low in ("1", "true", "yes", "on"):
+                return True
+            if low in ("0", "false", "no", "off", ""):
+                return False
+            raise ValueError(raw)
+        if t == "int":
+            return int(float(raw)) if "e" in raw.lower() else int(raw, 0)
+        if t == "float":
+            return float(raw)
+        return raw
+    except ValueError as e:
+        raise ValueError(f"env {key}={raw!r} is not a valid {t}") from e
+
+
+_current: Optional[RLAConfig] = None
+
+
+def get_config() -> RLAConfig:
+    """The process's config: the one installed by the accelerator, else env."""
+    global _current
+    if _current is None:
+        _current = RLAConfig.from_env()
+    return _current
+
+
+def set_config(cfg: Optional[RLAConfig]) -> None:
+    """Install ``cfg`` for this process (None: re-read the environment lazily)."""
+    global _current
+    _current = cfg
+
+
+def log_config(rank: int, cfg: Optional[RLAConfig] = None) -> None:
+    if rank == 0:
+        log.info((cfg or get_config()).describe())

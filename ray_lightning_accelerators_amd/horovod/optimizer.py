@@ -22,6 +22,7 @@ import torch
 import torch.distributed as dist
 
 from .. import ops
+from ..config import get_config
 from . import Average, Compression, Sum, _comm_tensor, size
 
 
@@ -70,7 +71,7 @@ class _FusionState:
         # thread + comm stream.  Created here, where every rank is in lock-step.
         self.engine = None
         if (size() > 1 and compression is Compression.none and params and params[0].is_cuda
-                and os.environ.get("RLA_HVD_NATIVE", "1") == "1"):
+                and get_config().hvd_native):
             from ..parallel.comm import get_native_comm
 
             comm = get_native_comm()

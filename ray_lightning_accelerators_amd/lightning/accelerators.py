@@ -15,6 +15,7 @@ from typing import Any, List, Optional
 import torch
 import torch.distributed as dist
 
+from ..config import RLAConfig, get_config, log_config, set_config
 from .utilities import log, move_to_device, rank_zero_only_state, seed_everything
 
 
@@ -100,7 +101,7 @@ class Accelerator:
                 self.arena = ParamArena(model, params)
             except ValueError:
                 self.arena = None
-        if self.arena is not None and self.fused_optimizer and os.environ.get("RLA_FUSED_OPTIM", "1") == "1":
+        if self.arena is not None and self.fused_optimizer and get_config().fused_optimizer:
             for opt in optimizers:
                 if can_fuse(opt, self.arena):
                     fuse_optimizer(opt, self.arena, grad_scale_fn=lambda: self.grad_scale)
@@ -203,12 +204,19 @@ class DataParallelAccelerator(Accelerator):
     nickname = "ddp"
 
     def __init__(self, trainer=None, use_gpu: bool = False, bucket_cap_mb: Optional[float] = None,
-                 grad_dtype: str = "fp32", fused_optimizer: bool = True):
+                 grad_dtype: Optional[str] = None, fused_optimizer: bool = True,
+                 config: Optional[RLAConfig] = None, **knobs):
+        """``bucket_cap_mb`` / ``grad_dtype`` / any other :class:`RLAConfig` field
+        (``allreduce_algo=...``, ``use_hip_graph=...``) override ``config`` (default:
+        env ``RLA_*``); the resolved config travels to the workers."""
         super().__init__(trainer, use_gpu=use_gpu, fused_optimizer=fused_optimizer)
         self.global_rank = 0
         self.world_size = 1
-        self.bucket_cap_mb = bucket_cap_mb
-        self.grad_dtype = grad_dtype
+        base = config if config is not None else RLAConfig.from_env()
+        self.config = base.replace(**{k: v for k, v in dict(bucket_cap_mb=bucket_cap_mb, grad_dtype=grad_dtype,
+                                                             **knobs).items() if v is not None})
+        self.bucket_cap_mb = self.config.bucket_cap_mb
+        self.grad_dtype = self.config.grad_dtype
         self.ddp_address: Optional[str] = None
         self.results = None
         self.model_state_dict = None
@@ -240,7 +248,7 @@ class DataParallelAccelerator(Accelerator):
             self.sync = None
             return
         fused = any(getattr(o, "_rla_fused", False) for o in self.trainer.optimizers)
-        if self.arena.data.is_cuda and os.environ.get("RLA_NATIVE_COMM", "1") == "1":
+        if self.arena.data.is_cuda and get_config().native_comm:
             # bring the native data plane (RCCL + validated xGMI one-shot) up on every
             # rank together, before backward hooks start issuing collectives
             from ..parallel.comm import get_native_comm
@@ -253,11 +261,13 @@ class DataParallelAccelerator(Accelerator):
 
     def ddp_train(self, process_idx: int, model):
         t = self.trainer
+        set_config(self.config)  # every rank runs the driver-resolved knobs
         if "PL_GLOBAL_SEED" in os.environ:
             seed_everything(int(os.environ["PL_GLOBAL_SEED"]))
         self.set_world_ranks(process_idx)
         rank_zero_only_state.rank = t.global_rank
         self.init_ddp_connection(t.global_rank, t.world_size)
+        log_config(t.global_rank, self.config)
         self.init_device(process_idx, t.global_rank == 0)
         if t.sync_batchnorm and t.world_size > 1 and dist.is_initialized():
             # PL: Trainer(sync_batchnorm=True) -> BN statistics all-reduced across ranks

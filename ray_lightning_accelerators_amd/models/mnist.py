@@ -6,11 +6,16 @@ tests/test_ddp.py:11): MLP 784 -> layer_1 -> layer_2 -> 10 with ReLU and
 log_softmax, NLL loss, Adam(lr), metrics ``ptl/train_loss``,
 ``ptl/train_accuracy``, ``ptl/val_loss``, ``ptl/val_accuracy``.
 
-On an MI355X the training step of this module runs as ONE fused HIP kernel
-(``configure_fused_step``): the trainer hands it the epoch's sampler indices
-once, the images stay resident in HBM as uint8, and each step is a single
-launch (world size 1) or launch + flat-bucket allreduce + fused Adam (world
-size > 1).  CPU / unsupported shapes use the ordinary autograd path.
+On an MI355X the training step of this module runs on the fused HIP engine
+(``configure_fused_step`` -> parallel/mlp_engine.py, csrc/mlp_step3.hip): the
+trainer hands it the epoch's sampler indices once, the images stay resident in
+HBM as uint8, and each step is TWO launches -- a head kernel (forward, loss,
+backward of the small layers, next-batch gather) and a 49+ workgroup tail
+(dW1, Adam, the next step's layer-1 partial).  At world size > 1 the tail also
+exchanges the gradient tiles with the peers over xGMI inside its Adam epilogue
+(``RLAConfig.fused_dp``), else head / tail / allreduce / tail.  Batches the
+resident path cannot serve (e.g. user transforms) use a one-launch fp32-input
+kernel; CPU / unsupported shapes use the ordinary autograd path.
 """
 from __future__ import annotations
 
@@ -21,6 +26,7 @@ import torch
 import torch.nn.functional as F
 from torch.utils.data import DataLoader, Subset, random_split
 
+from ..config import get_config
 from ..lightning import LightningModule
 from ..lightning.metrics import Accuracy
 from ..ops import fused_mlp
@@ -167,10 +173,17 @@ class FusedMNISTStep:
         g = self.opt.param_groups[0]
         bufs = dict(params=self.arena.data[: self.np], grads=self.arena.grad[: self.np],
                     exp_avg=self.gs.m[: self.np], exp_avg_sq=self.gs.v[: self.np])
+        dp_ctx = None
+        if self.world > 1 and get_config().fused_dp:
+            from ..parallel.comm import get_native_comm
+
+            comm = get_native_comm()  # every rank reaches here together (first epoch)
+            if comm is not None:
+                dp_ctx = comm.dp_context(self.np)
         eng = FusedMLPEngine(self.L1, self.L2, B, lr=float(g["lr"]), betas=tuple(g["betas"]), eps=g["eps"],
                              weight_decay=g["weight_decay"], device=self.dev, world_size=self.world,
                              rank=self.trainer.global_rank, allreduce=self._allreduce, buffers=bufs,
-                             stats_ring=self.stats.size(0))
+                             stats_ring=self.stats.size(0), dp_context=dp_ctx)
         eng.set_step(self.gs.step)
         eng.lr_tensor = self.lr_tensor  # LR schedulers update one device scalar
         eng.attach_dataset(self._u8, self._labels)

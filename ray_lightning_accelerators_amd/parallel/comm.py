@@ -27,6 +27,8 @@ from typing import Callable, Optional
 import torch
 import torch.distributed as dist
 
+from ..config import get_config
+
 _mod = None
 _mod_err: Optional[BaseException] = None
 
@@ -57,8 +59,17 @@ class NativeCommunicator:
     the current stream (graph-capturable); ``average=True`` divides by world."""
 
     def __init__(self, group=None, device: Optional[int] = None, use_rccl: bool = True,
-                 use_xgmi: bool = True, xgmi_bytes: int = 2 << 20, validate: bool = True,
-                 spin_limit: Optional[int] = None, watchdog_ms: int = 100):
+                 use_xgmi: bool = True, xgmi_bytes: Optional[int] = None, validate: bool = True,
+                 spin_limit: Optional[int] = None, watchdog_ms: Optional[int] = None):
+        """Unset knobs come from :func:`~ray_lightning_accelerators_amd.config.get_config`
+        (``allreduce_algo="rccl"`` disables the xGMI path, ``"oneshot"`` forbids RCCL for
+        buckets that fit the one-shot area)."""
+        cfg = get_config()
+        self.algo = cfg.allreduce_algo
+        xgmi_bytes = cfg.xgmi_bytes if xgmi_bytes is None else xgmi_bytes
+        spin_limit = cfg.spin_limit if spin_limit is None else spin_limit
+        watchdog_ms = cfg.watchdog_ms if watchdog_ms is None else watchdog_ms
+        use_xgmi = use_xgmi and self.algo != "rccl"
         mod = native_comm_module()
         if mod is None:
             raise RuntimeError(f"native comm extension (_comm) unavailable: {_mod_err!r}")
@@ -181,16 +192,24 @@ class NativeCommunicator:
             t.div_(self.world)
         return t
 
-    def allreduce_async(self, t: torch.Tensor, average: bool = False) -> "_StreamWork":
+    def allreduce_async(self, t: torch.Tensor, average: bool = False,
+                        probe: Optional[torch.Tensor] = None) -> "_StreamWork":
         """Allreduce on this communicator's high-priority side stream, ordered after
         the current stream's pending work (the gradient producer); ``wait()``
-        makes the then-current stream wait for it -- DDP bucket overlap."""
+        makes the then-current stream wait for it -- DDP bucket overlap.
+        ``probe`` (fp64 [4], debug): slots 1 / 2 receive the checksum of ``t`` as
+        the comm stream sees it before / after the collective."""
         if self._stream is None:
             self._stream = torch.cuda.Stream(device=t.device, priority=-1)
         cur = torch.cuda.current_stream(t.device)
         self._stream.wait_stream(cur)
         with torch.cuda.stream(self._stream):
+            if probe is not None:
+                probe[1] = t.double().sum()
             self.allreduce_(t, average=average)
+            if probe is not None:
+                probe[2] = t.double().sum()
+                probe.record_stream(self._stream)
         ev = torch.cuda.Event()
         ev.record(self._stream)
         t.record_stream(self._stream)
@@ -260,7 +279,8 @@ def get_native_comm(create: bool = True, **kw) -> Optional[NativeCommunicator]:
     """Process-wide communicator for the default group (GPU ranks only)."""
     global _default
     if _default is None and create and torch.cuda.is_available() and dist.is_initialized() \
-            and os.environ.get("RLA_NATIVE_COMM", "1") == "1" and native_comm_module() is not None:
+            and get_config().native_comm and get_config().allreduce_algo != "torch" \
+            and native_comm_module() is not None:
         _default = NativeCommunicator(**kw)
     return _default
 

@@ -16,13 +16,16 @@ Design for MI355X + RCCL over xGMI:
     with the multi-tensor cast kernel before the collective;
   * the 1/world average is NOT applied here when the optimizer is fused
     (``grad_scale`` of the fused Adam/SGD kernel) -- one less pass over HBM;
+  * debug race detector (``RLAConfig.check_streams`` / ``RLA_CHECK_STREAMS=1``,
+    SURVEY.md §5.2): every bucket is checksummed on the producer stream, on
+    the comm stream before and after the collective, and on the consumer
+    stream after ``wait``; a mismatch means a missing stream dependency;
   * unused parameters (no grad this step) simply leave their bucket
     incomplete; ``finish()`` launches such buckets synchronously, so no
     autograd-graph walk (PL 1.1's find_unused_parameters=True) is needed.
 """
 from __future__ import annotations
 
-import os
 from typing import List, Optional
 
 import torch
@@ -30,8 +33,9 @@ import torch.distributed as dist
 from torch import nn
 
 from .. import ops
+from ..config import get_config
 from .arena import ParamArena
-from .comm import allreduce_async
+from .comm import allreduce_async, get_native_comm
 
 
 class Bucket:
@@ -42,6 +46,7 @@ class Bucket:
         self.pending = len(param_ids)
         self.work = None
         self.comm_buf: Optional[torch.Tensor] = None
+        self.probe: Optional[torch.Tensor] = None  # check_streams debug checksums
 
 
 class GradSynchronizer:
@@ -55,6 +60,8 @@ class GradSynchronizer:
         self.average_in_optimizer = average_in_optimizer
         self.broadcast_buffers = broadcast_buffers and any(True for _ in module.buffers())
         self.enabled = True
+        self.check_streams = bool(get_config().check_streams)
+        self.probes_checked = 0
         cap = int(bucket_cap_mb * 1024 * 1024 / 4)
         self.buckets: List[Bucket] = []
         self.param_bucket: List[int] = [0] * len(arena.params)
@@ -75,7 +82,7 @@ class GradSynchronizer:
         # owns readiness counting, in-order launch on its comm stream, and events
         self._native = None
         if (self.world > 1 and process_group is None and grad_dtype == "fp32" and arena.grad.is_cuda
-                and os.environ.get("RLA_NATIVE_REDUCER", "1") == "1"):
+                and get_config().native_reducer and not get_config().check_streams):
             from .comm import get_native_comm, native_comm_module
 
             comm = get_native_comm()
@@ -172,6 +179,12 @@ class GradSynchronizer:
                 b.comm_buf = torch.empty(grad.numel(), dtype=torch.bfloat16, device=grad.device)
             ops.multi_copy([(grad, b.comm_buf)])
             b.work = dist.all_reduce(b.comm_buf, group=self.pg, async_op=True)
+        elif self.check_streams and grad.is_cuda and self.pg is None and get_native_comm() is not None:
+            # debug race detector: checksum of the bucket on the producer stream now,
+            # on the comm stream before/after the collective, on the consumer after wait
+            b.probe = torch.zeros(4, dtype=torch.float64, device=grad.device)
+            b.probe[0] = grad.double().sum()
+            b.work = get_native_comm().allreduce_async(grad, probe=b.probe)
         else:
             # GPU: the native engine's side stream (xGMI one-shot / RCCL); CPU: gloo
             b.work = allreduce_async(grad, group=self.pg)
@@ -195,10 +208,29 @@ class GradSynchronizer:
             if b.comm_buf is not None and self.grad_dtype == "bf16":
                 ops.multi_copy([(b.comm_buf, self.arena.grad[b.start:b.end])])
             b.work = None
+            if b.probe is not None:
+                b.probe[3] = self.arena.grad[b.start:b.end].double().sum()
+        if self.check_streams:
+            self._verify_probes()
         if not self.average_in_optimizer:
             ops.scale_(self.arena.grad, 1.0 / self.world)
         self._started = False
         self._next = 0
+
+    def _verify_probes(self) -> None:
+        """Host-side check of the stream-ordering probes (debug mode only: syncs)."""
+        for b in self.buckets:
+            if b.probe is None:
+                continue
+            p = b.probe.tolist()
+            b.probe = None
+            self.probes_checked += 1
+            if p[0] != p[1]:
+                raise RuntimeError(f"stream-ordering violation: bucket {b.index} was read by the comm stream "
+                                   f"before its producer finished (checksum {p[0]!r} vs {p[1]!r})")
+            if p[2] != p[3]:
+                raise RuntimeError(f"stream-ordering violation: bucket {b.index} was consumed before the "
+                                   f"collective finished (checksum {p[2]!r} vs {p[3]!r})")
 
     @property
     def grad_scale(self) -> float:
@@ -211,4 +243,4 @@ class GradSynchronizer:
 
 
 def default_bucket_cap_mb() -> float:
-    return float(os.environ.get("RLA_BUCKET_CAP_MB", "8"))
+    return float(get_config().bucket_cap_mb)

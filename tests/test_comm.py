@@ -144,9 +144,14 @@ def _gpu_worker(rank, world, port, q, mode):
             res["match"] = all(bool(torch.allclose(a, b, atol=1e-5)) for a, b in
                                zip(model.parameters(), ref.parameters()))
             res["batches"] = opt._hvd_state.engine.batches_executed if res["native_engine"] else 0
-        elif mode == "reducer":
+        elif mode in ("reducer", "reducer_check"):
             # GradSynchronizer on the C++ reducer: several in-order buckets, averaged grads
+            # (reducer_check: the Python path with the stream-ordering race detector on)
+            from ray_lightning_accelerators_amd.config import RLAConfig, set_config
             from ray_lightning_accelerators_amd.parallel import comm as comm_mod
+
+            if mode == "reducer_check":
+                set_config(RLAConfig(check_streams=True))
             from ray_lightning_accelerators_amd.parallel.arena import ParamArena
             from ray_lightning_accelerators_amd.parallel.ddp import GradSynchronizer
 
@@ -180,6 +185,7 @@ def _gpu_worker(rank, world, port, q, mode):
             res["match"] = all(bool(torch.allclose(p.grad, q.grad, atol=1e-6)) for p, q in
                                zip(model.parameters(), ref.parameters()))
             res["launched"] = sync._native.launched if sync._native is not None else 0
+            res["probes"] = sync.probes_checked
         elif mode in ("mlp_dp", "mlp_dp_timeout"):
             # fused data-parallel MLP step (gradient exchange inside the tail kernel)
             # vs. the split head / tail(grad) / allreduce / tail(adam) path
@@ -290,6 +296,14 @@ def test_ddp_native_reducer_two_ranks():
     for r, res in out.items():
         assert res["native_reducer"] and res["match"], (r, res)
         assert res["buckets"] >= 3 and res["launched"] == 2 * res["buckets"]
+
+
+@gpu
+def test_ddp_stream_ordering_checker_two_ranks():
+    out = _run_gpu("reducer_check")
+    for r, res in out.items():
+        assert not res["native_reducer"] and res["match"], (r, res)
+        assert res["probes"] == 2 * res["buckets"], (r, res)
 
 
 @gpu
