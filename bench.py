@@ -60,6 +60,8 @@ def parse():
                     help="optimizer steps per captured hipGraph (native); 0 = eager launches")
     ap.add_argument("--n-data", type=int, default=55000)
     ap.add_argument("--bucket-mb", type=float, default=8.0, help="resnet50 DDP bucket cap (MiB)")
+    ap.add_argument("--grad-dtype", choices=["fp32", "bf16"], default="fp32",
+                    help="resnet50 gradient wire dtype (bf16: converted inside the xGMI two-shot kernel)")
     ap.add_argument("--dp", choices=["fused", "split"], default="fused",
                     help="mnist N>1: 'fused' exchanges gradients inside the tail kernel over xGMI "
                          "(falls back to 'split' = head/tail/allreduce/tail when xGMI is unavailable)")
@@ -117,8 +119,10 @@ def make_native(args, world, rank, dev, x, y):
 
         comm = None
         if args.comm != "torch":
+            # one 109-532 KiB bucket per step: the one-shot area covers it, so no
+            # two-shot region is allocated
             comm = get_native_comm(use_xgmi=args.comm in ("auto", "xgmi"),
-                                   use_rccl=dist.get_backend() == "nccl")
+                                   use_rccl=dist.get_backend() == "nccl", twoshot_bytes=0)
         if comm is not None:
             if rank == 0:
                 print(comm.describe(), file=sys.stderr, flush=True)
@@ -217,7 +221,8 @@ def make_resnet(args, world, rank, dev, x, y):
             from ray_lightning_accelerators_amd.parallel.comm import get_native_comm
 
             get_native_comm()
-            sync = GradSynchronizer(model, arena, bucket_cap_mb=args.bucket_mb, average_in_optimizer=True)
+            sync = GradSynchronizer(model, arena, bucket_cap_mb=args.bucket_mb, grad_dtype=args.grad_dtype,
+                                    average_in_optimizer=True)
             sync.broadcast_parameters(0)
         opt = fuse_optimizer(torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5), arena,
                              grad_scale_fn=(lambda: sync.grad_scale) if sync is not None else None)

@@ -51,7 +51,7 @@ EXTENSIONS = {
         "libs": [],
     },
     "_comm": {
-        "hip": ["comm/xgmi_allreduce.hip", "comm/pack.hip"],
+        "hip": ["comm/xgmi_allreduce.hip", "comm/xgmi_twoshot.hip", "comm/pack.hip"],
         "cpp": ["comm/comm_bindings.cpp", "comm/communicator.cpp", "comm/fusion_engine.cpp", "comm/reducer.cpp"],
         "torch": True,
         "libs": ["rccl"],

@@ -52,8 +52,9 @@ class RLAConfig:
     allreduce_algo: str = "auto"
     # one-shot receive area per rank (bytes); the MNIST gradient is 109-532 KiB
     xgmi_bytes: int = 2 << 20
-    # two-shot scratch per rank (bytes); 0 disables two-shot in "auto"
-    twoshot_bytes: int = 0
+    # largest bucket (bytes) of the xGMI two-shot (reduce-scatter + all-gather);
+    # its region costs ~4x this per GPU (256 MiB of 288 GB); 0 disables two-shot
+    twoshot_bytes: int = 64 << 20
     # native C++ communicator / reducer / Horovod fusion engine (else torch.distributed)
     native_comm: bool = True
     native_reducer: bool = True

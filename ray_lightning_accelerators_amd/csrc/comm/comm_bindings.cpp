@@ -98,6 +98,41 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              TORCH_CHECK(t.scalar_type() == at::kFloat, "xGMI one-shot allreduce is fp32");
              c.allreduce_xgmi(t.data_ptr<float>(), t.numel(), cur_stream(t));
            })
+      .def("twoshot_handle", [](Communicator& c, int64_t cap) { return py::bytes(c.twoshot_handle(cap)); })
+      .def("twoshot_open",
+           [](Communicator& c, std::vector<py::bytes> hs) {
+             std::vector<std::string> v;
+             for (auto& h : hs) v.emplace_back(std::string(h));
+             c.twoshot_open(v);
+           })
+      .def_property_readonly("has_twoshot", &Communicator::has_twoshot)
+      .def_property_readonly("twoshot_capacity", &Communicator::twoshot_capacity)
+      .def("allreduce_twoshot",
+           [](Communicator& c, Tensor t, bool bf16_wire) {
+             check(t, "tensor");
+             TORCH_CHECK(t.scalar_type() == at::kFloat, "xGMI two-shot allreduce takes fp32 buckets");
+             c.allreduce_twoshot(t.data_ptr<float>(), t.numel(), bf16_wire, cur_stream(t));
+           },
+           py::arg("tensor"), py::arg("bf16_wire") = false)
+      .def("set_route_limits", &Communicator::set_route_limits, py::arg("oneshot_max_floats"),
+           py::arg("twoshot_max_floats"))
+      .def("route",
+           [](Communicator& c, Tensor t) {
+             check(t, "tensor");
+             return c.route(t.data_ptr<float>(), t.numel());
+           })
+      .def("allreduce_f32",
+           [](Communicator& c, Tensor t) {
+             check(t, "tensor");
+             TORCH_CHECK(t.scalar_type() == at::kFloat, "allreduce_f32 takes fp32 tensors");
+             c.allreduce_f32(t.data_ptr<float>(), t.numel(), cur_stream(t));
+           })
+      .def("allreduce_bf16wire",
+           [](Communicator& c, Tensor t) {
+             check(t, "tensor");
+             TORCH_CHECK(t.scalar_type() == at::kFloat, "bf16-wire allreduce takes fp32 tensors");
+             return c.allreduce_f32_bf16wire(t.data_ptr<float>(), t.numel(), cur_stream(t));
+           })
       .def("aux_handle", [](Communicator& c, int64_t cap) { return py::bytes(c.aux_handle(cap)); })
       .def("aux_open",
            [](Communicator& c, std::vector<py::bytes> hs) {

@@ -53,7 +53,10 @@ Communicator::~Communicator() {
   for (int r = 0; r < world_ && r < kXgmiMaxRanks; ++r) {
     if (peers_[r] && peers_[r] != region_) hipIpcCloseMemHandle(peers_[r]);
     if (aux_peers_[r] && aux_peers_[r] != aux_region_) hipIpcCloseMemHandle(aux_peers_[r]);
+    if (ts_peers_[r] && ts_peers_[r] != ts_region_) hipIpcCloseMemHandle(ts_peers_[r]);
   }
+  if (ts_region_) hipFree(ts_region_);
+  if (ts_gen_) hipFree(ts_gen_);
   if (region_) hipFree(region_);
   if (aux_region_) hipFree(aux_region_);
   if (aux_gen_) hipFree(aux_gen_);
@@ -163,6 +166,91 @@ void Communicator::allreduce_xgmi(float* buf, int64_t count, hipStream_t s) {
   l.slot_stride = slot_stride_;
   l.spin_limit = spin_limit_;
   if (launch_xgmi_oneshot(l, s) != 0) throw std::runtime_error("xGMI one-shot launch failed");
+}
+
+std::string Communicator::twoshot_handle(int64_t capacity_floats) {
+  if (world_ > kXgmiMaxRanks) throw std::runtime_error("xGMI two-shot supports at most 8 ranks");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  if (!err_host_) {
+    hip_check(hipHostMalloc(reinterpret_cast<void**>(&err_host_), sizeof(int), hipHostMallocMapped),
+              "hipHostMalloc(error)");
+    *err_host_ = 0;
+    hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_dev_), err_host_, 0), "hipHostGetDevicePointer");
+  }
+  if (!ts_region_) {
+    // chunk stride: a bucket of capacity_floats split W ways, rounded to 64 floats
+    ts_stride_ = ((capacity_floats + world_ - 1) / world_ + 4 + 63) / 64 * 64;
+    const int64_t bytes = twoshot_region_bytes(ts_stride_, world_);
+    hip_check(hipExtMallocWithFlags(reinterpret_cast<void**>(&ts_region_), (size_t)bytes, hipDeviceMallocUncached),
+              "hipExtMallocWithFlags(uncached two-shot)");
+    hip_check(hipMemset(ts_region_, 0, (size_t)bytes), "hipMemset(two-shot)");
+    hip_check(hipMalloc(reinterpret_cast<void**>(&ts_gen_), kTwoShotMaxBlocks * sizeof(uint32_t)),
+              "hipMalloc(two-shot gen)");
+    hip_check(hipMemset(ts_gen_, 0, kTwoShotMaxBlocks * sizeof(uint32_t)), "hipMemset(two-shot gen)");
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  }
+  hipIpcMemHandle_t h;
+  hip_check(hipIpcGetMemHandle(&h, ts_region_), "hipIpcGetMemHandle(two-shot)");
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void Communicator::twoshot_open(const std::vector<std::string>& handles) {
+  if ((int)handles.size() != world_) throw std::runtime_error("need one IPC handle per rank");
+  if (!ts_region_) throw std::runtime_error("twoshot_handle() first");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  for (int r = 0; r < world_; ++r) {
+    if (r == rank_) {
+      ts_peers_[r] = ts_region_;
+      continue;
+    }
+    if (handles[r].size() != sizeof(hipIpcMemHandle_t)) throw std::runtime_error("bad IPC handle size");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handles[r].data(), sizeof(h));
+    void* p = nullptr;
+    hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle(two-shot)");
+    ts_peers_[r] = static_cast<char*>(p);
+  }
+  ts_ready_ = true;
+}
+
+void Communicator::allreduce_twoshot(float* buf, int64_t count, bool bf16_wire, hipStream_t s) {
+  if (!ts_ready_) throw std::runtime_error("xGMI two-shot peers not open");
+  XgmiLaunch l{};
+  l.x = buf;
+  l.n = count;
+  for (int r = 0; r < world_; ++r) l.regions[r] = ts_peers_[r];
+  l.rank = rank_;
+  l.world = world_;
+  l.gen = ts_gen_;
+  l.error = err_dev_;
+  l.slot_stride = ts_stride_;
+  l.spin_limit = spin_limit_;
+  if (launch_xgmi_twoshot(l, bf16_wire, s) != 0)
+    throw std::runtime_error("xGMI two-shot: bucket exceeds capacity, buffer not 16-byte aligned, or launch failed");
+}
+
+int Communicator::route(const float* buf, int64_t count) const {
+  const bool aligned = (reinterpret_cast<uintptr_t>(buf) & 15) == 0;
+  if (world_ == 1) return 2;
+  if (xgmi_ready_ && aligned && count <= slot_stride_ && count <= oneshot_max_) return 0;
+  if (ts_ready_ && aligned && count <= twoshot_max_ && twoshot_plan(count, world_).cs <= ts_stride_) return 1;
+  return comm_ ? 2 : -1;
+}
+
+void Communicator::allreduce_f32(float* buf, int64_t count, hipStream_t s) {
+  switch (route(buf, count)) {
+    case 0: allreduce_xgmi(buf, count, s); return;
+    case 1: allreduce_twoshot(buf, count, false, s); return;
+    case 2: allreduce(buf, count, DType::kF32, RedOp::kSum, s); return;
+    default: throw std::runtime_error("no allreduce path for this bucket (xGMI capacity exceeded and no RCCL)");
+  }
+}
+
+bool Communicator::allreduce_f32_bf16wire(float* buf, int64_t count, hipStream_t s) {
+  if (!ts_ready_ || (reinterpret_cast<uintptr_t>(buf) & 15) || twoshot_plan(count, world_).cs > ts_stride_)
+    return false;
+  allreduce_twoshot(buf, count, true, s);
+  return true;
 }
 
 std::string Communicator::aux_handle(int64_t capacity_floats) {

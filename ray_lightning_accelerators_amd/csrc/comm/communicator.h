@@ -58,6 +58,29 @@ class Communicator {
   void allreduce_xgmi(float* buf, int64_t count, hipStream_t s);
   void set_spin_limit(int64_t n) { spin_limit_ = n; }
 
+  // ---- xGMI two-shot (reduce-scatter + all-gather, medium/large buckets) ----
+  // Own region sized for buckets of up to capacity_floats; same handle exchange.
+  std::string twoshot_handle(int64_t capacity_floats);
+  void twoshot_open(const std::vector<std::string>& handles);
+  bool has_twoshot() const { return ts_ready_; }
+  // largest bucket (floats) the two-shot region holds
+  int64_t twoshot_capacity() const { return ts_ready_ ? ts_stride_ * world_ : 0; }
+  void allreduce_twoshot(float* buf, int64_t count, bool bf16_wire, hipStream_t s);
+
+  // ---- routing of fp32 SUM allreduces (DDP reducer, fusion engine, Python) ----
+  // one-shot up to min(one-shot capacity, oneshot_max), then two-shot up to
+  // min(two-shot capacity, twoshot_max), then RCCL.  Every rank must set the same
+  // limits (the Python layer agrees on them over the bootstrap group).
+  void set_route_limits(int64_t oneshot_max_floats, int64_t twoshot_max_floats) {
+    oneshot_max_ = oneshot_max_floats;
+    twoshot_max_ = twoshot_max_floats;
+  }
+  // 0 = one-shot, 1 = two-shot, 2 = RCCL, -1 = no path
+  int route(const float* buf, int64_t count) const;
+  void allreduce_f32(float* buf, int64_t count, hipStream_t s);
+  // bf16 wire: two-shot whenever it fits, else RCCL on a bf16 copy is the caller's job
+  bool allreduce_f32_bf16wire(float* buf, int64_t count, hipStream_t s);
+
   // ---- auxiliary peer region for kernels that exchange data themselves ----
   // (the fused data-parallel MLP tail pushes its gradient tiles straight into the
   // peers' receive areas; a separate region so it never aliases the one-shot
@@ -90,6 +113,14 @@ class Communicator {
   int* err_host_ = nullptr;                // host-mapped error word
   int* err_dev_ = nullptr;
   int64_t spin_limit_ = int64_t(1) << 24;  // ~2-4 s of s_sleep polling
+  // two-shot region
+  char* ts_region_ = nullptr;
+  char* ts_peers_[kXgmiMaxRanks] = {};
+  uint32_t* ts_gen_ = nullptr;             // device: per-block generations
+  int64_t ts_stride_ = 0;                  // chunk stride (fp32 elements)
+  bool ts_ready_ = false;
+  int64_t oneshot_max_ = INT64_MAX;
+  int64_t twoshot_max_ = INT64_MAX;
   // auxiliary region
   char* aux_region_ = nullptr;
   char* aux_peers_[kXgmiMaxRanks] = {};

@@ -110,12 +110,7 @@ std::string FusionEngine::last_error() {
 void FusionEngine::execute(Batch& b) {
   hip_check(hipSetDevice(device_), "hipSetDevice");
   for (auto& r : b.reqs) hip_check(hipStreamWaitEvent(stream_, r.ready, 0), "hipStreamWaitEvent(ready)");
-  const bool xgmi = comm_->has_xgmi();
-  auto reduce = [&](float* p, int64_t n) {
-    if (xgmi && (reinterpret_cast<uintptr_t>(p) & 15) == 0 && n <= comm_->xgmi_capacity())
-      comm_->allreduce_xgmi(p, n, stream_);
-    else comm_->allreduce(p, n, DType::kF32, RedOp::kSum, stream_);
-  };
+  auto reduce = [&](float* p, int64_t n) { comm_->allreduce_f32(p, n, stream_); };
   auto copy = [&](bool in, float scale_override, bool use_req_scale) {
     PackTable t{};
     int64_t off = 0;

@@ -62,10 +62,7 @@ void Reducer::launch(int b, hipStream_t producer) {
   hip_check(hipStreamWaitEvent(stream_, ready_[b], 0), "hipStreamWaitEvent(ready)");
   float* p = grad_ + starts_[b];
   const int64_t n = ends_[b] - starts_[b];
-  if (comm_->has_xgmi() && n <= comm_->xgmi_capacity() && (reinterpret_cast<uintptr_t>(p) & 15) == 0)
-    comm_->allreduce_xgmi(p, n, stream_);
-  else
-    comm_->allreduce(p, n, DType::kF32, RedOp::kSum, stream_);
+  comm_->allreduce_f32(p, n, stream_);  // xGMI one-shot / two-shot / RCCL by size
   hip_check(hipEventRecord(done_[b], stream_), "hipEventRecord(done)");
   launched_[b] = 1;
   ++launched_total_;

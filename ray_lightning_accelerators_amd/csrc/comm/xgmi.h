@@ -34,5 +34,22 @@ struct XgmiLaunch {
 int xgmi_blocks_for(int64_t n);
 int launch_xgmi_oneshot(const XgmiLaunch& l, hipStream_t stream);
 
+// Two-shot (reduce-scatter + all-gather) region of one rank (xgmi_twoshot.hip):
+// flags [2 slots][2 phases][kTwoShotMaxBlocks][kXgmiMaxRanks] uint32 in the 64 KiB
+// header, then [2 slots][2 areas: scatter, gather][world][chunk_stride] wire elements.
+// XgmiLaunch::slot_stride is the chunk stride there, in fp32 elements.
+constexpr int kTwoShotMaxBlocks = 128;
+inline int64_t twoshot_region_bytes(int64_t chunk_stride_floats, int world) {
+  return kXgmiFlagBytes + 4 * (int64_t)world * chunk_stride_floats * 4;
+}
+struct TwoShotPlan {
+  int64_t cs;    // chunk length (floats, multiple of 4); chunk c = [c*cs, min((c+1)*cs, n))
+  int64_t per4;  // float4s of each chunk per block
+  int blocks;
+};
+TwoShotPlan twoshot_plan(int64_t n, int world);
+// bf16_wire: links carry bf16 (fp32 accumulate, result rounded to bf16 once)
+int launch_xgmi_twoshot(const XgmiLaunch& l, bool bf16_wire, hipStream_t stream);
+
 }  // namespace comm
 }  // namespace rla

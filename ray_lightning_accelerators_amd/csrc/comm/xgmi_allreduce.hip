@@ -106,6 +106,11 @@ __global__ __launch_bounds__(kThreads) void oneshot_allreduce_kernel(Args a) {
   }
   __threadfence_system();
   __syncthreads();
+  // every generation entry advances on every launch (also the block indices a
+  // smaller grid does not have), so all blocks of a launch agree on the slot
+  // parity when consecutive buckets differ in size (see xgmi_twoshot.hip)
+  if (blk == 0)
+    for (int k = nblk + tid; k < kXgmiMaxBlocks; k += kThreads) a.gen[k] = gen;
   if (sh_fail) {
     if (tid == 0) {
       __hip_atomic_store(a.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -60,7 +60,8 @@ class NativeCommunicator:
 
     def __init__(self, group=None, device: Optional[int] = None, use_rccl: bool = True,
                  use_xgmi: bool = True, xgmi_bytes: Optional[int] = None, validate: bool = True,
-                 spin_limit: Optional[int] = None, watchdog_ms: Optional[int] = None):
+                 spin_limit: Optional[int] = None, watchdog_ms: Optional[int] = None,
+                 twoshot_bytes: Optional[int] = None):
         """Unset knobs come from :func:`~ray_lightning_accelerators_amd.config.get_config`
         (``allreduce_algo="rccl"`` disables the xGMI path, ``"oneshot"`` forbids RCCL for
         buckets that fit the one-shot area)."""
@@ -91,8 +92,17 @@ class NativeCommunicator:
             except RuntimeError:
                 ok = False
             self.rccl = _agree(ok, group)
+        self.twoshot = False
         if use_xgmi and 1 < self.world <= mod.XGMI_MAX_RANKS and os.environ.get("RLA_DISABLE_XGMI", "0") != "1":
             self._setup_xgmi(xgmi_bytes, validate, spin_limit, group)
+            tbytes = cfg.twoshot_bytes if twoshot_bytes is None else twoshot_bytes
+            if tbytes > 0 and self.algo in ("auto", "twoshot"):
+                self._setup_twoshot(tbytes, validate, spin_limit, group)
+        # routing limits of the C++ side (reducer / fusion engine / allreduce_f32):
+        # "oneshot" never uses two-shot, "twoshot" never uses one-shot
+        one_max = 0 if self.algo == "twoshot" else (1 << 62)
+        two_max = 0 if self.algo == "oneshot" else (1 << 62)
+        self._c.set_route_limits(one_max, two_max)
         if watchdog_ms > 0:
             self._c.start_watchdog(watchdog_ms)
 
@@ -123,7 +133,7 @@ class NativeCommunicator:
         self.xgmi = True
 
     def _validate_xgmi(self, group) -> bool:
-        n = 4096 + 4
+        n = min(4096 + 4, int(self._c.xgmi_capacity))
         dev = torch.device("cuda", self.device)
         ok = True
         for it in range(3):  # both receive-area parities + one reuse
@@ -140,9 +150,76 @@ class NativeCommunicator:
             ok = ok and self._c.error_state() == 0 and bool(torch.equal(x, want))
         return ok
 
+    def _setup_twoshot(self, tbytes, validate, spin_limit, group):
+        """Two-shot region (reduce-scatter + all-gather over xGMI) for buckets above
+        the one-shot area; same all-or-nothing agreement as the one-shot."""
+        ok = True
+        handle = b""
+        try:
+            handle = self._c.twoshot_handle(max(4 * self.world, int(tbytes) // 4))
+        except RuntimeError:
+            ok = False
+        handles = [None] * self.world
+        dist.all_gather_object(handles, handle if ok else b"", group=group)
+        ok = ok and all(h for h in handles)
+        if ok:
+            try:
+                self._c.twoshot_open(handles)
+            except RuntimeError:
+                ok = False
+        if not _agree(ok, group):
+            return
+        if spin_limit is not None:
+            self._c.set_spin_limit(int(spin_limit))
+        if validate:
+            ok = self._validate_twoshot(group)
+            if not _agree(ok, group):
+                return
+        self.twoshot = True
+
+    def _validate_twoshot(self, group) -> bool:
+        dev = torch.device("cuda", self.device)
+        ok = True
+        # both parities, a reuse, a ragged size (chunk tails) and a bf16-wire pass
+        big = min(8192 * self.world + 12, int(self._c.twoshot_capacity))
+        for it, n in enumerate((big, min(4097, big), big)):
+            base = torch.arange(n, device=dev, dtype=torch.float32) % 97
+            x = base * (self.rank + 1) + it
+            want = base * (self.world * (self.world + 1) / 2) + it * self.world
+            torch.cuda.synchronize(dev)
+            dist.barrier(group=group)
+            try:
+                self._c.allreduce_twoshot(x, False)
+                torch.cuda.synchronize(dev)
+            except RuntimeError:
+                return False
+            ok = ok and self._c.error_state() == 0 and bool(torch.equal(x, want))
+        x = torch.full((min(4100, big),), float(self.rank + 1), device=dev)
+        dist.barrier(group=group)
+        try:
+            self._c.allreduce_twoshot(x, True)  # small integers are exact in bf16
+            torch.cuda.synchronize(dev)
+        except RuntimeError:
+            return False
+        return ok and self._c.error_state() == 0 and bool(torch.all(x == self.world * (self.world + 1) / 2))
+
     @property
     def xgmi_capacity(self) -> int:
         return int(self._c.xgmi_capacity) if self.xgmi else 0
+
+    @property
+    def twoshot_capacity(self) -> int:
+        return int(self._c.twoshot_capacity) if self.twoshot else 0
+
+    def route(self, t: torch.Tensor) -> str:
+        """Which path ``allreduce_`` takes for this fp32 GPU tensor."""
+        if self.world == 1:
+            return "none"
+        if self.xgmi or self.twoshot:
+            r = int(self._c.route(t))
+            if r >= 0 and not (r == 2 and not self.rccl):
+                return ("oneshot", "twoshot", "rccl")[r]
+        return "rccl" if self.rccl else "torch"
 
     def dp_context(self, capacity_floats: int) -> Optional[list]:
         """Open the auxiliary peer region that a compute kernel exchanges through
@@ -174,12 +251,21 @@ class NativeCommunicator:
         return list(self._c.aux_context())
 
     # ------------------------------------------------------- collectives
-    def allreduce_(self, t: torch.Tensor, average: bool = False) -> torch.Tensor:
+    def allreduce_(self, t: torch.Tensor, average: bool = False, bf16_wire: bool = False) -> torch.Tensor:
+        """In-place SUM (``average``: mean).  fp32 GPU buckets go through the C++
+        router: xGMI one-shot (small), xGMI two-shot (medium/large), RCCL (rest).
+        ``bf16_wire``: carry bf16 over the links (two-shot; fp32 accumulate)."""
         if self.world == 1:
             return t
-        if (self.xgmi and t.dtype == torch.float32 and t.is_contiguous() and t.data_ptr() % 16 == 0
-                and t.numel() <= self.xgmi_capacity):
-            self._c.allreduce_xgmi(t)
+        fp32 = t.dtype == torch.float32 and t.is_cuda and t.is_contiguous()
+        if bf16_wire and fp32 and self.twoshot and self._c.allreduce_bf16wire(t):
+            pass
+        elif bf16_wire and fp32:
+            w = t.to(torch.bfloat16)  # no two-shot region for it: compress around the generic path
+            self.allreduce_(w)
+            t.copy_(w)
+        elif fp32 and (self.xgmi or self.twoshot) and self.route(t) in ("oneshot", "twoshot", "rccl"):
+            self._c.allreduce_f32(t)
         elif self.rccl:
             self._c.allreduce(t, 0)
         elif t.is_cuda and dist.get_backend(self.group) == "gloo":
@@ -193,7 +279,7 @@ class NativeCommunicator:
         return t
 
     def allreduce_async(self, t: torch.Tensor, average: bool = False,
-                        probe: Optional[torch.Tensor] = None) -> "_StreamWork":
+                        probe: Optional[torch.Tensor] = None, bf16_wire: bool = False) -> "_StreamWork":
         """Allreduce on this communicator's high-priority side stream, ordered after
         the current stream's pending work (the gradient producer); ``wait()``
         makes the then-current stream wait for it -- DDP bucket overlap.
@@ -206,7 +292,7 @@ class NativeCommunicator:
         with torch.cuda.stream(self._stream):
             if probe is not None:
                 probe[1] = t.double().sum()
-            self.allreduce_(t, average=average)
+            self.allreduce_(t, average=average, bf16_wire=bf16_wire)
             if probe is not None:
                 probe[2] = t.double().sum()
                 probe.record_stream(self._stream)
@@ -255,7 +341,8 @@ class NativeCommunicator:
 
     def describe(self) -> str:
         return (f"NativeCommunicator(rank={self.rank}, world={self.world}, rccl={self.rccl}, "
-                f"xgmi={self.xgmi}, xgmi_capacity={self.xgmi_capacity})")
+                f"xgmi={self.xgmi}, xgmi_capacity={self.xgmi_capacity}, twoshot={self.twoshot}, "
+                f"twoshot_capacity={self.twoshot_capacity})")
 
 
 class _StreamWork:

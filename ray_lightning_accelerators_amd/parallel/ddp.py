@@ -12,8 +12,13 @@ Design for MI355X + RCCL over xGMI:
     microseconds, so buckets far below ~1 MiB pay latency while buckets far
     above ~16 MiB delay the first launch; 8 MiB keeps ~4 buckets in flight on
     ResNet-50 (97.5 MiB fp32) and ONE bucket for the MNIST MLP (109 KiB);
-  * optional bf16 gradient compression (``grad_dtype="bf16"``) packs a bucket
-    with the multi-tensor cast kernel before the collective;
+  * optional bf16 gradient compression (``grad_dtype="bf16"``): on the native
+    engine the xGMI two-shot kernel converts while it pushes (bf16 on the
+    links, fp32 accumulation, identical rounded result on every rank); on c10d
+    the bucket is packed with the multi-tensor cast kernel first;
+  * buckets above the one-shot area go through the xGMI two-shot
+    (reduce-scatter + all-gather, 2S/W per link) up to ``twoshot_bytes``, RCCL
+    above that (csrc/comm/communicator.cpp ``route``);
   * the 1/world average is NOT applied here when the optimizer is fused
     (``grad_scale`` of the fused Adam/SGD kernel) -- one less pass over HBM;
   * debug race detector (``RLAConfig.check_streams`` / ``RLA_CHECK_STREAMS=1``,
@@ -174,7 +179,11 @@ class GradSynchronizer:
 
     def _launch(self, b: Bucket) -> None:
         grad = self.arena.grad[b.start:b.end]
-        if self.grad_dtype == "bf16" and grad.is_cuda:
+        native = get_native_comm() if (grad.is_cuda and self.pg is None) else None
+        if self.grad_dtype == "bf16" and native is not None:
+            # bf16 on the wire inside the xGMI two-shot kernel: no pack/unpack passes
+            b.work = native.allreduce_async(grad, bf16_wire=True)
+        elif self.grad_dtype == "bf16" and grad.is_cuda:
             if b.comm_buf is None or b.comm_buf.numel() != grad.numel():
                 b.comm_buf = torch.empty(grad.numel(), dtype=torch.bfloat16, device=grad.device)
             ops.multi_copy([(grad, b.comm_buf)])

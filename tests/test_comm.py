@@ -69,10 +69,101 @@ def _gpu_worker(rank, world, port, q, mode):
         _init(rank, world, port)
         from ray_lightning_accelerators_amd.parallel.comm import NativeCommunicator
 
-        comm = NativeCommunicator(use_rccl=False, use_xgmi=True, xgmi_bytes=1 << 20, spin_limit=1 << 20)
-        res = {"xgmi": comm.xgmi}
+        ts_modes = ("twoshot", "twoshot_timeout", "reducer_ts", "reducer_bf16")
+        comm = NativeCommunicator(use_rccl=False, use_xgmi=True,
+                                  xgmi_bytes=(1 << 10) if mode in ts_modes else (1 << 20),
+                                  twoshot_bytes=(4 << 20) if mode in ts_modes else 0, spin_limit=1 << 20)
+        res = {"xgmi": comm.xgmi, "twoshot": comm.twoshot}
         dev = torch.device("cuda", 0)
-        if mode == "allreduce":
+        if mode == "twoshot":
+            # exact fp32 sums of integer-valued data, ragged sizes (chunk tails, empty chunks)
+            for n in (1, 3, 4, 5, 17, 255, 4099, 70001, 262147, 1000003):
+                base = torch.arange(n, device=dev, dtype=torch.float32) % 97
+                x = base * (rank + 1) + rank
+                comm._c.allreduce_twoshot(x, False)
+                torch.cuda.synchronize()
+                want = base * (world * (world + 1) / 2) + sum(range(world))
+                res[f"fp32_{n}"] = bool(torch.equal(x, want))
+            # router: small buckets one-shot, larger ones two-shot, all exact
+            routes = {}
+            for n in (200, 5000, 300001):
+                x = torch.full((n,), float(rank + 1), device=dev)
+                routes[n] = comm.route(x)
+                comm.allreduce_(x)
+                torch.cuda.synchronize()
+                res[f"routed_{n}"] = bool(torch.all(x == world * (world + 1) / 2))
+            res["routes"] = routes
+            # bf16 wire: fp32 accumulate of bf16-rounded inputs, identical bits on every rank
+            g = torch.Generator(device=dev).manual_seed(10 + rank)
+            x = torch.randn(123457, device=dev, generator=g)
+            ref = [torch.randn(123457, device=dev, generator=torch.Generator(device=dev).manual_seed(10 + r))
+                   .to(torch.bfloat16).float() for r in range(world)]
+            want = sum(ref[1:], ref[0]).to(torch.bfloat16).float()
+            comm.allreduce_(x, bf16_wire=True)
+            torch.cuda.synchronize()
+            res["bf16_close"] = bool(torch.allclose(x, want, rtol=1e-2, atol=1e-2))
+            res["bf16_bytes"] = x.cpu().numpy().tobytes()
+            # hipGraph capture: replays advance the per-block generations
+            y = torch.ones(300001, device=dev)
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr, stream=s):
+                comm.allreduce_(y)
+            for k in range(3):
+                y.fill_(rank + 1.0 + k)
+                gr.replay()
+                torch.cuda.synchronize()
+                res[f"graph{k}"] = bool(torch.all(y == world * (world + 1) / 2 + world * k).item())
+            comm.check()
+        elif mode == "twoshot_timeout":
+            x = torch.ones(100000, device=dev)
+            if rank == 0:
+                comm._c.allreduce_twoshot(x, False)  # the peers never join: bounded polls give up
+                torch.cuda.synchronize()
+            dist.barrier()
+            res["state"] = comm._c.error_state()
+        elif mode in ("reducer_ts", "reducer_bf16"):
+            # GradSynchronizer buckets above the (tiny) one-shot area -> C++ reducer -> two-shot
+            from ray_lightning_accelerators_amd.parallel import comm as comm_mod
+            from ray_lightning_accelerators_amd.parallel.arena import ParamArena
+            from ray_lightning_accelerators_amd.parallel.ddp import GradSynchronizer
+
+            comm_mod._default = comm
+
+            def make():
+                torch.manual_seed(0)
+                return torch.nn.Sequential(torch.nn.Linear(256, 300), torch.nn.ReLU(), torch.nn.Linear(300, 77),
+                                           torch.nn.ReLU(), torch.nn.Linear(77, 5)).to(dev)
+
+            def data(r):
+                g = torch.Generator().manual_seed(300 + r)
+                return torch.randn(32, 256, generator=g).to(dev), torch.randn(32, 5, generator=g).to(dev)
+
+            model = make()
+            arena = ParamArena(model)
+            gdt = "bf16" if mode == "reducer_bf16" else "fp32"
+            sync = GradSynchronizer(model, arena, bucket_cap_mb=0.05, grad_dtype=gdt, average_in_optimizer=False)
+            res["native_reducer"] = sync._native is not None
+            res["buckets"] = len(sync.buckets)
+            res["bucket_routes"] = sorted({comm.route(arena.grad[b.start:b.end]) for b in sync.buckets})
+            for _ in range(2):
+                arena.zero_grad()
+                sync.prepare_for_backward()
+                x, y = data(rank)
+                torch.nn.functional.mse_loss(model(x), y).backward()
+                sync.finish()
+            ref = make()
+            for r in range(world):
+                x, y = data(r)
+                (torch.nn.functional.mse_loss(ref(x), y) / world).backward()
+            torch.cuda.synchronize()
+            tol = 2e-2 if gdt == "bf16" else 1e-6
+            res["match"] = all(bool(torch.allclose(p.grad, q.grad, atol=tol, rtol=tol)) for p, q in
+                               zip(model.parameters(), ref.parameters()))
+            res["grad_bytes"] = arena.grad.cpu().numpy().tobytes()
+            comm.check()
+        elif mode == "allreduce":
             for n in (1, 3, 4, 1024, 27882, 27884, 262143):  # incl. the 32/64 MLP arena (27,882)
                 x = torch.arange(n, device=dev, dtype=torch.float32) * 0.5 + rank
                 comm.allreduce_(x)
@@ -271,7 +362,7 @@ def test_xgmi_oneshot_allreduce_two_ranks():
     out = _run_gpu("allreduce")
     for r, res in out.items():
         assert res["xgmi"], res
-        assert all(v for k, v in res.items()), (r, res)
+        assert all(v for k, v in res.items() if k != "twoshot"), (r, res)
 
 
 @gpu
@@ -327,6 +418,37 @@ def test_fused_dp_mlp_step_matches_split_allreduce():
 def test_fused_dp_mlp_step_dead_peer_times_out():
     out = _run_gpu("mlp_dp_timeout")
     assert out[0]["state"] == 1 and out[1]["state"] == 0, out
+
+
+@gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_xgmi_twoshot_allreduce(world):
+    out = _run_gpu("twoshot", world=world)
+    for r, res in out.items():
+        assert res["xgmi"] and res["twoshot"], (r, {k: v for k, v in res.items() if k != "bf16_bytes"})
+        bad = {k: v for k, v in res.items() if v is False}
+        assert not bad, (r, bad)
+        assert res["routes"] == {200: "oneshot", 5000: "twoshot", 300001: "twoshot"}, res["routes"]
+    # bf16 wire: every replica holds the same bits
+    assert len({res["bf16_bytes"] for res in out.values()}) == 1
+
+
+@gpu
+def test_xgmi_twoshot_dead_peer_times_out():
+    out = _run_gpu("twoshot_timeout")
+    assert out[0]["state"] == 1 and out[1]["state"] == 0, out
+
+
+@gpu
+@pytest.mark.parametrize("mode", ["reducer_ts", "reducer_bf16"])
+def test_ddp_reducer_over_twoshot(mode):
+    out = _run_gpu(mode)
+    for r, res in out.items():
+        assert res["twoshot"] and res["match"], (r, {k: v for k, v in res.items() if k != "grad_bytes"})
+        assert res["buckets"] >= 2 and "twoshot" in res["bucket_routes"], res
+        if mode == "reducer_ts":
+            assert res["native_reducer"]
+    assert out[0]["grad_bytes"] == out[1]["grad_bytes"]  # replicas identical
 
 
 @gpu
