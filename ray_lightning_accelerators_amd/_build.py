@@ -129,6 +129,51 @@ def build_extension(name: str, force: bool = False, jobs: int = 4, verbose: bool
     return target
 
 
+SELFTEST_SOURCES = ["comm/selftest.cpp", "comm/communicator.cpp", "comm/fusion_engine.cpp", "comm/reducer.cpp",
+                    "comm/xgmi_allreduce.hip", "comm/xgmi_twoshot.hip", "comm/pack.hip"]
+# host-only sanitizers: each -fsanitize= directly after -Xarch_host, device code untouched
+SANITIZE_HOST = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+                 "-Xarch_host", "-fno-omit-frame-pointer"]
+CLANGXX = os.environ.get("RLA_CLANGXX", "/opt/rocm/lib/llvm/bin/clang++")
+
+
+def selftest_path(sanitize: bool) -> Path:
+    return BUILD_DIR.parent / ("comm_selftest_asan" if sanitize else "comm_selftest")
+
+
+def build_selftest(sanitize: bool = False, force: bool = False, jobs: int = 4, verbose: bool = False) -> Path:
+    """Standalone native test of the comm engine (csrc/comm/selftest.cpp): no torch,
+    forks W ranks that drive the xGMI kernels, fusion engine and reducer.  The
+    ``sanitize`` build instruments the HOST code with ASan + UBSan (+ LeakSanitizer)."""
+    target = selftest_path(sanitize)
+    srcs = [CSRC / s for s in SELFTEST_SOURCES]
+    if not force and not _needs_build(target, srcs):
+        return target
+    BUILD_DIR.mkdir(parents=True, exist_ok=True)
+    tag = "asan" if sanitize else "plain"
+    flags = ["-O1" if sanitize else "-O2", "-g", "-std=c++17", f"-I{CSRC}", "-D__HIP_PLATFORM_AMD__=1"]
+    if sanitize:
+        flags += SANITIZE_HOST
+    objs, cmds = [], []
+    for src in srcs:
+        obj = BUILD_DIR / f"selftest_{tag}__{src.stem}.o"
+        objs.append(obj)
+        # every TU as HIP: the .cpp files include hip_runtime and launch through it
+        cmds.append([HIPCC, "-x", "hip", f"--offload-arch={ARCH}", *flags, "-c", str(src), "-o", str(obj)])
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        for f in [ex.submit(_run, c) for c in cmds]:
+            f.result()
+    link = [CLANGXX, *map(str, objs), "-o", str(target) + ".tmp", "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib",
+            "-lamdhip64", "-lrccl", "-lpthread"]
+    if sanitize:
+        link += ["-fsanitize=address,undefined"]
+    _run(link)
+    os.replace(str(target) + ".tmp", target)
+    if verbose:
+        print(f"built {target}")
+    return target
+
+
 def build_all(force: bool = False, jobs: int = 4, verbose: bool = False, names=None) -> List[Path]:
     out = []
     for name in names or EXTENSIONS:
@@ -146,9 +191,14 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=int(os.environ.get("MAX_JOBS", "4")))
+    ap.add_argument("--selftest", action="store_true",
+                    help="also build the native comm self-test (plain + host ASan/UBSan)")
     ap.add_argument("names", nargs="*")
     args = ap.parse_args(argv)
     build_all(force=args.force, jobs=min(args.jobs, 16), verbose=True, names=args.names or None)
+    if args.selftest:
+        for san in (False, True):
+            build_selftest(sanitize=san, force=args.force, jobs=min(args.jobs, 16), verbose=True)
     return 0
 
 
