@@ -130,6 +130,7 @@ class Accelerator:
         if self.arena is not None:
             from .. import ops
 
+            self.arena.gather_grads()  # stolen (non-arena) grads first
             norm = ops.sumsq(self.arena.grad).sqrt() * self.grad_scale
             coef = (max_norm / (norm + 1e-6)).clamp(max=1.0)
             self.arena.grad.mul_(coef)

@@ -12,14 +12,22 @@ buffer.  Consequences on MI355X:
 """
 from __future__ import annotations
 
-from typing import Dict, List, Optional, Tuple
+from collections import OrderedDict
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 from torch import nn
 
 
 class ParamArena:
-    def __init__(self, module: nn.Module, params: Optional[List[nn.Parameter]] = None, align: int = 4):
+    """``steal_grads`` (default on GPU): ``zero_grad`` sets ``.grad = None`` so
+    autograd hands over freshly produced gradient tensors (no zero-fill of the
+    arena, no per-parameter accumulate kernel -- ResNet-50 has 161 of them), and
+    :meth:`gather_grads` moves a whole bucket / step of them into the arena with
+    ONE multi-tensor copy launch whose chunk table is cached per address set."""
+
+    def __init__(self, module: nn.Module, params: Optional[List[nn.Parameter]] = None, align: int = 4,
+                 steal_grads: Optional[bool] = None):
         if params is None:
             params = [p for p in module.parameters() if p.requires_grad]
         if not params:
@@ -49,6 +57,8 @@ class ParamArena:
                 p.data = view
                 p.grad = self.grad[o:o + n].view_as(p)
         self._index: Dict[int, int] = {id(p): i for i, p in enumerate(params)}
+        self.steal_grads = (dev.type == "cuda") if steal_grads is None else bool(steal_grads)
+        self._tables: "OrderedDict[tuple, torch.Tensor]" = OrderedDict()
 
     def param_view(self, i: int) -> torch.Tensor:
         o, n = self.offsets[i]
@@ -84,10 +94,52 @@ class ParamArena:
                 with torch.no_grad():
                     self.data[o:o + n].view_as(p).copy_(p.data)
                 p.data = self.data[o:o + n].view_as(p)
-            if not self.owns_grad(i):
+        self.gather_grads()
+
+    def gather_grads(self, indices: Optional[Sequence[int]] = None) -> None:
+        """Move every non-arena ``.grad`` of ``indices`` (default: all) into the
+        arena -- one multi-tensor copy launch on the current stream -- and rebind
+        ``.grad`` to the arena views; a missing grad becomes a zero view."""
+        idx = range(len(self.params)) if indices is None else indices
+        pairs, moved = [], []
+        for i in idx:
+            p = self.params[i]
+            g = p.grad
+            if g is None or self.owns_grad(i):
+                if g is None:
+                    self.rebind_grad(i)
+                continue
+            if g.dtype != torch.float32 or not g.is_contiguous() or g.device != self.device:
                 self.rebind_grad(i)
+                continue
+            o, n = self.offsets[i]
+            pairs.append((g.reshape(-1), self.grad[o:o + n]))
+            moved.append(i)
+        if not pairs:
+            return
+        if self.device.type == "cuda":
+            from ..ops.optim import build_copy_table, multi_copy
+
+            key = tuple(moved) + tuple(s.data_ptr() for s, _ in pairs)
+            table = self._tables.get(key)
+            if table is None:
+                table = build_copy_table(pairs)
+                self._tables[key] = table
+                if len(self._tables) > 64:  # address sets are stable under the caching allocator
+                    self._tables.popitem(last=False)
+            multi_copy(pairs, table=table)
+        else:
+            with torch.no_grad():
+                for s, d in pairs:
+                    d.copy_(s)
+        for i in moved:
+            self.params[i].grad = self.grad_view(i)
 
     def zero_grad(self) -> None:
+        if self.steal_grads:
+            for p in self.params:
+                p.grad = None
+            return
         self.grad.zero_()
         for i, p in enumerate(self.params):
             if not self.owns_grad(i):

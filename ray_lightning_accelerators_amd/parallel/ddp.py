@@ -156,16 +156,21 @@ class GradSynchronizer:
 
     def _make_hook(self, i: int):
         def hook(p: torch.Tensor) -> None:
-            if not self.arena.owns_grad(i):
+            steal = self.arena.steal_grads
+            if not steal and not self.arena.owns_grad(i):
                 self.arena.rebind_grad(i)
             if not self.enabled or not self._started:
-                return
-            if self._native is not None:
-                self._native.mark_ready(i, self.arena.grad)
-                return
+                return  # (steal mode: the optimizer's rebind_all gathers the grads)
             b = self.buckets[self.param_bucket[i]]
             b.pending -= 1
-            if b.pending == 0:
+            if b.pending > 0:
+                return
+            if steal:
+                self.arena.gather_grads(b.param_ids)  # ONE copy launch for the whole bucket
+            if self._native is not None:
+                for j in b.param_ids:
+                    self._native.mark_ready(j, self.arena.grad)
+            else:
                 self._launch_ready()
 
         return hook
@@ -203,6 +208,11 @@ class GradSynchronizer:
         if not self.enabled:
             self._started = False
             return
+        if self.arena.steal_grads:
+            # buckets that unused parameters left incomplete: gather what they have
+            for b in self.buckets:
+                if b.pending > 0:
+                    self.arena.gather_grads(b.param_ids)
         if self._native is not None:
             self._native.finish(self.arena.grad)
             if not self.average_in_optimizer:

@@ -1,0 +1,75 @@
+"""Flat parameter arena: grad stealing + one-launch gather (parallel/arena.py)."""
+import pytest
+import torch
+
+from ray_lightning_accelerators_amd.parallel.arena import ParamArena
+from ray_lightning_accelerators_amd.parallel.fused_optim import fuse_optimizer
+
+
+def _model(dev):
+    torch.manual_seed(0)
+    return torch.nn.Sequential(torch.nn.Linear(33, 65), torch.nn.ReLU(), torch.nn.Linear(65, 7),
+                               torch.nn.ReLU(), torch.nn.Linear(7, 3)).to(dev)
+
+
+def _train(dev, steal, steps=4, accumulate=1):
+    model = _model(dev)
+    arena = ParamArena(model, steal_grads=steal)
+    opt = fuse_optimizer(torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4), arena)
+    g = torch.Generator().manual_seed(1)
+    for _ in range(steps):
+        opt.zero_grad()
+        for _ in range(accumulate):
+            x, y = torch.randn(16, 33, generator=g).to(dev), torch.randn(16, 3, generator=g).to(dev)
+            torch.nn.functional.mse_loss(model(x), y).backward()
+        opt.step()
+    return model, arena
+
+
+def _reference(dev, steps=4, accumulate=1):
+    model = _model(dev)
+    opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    g = torch.Generator().manual_seed(1)
+    for _ in range(steps):
+        opt.zero_grad()
+        for _ in range(accumulate):
+            x, y = torch.randn(16, 33, generator=g).to(dev), torch.randn(16, 3, generator=g).to(dev)
+            torch.nn.functional.mse_loss(model(x), y).backward()
+        opt.step()
+    return model
+
+
+@pytest.mark.parametrize("accumulate", [1, 2])
+def test_steal_grads_matches_torch_cpu(accumulate):
+    model, arena = _train("cpu", steal=True, accumulate=accumulate)
+    ref = _reference("cpu", accumulate=accumulate)
+    for p, q in zip(model.parameters(), ref.parameters()):
+        assert torch.allclose(p, q, atol=1e-6), (p - q).abs().max()
+    # after the step every grad is an arena view again
+    assert all(arena.owns_grad(i) for i in range(len(arena.params)))
+
+
+def test_zero_grad_steal_sets_none_and_gather_restores_views():
+    model = _model("cpu")
+    arena = ParamArena(model, steal_grads=True)
+    arena.zero_grad()
+    assert all(p.grad is None for p in model.parameters())
+    torch.nn.functional.mse_loss(model(torch.randn(4, 33)), torch.zeros(4, 3)).backward()
+    assert not arena.owns_grad(0)
+    grads = [p.grad.clone() for p in model.parameters()]
+    arena.gather_grads([0, 1])
+    assert arena.owns_grad(0) and arena.owns_grad(1) and not arena.owns_grad(2)
+    arena.gather_grads()
+    for i, (p, g) in enumerate(zip(model.parameters(), grads)):
+        assert arena.owns_grad(i) and torch.equal(p.grad, g)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("accumulate", [1, 2])
+def test_steal_grads_matches_torch_gpu(accumulate):
+    model, arena = _train("cuda", steal=None, accumulate=accumulate)  # GPU default: steal
+    assert arena.steal_grads
+    ref = _reference("cuda", accumulate=accumulate)
+    for p, q in zip(model.parameters(), ref.parameters()):
+        assert torch.allclose(p, q, atol=1e-5), (p - q).abs().max()
+    assert len(arena._tables) >= 1  # the gather ran through the cached multi-copy table
