@@ -204,7 +204,8 @@ def make_resnet(args, world, rank, dev, x, y):
     from ray_lightning_accelerators_amd.models.resnet import resnet50
 
     torch.manual_seed(0)
-    model = resnet50().to(dev).to(memory_format=torch.channels_last)
+    # native: BatchNorm+ReLU(+residual add) in the fused gfx950 kernels (ops/bn.py)
+    model = resnet50(fused_bn=args.impl == "native").to(dev).to(memory_format=torch.channels_last)
     B = args.batch_size
     g = torch.Generator(device=dev).manual_seed(rank)
     xb = torch.randn(B, 3, 224, 224, device=dev, generator=g).contiguous(memory_format=torch.channels_last)

@@ -372,6 +372,130 @@ void mlp_eval(optional<Tensor> x_u8, optional<Tensor> x_f32, Tensor labels, opti
   TORCH_CHECK(rla::launch_mlp_eval(a, cur_stream(params)) == 0, "fused MLP eval launch failed");
 }
 
+// ---- fused BatchNorm(+ReLU)(+residual add) over NHWC bf16 activations --------------
+// Tensors are passed as contiguous [..., C] views (channels_last NCHW permuted to
+// NHWC): every shape / alignment assumption of csrc/bn_act.hip is checked here.
+int64_t bn_rows(const Tensor& x, const char* name, int64_t C) {
+  check_dev(x, name, at::kBFloat16);
+  TORCH_CHECK(C > 0 && C % 8 == 0 && C <= rla::kBnMaxC, "fused BN: C must be a multiple of 8 and <= ",
+              rla::kBnMaxC, ", got ", C);
+  TORCH_CHECK(x.dim() >= 1 && x.size(-1) == C, name, " must have C=", C, " as its innermost dimension");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0, name, " must be 16-byte aligned");
+  return x.numel() / C;
+}
+
+void bn_same(const Tensor& a, const Tensor& b, const char* name, int64_t C) {
+  TORCH_CHECK(bn_rows(b, name, C) * C == a.numel(), name, " size mismatch");
+}
+
+const float* f32_vec(const optional<Tensor>& t, const char* name, int64_t C) {
+  return ptr_or_null<const float>(t, name, at::kFloat, C);
+}
+
+Tensor bn_partial(Tensor x, optional<Tensor> y, optional<Tensor> dy, int64_t C, int64_t mode, bool relu,
+                  optional<Tensor> nbt) {
+  const int64_t M = bn_rows(x, "x", C);
+  TORCH_CHECK(M > 0, "fused BN: empty input");
+  TORCH_CHECK(mode == 0 || mode == 1, "fused BN: mode 0 (forward) or 1 (backward)");
+  const uint16_t* yp = nullptr;
+  const uint16_t* dyp = nullptr;
+  if (mode == 1) {
+    TORCH_CHECK(dy.has_value(), "backward partial needs dy");
+    bn_same(x, *dy, "dy", C);
+    dyp = reinterpret_cast<const uint16_t*>(dy->data_ptr());
+    if (relu) {
+      TORCH_CHECK(y.has_value(), "ReLU backward needs the saved output y");
+      bn_same(x, *y, "y", C);
+      yp = reinterpret_cast<const uint16_t*>(y->data_ptr());
+    }
+  }
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const rla::BnPlan plan = rla::bn_plan(M, (int)C);
+  Tensor part = at::empty({plan.blocks, 2, C}, x.options().dtype(at::kFloat));
+  int64_t* nbtp = mode == 0 ? ptr_or_null<int64_t>(nbt, "num_batches_tracked", at::kLong, 1) : nullptr;
+  rla::launch_bn_partial(reinterpret_cast<const uint16_t*>(x.data_ptr()), yp, dyp, M, (int)C, (int)mode, relu,
+                         plan, part.data_ptr<float>(), nbtp, cur_stream(x));
+  return part;
+}
+
+Tensor bn_finalize(Tensor part, double count, optional<Tensor> weight, optional<Tensor> bias,
+                   optional<Tensor> running_mean, optional<Tensor> running_var, optional<Tensor> nbt,
+                   double momentum, double eps) {
+  check_dev(part, "partials", at::kFloat);
+  TORCH_CHECK(part.dim() == 3 && part.size(1) == 2, "partials must be [blocks, 2, C]");
+  const int64_t C = part.size(2);
+  TORCH_CHECK(count > 0, "fused BN: count must be > 0");
+  float* rm = ptr_or_null<float>(running_mean, "running_mean", at::kFloat, C);
+  float* rv = ptr_or_null<float>(running_var, "running_var", at::kFloat, C);
+  TORCH_CHECK((rm == nullptr) == (rv == nullptr), "running_mean / running_var go together");
+  const int64_t* nbtp = ptr_or_null<const int64_t>(nbt, "num_batches_tracked", at::kLong, 1);
+  TORCH_CHECK(momentum >= 0 || nbtp, "cumulative averaging (momentum=None) needs num_batches_tracked");
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(part.device());
+  Tensor stats = at::empty({4, C}, part.options());
+  rla::launch_bn_finalize(part.data_ptr<float>(), (int)part.size(0), (int)C, count, f32_vec(weight, "weight", C),
+                          f32_vec(bias, "bias", C), rm, rv, nbtp, (float)momentum, (float)eps,
+                          stats.data_ptr<float>(), cur_stream(part));
+  return stats;
+}
+
+Tensor bn_bwd_finalize(Tensor part, double count, optional<Tensor> weight, Tensor mean, Tensor invstd) {
+  check_dev(part, "partials", at::kFloat);
+  TORCH_CHECK(part.dim() == 3 && part.size(1) == 2, "partials must be [blocks, 2, C]");
+  const int64_t C = part.size(2);
+  check_dev(mean, "mean", at::kFloat);
+  check_dev(invstd, "invstd", at::kFloat);
+  TORCH_CHECK(mean.numel() == C && invstd.numel() == C, "mean / invstd must have C elements");
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(part.device());
+  Tensor coef = at::empty({5, C}, part.options());
+  rla::launch_bn_bwd_finalize(part.data_ptr<float>(), (int)part.size(0), (int)C, count,
+                              f32_vec(weight, "weight", C), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                              coef.data_ptr<float>(), cur_stream(part));
+  return coef;
+}
+
+void bn_apply(Tensor x, Tensor scale, Tensor shift, optional<Tensor> res, bool relu, Tensor y) {
+  const int64_t C = scale.numel();
+  const int64_t M = bn_rows(x, "x", C);
+  bn_same(x, y, "y", C);
+  check_dev(scale, "scale", at::kFloat);
+  check_dev(shift, "shift", at::kFloat);
+  TORCH_CHECK(shift.numel() == C, "shift must have C elements");
+  const uint16_t* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    bn_same(x, *res, "residual", C);
+    rp = reinterpret_cast<const uint16_t*>(res->data_ptr());
+  }
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  rla::launch_bn_apply(reinterpret_cast<const uint16_t*>(x.data_ptr()), rp, scale.data_ptr<float>(),
+                       shift.data_ptr<float>(), M, (int)C, relu, reinterpret_cast<uint16_t*>(y.data_ptr()),
+                       cur_stream(x));
+}
+
+void bn_bwd_apply(Tensor x, optional<Tensor> y, Tensor dy, Tensor coef, bool relu, Tensor dx,
+                  optional<Tensor> dres) {
+  check_dev(coef, "coef", at::kFloat);
+  TORCH_CHECK(coef.dim() == 2 && coef.size(0) == 5, "coef must be [5, C]");
+  const int64_t C = coef.size(1);
+  const int64_t M = bn_rows(x, "x", C);
+  bn_same(x, dy, "dy", C);
+  bn_same(x, dx, "dx", C);
+  const uint16_t* yp = nullptr;
+  if (relu) {
+    TORCH_CHECK(y.has_value(), "ReLU backward needs the saved output y");
+    bn_same(x, *y, "y", C);
+    yp = reinterpret_cast<const uint16_t*>(y->data_ptr());
+  }
+  uint16_t* drp = nullptr;
+  if (dres.has_value() && dres->defined()) {
+    bn_same(x, *dres, "dres", C);
+    drp = reinterpret_cast<uint16_t*>(dres->data_ptr());
+  }
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  rla::launch_bn_bwd_apply(reinterpret_cast<const uint16_t*>(x.data_ptr()), yp,
+                           reinterpret_cast<const uint16_t*>(dy.data_ptr()), coef.data_ptr<float>(), M, (int)C,
+                           relu, reinterpret_cast<uint16_t*>(dx.data_ptr()), drp, cur_stream(x));
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -396,5 +520,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp_shadow_size", [](int64_t l1, int64_t l2) { return rla::mlp_shadow_layout((int)l1, (int)l2).total; });
   m.def("mlp_supported", [](int64_t a, int64_t b) { return rla::mlp_supported((int)a, (int)b); });
   m.def("mlp_param_count", &mlp_param_count);
+  m.def("bn_partial", &bn_partial, "fused BN: per-block partial sums (mode 0 fwd stats, 1 bwd dz/dz*x)",
+        py::arg("x"), py::arg("y"), py::arg("dy"), py::arg("C"), py::arg("mode"), py::arg("relu"), py::arg("nbt"));
+  m.def("bn_finalize", &bn_finalize, "fused BN: mean/invstd/scale/shift + running stats from partials");
+  m.def("bn_bwd_finalize", &bn_bwd_finalize, "fused BN backward: dgamma/dbeta + dx coefficients");
+  m.def("bn_apply", &bn_apply, "fused BN apply: y = act(x*scale + shift (+res))");
+  m.def("bn_bwd_apply", &bn_bwd_apply, "fused BN backward apply: dx (+ dres = relu-masked dy)");
   m.attr("ARCH") = "gfx950";
 }

@@ -1,0 +1,333 @@
+// Fused BatchNorm (+ReLU) (+residual add) over NHWC bf16 activations, gfx950.
+//
+// Why (profiles/r1_resnet50_v2): in PyTorch-ROCm ResNet-50 (bs 128, bf16,
+// channels_last) MIOpen's NHWC batch norm (6 kernels per layer) plus the
+// separate ReLU / residual-add / ReLU-backward elementwise kernels take ~9.5 of
+// ~25.6 ms per step.  All of it is HBM-bound, so the win is fewer passes:
+//   forward:  partial (read x) -> finalize ([C] only) -> apply (read x [+res], write y)
+//   backward: partial (read x, y, dy) -> finalize -> apply (read x, y, dy, write dx [+dres])
+// ReLU and the bottleneck's residual add live in `apply`; their backward (the
+// mask comes from the saved output y) in the backward kernels; the running
+// statistics and num_batches_tracked are updated by the small kernels, so no
+// extra elementwise launches remain.
+//
+// Layout: [M, C] rows (NHWC = channels_last, M = N*H*W), C % 8 == 0, C <= 2048.
+// A thread owns 8 consecutive channels (one 16-byte bf16x8 vector) and walks
+// rows with stride rpi = 256 / (C/8); each wave therefore reads whole 128-byte
+// row segments.  Per-block fp32 partial sums go to a [blocks, 2, C] workspace
+// that the finalize kernel reduces in fp64.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace rla {
+namespace {
+
+typedef float f8 __attribute__((ext_vector_type(8)));
+typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+typedef uint16_t u8x16 __attribute__((ext_vector_type(8)));  // 8 raw bf16 = 16 bytes
+
+__device__ __forceinline__ f8 ld8(const uint16_t* p) {
+  const u8x16 raw = *reinterpret_cast<const u8x16*>(p);
+  return __builtin_convertvector(__builtin_bit_cast(b8, raw), f8);
+}
+
+__device__ __forceinline__ void st8(uint16_t* p, f8 v) {
+  *reinterpret_cast<u8x16*>(p) = __builtin_bit_cast(u8x16, __builtin_convertvector(v, b8));
+}
+
+__device__ __forceinline__ f8 splat(float v) {
+  f8 r;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = v;
+  return r;
+}
+
+__device__ __forceinline__ f8 ld8f(const float* p) {  // 8 fp32 per-channel coefficients
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  f8 r;
+  r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = a.w;
+  r[4] = b.x; r[5] = b.y; r[6] = b.z; r[7] = b.w;
+  return r;
+}
+
+__device__ __forceinline__ f8 relu_mask(f8 d, f8 y) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) d[k] = y[k] > 0.f ? d[k] : 0.f;
+  return d;
+}
+
+// ---------------------------------------------------------------- partial sums
+template <int MODE, bool RELU>
+__global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(const uint16_t* __restrict__ x,
+                                                                const uint16_t* __restrict__ y,
+                                                                const uint16_t* __restrict__ dy, int64_t M, int C,
+                                                                int64_t rows_per_blk, float* __restrict__ part,
+                                                                int64_t* nbt) {
+  __shared__ float sh[2][kBnThreads * 8];
+  const int G = C >> 3, rpi = kBnThreads / G, tid = threadIdx.x;
+  const int g = tid % G, r0 = tid / G;
+  if (MODE == 0 && nbt && blockIdx.x == 0 && tid == 0) nbt[0] += 1;  // torch: += 1 before the momentum
+  f8 s = splat(0.f), q = splat(0.f);
+  const int64_t rb = (int64_t)blockIdx.x * rows_per_blk;
+  const int64_t re = rb + rows_per_blk < M ? rb + rows_per_blk : M;
+  if (r0 < rpi) {
+    const int64_t col = (int64_t)g * 8, step = (int64_t)rpi * C;
+    int64_t r = rb + r0;
+    const uint16_t* px = x + r * C + col;
+    // 4 rows in flight per thread (x, and dy / y in the backward)
+    for (; r + 3 * rpi < re; r += 4 * rpi, px += 4 * step) {
+      f8 xv[4], dv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        xv[u] = ld8(px + u * step);
+        if (MODE == 1) {
+          const int64_t off = (px - x) + u * step;
+          dv[u] = ld8(dy + off);
+          if (RELU) dv[u] = relu_mask(dv[u], ld8(y + off));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (MODE == 0) {
+          s += xv[u];
+          q += xv[u] * xv[u];
+        } else {
+          s += dv[u];
+          q += dv[u] * xv[u];
+        }
+      }
+    }
+    for (; r < re; r += rpi, px += step) {
+      const f8 xv = ld8(px);
+      if (MODE == 0) {
+        s += xv;
+        q += xv * xv;
+      } else {
+        const int64_t off = px - x;
+        f8 d = ld8(dy + off);
+        if (RELU) d = relu_mask(d, ld8(y + off));
+        s += d;
+        q += d * xv;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sh[0][r0 * C + g * 8 + k] = s[k];
+      sh[1][r0 * C + g * 8 + k] = q[k];
+    }
+  }
+  __syncthreads();
+  float* out = part + (int64_t)blockIdx.x * 2 * C;
+  for (int c = tid; c < C; c += kBnThreads) {
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < rpi; ++r) {
+      a += sh[0][r * C + c];
+      b += sh[1][r * C + c];
+    }
+    out[c] = a;
+    out[C + c] = b;
+  }
+}
+
+// ---------------------------------------------------------------- finalize
+// 64 channels per block, 4 slices of the partial rows each, fp64 accumulation.
+template <bool BWD>
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ part, int nparts, int C,
+                                                          double count, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float* running_mean,
+                                                          float* running_var, const int64_t* nbt, float momentum,
+                                                          float eps, const float* __restrict__ mean_in,
+                                                          const float* __restrict__ invstd_in, float* __restrict__ out) {
+  __shared__ double sh[2][4][64];
+  const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double a = 0.0, b = 0.0;
+  if (c < C)
+    for (int p = sl; p < nparts; p += 4) {
+      a += part[(int64_t)p * 2 * C + c];
+      b += part[(int64_t)p * 2 * C + C + c];
+    }
+  sh[0][sl][cl] = a;
+  sh[1][sl][cl] = b;
+  __syncthreads();
+  if (sl != 0 || c >= C) return;
+  a = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
+  b = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
+  const float g = gamma ? gamma[c] : 1.f;
+  if (!BWD) {
+    const double mean = a / count;
+    double var = b / count - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = g * invstd;
+    out[c] = (float)mean;
+    out[C + c] = invstd;
+    out[2 * C + c] = sc;
+    out[3 * C + c] = (beta ? beta[c] : 0.f) - (float)mean * sc;
+    if (running_mean) {
+      // momentum < 0: cumulative moving average, factor 1 / num_batches_tracked
+      const float mom = momentum >= 0.f ? momentum : 1.f / (float)(nbt ? nbt[0] : 1);
+      const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
+      running_mean[c] = (1.f - mom) * running_mean[c] + mom * (float)mean;
+      running_var[c] = (1.f - mom) * running_var[c] + mom * (float)unbiased;
+    }
+  } else {
+    const float mean = mean_in[c], istd = invstd_in[c];
+    const float dbeta = (float)a;
+    const float dgamma = (float)((b - (double)mean * a) * (double)istd);
+    const float A = g * istd;
+    const float B = -A * istd * dgamma / (float)count;
+    out[c] = dgamma;
+    out[C + c] = dbeta;
+    out[2 * C + c] = A;
+    out[3 * C + c] = B;
+    out[4 * C + c] = -A * dbeta / (float)count - B * mean;
+  }
+}
+
+// ---------------------------------------------------------------- elementwise
+template <bool RELU, bool RES>
+__global__ __launch_bounds__(kBnThreads) void bn_apply_kernel(const uint16_t* __restrict__ x,
+                                                              const uint16_t* __restrict__ res,
+                                                              const float* __restrict__ scale,
+                                                              const float* __restrict__ shift, int64_t M, int C,
+                                                              uint16_t* __restrict__ y) {
+  const int G = C >> 3, rpi = kBnThreads / G, tid = threadIdx.x;
+  const int g = tid % G, r0 = tid / G;
+  if (r0 >= rpi) return;
+  const f8 sc = ld8f(scale + g * 8), sf = ld8f(shift + g * 8);
+  const int64_t col = (int64_t)g * 8, rstride = (int64_t)gridDim.x * rpi;
+  int64_t r = (int64_t)blockIdx.x * rpi + r0;
+  for (; r + rstride < M; r += 2 * rstride) {  // two rows in flight
+    const int64_t o0 = r * C + col, o1 = (r + rstride) * C + col;
+    f8 v0 = ld8(x + o0), v1 = ld8(x + o1);
+    f8 a0, a1;
+    if (RES) {
+      a0 = ld8(res + o0);
+      a1 = ld8(res + o1);
+    }
+    v0 = v0 * sc + sf;
+    v1 = v1 * sc + sf;
+    if (RES) {
+      v0 += a0;
+      v1 += a1;
+    }
+    if (RELU) {
+      v0 = relu_mask(v0, v0);
+      v1 = relu_mask(v1, v1);
+    }
+    st8(y + o0, v0);
+    st8(y + o1, v1);
+  }
+  if (r < M) {
+    const int64_t o = r * C + col;
+    f8 v = ld8(x + o) * sc + sf;
+    if (RES) v += ld8(res + o);
+    if (RELU) v = relu_mask(v, v);
+    st8(y + o, v);
+  }
+}
+
+template <bool RELU, bool DRES>
+__global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_kernel(const uint16_t* __restrict__ x,
+                                                                  const uint16_t* __restrict__ y,
+                                                                  const uint16_t* __restrict__ dy,
+                                                                  const float* __restrict__ coef, int64_t M, int C,
+                                                                  uint16_t* __restrict__ dx,
+                                                                  uint16_t* __restrict__ dres) {
+  const int G = C >> 3, rpi = kBnThreads / G, tid = threadIdx.x;
+  const int g = tid % G, r0 = tid / G;
+  if (r0 >= rpi) return;
+  const f8 A = ld8f(coef + 2 * C + g * 8), B = ld8f(coef + 3 * C + g * 8), Cc = ld8f(coef + 4 * C + g * 8);
+  const int64_t col = (int64_t)g * 8, rstride = (int64_t)gridDim.x * rpi;
+  for (int64_t r = (int64_t)blockIdx.x * rpi + r0; r < M; r += rstride) {
+    const int64_t o = r * C + col;
+    f8 d = ld8(dy + o);
+    if (RELU) d = relu_mask(d, ld8(y + o));
+    const f8 xv = ld8(x + o);
+    st8(dx + o, A * d + B * xv + Cc);
+    if (DRES) st8(dres + o, d);
+  }
+}
+
+int apply_grid(int64_t M, int C) {
+  const int rpi = kBnThreads / (C >> 3);
+  int64_t b = (M + rpi - 1) / rpi;
+  if (b > 2048) b = 2048;  // 8 blocks per CU; each thread then walks ~M/(2048*rpi) rows
+  return (int)(b < 1 ? 1 : b);
+}
+
+}  // namespace
+
+BnPlan bn_plan(int64_t M, int C) {
+  const int rpi = kBnThreads / (C >> 3);
+  // >= 16 row iterations per thread, at most 1024 blocks and 256K partial floats
+  int64_t blocks = (M + (int64_t)rpi * 16 - 1) / ((int64_t)rpi * 16);
+  int64_t cap = (int64_t(1) << 18) / C;
+  if (cap > 1024) cap = 1024;
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  BnPlan p;
+  p.rows_per_blk = (M + blocks - 1) / blocks;
+  p.blocks = (int)((M + p.rows_per_blk - 1) / p.rows_per_blk);
+  if (p.blocks < 1) p.blocks = 1;
+  return p;
+}
+
+void launch_bn_partial(const uint16_t* x, const uint16_t* y, const uint16_t* dy, int64_t M, int C, int mode,
+                       bool relu, const BnPlan& plan, float* part, int64_t* nbt, hipStream_t s) {
+  const dim3 grid(plan.blocks), block(kBnThreads);
+  if (mode == 0)
+    hipLaunchKernelGGL((bn_partial_kernel<0, false>), grid, block, 0, s, x, y, dy, M, C, plan.rows_per_blk, part,
+                       nbt);
+  else if (relu)
+    hipLaunchKernelGGL((bn_partial_kernel<1, true>), grid, block, 0, s, x, y, dy, M, C, plan.rows_per_blk, part,
+                       nullptr);
+  else
+    hipLaunchKernelGGL((bn_partial_kernel<1, false>), grid, block, 0, s, x, y, dy, M, C, plan.rows_per_blk, part,
+                       nullptr);
+}
+
+void launch_bn_finalize(const float* part, int nparts, int C, double count, const float* gamma,
+                        const float* beta, float* running_mean, float* running_var, const int64_t* nbt,
+                        float momentum, float eps, float* stats, hipStream_t s) {
+  hipLaunchKernelGGL((bn_finalize_kernel<false>), dim3((C + 63) / 64), dim3(256), 0, s, part, nparts, C, count,
+                     gamma, beta, running_mean, running_var, nbt, momentum, eps, nullptr, nullptr, stats);
+}
+
+void launch_bn_bwd_finalize(const float* part, int nparts, int C, double count, const float* gamma,
+                            const float* mean, const float* invstd, float* coef, hipStream_t s) {
+  hipLaunchKernelGGL((bn_finalize_kernel<true>), dim3((C + 63) / 64), dim3(256), 0, s, part, nparts, C, count,
+                     gamma, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, mean, invstd, coef);
+}
+
+void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* scale, const float* shift, int64_t M,
+                     int C, bool relu, uint16_t* y, hipStream_t s) {
+  const dim3 grid(apply_grid(M, C)), block(kBnThreads);
+  if (relu && res)
+    hipLaunchKernelGGL((bn_apply_kernel<true, true>), grid, block, 0, s, x, res, scale, shift, M, C, y);
+  else if (relu)
+    hipLaunchKernelGGL((bn_apply_kernel<true, false>), grid, block, 0, s, x, res, scale, shift, M, C, y);
+  else if (res)
+    hipLaunchKernelGGL((bn_apply_kernel<false, true>), grid, block, 0, s, x, res, scale, shift, M, C, y);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<false, false>), grid, block, 0, s, x, res, scale, shift, M, C, y);
+}
+
+void launch_bn_bwd_apply(const uint16_t* x, const uint16_t* y, const uint16_t* dy, const float* coef, int64_t M,
+                         int C, bool relu, uint16_t* dx, uint16_t* dres, hipStream_t s) {
+  const dim3 grid(apply_grid(M, C)), block(kBnThreads);
+  if (relu && dres)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<true, true>), grid, block, 0, s, x, y, dy, coef, M, C, dx, dres);
+  else if (relu)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false>), grid, block, 0, s, x, y, dy, coef, M, C, dx, dres);
+  else if (dres)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true>), grid, block, 0, s, x, y, dy, coef, M, C, dx, dres);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<false, false>), grid, block, 0, s, x, y, dy, coef, M, C, dx, dres);
+}
+
+}  // namespace rla

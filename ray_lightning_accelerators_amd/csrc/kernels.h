@@ -42,6 +42,43 @@ void launch_scale(float* x, int64_t n, float s, hipStream_t stream);
 void launch_sumsq(const float* x, int64_t n, float* out, hipStream_t stream);
 
 // ---------------------------------------------------------------------------
+// Fused BatchNorm(+ReLU)(+residual add) over NHWC bf16 activations viewed as
+// [M, C] rows (csrc/bn_act.hip).  C % 8 == 0 and C <= kBnMaxC.
+// ---------------------------------------------------------------------------
+constexpr int kBnThreads = 256;
+constexpr int kBnMaxC = 2048;  // 8 channels per thread x 256 threads per row
+
+struct BnPlan {
+  int64_t rows_per_blk;  // rows each block of the partial kernels reduces
+  int blocks;
+};
+BnPlan bn_plan(int64_t M, int C);
+
+// per-block partial sums part[b][0][c], part[b][1][c]:
+//   mode 0 (forward):  sum x, sum x^2   (nbt, if given, is incremented by block 0)
+//   mode 1 (backward): sum dz, sum dz*x with dz = dy * (y > 0 if relu)
+void launch_bn_partial(const uint16_t* x, const uint16_t* y, const uint16_t* dy, int64_t M, int C, int mode,
+                       bool relu, const BnPlan& plan, float* part, int64_t* nbt, hipStream_t s);
+
+// forward finalize of `nparts` partial rows: stats[0]=mean [1]=invstd [2]=scale [3]=shift ([4, C]);
+// running stats update (momentum < 0: cumulative average over num_batches_tracked)
+void launch_bn_finalize(const float* part, int nparts, int C, double count, const float* gamma,
+                        const float* beta, float* running_mean, float* running_var, const int64_t* nbt,
+                        float momentum, float eps, float* stats, hipStream_t s);
+
+// backward finalize: coef[0]=dgamma [1]=dbeta [2]=A [3]=B [4]=Cc ([5, C]); dx = A*dz + B*x + Cc
+void launch_bn_bwd_finalize(const float* part, int nparts, int C, double count, const float* gamma,
+                            const float* mean, const float* invstd, float* coef, hipStream_t s);
+
+// y = act(x*scale + shift (+ res))
+void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* scale, const float* shift, int64_t M,
+                     int C, bool relu, uint16_t* y, hipStream_t s);
+
+// dz = dy * (y > 0 if relu); dx = A*dz + B*x + Cc; dres = dz (if dres)
+void launch_bn_bwd_apply(const uint16_t* x, const uint16_t* y, const uint16_t* dy, const float* coef, int64_t M,
+                         int C, bool relu, uint16_t* dx, uint16_t* dres, hipStream_t s);
+
+// ---------------------------------------------------------------------------
 // Fused MNIST-MLP training step (784 -> L1 -> L2 -> 10, ReLU, log_softmax+NLL).
 // ---------------------------------------------------------------------------
 struct MLPStepArgs {

@@ -272,7 +272,10 @@ class DataParallelAccelerator(Accelerator):
         self.init_device(process_idx, t.global_rank == 0)
         if t.sync_batchnorm and t.world_size > 1 and dist.is_initialized():
             # PL: Trainer(sync_batchnorm=True) -> BN statistics all-reduced across ranks
-            torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
+            # (fused BN+ReLU layers stay fused and all-reduce their per-channel sums)
+            from ..ops.bn import convert_sync_batchnorm
+
+            convert_sync_batchnorm(model)
         self.model_to_device(model)
         results = t._run(model)
         self.transfer_distrib_spawn_state_on_fit_end(model, results)

@@ -23,6 +23,7 @@ from torch import nn
 from torch.utils.data import Dataset
 
 from ..lightning import LightningModule
+from ..ops.bn import BatchNormAct2d
 
 
 def _conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -33,22 +34,33 @@ def _conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
     return nn.Conv2d(cin, cout, 1, stride, bias=False)
 
 
+def _bn(c: int, fused: bool, act: Optional[str] = "relu") -> nn.BatchNorm2d:
+    # fused: BatchNorm + ReLU (+ residual add) in the gfx950 kernels of csrc/bn_act.hip;
+    # same parameters / buffers / state-dict keys as nn.BatchNorm2d either way
+    return BatchNormAct2d(c, act=act) if fused else nn.BatchNorm2d(c)
+
+
 class Bottleneck(nn.Module):
     expansion = 4
 
-    def __init__(self, cin: int, width: int, stride: int = 1, downsample: Optional[nn.Module] = None):
+    def __init__(self, cin: int, width: int, stride: int = 1, downsample: Optional[nn.Module] = None,
+                 fused_bn: bool = False):
         super().__init__()
         cout = width * self.expansion
+        self.fused_bn = fused_bn
         self.conv1 = _conv1x1(cin, width)
-        self.bn1 = nn.BatchNorm2d(width)
+        self.bn1 = _bn(width, fused_bn)
         self.conv2 = _conv3x3(width, width, stride)
-        self.bn2 = nn.BatchNorm2d(width)
+        self.bn2 = _bn(width, fused_bn)
         self.conv3 = _conv1x1(width, cout)
-        self.bn3 = nn.BatchNorm2d(cout)
+        self.bn3 = _bn(cout, fused_bn)  # fused: relu(bn3(x) + identity) in one pass
         self.downsample = downsample
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
+        if self.fused_bn:
+            out = self.bn2(self.conv2(self.bn1(self.conv1(x))))
+            return self.bn3(self.conv3(out), idt)
         out = F.relu(self.bn1(self.conv1(x)), inplace=True)
         out = F.relu(self.bn2(self.conv2(out)), inplace=True)
         out = self.bn3(self.conv3(out))
@@ -56,11 +68,13 @@ class Bottleneck(nn.Module):
 
 
 class ResNet(nn.Module):
-    def __init__(self, layers: List[int], num_classes: int = 1000, zero_init_residual: bool = False):
+    def __init__(self, layers: List[int], num_classes: int = 1000, zero_init_residual: bool = False,
+                 fused_bn: bool = False):
         super().__init__()
         self.inplanes = 64
+        self.fused_bn = fused_bn
         self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
-        self.bn1 = nn.BatchNorm2d(64)
+        self.bn1 = _bn(64, fused_bn)
         self.maxpool = nn.MaxPool2d(3, 2, 1)
         self.layer1 = self._make(64, layers[0])
         self.layer2 = self._make(128, layers[1], 2)
@@ -82,20 +96,23 @@ class ResNet(nn.Module):
         down = None
         cout = width * Bottleneck.expansion
         if stride != 1 or self.inplanes != cout:
-            down = nn.Sequential(_conv1x1(self.inplanes, cout, stride), nn.BatchNorm2d(cout))
-        layers = [Bottleneck(self.inplanes, width, stride, down)]
+            down = nn.Sequential(_conv1x1(self.inplanes, cout, stride), _bn(cout, self.fused_bn, act=None))
+        layers = [Bottleneck(self.inplanes, width, stride, down, self.fused_bn)]
         self.inplanes = cout
-        layers += [Bottleneck(cout, width) for _ in range(1, blocks)]
+        layers += [Bottleneck(cout, width, fused_bn=self.fused_bn) for _ in range(1, blocks)]
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(F.relu(self.bn1(self.conv1(x)), inplace=True))
+        x = self.bn1(self.conv1(x))
+        x = self.maxpool(x if self.fused_bn else F.relu(x, inplace=True))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
 
 
-def resnet50(num_classes: int = 1000, zero_init_residual: bool = False) -> ResNet:
-    return ResNet([3, 4, 6, 3], num_classes, zero_init_residual)
+def resnet50(num_classes: int = 1000, zero_init_residual: bool = False, fused_bn: bool = False) -> ResNet:
+    """``fused_bn``: BatchNorm+ReLU(+residual add) layers run the gfx950 fused kernels
+    (``ops.bn.BatchNormAct2d``) -- identical parameters and state-dict keys."""
+    return ResNet([3, 4, 6, 3], num_classes, zero_init_residual, fused_bn)
 
 
 RESNET50_PARAMS = 25_557_032
@@ -121,10 +138,10 @@ class LightningResNet50(LightningModule):
     def __init__(self, config: Optional[dict] = None):
         super().__init__()
         cfg = dict(lr=0.1, momentum=0.9, weight_decay=5e-5, batch_size=64, num_classes=1000,
-                   image_size=224, n_train=512)
+                   image_size=224, n_train=512, fused_bn=True)
         cfg.update(config or {})
         self.cfg = cfg
-        self.model = resnet50(cfg["num_classes"])
+        self.model = resnet50(cfg["num_classes"], fused_bn=cfg["fused_bn"])
 
     def forward(self, x):
         return self.model(x)

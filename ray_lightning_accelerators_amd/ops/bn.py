@@ -1,0 +1,171 @@
+"""Fused BatchNorm (+ReLU) (+residual add) for NHWC bf16 activations.
+
+``BatchNormAct2d`` is a drop-in ``nn.BatchNorm2d`` (same parameters, buffers
+and state-dict keys, so Lightning checkpoints are interchangeable) whose
+forward is ``act(bn(x) + residual)``.  On an MI355X with channels_last bf16
+activations (ResNet-50 under bf16 autocast) it runs the gfx950 kernels of
+``csrc/bn_act.hip``:
+
+  forward   partial sums (1 read of x) -> finalize ([C]; running stats and
+            num_batches_tracked updated in-kernel) -> apply (read x [+res], write y)
+  backward  partial sums (read x, y, dy) -> finalize -> apply (write dx [+dres])
+
+which replaces MIOpen's six batch-norm kernels per layer plus the separate
+ReLU, residual-add and ReLU-backward passes (profiles/r1_resnet50_v2).
+``Trainer(sync_batchnorm=True)`` goes through :func:`convert_sync_batchnorm`,
+which keeps the fusion and all-reduces the per-channel sums (SyncBatchNorm
+semantics: global statistics, local weight/bias gradients).
+
+Anything the kernels do not cover (CPU, fp32 / NCHW input, C % 8 != 0 or
+C > 2048, eval with autograd) runs the plain PyTorch composition.
+"""
+from __future__ import annotations
+
+import warnings
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+from torch import nn
+
+from . import require, use_native
+
+MAX_C = 2048
+stats = {"fused": 0, "fallback": 0}
+
+
+def _nhwc(t: torch.Tensor) -> torch.Tensor:
+    return t.permute(0, 2, 3, 1)
+
+
+def fused_ok(x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> bool:
+    if not (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and x.numel() > 0):
+        return False
+    c = x.size(1)
+    if c % 8 or c > MAX_C or not _nhwc(x).is_contiguous() or x.data_ptr() % 16:
+        return False
+    if residual is not None:
+        if residual.shape != x.shape or residual.dtype != torch.bfloat16 or not _nhwc(residual).is_contiguous() \
+                or residual.data_ptr() % 16:
+            return False
+    return use_native(x)
+
+
+class _BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu, group):
+        mod = require()
+        C = x.size(1)
+        xv = _nhwc(x)
+        count = float(xv.numel() // C)
+        part = mod.bn_partial(xv, None, None, C, 0, False, nbt)
+        if group is not None:
+            # SyncBatchNorm: global per-channel sums (equal per-rank batches, as the
+            # DistributedSampler shards are)
+            part = part.sum(0, keepdim=True)
+            dist.all_reduce(part, group=group)
+            count *= dist.get_world_size(group)
+        st = mod.bn_finalize(part, count, weight, bias, running_mean, running_var, nbt, momentum, eps)
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+        mod.bn_apply(xv, st[2], st[3], _nhwc(residual) if residual is not None else None, relu, _nhwc(y))
+        ctx.relu, ctx.has_res, ctx.group, ctx.count = relu, residual is not None, group, count
+        ctx.save_for_backward(x, y if relu else None, weight, st[0], st[1])
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        mod = require()
+        x, y, weight, mean, invstd = ctx.saved_tensors
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        C = x.size(1)
+        xv, dyv = _nhwc(x), _nhwc(dy)
+        yv = _nhwc(y) if ctx.relu else None
+        part = mod.bn_partial(xv, yv, dyv, C, 1, ctx.relu, None)
+        local = None
+        if ctx.group is not None:
+            local = mod.bn_bwd_finalize(part, ctx.count, weight, mean, invstd)  # local dgamma / dbeta
+            part = part.sum(0, keepdim=True)
+            dist.all_reduce(part, group=ctx.group)
+        coef = mod.bn_bwd_finalize(part, ctx.count, weight, mean, invstd)
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
+        mod.bn_bwd_apply(xv, yv, dyv, coef, ctx.relu, _nhwc(dx), _nhwc(dres) if dres is not None else None)
+        wsrc = local if local is not None else coef
+        dgamma = wsrc[0].clone() if weight is not None and ctx.needs_input_grad[1] else None
+        dbeta = wsrc[1].clone() if ctx.needs_input_grad[2] else None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None
+
+
+class BatchNormAct2d(nn.BatchNorm2d):
+    """``act(BatchNorm2d(x) + residual)`` with ``act`` in {"relu", None}."""
+
+    def __init__(self, num_features: int, act: Optional[str] = "relu", eps: float = 1e-5,
+                 momentum: Optional[float] = 0.1, affine: bool = True, track_running_stats: bool = True,
+                 device=None, dtype=None):
+        super().__init__(num_features, eps, momentum, affine, track_running_stats, device=device, dtype=dtype)
+        if act not in ("relu", None):
+            raise ValueError(f"act must be 'relu' or None, got {act!r}")
+        self.act = act
+        self.sync = False
+        self.process_group = None
+        self._warned = False
+
+    def extra_repr(self) -> str:
+        return super().extra_repr() + f", act={self.act}, sync={self.sync}"
+
+    def _group(self):
+        if self.sync and self.training and dist.is_available() and dist.is_initialized() \
+                and dist.get_world_size(self.process_group) > 1:
+            return self.process_group if self.process_group is not None else dist.group.WORLD
+        return None
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        relu = self.act == "relu"
+        use_batch_stats = self.training or not self.track_running_stats
+        if fused_ok(x, residual):
+            if use_batch_stats:
+                stats["fused"] += 1
+                track = self.training and self.track_running_stats
+                momentum = -1.0 if self.momentum is None else float(self.momentum)
+                return _BNActFn.apply(
+                    x, self.weight, self.bias, residual,
+                    self.running_mean if track else None, self.running_var if track else None,
+                    self.num_batches_tracked if track else None, momentum, float(self.eps), relu, self._group())
+            if not torch.is_grad_enabled() or not (x.requires_grad or (self.weight is not None
+                                                                          and self.weight.requires_grad)):
+                stats["fused"] += 1
+                invstd = (self.running_var + self.eps).rsqrt()
+                scale = invstd * self.weight if self.weight is not None else invstd
+                shift = (self.bias if self.bias is not None else torch.zeros_like(invstd)) - self.running_mean * scale
+                y = torch.empty_like(x, memory_format=torch.channels_last)
+                require().bn_apply(_nhwc(x), scale.float().contiguous(), shift.float().contiguous(),
+                                   _nhwc(residual) if residual is not None else None, relu, _nhwc(y))
+                return y
+        stats["fallback"] += 1
+        if self._group() is not None and x.is_cuda:
+            y = nn.SyncBatchNorm.forward(self, x)  # torch's cross-rank statistics
+        else:
+            if self._group() is not None and not self._warned:
+                warnings.warn("BatchNormAct2d: synchronised statistics need GPU tensors; using local statistics")
+                self._warned = True
+            y = super().forward(x)
+        if residual is not None:
+            y = y + residual
+        return F.relu(y) if relu else y
+
+
+def convert_sync_batchnorm(module: nn.Module, process_group=None) -> nn.Module:
+    """``nn.SyncBatchNorm.convert_sync_batchnorm`` that keeps fused BN+act layers
+    fused (they switch to all-reduced statistics instead of being replaced)."""
+    if isinstance(module, BatchNormAct2d):
+        module.sync = True
+        module.process_group = process_group
+        return module
+    if isinstance(module, nn.modules.batchnorm._BatchNorm) and not isinstance(module, nn.SyncBatchNorm):
+        return nn.SyncBatchNorm.convert_sync_batchnorm(module, process_group)
+    for name, child in list(module.named_children()):
+        new = convert_sync_batchnorm(child, process_group)
+        if new is not child:
+            setattr(module, name, new)
+    return module
