@@ -133,29 +133,55 @@ __global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(const uint16_t* 
 }
 
 // ---------------------------------------------------------------- finalize
-// 64 channels per block, 4 slices of the partial rows each, fp64 accumulation.
+// 64 channels per block x 16 slices of the partial rows (1024 threads), 4 rows in
+// flight per thread, fp64 accumulation; the slices are combined through LDS.
+constexpr int kFinSlices = 16;
+
 template <bool BWD>
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ part, int nparts, int C,
-                                                          double count, const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta, float* running_mean,
-                                                          float* running_var, const int64_t* nbt, float momentum,
-                                                          float eps, const float* __restrict__ mean_in,
-                                                          const float* __restrict__ invstd_in, float* __restrict__ out) {
-  __shared__ double sh[2][4][64];
+__global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restrict__ part, int nparts, int C,
+                                                           double count, const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float* running_mean,
+                                                           float* running_var, const int64_t* nbt, float momentum,
+                                                           float eps, const float* __restrict__ mean_in,
+                                                           const float* __restrict__ invstd_in,
+                                                           float* __restrict__ out) {
+  __shared__ double sh[2][kFinSlices][64];
   const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   double a = 0.0, b = 0.0;
-  if (c < C)
-    for (int p = sl; p < nparts; p += 4) {
-      a += part[(int64_t)p * 2 * C + c];
-      b += part[(int64_t)p * 2 * C + C + c];
+  if (c < C) {
+    const int64_t rs = 2 * (int64_t)C;
+    const float* q = part + c;
+    int p = sl;
+    for (; p + 3 * kFinSlices < nparts; p += 4 * kFinSlices) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[2 * u] = q[(p + u * kFinSlices) * rs];
+        v[2 * u + 1] = q[(p + u * kFinSlices) * rs + C];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a += v[2 * u];
+        b += v[2 * u + 1];
+      }
     }
+    for (; p < nparts; p += kFinSlices) {
+      a += q[p * rs];
+      b += q[p * rs + C];
+    }
+  }
   sh[0][sl][cl] = a;
   sh[1][sl][cl] = b;
   __syncthreads();
   if (sl != 0 || c >= C) return;
-  a = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
-  b = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
+  a = 0.0;
+  b = 0.0;
+#pragma unroll
+  for (int k = 0; k < kFinSlices; ++k) {
+    a += sh[0][k][cl];
+    b += sh[1][k][cl];
+  }
   const float g = gamma ? gamma[c] : 1.f;
   if (!BWD) {
     const double mean = a / count;
@@ -264,10 +290,11 @@ int apply_grid(int64_t M, int C) {
 
 BnPlan bn_plan(int64_t M, int C) {
   const int rpi = kBnThreads / (C >> 3);
-  // >= 16 row iterations per thread, at most 1024 blocks and 256K partial floats
+  // >= 16 row iterations per thread, at most 512 blocks (2 per CU) and 128K partial
+  // floats, so the finalize kernel's 16 slices each sum <= 32 partial rows
   int64_t blocks = (M + (int64_t)rpi * 16 - 1) / ((int64_t)rpi * 16);
-  int64_t cap = (int64_t(1) << 18) / C;
-  if (cap > 1024) cap = 1024;
+  int64_t cap = (int64_t(1) << 17) / C;
+  if (cap > 512) cap = 512;
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   BnPlan p;
@@ -294,13 +321,13 @@ void launch_bn_partial(const uint16_t* x, const uint16_t* y, const uint16_t* dy,
 void launch_bn_finalize(const float* part, int nparts, int C, double count, const float* gamma,
                         const float* beta, float* running_mean, float* running_var, const int64_t* nbt,
                         float momentum, float eps, float* stats, hipStream_t s) {
-  hipLaunchKernelGGL((bn_finalize_kernel<false>), dim3((C + 63) / 64), dim3(256), 0, s, part, nparts, C, count,
+  hipLaunchKernelGGL((bn_finalize_kernel<false>), dim3((C + 63) / 64), dim3(1024), 0, s, part, nparts, C, count,
                      gamma, beta, running_mean, running_var, nbt, momentum, eps, nullptr, nullptr, stats);
 }
 
 void launch_bn_bwd_finalize(const float* part, int nparts, int C, double count, const float* gamma,
                             const float* mean, const float* invstd, float* coef, hipStream_t s) {
-  hipLaunchKernelGGL((bn_finalize_kernel<true>), dim3((C + 63) / 64), dim3(256), 0, s, part, nparts, C, count,
+  hipLaunchKernelGGL((bn_finalize_kernel<true>), dim3((C + 63) / 64), dim3(1024), 0, s, part, nparts, C, count,
                      gamma, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, mean, invstd, coef);
 }
 

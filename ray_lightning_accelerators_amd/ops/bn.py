@@ -92,8 +92,9 @@ class _BNActFn(torch.autograd.Function):
         dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
         mod.bn_bwd_apply(xv, yv, dyv, coef, ctx.relu, _nhwc(dx), _nhwc(dres) if dres is not None else None)
         wsrc = local if local is not None else coef
-        dgamma = wsrc[0].clone() if weight is not None and ctx.needs_input_grad[1] else None
-        dbeta = wsrc[1].clone() if ctx.needs_input_grad[2] else None
+        # views of the coefficient tensor (no copy kernels): autograd hands them to .grad
+        dgamma = wsrc[0] if weight is not None and ctx.needs_input_grad[1] else None
+        dbeta = wsrc[1] if ctx.needs_input_grad[2] else None
         return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None
 
 
