@@ -70,9 +70,13 @@ def _gpu_worker(rank, world, port, q, mode):
         from ray_lightning_accelerators_amd.parallel.comm import NativeCommunicator
 
         ts_modes = ("twoshot", "twoshot_timeout", "reducer_ts", "reducer_bf16")
-        comm = NativeCommunicator(use_rccl=False, use_xgmi=True,
-                                  xgmi_bytes=(1 << 10) if mode in ts_modes else (1 << 20),
-                                  twoshot_bytes=(4 << 20) if mode in ts_modes else 0, spin_limit=1 << 20)
+        if mode == "matrix":
+            comm = NativeCommunicator(use_rccl=False, use_xgmi=True, xgmi_bytes=2 << 20, twoshot_bytes=32 << 20,
+                                      spin_limit=1 << 22)
+        else:
+            comm = NativeCommunicator(use_rccl=False, use_xgmi=True,
+                                      xgmi_bytes=(1 << 10) if mode in ts_modes else (1 << 20),
+                                      twoshot_bytes=(4 << 20) if mode in ts_modes else 0, spin_limit=1 << 20)
         res = {"xgmi": comm.xgmi, "twoshot": comm.twoshot}
         dev = torch.device("cuda", 0)
         if mode == "twoshot":
@@ -115,6 +119,30 @@ def _gpu_worker(rank, world, port, q, mode):
                 gr.replay()
                 torch.cuda.synchronize()
                 res[f"graph{k}"] = bool(torch.all(y == world * (world + 1) / 2 + world * k).item())
+            comm.check()
+        elif mode == "matrix":
+            # correctness matrix: 4 B ... 32 MiB x {one-shot, two-shot fp32,
+            # two-shot bf16 wire, router}; integer-valued data so fp32 sums are exact
+            bad = []
+            sizes = [1, 2, 7, 64, 1000, 4096 + 3, 65536, 262147, 1 << 20, (1 << 21) + 5, 8 << 20]
+            for n in sizes:
+                base = (torch.arange(n, device=dev, dtype=torch.float32) % 31) - 15
+                want = base * (world * (world + 1) / 2)
+                paths = ["router", "twoshot", "bf16"] + (["oneshot"] if n <= comm.xgmi_capacity else [])
+                for path in paths:
+                    x = base * (rank + 1)
+                    if path == "oneshot":
+                        comm._c.allreduce_xgmi(x)
+                    elif path == "twoshot":
+                        comm._c.allreduce_twoshot(x, False)
+                    elif path == "bf16":
+                        comm._c.allreduce_twoshot(x, True)  # |values| <= 150: exact in bf16
+                    else:
+                        comm.allreduce_(x)
+                    torch.cuda.synchronize()
+                    if not torch.equal(x, want):
+                        bad.append((n, path, float((x - want).abs().max())))
+            res["bad"] = bad
             comm.check()
         elif mode == "twoshot_timeout":
             x = torch.ones(100000, device=dev)
@@ -267,6 +295,10 @@ def _gpu_worker(rank, world, port, q, mode):
                 sync.prepare_for_backward()
                 x, y = data(rank)
                 torch.nn.functional.mse_loss(model(x), y).backward()
+                # overlap: buckets are launched from the grad hooks DURING backward,
+                # not by finish()
+                res["launched_in_backward"] = (sync._native.launched if sync._native is not None
+                                               else sum(b.work is not None for b in sync.buckets))
                 sync.finish()
             ref = make()
             for r in range(world):
@@ -387,6 +419,8 @@ def test_ddp_native_reducer_two_ranks():
     for r, res in out.items():
         assert res["native_reducer"] and res["match"], (r, res)
         assert res["buckets"] >= 3 and res["launched"] == 2 * res["buckets"]
+        # every bucket went out from the hooks while backward was still running
+        assert res["launched_in_backward"] == 2 * res["buckets"], res
 
 
 @gpu
@@ -431,6 +465,15 @@ def test_xgmi_twoshot_allreduce(world):
         assert res["routes"] == {200: "oneshot", 5000: "twoshot", 300001: "twoshot"}, res["routes"]
     # bf16 wire: every replica holds the same bits
     assert len({res["bf16_bytes"] for res in out.values()}) == 1
+
+
+@gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_comm_correctness_matrix(world):
+    out = _run_gpu("matrix", world=world)
+    for r, res in out.items():
+        assert res["xgmi"] and res["twoshot"], (r, res)
+        assert not res["bad"], (r, res["bad"][:10])
 
 
 @gpu
