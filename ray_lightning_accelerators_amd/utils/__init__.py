@@ -1,1 +1,2 @@
-"""Utilities: profiling / tracing (profiling.py) and fault injection (faults.py)."""
+"""Utilities: profiling / tracing (profiling.py), fault injection (faults.py),
+throughput monitoring and the Prometheus exporter (metrics.py)."""
