@@ -60,6 +60,8 @@ def parse():
                     help="optimizer steps per captured hipGraph (native); 0 = eager launches")
     ap.add_argument("--n-data", type=int, default=55000)
     ap.add_argument("--bucket-mb", type=float, default=8.0, help="resnet50 DDP bucket cap (MiB)")
+    ap.add_argument("--benchmark-algos", type=int, default=1,
+                    help="resnet50: torch.backends.cudnn.benchmark (MIOpen find per shape), both impls")
     ap.add_argument("--grad-dtype", choices=["fp32", "bf16"], default="fp32",
                     help="resnet50 gradient wire dtype (bf16: converted inside the xGMI two-shot kernel)")
     ap.add_argument("--dp", choices=["fused", "split"], default="fused",
@@ -204,6 +206,7 @@ def make_resnet(args, world, rank, dev, x, y):
     from ray_lightning_accelerators_amd.models.resnet import resnet50
 
     torch.manual_seed(0)
+    torch.backends.cudnn.benchmark = bool(args.benchmark_algos)
     # native: BatchNorm+ReLU(+residual add) in the fused gfx950 kernels (ops/bn.py)
     model = resnet50(fused_bn=args.impl == "native").to(dev).to(memory_format=torch.channels_last)
     B = args.batch_size
