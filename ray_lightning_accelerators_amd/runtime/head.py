@@ -137,6 +137,12 @@ class Head:
             env["CUDA_VISIBLE_DEVICES"] = ""
         env["RLA_GPU_IDS"] = ",".join(gpu_ids)
         env["PYTHONUNBUFFERED"] = "1"
+        # Ray's contract: an actor's intra-op thread pools are sized to the CPUs it
+        # reserved (OMP_NUM_THREADS = num_cpus, at least 1) unless the caller chose;
+        # N workers x all-core OpenMP pools oversubscribe the node (measured: 2 MNIST
+        # workers on 8 CPUs ran 64 ms/step instead of ~2 ms)
+        if "OMP_NUM_THREADS" not in (msg.get("env") or {}):
+            env["OMP_NUM_THREADS"] = str(max(1, int(req.get("CPU", 1) or 1)))
         log = open(os.path.join(self.log_dir, f"worker-{actor_id[:8]}.log"), "ab")
         cmd = [sys.executable, "-m", "ray_lightning_accelerators_amd.runtime.worker"]
         proc = subprocess.Popen(cmd, env=env, stdout=log if msg.get("capture_output", True) else None,
