@@ -85,3 +85,44 @@ def test_sample_space():
     assert len(cfgs) == 12
     assert all(c["a"] in (32, 64) and 1e-4 <= c["lr"] <= 1e-1 for c in cfgs)
     assert sorted({c["g"] for c in cfgs}) == [1, 2, 3]
+
+
+class _GpuProbe:
+    """Stands in for one RayAccelerator GPU worker: reports its pinned device and
+    holds it for a moment, so concurrently running trials overlap."""
+
+    def hold(self, seconds):
+        import os
+        import time
+
+        t0 = time.time()
+        time.sleep(seconds)
+        return os.environ.get("HIP_VISIBLE_DEVICES"), t0, time.time()
+
+
+def _packing_trainable(config):
+    workers = [ray.remote(_GpuProbe).options(num_cpus=1, num_gpus=1).remote() for _ in range(2)]
+    out = ray.get([w.hold.remote(2.0) for w in workers])
+    for w in workers:
+        ray.kill(w)
+    tune.report(devices=",".join(d for d, _, _ in out), start=min(s for _, s, _ in out),
+                end=max(e for _, _, e in out))
+
+
+def test_tune_packs_4_trials_x_2_gpu_workers_on_8_gpus(tmpdir):
+    """BASELINE config 4 topology: 4 trials x RayAccelerator(num_workers=2, use_gpu=True) on one
+    8-GPU node (virtual GPU ledger: every device pinned to exactly one worker at a time)."""
+    ray.init(num_cpus=16, num_gpus=0, _nodes=[{"ip": "127.0.0.1", "num_cpus": 16, "num_gpus": 8,
+                                               "gpu_ids": [str(i) for i in range(8)]}])
+    try:
+        analysis = tune.run(_packing_trainable, config={"x": tune.choice([1, 2])}, num_samples=4,
+                            resources_per_trial={"cpu": 1, "extra_cpu": 2, "extra_gpu": 2},
+                            local_dir=str(tmpdir))
+        df = analysis.results_df
+        assert len(df) == 4
+        devs = [d for s in df["devices"] for d in s.split(",")]
+        assert sorted(devs) == [str(i) for i in range(8)], devs  # 8 distinct GPUs, one per worker
+        starts, ends = list(df["start"]), list(df["end"])
+        assert max(starts) < min(ends), "the 4 trials must run concurrently"
+    finally:
+        ray.shutdown()
