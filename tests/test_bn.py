@@ -167,3 +167,83 @@ def test_resnet50_fused_bn_matches_unfused_step():
     for (n, ra), rr in zip(a.named_buffers(), ref.buffers()):
         if "running_mean" in n:
             assert torch.allclose(ra, rr, atol=5e-2, rtol=5e-2), n
+
+
+# ------------------------------------------------------------- SyncBN (2 ranks)
+def _sync_worker(rank, world, port, q):
+    import os
+
+    import torch.distributed as dist
+
+    try:
+        torch.cuda.set_device(0)
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cuda", 0)
+        g = torch.Generator().manual_seed(5)
+        full = (torch.randn(4 * world, 64, 6, 6, generator=g) * 1.5 + 0.3).to(dev).to(torch.bfloat16)
+        dy_full = torch.randn(4 * world, 64, 6, 6, generator=g).to(dev).to(torch.bfloat16)
+        m = convert_sync_batchnorm(nn.Sequential(BatchNormAct2d(64))).to(dev)[0]
+        x = full[4 * rank:4 * (rank + 1)].contiguous(memory_format=torch.channels_last).requires_grad_()
+        y = m(x)
+        y.backward(dy_full[4 * rank:4 * (rank + 1)].contiguous(memory_format=torch.channels_last))
+        # reference: one process over the whole batch, fp32
+        ref = nn.BatchNorm2d(64).to(dev)
+        xr = full.float().requires_grad_()
+        yr = F.relu(ref(xr))
+        yr.backward(dy_full.float())
+        sl = slice(4 * rank, 4 * (rank + 1))
+        dg = m.weight.grad.clone()
+        dist.all_reduce(dg)  # local grads sum to the full-batch grad
+        q.put((rank, {
+            "fused": bnmod.stats["fused"] > 0,
+            "y": bool(torch.allclose(y.float(), yr[sl].detach(), atol=4e-2, rtol=2e-2)),
+            "rm": bool(torch.allclose(m.running_mean, ref.running_mean, atol=1e-4)),
+            "dx": float((x.grad.float() - xr.grad[sl]).abs().max() / xr.grad.abs().max()),
+            "dg": float((dg - ref.weight.grad).abs().max() / ref.weight.grad.abs().max()),
+        }))
+    except Exception:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sync_batchnorm_fused_two_ranks():
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_sync_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    for r, res in out.items():
+        assert isinstance(res, dict), res
+        assert res["fused"] and res["y"] and res["rm"], (r, res)
+        assert res["dx"] < 3e-2 and res["dg"] < 3e-2, (r, res)
+
+
+@pytest.mark.gpu
+def test_lightning_resnet50_trainer_gpu_fused_bn(tmpdir):
+    import ray_lightning_accelerators_amd.lightning as pl
+    from ray_lightning_accelerators_amd.models.resnet import LightningResNet50
+
+    before = bnmod.stats["fused"]
+    model = LightningResNet50({"image_size": 64, "num_classes": 10, "batch_size": 8, "n_train": 16, "lr": 0.01})
+    trainer = pl.Trainer(default_root_dir=str(tmpdir), gpus=1, max_epochs=1, limit_train_batches=2,
+                         checkpoint_callback=False)
+    assert trainer.fit(model) == 1
+    assert bnmod.stats["fused"] - before >= 2 * 53
+    assert torch.isfinite(torch.as_tensor(float(trainer.callback_metrics["train_loss"])))
