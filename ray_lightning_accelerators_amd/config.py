@@ -68,7 +68,9 @@ class RLAConfig:
     # generic-model compute precision ("32" or "bf16" autocast)
     precision: str = "32"
     # bounded polls of the xGMI kernels (iterations) and the watchdog period (ms)
-    spin_limit: int = 1 << 24
+    # (2^27 polls with s_sleep: minutes -- long enough for a legitimately slow peer,
+    # e.g. a rank still writing a checkpoint; a truly dead peer still ends the kernel)
+    spin_limit: int = 1 << 27
     watchdog_ms: int = 100
     # debug: verify that every DDP bucket the comm stream reads equals what the
     # compute stream produced (stream-ordering race detector)

@@ -593,6 +593,13 @@ class Trainer:
         metrics.update(self._reduce_epoch_metrics(f"{stage}_epoch_end"))
         self.call_hook(f"on_{stage}_epoch_end")
         self.call_hook(f"on_{stage}_end")
+        if stage == "validation" and getattr(self, "world_size", 1) > 1:
+            # ModelCheckpoint (on_validation_end) may have rank 0 writing a file: the
+            # other ranks wait for it here, not inside the next step's gradient
+            # collective, where a long write would look like a stalled peer
+            acc = self.accelerator_backend
+            if acc is not None and hasattr(acc, "barrier"):
+                acc.barrier("validation_end")
         if was_training:
             model.train()
         if not self.running_sanity_check:
@@ -701,6 +708,18 @@ class Trainer:
         self._update_lr_schedulers("epoch")
         if not validated:
             self._flush_logger()
+        self._check_collectives()
+
+    def _check_collectives(self) -> None:
+        """Fail fast on a collective that went wrong this epoch: the xGMI kernels'
+        bounded polls set an error word instead of hanging on a dead / stalled peer
+        (and skip that block's reduction), RCCL reports async errors -- surface
+        either as an exception on every rank."""
+        from ..parallel.comm import get_native_comm
+
+        comm = get_native_comm(create=False)
+        if comm is not None:
+            comm.check()
 
     def _batch_hooks_overridden(self, model: LightningModule) -> bool:
         names = ("on_train_batch_start", "on_train_batch_end", "on_batch_start", "on_batch_end")

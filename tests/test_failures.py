@@ -67,3 +67,23 @@ def test_profiler_resolution():
     with pytest.raises(ValueError):
         resolve_profiler("nope")
     assert StepTimer().summary() == {}
+
+
+def test_trainer_surfaces_collective_error(tmpdir, monkeypatch):
+    """A timed-out xGMI poll / RCCL async error recorded by the native communicator
+    is raised at the end of the epoch (fail-fast), not silently trained through."""
+    import pytest
+
+    import ray_lightning_accelerators_amd.lightning as pl
+    from ray_lightning_accelerators_amd.models.boring import BoringModel
+    from ray_lightning_accelerators_amd.parallel import comm as comm_mod
+
+    class _BadComm:
+        def check(self):
+            raise RuntimeError("collective failure on rank 0: xGMI allreduce: peer flag poll timed out")
+
+    monkeypatch.setattr(comm_mod, "get_native_comm", lambda create=True, **kw: _BadComm())
+    trainer = pl.Trainer(default_root_dir=str(tmpdir), max_epochs=1, limit_train_batches=2, limit_val_batches=1,
+                         checkpoint_callback=False)
+    with pytest.raises(RuntimeError, match="peer flag poll timed out"):
+        trainer.fit(BoringModel())
