@@ -84,7 +84,13 @@ void Communicator::init_rccl(const std::string& uid) {
   hip_check(hipSetDevice(device_), "hipSetDevice");
   ncclUniqueId id;
   std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
-  check_rccl(ncclCommInitRank(&comm_, world_, id, rank_), "ncclCommInitRank");
+  // a failed bring-up is not a collective failure: the caller falls back (e.g. two
+  // ranks sharing one device, which RCCL refuses) and the health state stays clean
+  const ncclResult_t r = ncclCommInitRank(&comm_, world_, id, rank_);
+  if (r != ncclSuccess) {
+    comm_ = nullptr;
+    throw std::runtime_error(std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  }
 }
 
 void Communicator::allreduce(void* buf, int64_t count, DType dt, RedOp op, hipStream_t s) {
