@@ -65,6 +65,10 @@ class RLAConfig:
     fused_dp: bool = True
     # capture the resident MNIST step into hipGraphs
     use_hip_graph: bool = True
+    # Trainer: fused resident steps issued per host dispatch when nothing observes
+    # single batches (chunks also end at log / validation / max_steps boundaries);
+    # 1 = one dispatch per batch.  Capped by the fused step's stats ring (64).
+    steps_per_dispatch: int = 64
     # generic-model compute precision ("32" or "bf16" autocast)
     precision: str = "32"
     # bounded polls of the xGMI kernels (iterations) and the watchdog period (ms)

@@ -27,6 +27,7 @@ from .callbacks import Callback, EarlyStopping, ModelCheckpoint
 from .core import LightningDataModule, LightningModule, _normalize_optimizers
 from .loggers import CSVLogger, LightningLoggerBase
 from .utilities import atomic_save, load_checkpoint, log, move_to_device, rank_zero_warn
+from ..config import get_config
 from ..utils.faults import maybe_inject as maybe_inject_fault
 from ..utils.profiling import resolve_profiler
 
@@ -116,6 +117,7 @@ class Trainer:
         replace_sampler_ddp: bool = True,
         reload_dataloaders_every_epoch: bool = False,
         fused_step: Optional[bool] = None,
+        steps_per_dispatch: Optional[int] = None,
         profiler=None,
         **kwargs,
     ):
@@ -154,6 +156,7 @@ class Trainer:
         self.reload_dataloaders_every_epoch = reload_dataloaders_every_epoch
         self.weights_summary = weights_summary
         self.fused_step = fused_step
+        self.steps_per_dispatch = steps_per_dispatch  # None: RLAConfig.steps_per_dispatch
         self.profiler = resolve_profiler(profiler)
         self.profiler_summary = ""
         if deterministic:
@@ -671,12 +674,15 @@ class Trainer:
         n = self.num_training_batches
         validated = False
         batches = None
+        chunk = self._dispatch_chunk(model)
         if self._fused is not None and hasattr(self._fused, "make_epoch_batches") and \
-                not self._batch_hooks_overridden(model) and dl is not None and n > 0:
+                (chunk > 1 or not self._batch_hooks_overridden(model)) and dl is not None and n > 0:
             batches = self._fused.make_epoch_batches(dl, n)  # data stays resident on the device
             if batches is not None:
                 n = min(n, len(batches))
-        if dl is not None and n > 0:
+        if dl is not None and n > 0 and chunk > 1 and batches is not None:
+            validated = self._run_chunked(model, n, chunk, epoch_outputs)
+        elif dl is not None and n > 0:
             for batch_idx, batch in enumerate(batches if batches is not None else dl):
                 if batch_idx >= n:
                     break
@@ -721,9 +727,72 @@ class Trainer:
         if comm is not None:
             comm.check()
 
-    def _batch_hooks_overridden(self, model: LightningModule) -> bool:
+    def _dispatch_chunk(self, model: LightningModule) -> int:
+        """Steps per host dispatch of the fused resident step (1 = one per batch).
+
+        Several steps go out at once (hipGraph replays, no per-batch Python) only
+        when nothing observes single batches: no batch hooks (callbacks that
+        implement ``on_train_chunk_end`` are chunk-aware and fine), no
+        step-interval LR scheduler, no fault injection at a given step."""
+        f = self._fused
+        if f is None or not hasattr(f, "train_chunk"):
+            return 1
+        k = self.steps_per_dispatch if self.steps_per_dispatch is not None else get_config().steps_per_dispatch
+        k = min(int(k), int(getattr(f, "max_chunk", 1)))
+        if k <= 1 or self._batch_hooks_overridden(model, chunk_aware_ok=True):
+            return 1
+        if any(getattr(model, nm, None) is not None for nm in ("on_batch_start", "on_batch_end")):
+            return 1
+        if any(s.get("interval", "epoch") == "step" for s in self.lr_schedulers):
+            return 1
+        if os.environ.get("RLA_FAULT_STEP") is not None:
+            return 1
+        return k
+
+    def _run_chunked(self, model: LightningModule, n: int, chunk: int, epoch_outputs: List[Any]) -> bool:
+        """The epoch's ``n`` resident batches in dispatches of <= ``chunk`` steps.
+        A dispatch ends where the per-batch loop would do host work: a logger
+        flush (``log_every_n_steps``), a validation point, ``max_steps`` or the
+        epoch end -- so metrics, checkpoints and Tune reports land on the same
+        steps as with per-batch dispatch.  Returns whether validation ran."""
+        every = max(1, self.log_every_n_steps)
+        bsz = int(getattr(self._fused, "_B", 0))
+        validated = False
+        b = 0
+        while b < n:
+            e = b
+            while True:
+                e += 1
+                gs = self.global_step + (e - b)
+                if (e >= n or e - b >= chunk or gs % every == 0 or self._should_validate(e - 1, False)
+                        or (self.max_steps is not None and gs >= self.max_steps)):
+                    break
+            k = e - b
+            self.profiler.start("run_training_batch")
+            outs = self._fused.train_chunk(k)
+            self.profiler.stop("run_training_batch")
+            self.global_step += k
+            epoch_outputs.extend(outs)
+            for cb in self.callbacks:
+                fn = getattr(cb, "on_train_chunk_end", None)
+                if fn is not None:
+                    fn(self, model, outs, k, k * bsz)
+            if self.global_step % every == 0:
+                self._flush_logger()
+            is_last = e >= n or (self.max_steps is not None and self.global_step >= self.max_steps)
+            if self._should_validate(e - 1, is_last):
+                self.run_evaluation(test_mode=False)
+                validated = True
+            if is_last or self.should_stop:
+                break
+            b = e
+        return validated
+
+    def _batch_hooks_overridden(self, model: LightningModule, chunk_aware_ok: bool = False) -> bool:
         names = ("on_train_batch_start", "on_train_batch_end", "on_batch_start", "on_batch_end")
         for cb in self.callbacks:
+            if chunk_aware_ok and callable(getattr(cb, "on_train_chunk_end", None)):
+                continue
             for nm in names:
                 if getattr(type(cb), nm, None) is not getattr(Callback, nm):
                     return True

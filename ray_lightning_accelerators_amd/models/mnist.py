@@ -159,6 +159,7 @@ class FusedMNISTStep:
         self._epoch_key = None
         self.eng = None  # v3 pipelined engine (resident-data mode), bound to the arena
         self._allreduce = None
+        self._capture_failed = False
         if self.world > 1:
             from ..parallel.comm import make_allreduce
 
@@ -270,6 +271,43 @@ class FusedMNISTStep:
         self.model.log("ptl/train_accuracy", stats[slot, 1] / stats[slot, 2].clamp(min=1))
         self.trainer.callback_metrics["loss"] = loss
         return {"loss": loss}
+
+    @property
+    def max_chunk(self) -> int:
+        """Most steps one :meth:`train_chunk` can report per-step losses for."""
+        return int(self.stats.size(0))  # the engine's stats ring has this size
+
+    def train_chunk(self, n_steps: int, graph_steps: int = 8):
+        """``n_steps`` consecutive resident-mode steps in one dispatch (hipGraph
+        replays of ``graph_steps`` steps each, captured once per epoch); the
+        Trainer uses it when nothing observes individual batches.  Returns the
+        per-step ``{"loss"}`` outputs (rows of one device gather, no host sync)."""
+        eng = self.eng
+        self._sync_lr()
+        g = self.opt.param_groups[0]
+        eng.lr, eng.betas, eng.eps, eng.wd = self.lr_val, tuple(g["betas"]), g["eps"], g["weight_decay"]
+        done = 0
+        if graph_steps > 1 and eng._graph is None and not self._capture_failed and get_config().use_hip_graph \
+                and n_steps > graph_steps and eng.steps_to_epoch_end() > graph_steps:
+            # one real (warm-up) step, then the recording; identical on every rank
+            self._capture_failed = not eng.capture(graph_steps)
+            done = 1
+        eng.run(n_steps - done)
+        first = self.gs.step
+        self.gs.step += n_steps
+        for q in g["params"]:
+            st = self.opt.state.get(q)
+            if st is not None and "step" in st:
+                st["step"].fill_(float(self.gs.step))
+        ring = eng.stats.size(0)
+        k = min(n_steps, ring)
+        slots = torch.tensor([(first + n_steps - k + i) % ring for i in range(k)], device=self.dev)
+        rows = eng.stats.index_select(0, slots)  # snapshot: the ring wraps in later chunks
+        last = rows[-1]
+        self.model.log("ptl/train_loss", last[0])
+        self.model.log("ptl/train_accuracy", last[1] / last[2].clamp(min=1))
+        self.trainer.callback_metrics["loss"] = last[0]
+        return [{"loss": rows[i, 0]} for i in range(k)]
 
     # --------------------------------------------------------------- state
     def sync_params_to_module(self) -> None:

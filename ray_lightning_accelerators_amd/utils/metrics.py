@@ -53,6 +53,7 @@ class ThroughputMonitor(Callback):
     def _reset(self) -> None:
         self._events: List[torch.cuda.Event] = []
         self._times: List[float] = []
+        self._weights: List[int] = []  # steps covered by each marked interval
         self._samples = 0
 
     def _gpu(self, pl_module) -> bool:
@@ -78,6 +79,14 @@ class ThroughputMonitor(Callback):
     def on_train_batch_end(self, trainer, pl_module, outputs, batch, batch_idx, dataloader_idx):
         self._samples += _batch_size(batch)
         self._mark(self._gpu(pl_module))
+        self._weights.append(1)
+
+    def on_train_chunk_end(self, trainer, pl_module, outputs, n_steps, n_samples):
+        """Multi-step dispatch (Trainer ``steps_per_dispatch``): one mark per chunk;
+        per-step times are the chunk's mean."""
+        self._samples += int(n_samples)
+        self._mark(self._gpu(pl_module))
+        self._weights.append(max(1, int(n_steps)))
 
     def _local(self) -> Dict[str, float]:
         if len(self._events) >= 2:
@@ -88,9 +97,11 @@ class ThroughputMonitor(Callback):
         if not d:
             return {"steps": 0.0, "samples": float(self._samples), "total_ms": 0.0}
         t = torch.tensor(d, dtype=torch.float64)
-        return {"steps": float(t.numel()), "samples": float(self._samples), "total_ms": float(t.sum()),
-                "mean_ms": float(t.mean()), "p50_ms": float(t.median()),
-                "p99_ms": float(torch.quantile(t, 0.99)), "max_ms": float(t.max())}
+        w = torch.tensor((self._weights + [1] * len(d))[: len(d)], dtype=torch.float64)
+        per = t / w
+        return {"steps": float(w.sum()), "samples": float(self._samples), "total_ms": float(t.sum()),
+                "mean_ms": float(t.sum() / w.sum()), "p50_ms": float(per.median()),
+                "p99_ms": float(torch.quantile(per, 0.99)), "max_ms": float(per.max())}
 
     def on_train_epoch_end(self, trainer, pl_module, outputs=None):
         ranks = gather_summaries(self._local())
@@ -174,6 +185,12 @@ class PrometheusExporter(Callback):
 
     def on_train_batch_end(self, trainer, pl_module, outputs, batch, batch_idx, dataloader_idx):
         if self._server is not None and (trainer.global_step + 1) % self.every == 0:
+            self._publish(trainer)
+
+    def on_train_chunk_end(self, trainer, pl_module, outputs, n_steps, n_samples):
+        # the Trainer already advanced global_step by the chunk
+        if self._server is not None and \
+                trainer.global_step // self.every != (trainer.global_step - int(n_steps)) // self.every:
             self._publish(trainer)
 
     def on_train_epoch_end(self, trainer, pl_module, outputs=None):
