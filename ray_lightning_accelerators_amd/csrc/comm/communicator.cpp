@@ -1,5 +1,6 @@
 #include "comm/communicator.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
@@ -240,7 +241,21 @@ int Communicator::route(const float* buf, int64_t count) const {
   if (world_ == 1) return 2;
   if (xgmi_ready_ && aligned && count <= slot_stride_ && count <= oneshot_max_) return 0;
   if (ts_ready_ && aligned && count <= twoshot_max_ && twoshot_plan(count, world_).cs <= ts_stride_) return 1;
+  // larger than the two-shot region: RCCL, unless there is none or two-shot is
+  // forced (allreduce_algo="twoshot" zeroes the one-shot limit) -- then the
+  // bucket goes through the region in consecutive region-sized launches
+  if (ts_ready_ && aligned && count <= twoshot_max_ && (!comm_ || oneshot_max_ == 0)) return 3;
   return comm_ ? 2 : -1;
+}
+
+int64_t Communicator::twoshot_launch_floats() const {
+  // n <= W * stride  <=>  ceil(ceil(n / W) / 4) * 4 <= stride (stride is a multiple of 64)
+  return ts_stride_ * world_;
+}
+
+void Communicator::allreduce_twoshot_chunked(float* buf, int64_t count, bool bf16_wire, hipStream_t s) {
+  const int64_t m = twoshot_launch_floats();  // multiple of 4: every piece stays 16-byte aligned
+  for (int64_t off = 0; off < count; off += m) allreduce_twoshot(buf + off, std::min(m, count - off), bf16_wire, s);
 }
 
 void Communicator::allreduce_f32(float* buf, int64_t count, hipStream_t s) {
@@ -248,14 +263,14 @@ void Communicator::allreduce_f32(float* buf, int64_t count, hipStream_t s) {
     case 0: allreduce_xgmi(buf, count, s); return;
     case 1: allreduce_twoshot(buf, count, false, s); return;
     case 2: allreduce(buf, count, DType::kF32, RedOp::kSum, s); return;
+    case 3: allreduce_twoshot_chunked(buf, count, false, s); return;
     default: throw std::runtime_error("no allreduce path for this bucket (xGMI capacity exceeded and no RCCL)");
   }
 }
 
 bool Communicator::allreduce_f32_bf16wire(float* buf, int64_t count, hipStream_t s) {
-  if (!ts_ready_ || (reinterpret_cast<uintptr_t>(buf) & 15) || twoshot_plan(count, world_).cs > ts_stride_)
-    return false;
-  allreduce_twoshot(buf, count, true, s);
+  if (!ts_ready_ || (reinterpret_cast<uintptr_t>(buf) & 15)) return false;
+  allreduce_twoshot_chunked(buf, count, true, s);  // one launch when it fits the region
   return true;
 }
 

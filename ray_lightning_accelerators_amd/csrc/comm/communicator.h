@@ -66,6 +66,9 @@ class Communicator {
   // largest bucket (floats) the two-shot region holds
   int64_t twoshot_capacity() const { return ts_ready_ ? ts_stride_ * world_ : 0; }
   void allreduce_twoshot(float* buf, int64_t count, bool bf16_wire, hipStream_t s);
+  // any length: consecutive launches of at most twoshot_launch_floats() each
+  void allreduce_twoshot_chunked(float* buf, int64_t count, bool bf16_wire, hipStream_t s);
+  int64_t twoshot_launch_floats() const;
 
   // ---- routing of fp32 SUM allreduces (DDP reducer, fusion engine, Python) ----
   // one-shot up to min(one-shot capacity, oneshot_max), then two-shot up to
@@ -75,10 +78,11 @@ class Communicator {
     oneshot_max_ = oneshot_max_floats;
     twoshot_max_ = twoshot_max_floats;
   }
-  // 0 = one-shot, 1 = two-shot, 2 = RCCL, -1 = no path
+  // 0 = one-shot, 1 = two-shot, 2 = RCCL, 3 = two-shot in region-sized launches
+  // (no RCCL, or two-shot forced), -1 = no path
   int route(const float* buf, int64_t count) const;
   void allreduce_f32(float* buf, int64_t count, hipStream_t s);
-  // bf16 wire: two-shot whenever it fits, else RCCL on a bf16 copy is the caller's job
+  // bf16 wire: two-shot (region-sized launches); false without a two-shot region
   bool allreduce_f32_bf16wire(float* buf, int64_t count, hipStream_t s);
 
   // ---- auxiliary peer region for kernels that exchange data themselves ----

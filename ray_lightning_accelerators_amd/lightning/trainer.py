@@ -15,6 +15,7 @@ Distribution is delegated to the accelerator object: the driver calls
 """
 from __future__ import annotations
 
+import gc
 import math
 import os
 from collections import defaultdict
@@ -212,6 +213,7 @@ class Trainer:
         self.interrupted = False
         self._has_val_loop = False
         self._fused = None
+        self._pending_log = None
         self._log_dir: Optional[str] = None
         self._train_dl_src = self._val_dl_src = self._test_dl_src = None
         self._results: Dict[str, Dict[str, list]] = {}
@@ -532,9 +534,29 @@ class Trainer:
             elif isinstance(v, torch.Tensor) and v.numel() == 1:
                 self.callback_metrics[k] = v.detach()
 
-    def _flush_logger(self) -> None:
-        if self.logger is not None and self.logged_metrics and self.is_global_zero:
-            self.logger.log_metrics({k: v for k, v in self.logged_metrics.items()}, step=self.global_step)
+    def _flush_logger(self, defer: bool = False) -> None:
+        """Hand ``logged_metrics`` to the logger.  ``defer`` (multi-step dispatch):
+        device values are copied to the host asynchronously and written at the
+        next flush, so a log point does not drain the GPU queue."""
+        self._write_pending_log()
+        if self.logger is None or not self.logged_metrics or not self.is_global_zero:
+            return
+        metrics = dict(self.logged_metrics)
+        if defer and any(isinstance(v, torch.Tensor) and v.is_cuda for v in metrics.values()):
+            snap = {k: (v.detach().to("cpu", non_blocking=True) if isinstance(v, torch.Tensor) and v.is_cuda else v)
+                    for k, v in metrics.items()}
+            ev = torch.cuda.Event()
+            ev.record()
+            self._pending_log = (snap, self.global_step, ev)
+            return
+        self.logger.log_metrics(metrics, step=self.global_step)
+
+    def _write_pending_log(self) -> None:
+        pending, self._pending_log = self._pending_log, None
+        if pending is not None:
+            snap, step, ev = pending
+            ev.synchronize()
+            self.logger.log_metrics(snap, step=step)
 
     # ---------------------------------------------------------- evaluation
     def run_sanity_check(self, model: LightningModule) -> None:
@@ -642,6 +664,12 @@ class Trainer:
                 self.logger.log_hyperparams(model.hparams)
         self.run_sanity_check(model)
         self.call_hook("on_train_start")
+        # Everything alive now (torch, the model, the data) is long-lived: move it
+        # out of the cyclic GC's generations, so a full collection during the
+        # epochs scans only the loop's own garbage instead of pausing the
+        # dispatching host for ~100 ms (measured on the fused MNIST epochs).
+        gc.collect()
+        gc.freeze()
         try:
             while self.current_epoch < self.max_epochs:
                 self._run_epoch(model)
@@ -654,9 +682,12 @@ class Trainer:
         except KeyboardInterrupt:
             self.interrupted = True
             self.call_hook("on_keyboard_interrupt")
+        finally:
+            gc.unfreeze()
         self.call_hook("on_train_end")
         self.call_hook("on_fit_end")
         if self.logger is not None:
+            self._write_pending_log()
             self.logger.finalize("success")
         self.training = False
         self.profiler_summary = self.profiler.summary()
@@ -778,7 +809,7 @@ class Trainer:
                 if fn is not None:
                     fn(self, model, outs, k, k * bsz)
             if self.global_step % every == 0:
-                self._flush_logger()
+                self._flush_logger(defer=True)
             is_last = e >= n or (self.max_steps is not None and self.global_step >= self.max_steps)
             if self._should_validate(e - 1, is_last):
                 self.run_evaluation(test_mode=False)
@@ -902,6 +933,7 @@ class Trainer:
     def __getstate__(self):
         d = self.__dict__.copy()
         d["_fused"] = None
+        d["_pending_log"] = None
         d["accelerator_backend"] = None
         return d
 

@@ -24,7 +24,7 @@ from typing import Any, Dict, Optional
 
 import torch
 import torch.nn.functional as F
-from torch.utils.data import DataLoader, Subset, random_split
+from torch.utils.data import DataLoader, DistributedSampler, SequentialSampler, Subset, random_split
 
 from ..config import get_config
 from ..lightning import LightningModule
@@ -123,6 +123,33 @@ def _u8_source(dataset):
     return None
 
 
+def _sampler_order(sampler) -> torch.Tensor:
+    """The sampler's epoch order as an int64 tensor.  DistributedSampler /
+    RandomSampler(no replacement) / SequentialSampler orders are rebuilt with
+    tensor ops (bit-identical to iterating them: same generator draws), not a
+    55K-element Python list per epoch; anything else is iterated."""
+    n = None
+    if isinstance(sampler, DistributedSampler):
+        n = len(sampler.dataset)
+        if sampler.shuffle:
+            g = torch.Generator()
+            g.manual_seed(sampler.seed + sampler.epoch)
+            idx = torch.randperm(n, generator=g)
+        else:
+            idx = torch.arange(n)
+        total = sampler.total_size
+        if not sampler.drop_last:
+            pad = total - n
+            if pad > 0:
+                idx = torch.cat([idx, idx.repeat(-(-pad // n))[:pad]])
+        else:
+            idx = idx[:total]
+        return idx[sampler.rank:total:sampler.num_replicas].contiguous()
+    if isinstance(sampler, SequentialSampler):
+        return torch.arange(len(sampler.data_source))
+    return torch.as_tensor(list(iter(sampler)), dtype=torch.int64)
+
+
 class FusedMNISTStep:
     """Drives the fused HIP step from the Trainer's loop (replaces autograd + optimizer)."""
 
@@ -201,7 +228,7 @@ class FusedMNISTStep:
         if self._u8 is None:
             self._u8 = images.to(self.dev).contiguous()
             self._labels = targets.to(self.dev, torch.int64).contiguous()
-        order = torch.as_tensor(list(iter(dl.sampler)), dtype=torch.int64)
+        order = _sampler_order(dl.sampler)
         if idx_map is not None:
             order = idx_map[order]
         B = dl.batch_size
@@ -301,7 +328,8 @@ class FusedMNISTStep:
                 st["step"].fill_(float(self.gs.step))
         ring = eng.stats.size(0)
         k = min(n_steps, ring)
-        slots = torch.tensor([(first + n_steps - k + i) % ring for i in range(k)], device=self.dev)
+        # device-side slot list: a host list would be a blocking H2D copy (a sync) per chunk
+        slots = (torch.arange(k, device=self.dev) + (first + n_steps - k)) % ring
         rows = eng.stats.index_select(0, slots)  # snapshot: the ring wraps in later chunks
         last = rows[-1]
         self.model.log("ptl/train_loss", last[0])

@@ -218,7 +218,7 @@ class NativeCommunicator:
         if self.xgmi or self.twoshot:
             r = int(self._c.route(t))
             if r >= 0 and not (r == 2 and not self.rccl):
-                return ("oneshot", "twoshot", "rccl")[r]
+                return ("oneshot", "twoshot", "rccl", "twoshot")[r]  # 3: region-sized pieces
         return "rccl" if self.rccl else "torch"
 
     def dp_context(self, capacity_floats: int) -> Optional[list]:

@@ -163,17 +163,32 @@ class FusedMLPEngine:
         gather wraps into valid indices; the next ``begin_epoch`` re-primes."""
         order = order.reshape(-1)[: n_batches * self.B]
         assert n_batches >= 1 and order.numel() == n_batches * self.B
-        assert int(order.max()) < self.n_data and int(order.min()) >= 0  # the kernels trust indices
-        if self.order is None or self.order.size(1) != order.numel():
+        # the kernels trust indices (a host order is checked without a device sync)
+        assert int(order.max()) < self.n_data and int(order.min()) >= 0
+        if self.order is None or self.order.size(1) != order.numel() or self.n_batches != int(n_batches):
+            # the captured graph bakes the order pointer and n_batches: only a new
+            # shape forces a re-capture, a new epoch of the same shape reuses it
             self.order = torch.empty(2, order.numel(), dtype=torch.int64, device=self.device)
-        dev_order = order.to(self.device)
-        self.order[0].copy_(dev_order)
-        self.order[1].copy_(dev_order)
+            self._graph = None
+        if order.device.type == "cpu" and self.native:
+            # staged through a pinned buffer: an async H2D copy instead of a blocking
+            # pageable one; the previous epoch's copy must be done before reuse
+            if getattr(self, "_order_ev", None) is not None:
+                self._order_ev.synchronize()
+            pin = getattr(self, "_order_pin", None)
+            if pin is None or pin.numel() != order.numel():
+                pin = self._order_pin = torch.empty(order.numel(), dtype=torch.int64, pin_memory=True)
+            pin.copy_(order)
+            self.order[0].copy_(pin, non_blocking=True)
+            self._order_ev = torch.cuda.Event()
+            self._order_ev.record()
+        else:
+            self.order[0].copy_(order.to(self.device))
+        self.order[1].copy_(self.order[0])
         self.n_batches = int(n_batches)
         self.counters[1:5].zero_()
         self._publish_counters()
         self.step_in_epoch = 0
-        self._graph = None
         self._primed = False
 
     # ------------------------------------------------------------------ data

@@ -12,10 +12,12 @@ first epoch (allocator, graph capture, RCCL warm-up) is reported, not scored.
         [--epochs 3] [--steps-per-dispatch 64] [--use-gpu 1]
 """
 import argparse
+import gc
 import json
 import os
 import sys
 import tempfile
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -27,15 +29,37 @@ from ray_lightning_accelerators_amd.utils.metrics import ThroughputMonitor  # no
 
 
 class _Dump(ThroughputMonitor):
+    """Also records the cyclic-GC pauses of each epoch (host stalls the monitor's
+    HIP-event intervals would otherwise show without a cause)."""
+
     def __init__(self, path):
         super().__init__()
         self.path = path
+        self._gc = []
+
+    def _gc_cb(self, phase, info):
+        if phase == "start":
+            self._gc_t0 = time.perf_counter()
+        else:
+            self._gc.append((info.get("generation"), 1e3 * (time.perf_counter() - self._gc_t0)))
+
+    def __getstate__(self):
+        d = dict(self.__dict__)
+        d["_gc"] = []
+        return d
+
+    def on_train_epoch_start(self, trainer, pl_module):
+        super().on_train_epoch_start(trainer, pl_module)
+        self._gc = []
+        if self._gc_cb not in gc.callbacks:
+            gc.callbacks.append(self._gc_cb)
 
     def on_train_epoch_end(self, trainer, pl_module, outputs=None):
         super().on_train_epoch_end(trainer, pl_module, outputs)
         if trainer.global_rank == 0:
             row = dict(self.history[-1], global_step=trainer.global_step,
-                       fused=trainer._fused is not None and getattr(trainer._fused, "eng", None) is not None)
+                       fused=trainer._fused is not None and getattr(trainer._fused, "eng", None) is not None,
+                       gc_collections=len(self._gc), gc_ms_max=round(max((t for _, t in self._gc), default=0.0), 3))
             with open(self.path, "a") as f:
                 f.write(json.dumps(row) + "\n")
 
@@ -71,8 +95,8 @@ def main():
     finally:
         ray.shutdown()
     rows = [json.loads(line) for line in open(out)]
-    steady = rows[1:] or rows
-    best = max(steady, key=lambda r: r.get("samples_per_sec", 0.0))
+    steady = sorted((rows[1:] or rows), key=lambda r: r.get("samples_per_sec", 0.0))
+    best = steady[len(steady) // 2]  # median steady-state epoch
     print(json.dumps({
         "metric": f"samples/sec (whole job), MNISTClassifier Trainer.fit via {type(acc).__name__}",
         "value": round(best.get("samples_per_sec", 0.0), 1), "unit": "samples/s", "workers": args.workers,

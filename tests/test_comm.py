@@ -128,11 +128,17 @@ def _gpu_worker(rank, world, port, q, mode):
             # correctness matrix: 4 B ... 32 MiB x {one-shot, two-shot fp32,
             # two-shot bf16 wire, router}; integer-valued data so fp32 sums are exact
             bad = []
-            sizes = [1, 2, 7, 64, 1000, 4096 + 3, 65536, 262147, 1 << 20, (1 << 21) + 5, 8 << 20]
+            # 32 Mi floats = 128 MiB: above the two-shot region -> region-sized launches
+            sizes = [1, 2, 7, 64, 1000, 4096 + 3, 65536, 262147, 1 << 20, (1 << 21) + 5, 8 << 20,
+                     (20 << 20) + 12, 32 << 20]
             for n in sizes:
                 base = (torch.arange(n, device=dev, dtype=torch.float32) % 31) - 15
                 want = base * (world * (world + 1) / 2)
-                paths = ["router", "twoshot", "bf16"] + (["oneshot"] if n <= comm.xgmi_capacity else [])
+                if n > comm.twoshot_capacity:
+                    res.setdefault("big_routes", []).append(comm.route(base))
+                    paths = ["router", "bf16_routed"]
+                else:
+                    paths = ["router", "twoshot", "bf16"] + (["oneshot"] if n <= comm.xgmi_capacity else [])
                 for path in paths:
                     x = base * (rank + 1)
                     if path == "oneshot":
@@ -141,6 +147,8 @@ def _gpu_worker(rank, world, port, q, mode):
                         comm._c.allreduce_twoshot(x, False)
                     elif path == "bf16":
                         comm._c.allreduce_twoshot(x, True)  # |values| <= 150: exact in bf16
+                    elif path == "bf16_routed":
+                        comm.allreduce_(x, bf16_wire=True)
                     else:
                         comm.allreduce_(x)
                     torch.cuda.synchronize()
@@ -480,6 +488,7 @@ def test_comm_correctness_matrix(world):
     for r, res in out.items():
         assert res["xgmi"] and res["twoshot"], (r, res)
         assert not res["bad"], (r, res["bad"][:10])
+        assert res["big_routes"] == ["twoshot", "twoshot"], (r, res["big_routes"])  # no RCCL: chunked two-shot
 
 
 @gpu

@@ -167,3 +167,21 @@ def test_fused_mnist_chunked_dispatch_matches_per_batch(tmpdir):
     for k, v in res[1][0].items():
         assert torch.equal(v, res[64][0][k]), k
     assert res[1][1] == res[64][1]
+
+
+@pytest.mark.parametrize("shuffle", [True, False])
+@pytest.mark.parametrize("drop_last", [True, False])
+@pytest.mark.parametrize("world,rank", [(1, 0), (3, 2), (8, 5)])
+def test_sampler_order_matches_iteration(shuffle, drop_last, world, rank):
+    """The fused path's tensor rebuild of a sampler's epoch order == iterating it."""
+    from torch.utils.data import DistributedSampler, SequentialSampler
+
+    from ray_lightning_accelerators_amd.models.mnist import _sampler_order
+
+    ds = RandomDataset(4, 1003)
+    s = DistributedSampler(ds, num_replicas=world, rank=rank, shuffle=shuffle, drop_last=drop_last, seed=7)
+    for epoch in (0, 3):
+        s.set_epoch(epoch)
+        assert torch.equal(_sampler_order(s), torch.tensor(list(iter(s)))), epoch
+    q = SequentialSampler(ds)
+    assert torch.equal(_sampler_order(q), torch.tensor(list(iter(q))))
