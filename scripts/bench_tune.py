@@ -1,0 +1,62 @@
+"""Tune sweep throughput (BASELINE "Tune sweep" row): the reference's
+``tune_mnist`` example (examples/ray_ddp_tune.py -- search space
+layer_1 x layer_2 x lr x batch_size, TuneReportCheckpointCallback at every
+validation end) run end to end on the local runtime, timed on the driver.
+
+Reports trials/hour for the whole sweep, the per-trial wall time and how many
+trials ran concurrently (trials x workers packed onto the visible GPUs).
+
+    python scripts/bench_tune.py [--trials 4] [--workers 1] [--epochs 2] [--use-gpu 1]
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "examples"))
+
+from ray_lightning_accelerators_amd import runtime as ray  # noqa: E402
+
+import ray_ddp_tune  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trials", type=int, default=4)
+    ap.add_argument("--workers", type=int, default=1)
+    ap.add_argument("--epochs", type=int, default=2)
+    ap.add_argument("--use-gpu", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="GPUs the runtime may pack trials onto")
+    args = ap.parse_args()
+    gpu = bool(args.use_gpu)
+    if gpu:
+        import torch
+
+        n_gpus = args.gpus if args.gpus is not None else torch.cuda.device_count()
+    else:
+        n_gpus = 0
+    os.environ.setdefault("TUNE_RESULTS_DIR", tempfile.mkdtemp())
+    ray.init(num_cpus=max(2, (args.workers + 1) * args.trials), num_gpus=n_gpus)
+    t0 = time.perf_counter()
+    try:
+        analysis = ray_ddp_tune.tune_mnist(os.path.join(tempfile.gettempdir(), "mnist_data_"), args.trials,
+                                           args.epochs, args.workers, gpu)
+    finally:
+        ray.shutdown()
+    wall = time.perf_counter() - t0
+    df = analysis.results_df
+    iters = [int(v) for v in df["training_iteration"]] if "training_iteration" in df else []
+    print(json.dumps({
+        "metric": "Tune sweep trials/hour (tune_mnist, RayAccelerator workers)",
+        "value": round(args.trials / wall * 3600.0, 1), "unit": "trials/hour", "trials": args.trials,
+        "workers_per_trial": args.workers, "gpus": n_gpus, "epochs_per_trial": args.epochs,
+        "wall_s": round(wall, 2), "s_per_trial": round(wall / args.trials, 2), "reports_per_trial": iters,
+        "best_config": analysis.best_config, "data": "synthetic"}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
