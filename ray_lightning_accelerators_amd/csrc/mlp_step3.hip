@@ -16,7 +16,7 @@
 //   tail(t)   blocks [0, 49): one 16-pixel W1 column tile each: dW1 tile =
 //             X[t]_tile^T dH1 (MFMA; X^T by ds_read_b64_tr_b16), Adam on the
 //             tile, then gather X[t+1]'s tile (u8 -> bf16) and add
-//             X[t+1]_tile . W1_tile^T into H1pre[t+1] (fp32 agent-scope atomics,
+//             X[t+1]_tile . W1_tile^T into H1pre[t+1] (32.32 fixed-point integer atomics,
 //             49 adders per element) -- layer 1 is linear in W1 and this block
 //             holds the freshly updated tile in registers.  The X tile is parked
 //             in `xring` for tail(t+1)'s dW1.
@@ -35,8 +35,8 @@
 // reads, [4] which of the two `order` epoch buffers counters[1] indexes.
 // H1pre is stored in MFMA-fragment order (element (b, m) at
 // (((b/16 * L1/16 + m/16) * 4 + b%4) * 64 + (b%16/4) * 16 + m%16) so every atomic
-// wave-instruction covers 256 contiguous bytes.  The fp32 atomics make H1pre's
-// last bits depend on arrival order (run-to-run drift at rounding level).
+// wave-instruction covers 256 contiguous bytes.  The integer atomics are
+// associative, so H1pre (and the step) does not depend on arrival order.
 #include "common.h"
 #include "kernels.h"
 #include "mlp_common.h"
