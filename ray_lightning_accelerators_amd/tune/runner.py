@@ -117,6 +117,17 @@ def run(
     used_cpu = used_gpu = 0.0
     by_id = {t.trial_id: t for t in trials}
     failures = []
+
+    def _on_result(trial_id: str, result: Dict[str, Any]) -> None:
+        t = by_id.get(trial_id)
+        if t is None or t.status != "RUNNING":
+            return
+        ckpt = result.pop("_checkpoint", None)
+        result["config"] = t.config
+        t.add_result(result, ckpt)
+        decision = scheduler.on_trial_result(t, result)
+        if _should_stop(stop, trial_id, result) or decision == TrialScheduler.STOP:
+            t.stop_requested = True
     try:
         while pending or running:
             # launch what fits
@@ -136,21 +147,17 @@ def run(
                 scheduler.on_trial_add(t)
             # results
             for trial_id, result in reports.get_blocking_batch(timeout=0.2):
-                t = by_id.get(trial_id)
-                if t is None or t.status != "RUNNING":
-                    continue
-                ckpt = result.pop("_checkpoint", None)
-                result["config"] = t.config
-                t.add_result(result, ckpt)
-                decision = scheduler.on_trial_result(t, result)
-                if _should_stop(stop, trial_id, result) or decision == TrialScheduler.STOP:
-                    t.stop_requested = True
+                _on_result(trial_id, result)
             # completions
             for tid, t in list(running.items()):
                 done = t.future.done()
                 if not done and not t.stop_requested:
                     continue
                 if done:
+                    # reports the trial queued before returning may still be in flight:
+                    # take them (every trial's, in queue order) before it is released
+                    for trial_id, result in reports.drain():
+                        _on_result(trial_id, result)
                     try:
                         runtime.get(t.future)
                         t.status = "TERMINATED"
@@ -162,14 +169,6 @@ def run(
                             print(f"Trial {tid} errored: {t.error[:2000]}", file=sys.stderr)
                 else:
                     t.status = "TERMINATED"
-                # drain any late reports of this trial before releasing it
-                for trial_id, result in reports.drain():
-                    tt = by_id.get(trial_id)
-                    if tt is not None and tt.status in ("RUNNING", "TERMINATED") and tt.last_result is not None \
-                            and result.get("training_iteration", 0) > tt.last_result.get("training_iteration", 0):
-                        ckpt = result.pop("_checkpoint", None)
-                        result["config"] = tt.config
-                        tt.add_result(result, ckpt)
                 runtime.kill(t.actor)
                 t.end_time = time.time()
                 del running[tid]

@@ -126,3 +126,18 @@ def test_tune_packs_4_trials_x_2_gpu_workers_on_8_gpus(tmpdir):
         assert max(starts) < min(ends), "the 4 trials must run concurrently"
     finally:
         ray.shutdown()
+
+
+def _report_once_and_return(config):
+    tune.report(score=config["i"])
+
+
+def test_last_report_of_a_finishing_trial_is_kept(tmpdir, ray_start_4_cpus):
+    """A trial that reports once and returns at once: its report can still be in the
+    queue when the runner sees the trial finish; it must land in the results, as must
+    the first reports of other trials drained at that moment."""
+    analysis = tune.run(_report_once_and_return, config={"i": tune.grid_search(list(range(8)))},
+                        resources_per_trial={"cpu": 1}, local_dir=str(tmpdir))
+    df = analysis.results_df
+    assert len(df) == 8
+    assert sorted(df["score"]) == list(range(8))
