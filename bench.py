@@ -307,7 +307,9 @@ def main():
     loss = last_loss()
     if rank == 0:
         rn = args.model == "resnet50"
-        base = None if rn else STOCK_BASELINE.get(world)
+        # the stock number is for the default 784-32-64-10 / batch-32 config only
+        default_cfg = (args.layer_1, args.layer_2, args.batch_size) == (32, 64, 32)
+        base = STOCK_BASELINE.get(world) if (not rn and default_cfg) else None
         out = {
             "metric": RESNET_METRIC if rn else METRIC,
             "value": round(value, 1),
