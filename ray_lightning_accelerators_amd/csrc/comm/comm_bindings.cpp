@@ -145,6 +145,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_spin_limit", &Communicator::set_spin_limit)
       .def("error_state", &Communicator::error_state)
       .def("error_message", &Communicator::error_message)
+      .def("reset_error", &Communicator::reset_error)
+      .def("disable_path", &Communicator::disable_path)
       .def("start_watchdog", &Communicator::start_watchdog, py::arg("period_ms") = 100)
       .def("abort", &Communicator::abort);
 

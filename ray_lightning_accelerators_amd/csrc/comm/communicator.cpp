@@ -364,6 +364,25 @@ void Communicator::start_watchdog(int period_ms) {
   watchdog_ = std::thread([this, period_ms] { watchdog_loop(period_ms); });
 }
 
+void Communicator::reset_error() {
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  if (state_.load() > 1) throw std::runtime_error("reset_error: RCCL failure or abort is not recoverable");
+  if (err_host_) __atomic_store_n(err_host_, 0, __ATOMIC_RELEASE);
+  state_ = 0;
+  std::lock_guard<std::mutex> g(mu_);
+  message_.clear();
+}
+
+void Communicator::disable_path(int which) {
+  switch (which) {
+    case 0: xgmi_ready_ = false; return;
+    case 1: ts_ready_ = false; return;
+    case 2: aux_ready_ = false; return;
+    default: throw std::invalid_argument("disable_path: 0 one-shot, 1 two-shot, 2 aux");
+  }
+}
+
 void Communicator::abort() {
   stop_ = true;
   if (watchdog_.joinable() && watchdog_.get_id() != std::this_thread::get_id()) watchdog_.join();

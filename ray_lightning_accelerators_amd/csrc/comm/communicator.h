@@ -101,6 +101,13 @@ class Communicator {
   std::string error_message();
   void start_watchdog(int period_ms);
   void abort();
+  // After a failed xGMI validation: clear a latched poll timeout (state 1 only --
+  // RCCL errors and aborts stay latched) so the fallback path can be used.
+  // Collective: every rank calls it after a device sync + barrier.
+  void reset_error();
+  // Take a path that failed validation out of the C++ router (0 one-shot,
+  // 1 two-shot, 2 aux exchange); its generations are desynchronised for good.
+  void disable_path(int which);
 
  private:
   void check_rccl(ncclResult_t r, const char* what);

@@ -71,8 +71,6 @@ class _CheckpointConnector:
         model = t.get_model()
         model.on_load_checkpoint(ckpt)
         model.load_state_dict(ckpt["state_dict"])
-        if t._fused is not None:
-            t._fused.load_params_from_module()
         for cb in t.callbacks:
             st = ckpt.get("callbacks", {}).get(cb.state_key)
             if st is not None:
@@ -81,6 +79,10 @@ class _CheckpointConnector:
             opt.load_state_dict(st)
         for s, st in zip(t.lr_schedulers, ckpt.get("lr_schedulers", [])):
             s["scheduler"].load_state_dict(st)
+        if t._fused is not None:
+            # after the optimizer state: the fused step's device step counter (Adam
+            # bias correction) is re-read from the restored optimizer step
+            t._fused.load_params_from_module()
         t.current_epoch = ckpt.get("epoch", 0)
         t.global_step = ckpt.get("global_step", 0)
 

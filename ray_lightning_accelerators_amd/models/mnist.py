@@ -271,8 +271,8 @@ class FusedMNISTStep:
             stats = eng.stats
             fused = True  # optimizer already applied
         else:
-            if self.eng is not None:
-                self.counters[0] = self.gs.step
+            # the optimizer step may have moved outside this object (resume, engine steps)
+            self.counters[0] = self.gs.step
             x, y = batch
             x = x.to(self.dev, non_blocking=True).reshape(x.size(0), -1).float().contiguous()
             y = y.to(self.dev, non_blocking=True).long().contiguous()

@@ -80,6 +80,7 @@ class NativeCommunicator:
         self.device = torch.cuda.current_device() if device is None else int(device)
         self._c = mod.Communicator(self.rank, self.world, self.device)
         self._stream = None
+        self.fallbacks: list = []  # paths that failed validation (see _drop_failed_path)
         self.rccl = False
         self.xgmi = False
         if use_rccl and os.environ.get("RLA_DISABLE_RCCL", "0") != "1":
@@ -129,8 +130,30 @@ class NativeCommunicator:
         if validate:
             ok = self._validate_xgmi(group)
             if not _agree(ok, group):
+                self._drop_failed_path(0, "xGMI one-shot", group)
                 return
         self.xgmi = True
+
+    def _drop_failed_path(self, which: int, name: str, group) -> None:
+        """A validation failed on some rank: take the path out of the C++ router on
+        EVERY rank and clear a latched poll timeout, so the fallback (two-shot /
+        RCCL / c10d) starts from a healthy communicator.  Collective."""
+        torch.cuda.synchronize(self.device)  # a timed-out kernel has drained by now
+        dist.barrier(group=group)
+        self._c.disable_path(which)
+        self._c.reset_error()
+        dist.barrier(group=group)
+        self.fallbacks.append(name)
+        if self.rank == 0:
+            import sys
+
+            print(f"[rla.comm] {name} failed validation on some rank; falling back", file=sys.stderr, flush=True)
+
+    def _fault_validation(self) -> bool:
+        """Fault injection (tests): ``RLA_FAULT_XGMI_VALIDATION=<rank>`` makes that
+        rank skip its validation launches, so its peers' polls time out exactly as
+        they would over a broken link."""
+        return os.environ.get("RLA_FAULT_XGMI_VALIDATION", "") == str(self.rank)
 
     def _validate_xgmi(self, group) -> bool:
         n = min(4096 + 4, int(self._c.xgmi_capacity))
@@ -142,6 +165,9 @@ class NativeCommunicator:
                 + it * self.world
             torch.cuda.synchronize(dev)
             dist.barrier(group=group)
+            if self._fault_validation():
+                ok = False  # the peers' kernels time out waiting for this rank's push
+                continue
             try:
                 self._c.allreduce_xgmi(x)
                 torch.cuda.synchronize(dev)
@@ -174,6 +200,7 @@ class NativeCommunicator:
         if validate:
             ok = self._validate_twoshot(group)
             if not _agree(ok, group):
+                self._drop_failed_path(1, "xGMI two-shot", group)
                 return
         self.twoshot = True
 
@@ -188,6 +215,9 @@ class NativeCommunicator:
             want = base * (self.world * (self.world + 1) / 2) + it * self.world
             torch.cuda.synchronize(dev)
             dist.barrier(group=group)
+            if self._fault_validation():
+                ok = False
+                continue
             try:
                 self._c.allreduce_twoshot(x, False)
                 torch.cuda.synchronize(dev)
@@ -196,6 +226,8 @@ class NativeCommunicator:
             ok = ok and self._c.error_state() == 0 and bool(torch.equal(x, want))
         x = torch.full((min(4100, big),), float(self.rank + 1), device=dev)
         dist.barrier(group=group)
+        if self._fault_validation():
+            return False
         try:
             self._c.allreduce_twoshot(x, True)  # small integers are exact in bf16
             torch.cuda.synchronize(dev)
@@ -342,7 +374,7 @@ class NativeCommunicator:
     def describe(self) -> str:
         return (f"NativeCommunicator(rank={self.rank}, world={self.world}, rccl={self.rccl}, "
                 f"xgmi={self.xgmi}, xgmi_capacity={self.xgmi_capacity}, twoshot={self.twoshot}, "
-                f"twoshot_capacity={self.twoshot_capacity})")
+                f"twoshot_capacity={self.twoshot_capacity}, failed_validation={self.fallbacks})")
 
 
 class _StreamWork:

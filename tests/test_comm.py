@@ -69,7 +69,11 @@ def _gpu_worker(rank, world, port, q, mode):
         _init(rank, world, port)
         from ray_lightning_accelerators_amd.parallel.comm import NativeCommunicator
 
-        ts_modes = ("twoshot", "twoshot_timeout", "reducer_ts", "reducer_bf16")
+        ts_modes = ("twoshot", "twoshot_timeout", "reducer_ts", "reducer_bf16", "validation_fault")
+        if mode == "validation_fault":
+            # rank 1 skips its validation launches: rank 0's bounded polls time out (error
+            # word latched); both paths must be dropped on BOTH ranks and the error cleared
+            os.environ["RLA_FAULT_XGMI_VALIDATION"] = "1"
         if mode == "matrix":
             comm = NativeCommunicator(use_rccl=False, use_xgmi=True, xgmi_bytes=2 << 20, twoshot_bytes=32 << 20,
                                       spin_limit=1 << 22)
@@ -80,7 +84,7 @@ def _gpu_worker(rank, world, port, q, mode):
                                       # short bounded polls only where a dead peer is simulated: elsewhere a
                                       # slow-starting peer process must not trip the timeout (a timed-out
                                       # block skips its reduction -- comm.check() reports it)
-                                      spin_limit=(1 << 20) if "timeout" in mode else (1 << 24))
+                                      spin_limit=(1 << 20) if ("timeout" in mode or mode == "validation_fault") else (1 << 24))
         res = {"xgmi": comm.xgmi, "twoshot": comm.twoshot}
         dev = torch.device("cuda", 0)
         if mode == "twoshot":
@@ -156,6 +160,16 @@ def _gpu_worker(rank, world, port, q, mode):
                         bad.append((n, path, float((x - want).abs().max())))
             res["bad"] = bad
             comm.check()
+        elif mode == "validation_fault":
+            res["fallbacks"] = list(comm.fallbacks)
+            res["state_after_setup"] = comm._c.error_state()
+            x = torch.full((70001,), float(rank + 1), device=dev)
+            res["route"] = comm.route(x)
+            comm.allreduce_(x)  # gloo bootstrap fallback (RCCL refuses 2 ranks on one device)
+            torch.cuda.synchronize()
+            res["sum_ok"] = bool(torch.all(x == world * (world + 1) / 2))
+            comm.check()  # must not raise: the latched timeout was cleared
+            res["checked"] = True
         elif mode == "twoshot_timeout":
             x = torch.ones(100000, device=dev)
             if rank == 0:
@@ -489,6 +503,18 @@ def test_comm_correctness_matrix(world):
         assert res["xgmi"] and res["twoshot"], (r, res)
         assert not res["bad"], (r, res["bad"][:10])
         assert res["big_routes"] == ["twoshot", "twoshot"], (r, res["big_routes"])  # no RCCL: chunked two-shot
+
+
+@gpu
+def test_failed_xgmi_validation_falls_back_cleanly():
+    """a validation timeout latched the error word for good, so a run
+    that correctly fell back still failed at the first ``check()``."""
+    out = _run_gpu("validation_fault")
+    for r, res in out.items():
+        assert not res["xgmi"] and not res["twoshot"], (r, res)
+        assert res["fallbacks"] == ["xGMI one-shot", "xGMI two-shot"], (r, res)
+        assert res["state_after_setup"] == 0 and res["checked"], (r, res)
+        assert res["route"] == "torch" and res["sum_ok"], (r, res)
 
 
 @gpu
