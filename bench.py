@@ -4,30 +4,49 @@
 Metric / config come from BASELINE.json: whole-node samples/sec for
 MNISTClassifier (MLP 784->32->64->10, Adam, per-worker batch 32 -- the
 reference's default config, examples/ray_ddp_example.py:167) at 1/2/4/8
-workers, one process per MI355X (torchrun / RayAccelerator worker), RCCL
-allreduce over xGMI between ranks.  Weak scaling: per-GPU batch is fixed.
+workers, one process per MI355X, gradient allreduce over xGMI between ranks.
+Weak scaling: the per-GPU batch is fixed.
 
 Data: synthetic MNIST-shaped uint8 images + labels (55,000 train samples, the
 reference's train split), random-init weights; each rank trains on its
 DistributedSampler shard.  Every timed step is a full optimizer step:
 forward, NLL loss, backward, gradient allreduce (N > 1), Adam update.
 
-Implementations (``--impl``):
-  native  the framework's engine: fused gfx950 HIP step kernel (bf16 MFMA,
-          fp32 master weights/Adam), flat-arena allreduce, fused Adam,
-          hipGraph replay of the per-step device work.
-  torch   stock PyTorch-ROCm baseline: nn.Linear MLP under bf16 autocast,
-          torch.optim.Adam, DistributedDataParallel over RCCL (N > 1).
+Launch (one rank per GPU; the launching process never touches the GPU):
+  * ``python bench.py --gpus N`` starts N ``RayExecutor`` actors on the
+    framework's runtime -- the workers ``RayAccelerator(num_workers=N,
+    use_gpu=True)`` uses, each pinned to its GPU with HIP_VISIBLE_DEVICES
+    (reference ray_ddp.py:92-107) -- and prints rank 0's JSON line
+    (``--launcher spawn``: N plain child processes that see every GPU, as
+    torchrun starts them);
+  * ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``:
+    every process is one rank (RANK / LOCAL_RANK / WORLD_SIZE from the env).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N > 1 is launched by torch.distributed.run, one rank per GPU)
+Implementations (``--impl``):
+  native       the framework's engine: fused gfx950 HIP step kernels (bf16
+               MFMA, fp32 master weights/Adam), gradient exchange over xGMI
+               inside the tail kernel (N > 1), hipGraph replay.
+  torch        stock PyTorch-ROCm: nn.Linear MLP under bf16 autocast,
+               torch.optim.Adam, DistributedDataParallel over RCCL (N > 1).
+  torch-graph  the same stock step captured with torch.cuda.graph (capturable
+               Adam, device-side batch cursor), N = 1.
+
+``--via trainer``: the number is ``Trainer.fit`` of ``MNISTClassifier`` through
+``RayAccelerator`` (``--accelerator horovod``: ``HorovodRayAccelerator``),
+wall-clock over the steady epochs INCLUDING the full validation pass and the
+checkpoint write of every epoch (reference examples/ray_ddp_example.py:61-76).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--via engine|trainer]
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import statistics
+import subprocess
 import sys
+import tempfile
 import time
 
 import torch
@@ -37,39 +56,55 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+from ray_lightning_accelerators_amd.lightning.callbacks import Callback  # noqa: E402
+
 METRIC = "samples/sec (whole node) + DDP scaling eff, MNISTClassifier at 1/2/4/8 workers"
-# Our measured stock-PyTorch numbers on MI355X (BASELINE.md "Our MI355X measurements");
-# the reference itself publishes none.  None => vs_baseline is null.
 RESNET_METRIC = "images/sec (whole node), ResNet-50 synthetic ImageNet 224px"
-STOCK_BASELINE = {1: 53015.0}  # --impl torch, 1x MI355X (profiles/r1_first/bench_torch.jsonl)
+# Stock PyTorch-ROCm on one MI355X at the default 784-32-64-10 / batch-32 config
+# (BASELINE.md "Our MI355X measurements"; the reference publishes no numbers).
+# vs_baseline divides by the FASTER stock implementation.
+STOCK_BASELINE = {
+    "torch": 53015.0,        # eager nn.Linear + torch.optim.Adam (profiles/r1_first/bench_torch.jsonl)
+    "torch-graph": 165417.2,  # the same step under torch.cuda.graph, 8 steps/graph (profiles/r2_c03)
+}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU; CPU processes with --device cpu)")
     ap.add_argument("--steps", type=int, default=None, help="default 2000 (mnist) / 20 (resnet50)")
     ap.add_argument("--warmup", type=int, default=None, help="default 200 (mnist) / 5 (resnet50)")
     ap.add_argument("--model", choices=["mnist", "resnet50"], default="mnist",
                     help="mnist: the BASELINE headline (MNISTClassifier); resnet50: config 5 (bucket stress)")
-    ap.add_argument("--impl", choices=["native", "torch"], default="native")
+    ap.add_argument("--impl", choices=["native", "torch", "torch-graph"], default="native")
+    ap.add_argument("--via", choices=["engine", "trainer"], default="engine",
+                    help="engine: the worker hot loop; trainer: Trainer.fit through the accelerator")
+    ap.add_argument("--accelerator", choices=["ddp", "horovod"], default="ddp",
+                    help="ddp: RayAccelerator / DDP process group; horovod: HorovodRayAccelerator / hvd API")
+    ap.add_argument("--launcher", choices=["ray", "spawn"], default="ray",
+                    help="N>1 without torchrun: runtime actors (GPU-pinned) or plain child processes")
+    ap.add_argument("--device", choices=["auto", "cuda", "cpu"], default="auto")
     ap.add_argument("--batch-size", type=int, default=None, help="per GPU; default 32 (mnist) / 128 (resnet50)")
     ap.add_argument("--layer-1", type=int, default=32)
     ap.add_argument("--layer-2", type=int, default=64)
     ap.add_argument("--lr", type=float, default=1e-1)
     ap.add_argument("--graph-steps", type=int, default=8,
-                    help="optimizer steps per captured hipGraph (native); 0 = eager launches")
+                    help="optimizer steps per captured hipGraph (native, torch-graph); 0 = eager launches")
     ap.add_argument("--n-data", type=int, default=55000)
+    ap.add_argument("--trainer-epochs", type=int, default=4, help="--via trainer: epochs (the first is warm-up)")
     ap.add_argument("--bucket-mb", type=float, default=8.0, help="resnet50 DDP bucket cap (MiB)")
+    ap.add_argument("--bucket-sweep", type=str, default=None,
+                    help="resnet50: comma list of bucket caps (MiB) measured in one run, e.g. 1,2,4,8,16,25")
     ap.add_argument("--benchmark-algos", type=int, default=1,
                     help="resnet50: torch.backends.cudnn.benchmark (MIOpen find per shape), both impls")
     ap.add_argument("--grad-dtype", choices=["fp32", "bf16"], default="fp32",
                     help="resnet50 gradient wire dtype (bf16: converted inside the xGMI two-shot kernel)")
-    ap.add_argument("--dp", choices=["fused", "split"], default="fused",
-                    help="mnist N>1: 'fused' exchanges gradients inside the tail kernel over xGMI "
-                         "(falls back to 'split' = head/tail/allreduce/tail when xGMI is unavailable)")
+    ap.add_argument("--dp", choices=["fused", "split"], default=None,
+                    help="mnist N>1: 'fused' exchanges gradients inside the tail kernel over xGMI; 'split' = "
+                         "head/tail/allreduce/tail (default: fused for ddp, split for horovod)")
     ap.add_argument("--comm", choices=["auto", "xgmi", "rccl", "torch"], default="auto",
-                    help="N>1 gradient allreduce: native xGMI one-shot (auto/xgmi), native RCCL, or c10d")
-    args = ap.parse_args()
+                    help="N>1 gradient allreduce: native xGMI (auto/xgmi), native RCCL, or c10d")
+    args = ap.parse_args(argv)
     rn = args.model == "resnet50"
     if args.steps is None:
         args.steps = 20 if rn else 2000
@@ -77,30 +112,55 @@ def parse():
         args.warmup = 5 if rn else 200
     if args.batch_size is None:
         args.batch_size = 128 if rn else 32
+    if args.dp is None:
+        args.dp = "split" if args.accelerator == "horovod" else "fused"
+    if args.device == "auto":
+        # device_count() does not initialise HIP on this image (the launcher stays GPU-free)
+        args.device = "cuda" if torch.cuda.device_count() > 0 else "cpu"
     return args
 
 
-def setup_dist(args):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
-    if os.environ.get("RLA_BENCH_SHARE_GPU") == "1":
-        # rehearsal of the N>1 path on a 1-GPU box: every rank on device 0, gloo
-        # bootstrap, native xGMI-protocol allreduce through same-device IPC
-        # (throughput is meaningless in this mode; correctness is the point)
-        local = 0
-        torch.cuda.set_device(0)
-        if world > 1:
-            dist.init_process_group("gloo", rank=rank, world_size=world)
-        return world, rank, local
-    torch.cuda.set_device(local)
+# ------------------------------------------------------------------ ranks
+def rank_env():
+    """(world, rank, local) when this process is one rank of a launched job."""
+    if "RANK" in os.environ and "WORLD_SIZE" in os.environ:
+        return int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"]), int(os.environ.get("LOCAL_RANK", "0"))
+    return None
+
+
+def share_gpu() -> bool:
+    # rehearsal of the N>1 path on a 1-GPU box: every rank on device 0, gloo
+    # bootstrap, native xGMI-protocol collectives through same-device IPC
+    # (throughput is meaningless in this mode; correctness is the point)
+    return os.environ.get("RLA_BENCH_SHARE_GPU") == "1"
+
+
+def setup_dist(args, world, rank, local):
+    cpu = args.device == "cpu"
+    if cpu:
+        dev = torch.device("cpu")
+    else:
+        if share_gpu() or torch.cuda.device_count() == 1:
+            local = 0  # pinned worker (HIP_VISIBLE_DEVICES) or shared device
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local))
-    return world, rank, local
+        backend = "gloo" if (cpu or share_gpu()) else "nccl"
+        kw = {} if backend == "gloo" else {"device_id": dev}
+        if args.accelerator == "horovod":
+            import ray_lightning_accelerators_amd.horovod as hvd
+
+            os.environ.setdefault("HOROVOD_LOCAL_RANK", str(local))
+            if backend == "nccl":
+                os.environ["RLA_HVD_USE_GPU"] = "1"
+            if backend == "gloo":
+                dist.init_process_group("gloo", rank=rank, world_size=world)
+            hvd.init()
+            assert hvd.size() == world and hvd.rank() == rank
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+        assert dist.get_world_size() == world, (dist.get_world_size(), world)
+    return dev
 
 
 def barrier(world):
@@ -108,67 +168,135 @@ def barrier(world):
         dist.barrier()
 
 
-def make_native(args, world, rank, dev, x, y):
+def sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def log(rank, msg):
+    if rank == 0:
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+# ----------------------------------------------------------- native engine
+def make_native(args, world, rank, dev, x, y, force_split=False):
     from ray_lightning_accelerators_amd.parallel.mlp_engine import FusedMLPEngine
 
     allreduce = None
     dp_ctx = None
+    route = "single"
     if world > 1:
-        # native data plane: xGMI one-shot push allreduce for the gradient bucket
-        # (validated at setup, RCCL fallback), enqueued on the step's stream so
-        # the hipGraph captures it with the step kernels
         from ray_lightning_accelerators_amd.parallel.comm import get_native_comm
 
         comm = None
-        if args.comm != "torch":
-            # one 109-532 KiB bucket per step: the one-shot area covers it, so no
-            # two-shot region is allocated
+        if args.comm != "torch" and dev.type == "cuda":
+            # one 109-532 KiB bucket per step: the one-shot area covers it, no two-shot region
             comm = get_native_comm(use_xgmi=args.comm in ("auto", "xgmi"),
                                    use_rccl=dist.get_backend() == "nccl", twoshot_bytes=0)
         if comm is not None:
-            if rank == 0:
-                print(comm.describe(), file=sys.stderr, flush=True)
-            allreduce = comm.allreduce_
-            if args.dp == "fused":
+            log(rank, comm.describe())
+            assert comm.world == world
+            if args.accelerator == "horovod":
+                import ray_lightning_accelerators_amd.horovod as hvd
+
+                allreduce = lambda t: hvd.allreduce_(t, op=hvd.Sum)  # noqa: E731 - hvd API on the native engine
+            else:
+                allreduce = comm.allreduce_
+            if args.dp == "fused" and not force_split:
                 from ray_lightning_accelerators_amd.ops.fused_mlp import mlp_param_count
 
                 dp_ctx = comm.dp_context(mlp_param_count(args.layer_1, args.layer_2))
-                if rank == 0:
-                    print(f"fused data-parallel tail: {'on' if dp_ctx else 'unavailable (split path)'}",
-                          file=sys.stderr, flush=True)
+            route = "xgmi-fused" if dp_ctx else "split-native"
         else:
-            allreduce = dist.all_reduce
-
+            def allreduce(t):
+                if t.is_cuda and dist.get_backend() == "gloo":
+                    c = t.cpu()
+                    dist.all_reduce(c)
+                    t.copy_(c)
+                else:
+                    dist.all_reduce(t)
+            route = f"split-c10d-{dist.get_backend()}"
     eng = FusedMLPEngine(args.layer_1, args.layer_2, args.batch_size, lr=args.lr, device=dev,
                          world_size=world, rank=rank, allreduce=allreduce, seed=0, dp_context=dp_ctx)
     eng.set_data(x, y, shuffle=True)
     eng.broadcast_from(0)
-    if args.graph_steps > 0:
-        ok = eng.capture(args.graph_steps)
-        if not ok and rank == 0:
-            print("hipGraph capture failed; running eager", file=sys.stderr)
+    if route == "split-native":
+        from ray_lightning_accelerators_amd.parallel.comm import get_native_comm
+
+        route = f"split-{get_native_comm(create=False).route(eng.comm_buffer)}"  # oneshot / rccl / torch
+    graphed = False
+    if args.graph_steps > 0 and dev.type == "cuda" and route not in ("split-c10d-gloo", "split-torch"):
+        graphed = eng.capture(args.graph_steps)
+        if not graphed:
+            log(rank, "hipGraph capture failed; running eager launches")
+
     def replica_checksum():
         return float(eng.params.double().sum()) + 1e-3 * float(eng.params.double().abs().sum())
 
-    return eng.run, (lambda: float(eng.recent_stats(20)[:, 0].mean())), replica_checksum
+    info = {"route": route, "hip_graph_steps": args.graph_steps if graphed else 0}
+    return eng.run, (lambda: float(eng.recent_stats(20)[:, 0].mean())), replica_checksum, info
+
+
+def degrade_to_split(args, world, rank, dev, x, y):
+    """The fused xGMI exchange misbehaved in warm-up (timeout or diverged replicas):
+    drop every xGMI path on every rank, clear the latched error and rebuild the
+    engine on the split path over RCCL (c10d when RCCL is unavailable)."""
+    from ray_lightning_accelerators_amd.parallel.comm import get_native_comm
+
+    comm = get_native_comm(create=False)
+    if comm is not None:
+        sync(dev)
+        barrier(world)
+        for path in (0, 1, 2):
+            comm._c.disable_path(path)
+        comm.xgmi = comm.twoshot = False
+        try:
+            comm._c.reset_error()
+        except RuntimeError:
+            pass
+        barrier(world)
+    log(rank, "fused xGMI data path failed its warm-up check; re-running on the split RCCL path")
+    return make_native(args, world, rank, dev, x, y, force_split=True)
+
+
+def replicas_agree(world, checksum) -> bool:
+    sums = [None] * world
+    dist.all_gather_object(sums, checksum())
+    return all(v == sums[0] for v in sums)
+
+
+def comm_healthy(world) -> bool:
+    from ray_lightning_accelerators_amd.parallel.comm import _agree, get_native_comm
+
+    comm = get_native_comm(create=False)
+    ok = comm is None or comm._c.error_state() == 0
+    return _agree(ok)
+
+
+# ------------------------------------------------------------ stock torch
+def _stock_mlp(args, dev):
+    import torch.nn as nn
+
+    torch.manual_seed(0)
+    return nn.Sequential(nn.Linear(784, args.layer_1), nn.ReLU(), nn.Linear(args.layer_1, args.layer_2),
+                         nn.ReLU(), nn.Linear(args.layer_2, 10)).to(dev)
 
 
 def make_torch(args, world, rank, dev, x, y):
-    import torch.nn as nn
     import torch.nn.functional as F
+
     from ray_lightning_accelerators_amd.parallel.mlp_engine import shard_indices
 
-    torch.manual_seed(0)
-    model = nn.Sequential(nn.Linear(784, args.layer_1), nn.ReLU(), nn.Linear(args.layer_1, args.layer_2),
-                          nn.ReLU(), nn.Linear(args.layer_2, 10)).to(dev)
+    model = _stock_mlp(args, dev)
     if world > 1:
-        model = nn.parallel.DistributedDataParallel(model, device_ids=[dev.index])
+        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index] if dev.type == "cuda" else None)
     opt = torch.optim.Adam(model.parameters(), lr=args.lr)
     xd, yd = x.to(dev), y.to(dev)
     B = args.batch_size
     state = {"epoch": 0, "i": 0, "last": 0.0}
     per_rank = -(-x.size(0) // world)
     nb = per_rank // B
+    amp = dev.type == "cuda"
 
     def load(epoch):
         state["order"] = shard_indices(x.size(0), world, rank, epoch, 0, True, device=dev)[: nb * B]
@@ -186,25 +314,81 @@ def make_torch(args, world, rank, dev, x, y):
             xb = xd.index_select(0, idx).float().div_(255.0)
             yb = yd.index_select(0, idx)
             opt.zero_grad(set_to_none=True)
-            with torch.autocast("cuda", dtype=torch.bfloat16):
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
                 logits = model(xb)
             loss = F.nll_loss(F.log_softmax(logits.float(), dim=1), yb)
             loss.backward()
             opt.step()
             state["loss"] = loss
 
-    return run, (lambda: float(state["loss"].item()))
+    return run, (lambda: float(state["loss"].item())), None, {"route": "torch-ddp" if world > 1 else "single"}
 
 
-def make_resnet(args, world, rank, dev, x, y):
+def make_torch_graph(args, world, rank, dev, x, y):
+    """Stock step under torch.cuda.graph: capturable Adam, resident data, a device
+    batch cursor advanced inside the graph (so replays walk the epoch)."""
+    import torch.nn.functional as F
+
+    from ray_lightning_accelerators_amd.parallel.mlp_engine import shard_indices
+
+    if world > 1 or dev.type != "cuda":
+        raise SystemExit("--impl torch-graph measures the 1-GPU stock baseline only")
+    model = _stock_mlp(args, dev)
+    opt = torch.optim.Adam(model.parameters(), lr=args.lr, capturable=True)
+    B = args.batch_size
+    xd, yd = x.to(dev), y.to(dev)
+    nb = x.size(0) // B
+    order = shard_indices(x.size(0), 1, 0, 0, 0, True, device=dev)[: nb * B].view(nb, B)
+    cursor = torch.zeros((), dtype=torch.int64, device=dev)
+    loss_buf = torch.zeros((), device=dev)
+
+    def step():
+        idx = order.index_select(0, cursor.view(1)).view(B)
+        xb = xd.index_select(0, idx).float().div_(255.0)
+        yb = yd.index_select(0, idx)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            logits = model(xb)
+        loss = F.nll_loss(F.log_softmax(logits.float(), dim=1), yb)
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=False)
+        cursor.add_(1).remainder_(nb)
+        loss_buf.copy_(loss.detach())
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):  # warm-up outside capture (allocator, autograd state, Adam state)
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    G = max(1, args.graph_steps)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(G):
+            step()
+
+    def run(n):
+        for _ in range(n // G):
+            g.replay()
+        for _ in range(n % G):
+            step()
+
+    return run, (lambda: float(loss_buf.item())), None, {"route": "single", "hip_graph_steps": G}
+
+
+# ----------------------------------------------------------------- ResNet
+def make_resnet(args, world, rank, dev, x, y, bucket_mb=None):
     """ResNet-50, synthetic ImageNet batch resident on the GPU, bf16 autocast, NHWC.
 
     native: flat fp32 arena + ONE fused SGD-momentum launch, bucketed in-place
     allreduce on the native comm engine's side stream overlapping backward.
     torch:  torch DDP (RCCL) + torch.optim.SGD(foreach)."""
     import torch.nn.functional as F
+
     from ray_lightning_accelerators_amd.models.resnet import resnet50
 
+    if dev.type != "cuda":
+        raise SystemExit("--model resnet50 needs a GPU")
     torch.manual_seed(0)
     torch.backends.cudnn.benchmark = bool(args.benchmark_algos)
     # native: BatchNorm+ReLU(+residual add) in the fused gfx950 kernels (ops/bn.py)
@@ -214,40 +398,46 @@ def make_resnet(args, world, rank, dev, x, y):
     xb = torch.randn(B, 3, 224, 224, device=dev, generator=g).contiguous(memory_format=torch.channels_last)
     yb = torch.randint(0, 1000, (B,), device=dev, generator=g)
     state = {}
+    info = {"route": "single"}
     if args.impl == "native":
         from ray_lightning_accelerators_amd.parallel.arena import ParamArena
         from ray_lightning_accelerators_amd.parallel.ddp import GradSynchronizer
         from ray_lightning_accelerators_amd.parallel.fused_optim import fuse_optimizer
 
         arena = ParamArena(model)
-        sync = None
+        sync_ = None
         if world > 1:
             from ray_lightning_accelerators_amd.parallel.comm import get_native_comm
 
-            get_native_comm()
-            sync = GradSynchronizer(model, arena, bucket_cap_mb=args.bucket_mb, grad_dtype=args.grad_dtype,
-                                    average_in_optimizer=True)
-            sync.broadcast_parameters(0)
+            comm = get_native_comm()
+            if comm is not None:
+                log(rank, comm.describe())
+            sync_ = GradSynchronizer(model, arena, bucket_cap_mb=bucket_mb or args.bucket_mb,
+                                     grad_dtype=args.grad_dtype, average_in_optimizer=True)
+            sync_.broadcast_parameters(0)
+            info = {"route": "native-reducer", "bucket_mb": bucket_mb or args.bucket_mb}
         opt = fuse_optimizer(torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5), arena,
-                             grad_scale_fn=(lambda: sync.grad_scale) if sync is not None else None)
+                             grad_scale_fn=(lambda: sync_.grad_scale) if sync_ is not None else None)
 
         def run(n):
             for _ in range(n):
-                if sync is not None:
-                    sync.prepare_for_backward()
+                if sync_ is not None:
+                    sync_.prepare_for_backward()
                 with torch.autocast("cuda", dtype=torch.bfloat16):
                     out = model(xb)
                 loss = F.cross_entropy(out.float(), yb)
                 loss.backward()
-                if sync is not None:
-                    sync.finish()
+                if sync_ is not None:
+                    sync_.finish()
                 opt.step()
                 opt.zero_grad()
                 state["loss"] = loss
     else:
         m = model
         if world > 1:
-            m = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index])
+            m = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index],
+                                                          bucket_cap_mb=bucket_mb or args.bucket_mb)
+            info = {"route": "torch-ddp", "bucket_mb": bucket_mb or args.bucket_mb}
         opt = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5, foreach=True)
 
         def run(n):
@@ -260,30 +450,18 @@ def make_resnet(args, world, rank, dev, x, y):
                 opt.step()
                 state["loss"] = loss
 
-    return run, (lambda: float(state["loss"].item()))
+    return run, (lambda: float(state["loss"].item())), None, info
 
 
-def main():
-    args = parse()
-    world, rank, local = setup_dist(args)
-    dev = torch.device("cuda", local)
-    from ray_lightning_accelerators_amd.models.data import synthetic_mnist
-
-    if args.model == "resnet50":
-        x = y = None
-        maker = make_resnet
-    else:
-        x, y = synthetic_mnist(args.n_data, seed=0)
-        maker = make_native if args.impl == "native" else make_torch
-    run, last_loss, *extra = maker(args, world, rank, dev, x, y)
-    replica_checksum = extra[0] if extra else None
-
-    run(args.warmup)
+# ------------------------------------------------------------ measurement
+def timed(run, steps, world, dev) -> float:
+    """EXACTLY ``steps`` steps between barrier + device sync on both sides; the
+    slowest rank's time."""
     barrier(world)
-    torch.cuda.synchronize()
+    sync(dev)
     t0 = time.perf_counter()
-    run(args.steps)
-    torch.cuda.synchronize()
+    run(steps)
+    sync(dev)
     barrier(world)
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -291,53 +469,330 @@ def main():
                          device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    return elapsed
+
+
+def run_rank(args):
+    """One rank's measurement; returns rank 0's result dict (None elsewhere)."""
+    env = rank_env()
+    world, rank, local = env if env is not None else (1, 0, 0)
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started {world} ranks")
+    dev = setup_dist(args, world, rank, local)
+    from ray_lightning_accelerators_amd.models.data import synthetic_mnist
+
+    rn = args.model == "resnet50"
+    x = y = None
+    if not rn:
+        x, y = synthetic_mnist(args.n_data, seed=0)
+    maker = {"native": make_native, "torch": make_torch, "torch-graph": make_torch_graph}[args.impl]
+    if rn:
+        maker = make_resnet
+    sweep = None
+    if rn and args.bucket_sweep:
+        sweep = [float(v) for v in args.bucket_sweep.split(",") if v]
+    run, last_loss, checksum, info = maker(args, world, rank, dev, x, y)
+    run(args.warmup)
+    if world > 1 and args.impl == "native" and not rn:
+        # self-check of the fused xGMI exchange before anything is timed
+        if not (comm_healthy(world) and replicas_agree(world, checksum)):
+            run, last_loss, checksum, info = degrade_to_split(args, world, rank, dev, x, y)
+            run(args.warmup)
+    log(rank, f"world={world} route={info.get('route')} device={dev}")
+    elapsed = timed(run, args.steps, world, dev)
+    curve = None
+    if sweep:
+        curve = {}
+        for mb in sweep:
+            r2, *_ = make_resnet(args, world, rank, dev, x, y, bucket_mb=mb)
+            r2(args.warmup)
+            t = timed(r2, args.steps, world, dev)
+            curve[str(mb)] = round(args.steps * args.batch_size * world / t, 1)
+    if world > 1:
         from ray_lightning_accelerators_amd.parallel.comm import get_native_comm
 
         comm = get_native_comm(create=False)
         if comm is not None:
             comm.check()  # a timed-out xGMI poll or RCCL async error invalidates the run
-        if replica_checksum is not None:
-            # data-parallel replicas must still hold identical weights after the timed steps
-            sums = [None] * world
-            dist.all_gather_object(sums, replica_checksum())
-            if any(v != sums[0] for v in sums):
-                raise RuntimeError(f"replicas diverged: {sums}")
-    samples = args.steps * args.batch_size * world
-    value = samples / elapsed
+        if checksum is not None and not replicas_agree(world, checksum):
+            raise RuntimeError("data-parallel replicas diverged after the timed steps")
+    n_ranks = dist.get_world_size() if world > 1 else 1
+    value = args.steps * args.batch_size * n_ranks / elapsed
     loss = last_loss()
+    out = None
     if rank == 0:
-        rn = args.model == "resnet50"
-        # the stock number is for the default 784-32-64-10 / batch-32 config only
         default_cfg = (args.layer_1, args.layer_2, args.batch_size) == (32, 64, 32)
-        base = STOCK_BASELINE.get(world) if (not rn and default_cfg) else None
+        base_impl, base = None, None
+        if not rn and default_cfg and n_ranks == 1 and dev.type == "cuda":
+            known = {k: v for k, v in STOCK_BASELINE.items() if v}
+            if known:
+                base_impl = max(known, key=known.get)
+                base = known[base_impl]
         out = {
             "metric": RESNET_METRIC if rn else METRIC,
             "value": round(value, 1),
             "unit": "images/s" if rn else "samples/s",
-            "n_gpus": world,
+            "n_gpus": n_ranks,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 5),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (round(value / base, 3) if base else None),
-            "dtype": "bf16",
+            "baseline_impl": base_impl,
+            "baseline_value": base,
+            "dtype": "bf16" if dev.type == "cuda" else "fp32",
             "data": "synthetic",
             "config": {
                 "model": "ResNet-50" if rn else f"MNISTClassifier(784-{args.layer_1}-{args.layer_2}-10)",
-                "global_batch": args.batch_size * world,
+                "global_batch": args.batch_size * n_ranks,
                 "per_gpu_batch": args.batch_size,
                 "seq_len": None,
-                "parallelism": f"dp{world}",
+                "parallelism": f"dp{n_ranks}",
                 "impl": args.impl,
+                "accelerator": args.accelerator,
+                "launch": os.environ.get("RLA_BENCH_LAUNCHER", "torchrun" if env is not None else "single"),
                 "optimizer": "SGD-momentum" if rn else "Adam",
                 "final_train_loss": round(loss, 4),
+                **info,
             },
         }
-        print(json.dumps(out), flush=True)
+        if curve:
+            out["bucket_curve_images_per_s"] = curve
     if world > 1:
-        dist.destroy_process_group()
+        if args.accelerator == "horovod":
+            import ray_lightning_accelerators_amd.horovod as hvd
+
+            hvd.shutdown()
+        else:
+            from ray_lightning_accelerators_amd.parallel.comm import reset_native_comm
+
+            reset_native_comm()
+            dist.destroy_process_group()
+    return out
+
+
+# -------------------------------------------------------------- trainer
+class _EpochClock(Callback):
+    """Callback: wall-clock of every epoch from one epoch start to the next (so an
+    epoch's time includes its validation pass, checkpoint write and logging),
+    max over ranks; rank 0 writes the rows to ``path``."""
+
+    def __init__(self, path):
+        self.path = path
+        self.marks = []
+
+    def _mark(self, trainer):
+        if trainer.on_gpu:
+            torch.cuda.synchronize()
+        self.marks.append(time.perf_counter())
+
+    def on_train_epoch_start(self, trainer, pl_module):
+        self._mark(trainer)
+
+    def on_train_end(self, trainer, pl_module):
+        self._mark(trainer)
+        secs = torch.tensor([b - a for a, b in zip(self.marks, self.marks[1:])], dtype=torch.float64)
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            t = secs.to(trainer.accelerator_backend._comm_device())
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            secs = t.cpu()
+        if trainer.global_rank == 0:
+            with open(self.path, "w") as f:
+                json.dump({"epoch_s": secs.tolist(), "world": trainer.world_size,
+                           "batches": int(trainer.num_training_batches),
+                           "val_batches": [int(v) for v in trainer.num_val_batches],
+                           "fused": trainer._fused is not None,
+                           "val_loss": float(trainer.callback_metrics.get("ptl/val_loss", float("nan"))),
+                           "val_accuracy": float(trainer.callback_metrics.get("ptl/val_accuracy", float("nan"))),
+                           "best_model_path": getattr(trainer.checkpoint_callback, "best_model_path", None)}, f)
+
+
+def run_trainer(args):
+    """``Trainer.fit(MNISTClassifier)`` through the accelerator; the parent never
+    touches the GPU (workers are runtime actors) unless this process is itself a
+    torchrun rank (then the env-DDP accelerator runs the same worker flow)."""
+    import ray_lightning_accelerators_amd.lightning as pl
+    from ray_lightning_accelerators_amd import HorovodRayAccelerator, RayAccelerator
+    from ray_lightning_accelerators_amd import runtime as ray
+    from ray_lightning_accelerators_amd.models.mnist import MNISTClassifier
+
+    if args.model != "mnist" or args.impl != "native":
+        raise SystemExit("--via trainer runs MNISTClassifier on the framework path")
+    gpu = args.device == "cuda"
+    env = rank_env()
+    out_path = tempfile.mktemp(prefix="rla-bench-", suffix=".json")
+    clock = _EpochClock(out_path)
+    model = MNISTClassifier({"layer_1": args.layer_1, "layer_2": args.layer_2, "lr": args.lr,
+                             "batch_size": args.batch_size})
+    root = tempfile.mkdtemp(prefix="rla-bench-trainer-")
+    started = False
+    if env is not None:
+        acc = "ddp"  # torchrun rank: process group from the env (DDPAccelerator)
+        launch = "torchrun"
+    else:
+        ncpu = max(2, 2 * args.gpus)
+        if gpu and share_gpu():
+            os.environ["RLA_PG_BACKEND"] = "gloo"  # resolved into the accelerator's config below
+            ray.init(num_cpus=ncpu, _nodes=[{"ip": "127.0.0.1", "num_cpus": ncpu, "num_gpus": args.gpus,
+                                             "gpu_ids": ["0"] * args.gpus, "resources": {}}])
+        else:
+            ray.init(num_cpus=ncpu, num_gpus=args.gpus if gpu else 0)
+        started = True
+        if args.accelerator == "horovod":
+            acc = HorovodRayAccelerator(num_hosts=1, num_slots=args.gpus, use_gpu=gpu)
+        else:
+            acc = RayAccelerator(num_workers=args.gpus, use_gpu=gpu)
+        launch = "ray-actors"
+    try:
+        trainer = pl.Trainer(default_root_dir=root, max_epochs=args.trainer_epochs, gpus=int(gpu),
+                             progress_bar_refresh_rate=0, callbacks=[clock], accelerator=acc)
+        t0 = time.perf_counter()
+        assert trainer.fit(model) == 1
+        fit_s = time.perf_counter() - t0
+    finally:
+        if started:
+            ray.shutdown()
+    if env is not None and env[1] != 0:
+        return None
+    with open(out_path) as f:
+        rows = json.load(f)
+    os.unlink(out_path)
+    world = rows["world"]
+    nb = rows["batches"]
+    epochs = rows["epoch_s"]
+    steady = epochs[1:] or epochs
+    per_epoch = nb * args.batch_size * world
+    med = statistics.median(steady)
+    value = per_epoch * len(steady) / sum(steady)
+    return {
+        "metric": METRIC + " (Trainer.fit wall-clock incl. validation + checkpointing)",
+        "value": round(value, 1),
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": nb * len(steady),
+        "warmup": nb,
+        "ms_per_step": round(sum(steady) / (nb * len(steady)) * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16" if gpu else "fp32",
+        "data": "synthetic",
+        "config": {
+            "model": f"MNISTClassifier(784-{args.layer_1}-{args.layer_2}-10)",
+            "global_batch": args.batch_size * world,
+            "per_gpu_batch": args.batch_size,
+            "seq_len": None,
+            "parallelism": f"dp{world}",
+            "via": "trainer",
+            "accelerator": type(acc).__name__ if not isinstance(acc, str) else "DDPAccelerator(env)",
+            "launch": launch,
+            "epochs": args.trainer_epochs,
+            "val_batches_per_epoch": rows["val_batches"],
+            "checkpointing": True,
+            "fused_step": rows["fused"],
+        },
+        "epoch_wall_s": [round(v, 5) for v in epochs],
+        "median_steady_epoch_samples_per_s": round(per_epoch / med, 1),
+        "steady_epoch_spread": round(max(steady) / min(steady), 3),
+        "fit_wall_s": round(fit_s, 2),
+        "val_loss": rows["val_loss"],
+        "val_accuracy": rows["val_accuracy"],
+    }
+
+
+# --------------------------------------------------------------- launch
+def _rank_main(root, argv, rank, world, port, pinned, rla_env):
+    """Entry of one rank inside a runtime actor (pickled by value from __main__)."""
+    import importlib
+    import os as _os
+    import sys as _sys
+
+    if root not in _sys.path:
+        _sys.path.insert(0, root)
+    _os.environ.update(rla_env)  # the launcher's RLA_* knobs (the actor may descend from another env)
+    _os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": "0" if pinned else str(rank),
+                        "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                        "RLA_BENCH_LAUNCHER": "ray-actors"})
+    bench = importlib.import_module("bench")
+    return bench.run_rank(bench.parse(argv))
+
+
+def launch_ray(args, argv) -> int:
+    """N ranks as runtime actors -- the RayAccelerator worker path: RayExecutor
+    actors reserving one GPU each (HIP_VISIBLE_DEVICES-pinned), rendezvous port
+    chosen on worker 0 (reference ray_ddp.py:92-107, :161-163)."""
+    from ray_lightning_accelerators_amd import runtime as ray
+    from ray_lightning_accelerators_amd.accelerators.ray_ddp import RayExecutor, find_free_port
+
+    n = args.gpus
+    gpu = args.device == "cuda"
+    ncpu = n + 1
+    if gpu and share_gpu():
+        ray.init(num_cpus=ncpu, _nodes=[{"ip": "127.0.0.1", "num_cpus": ncpu, "num_gpus": n,
+                                         "gpu_ids": ["0"] * n, "resources": {}}])
+    else:
+        ray.init(num_cpus=ncpu, num_gpus=n if gpu else 0)
+    try:
+        workers = [RayExecutor.options(num_cpus=1, num_gpus=int(gpu)).remote() for _ in range(n)]
+        port = ray.get(workers[0].execute.remote(find_free_port))
+        rla_env = {k: v for k, v in os.environ.items() if k.startswith("RLA_")}
+        futures = [w.execute.remote(_rank_main, ROOT, argv, i, n, port, gpu, rla_env) for i, w in enumerate(workers)]
+        results = ray.get(futures)
+    finally:
+        ray.shutdown()
+    print(json.dumps(results[0]), flush=True)
+    return 0
+
+
+def launch_spawn(args, argv) -> int:
+    """N ranks as plain child processes that see every GPU (torchrun's layout)."""
+    from ray_lightning_accelerators_amd.accelerators.ray_ddp import find_free_port
+
+    port = find_free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_RANK=str(r),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   RLA_BENCH_LAUNCHER="spawn")
+        # intra-op pools sized to each rank's share of the CPUs (N all-core pools oversubscribe)
+        env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // args.gpus)))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in procs:  # a failed rank leaves its peers blocked in a collective
+                        q.kill()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            p.kill()
+    return rc
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
+    if args.via == "trainer":
+        res = run_trainer(args)
+        if res is not None:
+            print(json.dumps(res), flush=True)
+        return 0
+    if rank_env() is None and args.gpus > 1:
+        return launch_ray(args, argv) if args.launcher == "ray" else launch_spawn(args, argv)
+    res = run_rank(args)
+    if res is not None:
+        print(json.dumps(res), flush=True)
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

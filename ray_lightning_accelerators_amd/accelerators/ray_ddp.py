@@ -223,13 +223,16 @@ class RayAccelerator(DataParallelAccelerator):
         self.trainer.world_size = self.num_workers
 
     def init_ddp_connection(self, global_rank: int, world_size: int, is_slurm_managing_tasks: bool = True):
-        backend = "nccl" if self.use_gpu else "gloo"
+        from ..config import gpu_pg_backend
+
+        backend = gpu_pg_backend() if self.use_gpu else "gloo"
         if not dist.is_initialized():
             log.info(f"initializing ddp: GLOBAL_RANK: {global_rank}, MEMBER: {global_rank + 1}/{world_size}")
             kw = {}
             if self.use_gpu:
-                kw["device_id"] = torch.device("cuda", 0)
                 torch.cuda.set_device(0)
+                if backend == "nccl":
+                    kw["device_id"] = torch.device("cuda", 0)
             dist.init_process_group(backend=backend, init_method=self.ddp_address, rank=global_rank,
                                     world_size=world_size, **kw)
 

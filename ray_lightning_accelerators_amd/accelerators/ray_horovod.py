@@ -271,7 +271,7 @@ class HorovodRayAccelerator(Accelerator):
             optimizer.synchronize()
 
     def barrier(self, name=None) -> None:
-        hvd.join()
+        hvd.barrier()  # a barrier, not join(): join also waits out uneven final batches
 
     def broadcast(self, obj, src: int = 0):
         return hvd.broadcast_object(obj, src)

@@ -32,6 +32,7 @@ _CHOICES = {
     "grad_dtype": ("fp32", "bf16"),
     "allreduce_algo": ("auto", "oneshot", "twoshot", "rccl", "torch"),
     "precision": ("32", "bf16"),
+    "pg_backend": ("auto", "nccl", "gloo"),
 }
 
 # legacy env names kept working (first release used these spellings)
@@ -69,6 +70,9 @@ class RLAConfig:
     # single batches (chunks also end at log / validation / max_steps boundaries);
     # 1 = one dispatch per batch.  Capped by the fused step's stats ring (64).
     steps_per_dispatch: int = 64
+    # torch.distributed backend of GPU workers: auto = RCCL ("nccl"); "gloo" only
+    # for rehearsing N ranks on ONE device (RCCL refuses duplicate GPUs)
+    pg_backend: str = "auto"
     # generic-model compute precision ("32" or "bf16" autocast)
     precision: str = "32"
     # bounded polls of the xGMI kernels (iterations) and the watchdog period (ms)
@@ -174,3 +178,8 @@ def set_config(cfg: Optional[RLAConfig]) -> None:
 def log_config(rank: int, cfg: Optional[RLAConfig] = None) -> None:
     if rank == 0:
         log.info((cfg or get_config()).describe())
+
+
+def gpu_pg_backend() -> str:
+    """Process-group backend for a GPU worker under the current config."""
+    return "gloo" if get_config().pg_backend == "gloo" else "nccl"

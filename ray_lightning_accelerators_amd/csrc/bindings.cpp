@@ -165,65 +165,6 @@ void mlp_train_step(optional<Tensor> x_u8, optional<Tensor> x_f32, Tensor labels
   TORCH_CHECK(rla::launch_mlp_train_step(a, cur_stream(params)) == 0, "fused MLP launch failed");
 }
 
-void mlp_train_step2(optional<Tensor> x_u8, optional<Tensor> x_f32, Tensor labels, optional<Tensor> order,
-                     Tensor counters, int64_t n_batches, int64_t B, int64_t L1, int64_t L2, Tensor params,
-                     Tensor grads, optional<Tensor> exp_avg, optional<Tensor> exp_avg_sq, Tensor shadow,
-                     Tensor dh1t, optional<Tensor> stats, bool accumulate_grad, bool apply_adam,
-                     bool advance_step, double lr, double beta1, double beta2, double eps,
-                     double weight_decay, optional<Tensor> lr_t, bool adamw, optional<Tensor> stamps) {
-  TORCH_CHECK(rla::mlp_supported((int)L1, (int)L2), "no fused MLP kernel for layer sizes ", L1, "/", L2);
-  TORCH_CHECK(B >= 1 && B <= 256, "fused MLP step supports 1 <= batch <= 256");
-  const int64_t np = mlp_param_count(L1, L2);
-  const rla::MLPShadowLayout lay = rla::mlp_shadow_layout((int)L1, (int)L2);
-  check_dev(params, "params", at::kFloat);
-  check_dev(grads, "grads", at::kFloat);
-  TORCH_CHECK(params.numel() == np && grads.numel() == np, "param arena must hold ", np, " floats");
-  check_dev(shadow, "shadow", at::kBFloat16);
-  TORCH_CHECK(shadow.numel() >= lay.total, "shadow must hold ", lay.total, " bf16");
-  check_dev(dh1t, "dh1t", at::kBFloat16);
-  const int64_t Bp = (B + 31) / 32 * 32;
-  TORCH_CHECK(dh1t.numel() >= L1 * Bp, "dh1t scratch must hold L1 * round_up(B, 32)");
-  check_dev(counters, "counters", at::kLong);
-  TORCH_CHECK(counters.numel() >= 3, "counters must hold 3 int64 (step, cursor, last cursor)");
-  check_dev(labels, "labels", at::kLong);
-  const at::hip::HIPGuardMasqueradingAsCUDA guard(params.device());
-  rla::MLPStepArgs a{};
-  a.x_u8 = ptr_or_null<const uint8_t>(x_u8, "x_u8", at::kByte);
-  a.x_f32 = ptr_or_null<const float>(x_f32, "x_f32", at::kFloat);
-  TORCH_CHECK((a.x_u8 != nullptr) != (a.x_f32 != nullptr), "pass exactly one of x_u8 / x_f32");
-  if (a.x_u8) {
-    TORCH_CHECK(x_u8->dim() == 2 && x_u8->size(1) == 784, "x_u8 must be [N, 784]");
-    TORCH_CHECK(labels.numel() == x_u8->size(0), "labels must match the dataset");
-    a.order = ptr_or_null<const int64_t>(order, "order", at::kLong, n_batches * B);
-    TORCH_CHECK(a.order != nullptr && n_batches >= 1, "u8 mode needs order[n_batches * B]");
-  } else {
-    TORCH_CHECK(x_f32->numel() == B * 784, "x_f32 must be [B, 784]");
-    TORCH_CHECK(labels.numel() == B, "labels must be [B]");
-  }
-  a.labels = labels.data_ptr<int64_t>();
-  a.counters = counters.data_ptr<int64_t>();
-  a.n_batches = n_batches;
-  a.B = (int)B; a.L1 = (int)L1; a.L2 = (int)L2;
-  a.params = params.data_ptr<float>();
-  a.grads = grads.data_ptr<float>();
-  a.exp_avg = ptr_or_null<float>(exp_avg, "exp_avg", at::kFloat, np);
-  a.exp_avg_sq = ptr_or_null<float>(exp_avg_sq, "exp_avg_sq", at::kFloat, np);
-  TORCH_CHECK(!apply_adam || (a.exp_avg && a.exp_avg_sq), "apply_adam needs optimizer state");
-  a.shadow = reinterpret_cast<uint16_t*>(shadow.data_ptr());
-  a.dh1t = reinterpret_cast<uint16_t*>(dh1t.data_ptr());
-  a.stats = ptr_or_null<float>(stats, "stats", at::kFloat, 4);
-  a.stats_ring = a.stats ? (int)(stats->numel() / 4) : 0;
-  a.accumulate_grad = accumulate_grad;
-  a.apply_adam = apply_adam;
-  a.advance_step = advance_step;
-  a.lr = (float)lr; a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.eps = (float)eps;
-  a.weight_decay = (float)weight_decay;
-  a.lr_ptr = ptr_or_null<const float>(lr_t, "lr", at::kFloat, 1);
-  a.adamw = adamw;
-  a.stamps = ptr_or_null<int64_t>(stamps, "stamps", at::kLong, 16);
-  TORCH_CHECK(rla::launch_mlp_train_step2(a, cur_stream(params)) == 0, "fused MLP v2 launch failed");
-}
-
 // v3 pipelined step.  kind: 0 step (head + fused tail), 1 head only (grads),
 // 2 tail GRAD, 3 tail ADAM (after the allreduce), 4 PRIME (H1pre of the pending batch).
 void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counters, int64_t n_batches, int64_t B,
@@ -231,7 +172,7 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
           Tensor dh1t, Tensor xring, Tensor h1pre, Tensor act, Tensor yring, optional<Tensor> stats,
           bool advance_step, double lr,
           double beta1, double beta2, double eps, double weight_decay, double grad_scale, optional<Tensor> lr_t,
-          bool adamw, optional<Tensor> stamps, std::vector<int64_t> dp_ctx) {
+          bool adamw, optional<Tensor> stamps, std::vector<int64_t> dp_ctx, optional<Tensor> head_part) {
   TORCH_CHECK(kind >= 0 && kind <= 5, "mlp3: bad kind ", kind);
   TORCH_CHECK(rla::mlp_supported((int)L1, (int)L2), "no fused MLP kernel for layer sizes ", L1, "/", L2);
   TORCH_CHECK(B >= 1 && B <= 256, "fused MLP step supports 1 <= batch <= 256");
@@ -285,6 +226,8 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
   a.yring = yring.data_ptr<int>();
   a.stats = ptr_or_null<float>(stats, "stats", at::kFloat, 4);
   a.stats_ring = a.stats ? (int)(stats->numel() / 4) : 0;
+  a.head_part = ptr_or_null<float>(head_part, "head_part", at::kFloat, (Bp / 32) * 4);
+  TORCH_CHECK(B <= 32 || a.head_part != nullptr, "mlp3: batches above 32 rows need head_part [ceil(B/32), 4]");
   a.apply_adam = kind == rla::kMLP3Step;
   a.advance_step = advance_step;
   a.lr = (float)lr; a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.eps = (float)eps;
@@ -350,7 +293,11 @@ void mlp_eval(optional<Tensor> x_u8, optional<Tensor> x_f32, Tensor labels, opti
   TORCH_CHECK(params.numel() == mlp_param_count(L1, L2), "param arena size mismatch");
   check_dev(labels, "labels", at::kLong);
   check_dev(out, "out", at::kFloat);
-  TORCH_CHECK(out.numel() >= 2, "out must hold 2 floats");
+  TORCH_CHECK(out.is_contiguous(), "out must be contiguous");
+  // out [2] accumulates; out [ceil(B/32), 2] receives per-32-row-chunk partial sums
+  const bool partials = out.dim() == 2;
+  TORCH_CHECK(partials ? (out.size(0) == (B + 31) / 32 && out.size(1) == 2) : out.numel() >= 2,
+              "out must be [2] or [ceil(B/32), 2]");
   const at::hip::HIPGuardMasqueradingAsCUDA guard(params.device());
   rla::MLPEvalArgs a{};
   a.x_u8 = ptr_or_null<const uint8_t>(x_u8, "x_u8", at::kByte);
@@ -369,6 +316,7 @@ void mlp_eval(optional<Tensor> x_u8, optional<Tensor> x_f32, Tensor labels, opti
   a.params = params.data_ptr<float>();
   a.logits = ptr_or_null<float>(logits, "logits", at::kFloat, B * 10);
   a.out = out.data_ptr<float>();
+  a.partials = partials ? 1 : 0;
   TORCH_CHECK(rla::launch_mlp_eval(a, cur_stream(params)) == 0, "fused MLP eval launch failed");
 }
 
@@ -513,7 +461,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("weight_decay"), py::arg("lr_t"),
         py::arg("adamw"), py::arg("stamps") = py::none());
   m.def("mlp_eval", &mlp_eval, "fused MNIST-MLP forward + NLL/accuracy");
-  m.def("mlp_train_step2", &mlp_train_step2, "fused MNIST-MLP step v2 (head + W1 kernels, bf16 shadows)");
   m.def("mlp3", &mlp3, "fused MNIST-MLP step v3 (pipelined layer 1): kind 0 step, 1 head, 2 tail-grad, "
         "3 tail-adam, 4 prime");
   m.def("mlp_adam", &mlp_adam, "MLP arena Adam + bf16 shadow refresh (update=False: refresh only)");

@@ -141,6 +141,8 @@ struct MLPEvalArgs {
   const float* params;
   float* logits;            // optional [B, 10] output (log-probabilities)
   float* out;               // [2]: += sum of NLL, += correct count
+                            // (partials: [ceil(B/32), 2] per-32-row-chunk sums, overwritten)
+  int partials;
 };
 
 // v3 (cross-step pipelined layer 1, resident uint8 dataset only); see mlp_step3.hip.
@@ -164,6 +166,7 @@ struct MLP3Args {
   int* yring;               // [2][Bp] int32 staged labels (-1 past B), slot-indexed like xring
   float* stats;
   int stats_ring;
+  float* head_part;         // [ceil(B/32)][4] per-head-block (sum NLL, #correct, #rows); B > 32
   int apply_adam;           // head: Adam on the small parameters (world size 1)
   int advance_step;
   float lr, beta1, beta2, eps, weight_decay, grad_scale;
@@ -188,9 +191,6 @@ int mlp3_act_rows(int L1, int L2);
 int launch_mlp_train_step(const MLPStepArgs& a, hipStream_t stream);
 int launch_mlp_eval(const MLPEvalArgs& a, hipStream_t stream);
 bool mlp_supported(int L1, int L2);
-// v2: head kernel (1 WG: forward, loss, dH, small-param grads/Adam) + W1 kernel
-// (49 WGs: dW1 tile + Adam, bf16 shadow write).  counters needs 3 slots.
-int launch_mlp_train_step2(const MLPStepArgs& a, hipStream_t stream);
 int launch_mlp_adam(const MLPAdamArgs& a, hipStream_t stream);
 
 }  // namespace rla

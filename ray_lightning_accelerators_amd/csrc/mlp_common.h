@@ -1,5 +1,5 @@
-// Shared pieces of the fused MNIST-MLP step kernels (v2: mlp_step2.hip,
-// v3: mlp_step3.hip): arena offsets, Adam scalar math, LDS fragment loaders.
+// Shared pieces of the fused MNIST-MLP kernels (mlp_step3.hip step, mlp_adam.hip
+// arena Adam): arena offsets, Adam scalar math, LDS fragment loaders.
 #pragma once
 #include <math.h>
 

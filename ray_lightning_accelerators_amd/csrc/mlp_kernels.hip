@@ -572,6 +572,11 @@ __global__ __launch_bounds__(kThreads) void mlp_train_kernel(MLPStepArgs a) {
   }
 }
 
+// Forward-only evaluation (validation / test): one 32-row chunk per workgroup,
+// the chunks spread over the grid (a 5,000-sample validation split is ~160
+// workgroups, one wave of the chip).  ``partials`` mode writes each chunk's
+// (sum NLL, #correct) to out[2c..2c+1] -- no atomics, so the epoch's sums are
+// reduced deterministically by the caller; otherwise one atomic pair per block.
 template <int BC, int L1, int L2, bool U8>
 __global__ __launch_bounds__(kThreads) void mlp_eval_kernel(MLPEvalArgs a) {
   using C = Cfg<BC, L1, L2>;
@@ -579,35 +584,44 @@ __global__ __launch_bounds__(kThreads) void mlp_eval_kernel(MLPEvalArgs a) {
   const Smem s = carve<C>(smem);
   const int nchunks = (a.B + BC - 1) / BC;
   float loss_sum = 0.f, correct_sum = 0.f;
-  for (int c = 0; c < nchunks; ++c) {
+  for (int c = blockIdx.x; c < nchunks; c += gridDim.x) {
     const int row0 = c * BC;
     const int nvalid = min(BC, a.B - row0);
     stage_inputs<BC, L1, U8>(s, a.x_u8, a.x_f32, a.labels, a.index, row0, nvalid);
     __syncthreads();
     forward<BC, L1, L2>(s, a.params);
+    float l = 0.f, k = 0.f;
     if (threadIdx.x < BC) {
       const int r = threadIdx.x;
       float prob[kNC], loss, lse;
       int correct;
       if (row_softmax(s.Z + r * 16, s.ys[r], prob, loss, correct, lse)) {
-        loss_sum += loss;
-        correct_sum += (float)correct;
+        l = loss;
+        k = (float)correct;
         if (a.logits)
           for (int j = 0; j < kNC; ++j) a.logits[(int64_t)(row0 + r) * kNC + j] = s.Z[r * 16 + j] - lse;
       }
     }
+    if (threadIdx.x < 64) {  // wave 0 (BC <= 64 rows): full-wave reduction, every lane active
+      for (int off = 32; off > 0; off >>= 1) {
+        l += __shfl_down(l, off, 64);
+        k += __shfl_down(k, off, 64);
+      }
+      if (threadIdx.x == 0) {
+        if (a.partials) {
+          a.out[2 * c] = l;
+          a.out[2 * c + 1] = k;
+        } else {
+          loss_sum += l;
+          correct_sum += k;
+        }
+      }
+    }
     __syncthreads();
   }
-  if (threadIdx.x < BC) {
-    // wave-level reduce then one atomic per wave (BC <= 64: one or two waves)
-    for (int off = 32; off > 0; off >>= 1) {
-      loss_sum += __shfl_down(loss_sum, off, 64);
-      correct_sum += __shfl_down(correct_sum, off, 64);
-    }
-    if ((threadIdx.x & 63) == 0) {
-      atomicAdd(&a.out[0], loss_sum);
-      atomicAdd(&a.out[1], correct_sum);
-    }
+  if (!a.partials && threadIdx.x == 0 && blockIdx.x < nchunks) {
+    atomicAdd(&a.out[0], loss_sum);
+    atomicAdd(&a.out[1], correct_sum);
   }
 }
 
@@ -635,8 +649,12 @@ int dispatch_train(const MLPStepArgs& a, hipStream_t stream) {
 template <int L1, int L2>
 int dispatch_eval(const MLPEvalArgs& a, hipStream_t stream) {
   const bool u8 = a.x_u8 != nullptr;
-  if (u8) hipLaunchKernelGGL((mlp_eval_kernel<32, L1, L2, true>), dim3(1), dim3(kThreads), 0, stream, a);
-  else hipLaunchKernelGGL((mlp_eval_kernel<32, L1, L2, false>), dim3(1), dim3(kThreads), 0, stream, a);
+  const int nchunks = (a.B + 31) / 32;
+  // partials: one block per chunk (every chunk owns its output pair); atomics: a
+  // grid-stride over at most one block per CU
+  const int grid = a.partials ? nchunks : (nchunks < 256 ? nchunks : 256);
+  if (u8) hipLaunchKernelGGL((mlp_eval_kernel<32, L1, L2, true>), dim3(grid), dim3(kThreads), 0, stream, a);
+  else hipLaunchKernelGGL((mlp_eval_kernel<32, L1, L2, false>), dim3(grid), dim3(kThreads), 0, stream, a);
   return 0;
 }
 

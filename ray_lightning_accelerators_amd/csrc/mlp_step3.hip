@@ -1,18 +1,21 @@
 // Fused MNIST-MLP training step, v3: layer 1 pipelined across steps, every
 // weight-gradient epilogue spread over many CUs.
 //
-// v2 (mlp_step2.hip) measured 25 us/step on MI355X; 10 of its head kernel's
+// v2 (a head + W1 kernel pair, retired) measured 25 us/step on MI355X; 10 of its head kernel's
 // 17 us went to staging the X batch (50 KB gathered through the sample index)
 // plus the 784-deep layer-1 GEMM on ONE CU, and 4.4 us to the small-parameter
 // gradient/Adam epilogue on that same CU (profiles/r1_first/mlp_phases_v2.json).
 // v3 keeps only the inherently serial chain on the one-workgroup head and moves
 // everything else to a wide tail launch:
 //
-//   head(t)   1 workgroup: H1 = relu(H1pre[t] + b1) (4 KB read instead of X + W1),
+//   head(t)   one workgroup per 32 batch rows (the per-sample chain is row-
+//             independent): H1 = relu(H1pre[t] + b1) (4 KB read instead of X + W1),
 //             layers 2/3, log_softmax/NLL/accuracy, dH2, dH1.  Hands the
 //             transposed activations / deltas (H1^T, H2^T, dH2^T, dZ^T, dH1^T;
-//             bf16, [rows][Bp]) to the tail through HBM and zeroes the other
-//             H1pre slot.
+//             bf16, [rows][Bp]) to the tail through HBM and zeroes its rows of
+//             the other H1pre slot.  With several row blocks, each writes its
+//             (sum NLL, #correct, #rows) to `head_part` and tail block 0 reduces
+//             them in block order (deterministic) into the stats ring.
 //   tail(t)   blocks [0, 49): one 16-pixel W1 column tile each: dW1 tile =
 //             X[t]_tile^T dH1 (MFMA; X^T by ds_read_b64_tr_b16), Adam on the
 //             tile, then gather X[t+1]'s tile (u8 -> bf16) and add
@@ -56,6 +59,7 @@ constexpr int kDZS = 40;
 constexpr int kXSS = 24;   // LDS row stride of a 16-pixel X slice (bf16)
 constexpr int kBMax = 256;
 constexpr int kCnt = 5;  // counters: [0, 5) current state, [5, 10) the head's advanced copy
+constexpr int kHeadRows = 32;  // batch rows per head workgroup
 
 enum TailMode { kFused = 0, kGrad = 1, kAdam = 2, kPrime = 3, kFusedDP = 4 };
 
@@ -120,7 +124,8 @@ __device__ __forceinline__ void gather_tile(const MLP3Args& a, int kt, int64_t o
 }
 
 // ---------------------------------------------------------------------------
-// Head kernel (block 0: one workgroup, 8 waves; blocks 1..49: next-batch gather)
+// Head kernel (blocks [0, nchunks): one 8-wave workgroup per BC batch rows;
+// blocks [nchunks, nchunks + 49): next-batch gather)
 // ---------------------------------------------------------------------------
 template <int BC, int L1, int L2>
 __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
@@ -142,12 +147,14 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
   const __bf16* SH = reinterpret_cast<const __bf16*>(a.shadow);
   const float* P = a.params;
 
-  if (blockIdx.x > 0) {  // the NEXT batch's tiles, for this step's tail (xring / yring slot ^ 1)
+  const int nchunks = (a.B + BC - 1) / BC;
+  if ((int)blockIdx.x >= nchunks) {  // the NEXT batch's tiles, for this step's tail (xring / yring slot ^ 1)
     int64_t nc = a.counters[1] + 1, nob = a.counters[4];
     if (nc >= a.n_batches) { nc = 0; nob ^= 1; }
-    gather_tile(a, (int)blockIdx.x - 1, nob, nc, a.counters[3] ^ 1, kThreads);
+    gather_tile(a, (int)blockIdx.x - nchunks, nob, nc, a.counters[3] ^ 1, kThreads);
     return;
   }
+  const int c = blockIdx.x;  // this workgroup's batch rows [c * BC, c * BC + BC)
 
   // device counters: uniform scalar loads, no LDS broadcast round trip
   const int64_t t = a.counters[0] + 1;
@@ -165,15 +172,15 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
   }
   if (tid == 0) {
     misc[0] = 0.f; misc[1] = 0.f; misc[2] = 0.f;
-    if (a.stamps) a.stamps[0] = __builtin_amdgcn_s_memrealtime();
+    if (a.stamps && c == 0) a.stamps[0] = __builtin_amdgcn_s_memrealtime();
   }
-  // the tail of this step accumulates the next step's H1pre into the other slot
+  // the tail of this step accumulates the next step's H1pre into the other slot;
+  // in fragment order this block's rows are one contiguous BC * L1 range
   {
-    uint4* z = reinterpret_cast<uint4*>(a.h1pre + (slot ^ 1) * (int64_t)Bp * L1);
-    for (int i = tid; i < Bp * L1 / 2; i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
+    uint4* z = reinterpret_cast<uint4*>(a.h1pre + (slot ^ 1) * (int64_t)Bp * L1 + (int64_t)c * BC * L1);
+    for (int i = tid; i < BC * L1 / 2; i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
   }
   const float invB = 1.f / (float)a.B;
-  const int nchunks = (a.B + BC - 1) / BC;
   constexpr int KS2 = L1 / 32, KS3 = L2 / 32, KSH = L2 / 32;
   constexpr int P3 = KS3 < 4 ? KS3 : 4;
   constexpr int PH = KSH < 4 ? KSH : 4;
@@ -188,7 +195,7 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
     }
   };
 
-  for (int c = 0; c < nchunks; ++c) {
+  {
     const int row0 = c * BC;
 
     // ---- batch-independent weight fragments, issued first ----
@@ -403,7 +410,13 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
     __syncthreads();
     if (a.stamps && tid == 0 && c == 0) a.stamps[3] = __builtin_amdgcn_s_memrealtime();
   }
-  if (tid == 0) {
+  if (tid == 0 && nchunks > 1) {
+    // several row blocks: partial sums for tail block 0's ordered reduction
+    a.head_part[c * 4 + 0] = misc[0];
+    a.head_part[c * 4 + 1] = misc[1];
+    a.head_part[c * 4 + 2] = misc[2];
+  }
+  if (tid == 0 && c == 0) {
     // the advanced state goes to the NEXT copy: this launch's gather blocks are
     // still reading the current one (the tail publishes it, see mlp3_tail_kernel)
     int64_t* cn = a.counters + kCnt;
@@ -414,7 +427,7 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
     cn[1] = nc;
     cn[4] = nob;
     cn[3] = slot ^ 1;
-    if (a.stats) {
+    if (a.stats && nchunks == 1) {
       const int s = (int)((t - 1) % (a.stats_ring > 0 ? a.stats_ring : 1));
       float* st = a.stats + s * 4;
       st[0] = misc[0] * invB;
@@ -659,6 +672,21 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
   // block 0 publishes it as the current state for the next head
   const int64_t* cn = a.counters + kCnt;
   if (blockIdx.x == 0 && tid < kCnt) a.counters[tid] = cn[tid];
+  if (blockIdx.x == 0 && tid == 0 && a.stats && a.B > kHeadRows && do_grad) {
+    // multi-block head: its per-block (sum NLL, #correct, #rows), summed in block order
+    float l = 0.f, k = 0.f, n = 0.f;
+    for (int cb = 0; cb < (a.B + kHeadRows - 1) / kHeadRows; ++cb) {
+      l += a.head_part[cb * 4 + 0];
+      k += a.head_part[cb * 4 + 1];
+      n += a.head_part[cb * 4 + 2];
+    }
+    const int64_t t = cn[0];
+    float* st = a.stats + (int)((t - 1) % (a.stats_ring > 0 ? a.stats_ring : 1)) * 4;
+    st[0] = l / (float)a.B;
+    st[1] = k;
+    st[2] = n;
+    st[3] = (float)t;
+  }
   if (tid == 0 && do_adam) {
     const int64_t t = cn[0];  // already advanced by the head kernel
     adam_scalars(sh_o, t, a.lr_ptr ? a.lr_ptr[0] : a.lr, a.beta1, a.beta2, a.eps, a.weight_decay, a.adamw);
@@ -819,19 +847,10 @@ int dispatch3(const MLP3Args& a, int kind, hipStream_t stream) {
                               a.dp_stride < Off<L1, L2>::NP || kTiles + SmallTasks<L1, L2>::NBLK > kDpMaxBlocks))
     return -3;
   if (kind == kMLP3Step || kind == kMLP3Head || kind == kMLP3StepDP) {
-    // the smallest chunk that covers the batch, as LDS allows
-    bool launched = false;
-    if constexpr (fits3<128, L1, L2>()) {
-      if (a.B > 64) {
-        hipLaunchKernelGGL((mlp3_head_kernel<128, L1, L2>), dim3(1 + kTiles), dim3(kThreads), 0, stream, a);
-        launched = true;
-      }
-    }
-    if (!launched && a.B > 32) {
-      hipLaunchKernelGGL((mlp3_head_kernel<64, L1, L2>), dim3(1 + kTiles), dim3(kThreads), 0, stream, a);
-      launched = true;
-    }
-    if (!launched) hipLaunchKernelGGL((mlp3_head_kernel<32, L1, L2>), dim3(1 + kTiles), dim3(kThreads), 0, stream, a);
+    // one workgroup per 32 batch rows (concurrent), then the 49 gather blocks
+    const int nchunks = (a.B + kHeadRows - 1) / kHeadRows;
+    if (nchunks > 1 && !a.head_part) return -4;
+    hipLaunchKernelGGL((mlp3_head_kernel<kHeadRows, L1, L2>), dim3(nchunks + kTiles), dim3(kThreads), 0, stream, a);
   }
   int mode = -1, grid = kTiles;
   if (kind == kMLP3Step) { mode = kFused; grid += SmallTasks<L1, L2>::NBLK; }
@@ -848,7 +867,7 @@ int dispatch3(const MLP3Args& a, int kind, hipStream_t stream) {
   return 0;
 }
 
-static_assert(fits3<64, 128, 256>(), "v3 head LDS budget");
+static_assert(fits3<kHeadRows, 128, 256>(), "v3 head LDS budget");
 
 }  // namespace
 

@@ -80,12 +80,15 @@ def init(comm=None, process_sets=None) -> None:
     if size > 1 and not dist.is_initialized():
         addr = os.environ.get("HOROVOD_GLOO_RENDEZVOUS_ADDR", os.environ.get("MASTER_ADDR", "127.0.0.1"))
         port = os.environ.get("HOROVOD_GLOO_RENDEZVOUS_PORT", os.environ.get("MASTER_PORT", "29500"))
+        from ..config import gpu_pg_backend
+
         kw = {}
+        backend = gpu_pg_backend() if use_gpu else "gloo"
         if use_gpu:
             torch.cuda.set_device(local_rank if torch.cuda.device_count() > local_rank else 0)
-            kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
-        dist.init_process_group("nccl" if use_gpu else "gloo", init_method=f"tcp://{addr}:{port}", rank=rank,
-                                world_size=size, **kw)
+            if backend == "nccl":
+                kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
+        dist.init_process_group(backend, init_method=f"tcp://{addr}:{port}", rank=rank, world_size=size, **kw)
     _state.update(initialized=True, rank=rank, size=size, local_rank=local_rank, local_size=local_size,
                   cross_rank=cross_rank, cross_size=cross_size, use_gpu=use_gpu)
 
@@ -180,7 +183,14 @@ def _op_of(average: Optional[bool], op: Optional[str]) -> str:
 def _reduce_(t: torch.Tensor, op: str, prescale: float = 1.0, postscale: float = 1.0) -> torch.Tensor:
     if prescale != 1.0:
         t.mul_(prescale)
-    if size() > 1:
+    native = None
+    if size() > 1 and op in (Sum, Average) and t.is_cuda and t.dtype == torch.float32 and t.is_contiguous():
+        from ..parallel.comm import get_native_comm
+
+        native = get_native_comm()  # xGMI one-/two-shot or RCCL on the C++ engine (graph-capturable)
+    if native is not None:
+        native.allreduce_(t)
+    elif size() > 1:
         c, moved = _comm_tensor(t)
         rop = {Sum: dist.ReduceOp.SUM, Average: dist.ReduceOp.SUM, Min: dist.ReduceOp.MIN,
                Max: dist.ReduceOp.MAX}[op]
@@ -383,7 +393,9 @@ def join(device: int = -1) -> int:
 
 
 def barrier() -> None:
-    join()
+    _need()
+    if size() > 1:
+        dist.barrier()
 
 
 from .optimizer import DistributedOptimizer  # noqa: E402,F401

@@ -316,9 +316,11 @@ class DDPAccelerator(DataParallelAccelerator):
 
     def init_ddp_connection(self, global_rank: int, world_size: int) -> None:
         if world_size > 1 and not dist.is_initialized():
-            backend = "nccl" if self.use_gpu else "gloo"
+            from ..config import gpu_pg_backend
+
+            backend = gpu_pg_backend() if self.use_gpu else "gloo"
             kw = {}
-            if self.use_gpu:
+            if self.use_gpu and backend == "nccl":
                 kw["device_id"] = torch.device("cuda", self.trainer.local_rank)
             dist.init_process_group(backend, rank=global_rank, world_size=world_size, **kw)
 

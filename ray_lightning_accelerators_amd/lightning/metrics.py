@@ -1,7 +1,8 @@
 """Stateful metrics (``pl.metrics.Accuracy``, reference tests/utils.py:143).
 
-``compute()`` all-gathers the ``correct``/``total`` counters when a process
-group is up."""
+``compute()`` all-reduces the ``correct``/``total`` counters when a process
+group is up.  The counters stay on the predictions' device:
+``update`` never synchronises with the GPU."""
 from __future__ import annotations
 
 import torch
@@ -33,6 +34,7 @@ class Accuracy(Metric):
         self.reset()
 
     def reset(self) -> None:
+        # the counters live on the device of the first update (no host sync per batch)
         self.correct = torch.tensor(0.0)
         self.total = torch.tensor(0.0)
 
@@ -45,15 +47,18 @@ class Accuracy(Metric):
             pred_lbl = (preds >= self.threshold).long()
         else:
             pred_lbl = preds
-        self.correct = self.correct + (pred_lbl == target).sum().float().cpu()
+        if self.correct.device != preds.device:
+            self.correct = self.correct.to(preds.device)
+            self.total = self.total.to(preds.device)
+        self.correct = self.correct + (pred_lbl == target).sum().float()
         self.total = self.total + float(target.numel())
 
     def _snapshot(self):
         return (self.correct.clone(), self.total.clone())
 
     def _merge(self, saved) -> None:
-        self.correct = self.correct + saved[0]
-        self.total = self.total + saved[1]
+        self.correct = self.correct + saved[0].to(self.correct.device)
+        self.total = self.total + saved[1].to(self.total.device)
 
     def _compute_local(self) -> torch.Tensor:
         return self.correct / self.total.clamp(min=1.0)
@@ -61,9 +66,12 @@ class Accuracy(Metric):
     def compute(self) -> torch.Tensor:
         c, t = self.correct.clone(), self.total.clone()
         if dist.is_available() and dist.is_initialized():
+            dev = c.device
             buf = torch.stack([c, t])
             if dist.get_backend() == "nccl":
                 buf = buf.cuda()
+            elif buf.is_cuda:
+                buf = buf.cpu()  # gloo takes host tensors
             dist.all_reduce(buf)
-            c, t = buf[0].cpu(), buf[1].cpu()
+            c, t = buf[0].to(dev), buf[1].to(dev)
         return c / t.clamp(min=1.0)

@@ -586,14 +586,20 @@ class Trainer:
         model.eval()
         self.call_hook(f"on_{stage}_start")
         self.call_hook(f"on_{stage}_epoch_start")
-        fused_eval = (self._fused is not None and not test_mode and hasattr(self._fused, "eval_batch"))
+        fused_eval = (self._fused is not None and not test_mode and hasattr(self._fused, "eval_epoch")
+                      and len(dls) == 1 and self._fused.eval_compatible(model)
+                      and not self._eval_batch_hooks_overridden(model))
         all_outputs = []
         with torch.no_grad():
             for dl_idx, dl in enumerate(dls):
                 limit = nbs[dl_idx] if max_batches is None else min(max_batches, nbs[dl_idx])
                 outputs = []
-                if fused_eval:
-                    self._fused.sync_params_to_module()
+                res = self._fused.eval_epoch(dl, limit) if fused_eval else None
+                if res is not None:
+                    # the whole pass in one launch over the resident data: one output
+                    # standing for `limit` equal-size batches (same epoch-end mean)
+                    all_outputs.append([res])
+                    continue
                 for batch_idx, batch in enumerate(dl):
                     if batch_idx >= limit:
                         break
@@ -635,7 +641,6 @@ class Trainer:
 
     def run_test(self):
         model = self.get_model()
-        self.call_hook("on_test_start") if False else None
         results = self.run_evaluation(test_mode=True)
         self.test_results = results
         return results
@@ -820,6 +825,15 @@ class Trainer:
                 break
             b = e
         return validated
+
+    def _eval_batch_hooks_overridden(self, model: LightningModule) -> bool:
+        names = ("on_validation_batch_start", "on_validation_batch_end")
+        for cb in self.callbacks:
+            for nm in names:
+                if getattr(type(cb), nm, None) is not getattr(Callback, nm, None):
+                    return True
+        return any(getattr(type(model), nm, None) is not getattr(LightningModule, nm, None) or nm in model.__dict__
+                   for nm in names)
 
     def _batch_hooks_overridden(self, model: LightningModule, chunk_aware_ok: bool = False) -> bool:
         names = ("on_train_batch_start", "on_train_batch_end", "on_batch_start", "on_batch_end")

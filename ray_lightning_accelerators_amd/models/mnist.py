@@ -226,6 +226,7 @@ class FusedMNISTStep:
             return None
         images, targets, idx_map = src
         if self._u8 is None:
+            self._u8_host = images
             self._u8 = images.to(self.dev).contiguous()
             self._labels = targets.to(self.dev, torch.int64).contiguous()
         order = _sampler_order(dl.sampler)
@@ -336,6 +337,63 @@ class FusedMNISTStep:
         self.model.log("ptl/train_accuracy", last[1] / last[2].clamp(min=1))
         self.trainer.callback_metrics["loss"] = last[0]
         return [{"loss": rows[i, 0]} for i in range(k)]
+
+    # ---------------------------------------------------------- validation
+    def eval_compatible(self, model) -> bool:
+        """The stock validation_step / _end / _epoch_end: per-batch mean NLL and
+        accuracy, averaged over the (equal-size) batches."""
+        t = type(model)
+        return (t.validation_step is LightningMNISTClassifier.validation_step
+                and t.validation_epoch_end is LightningMNISTClassifier.validation_epoch_end
+                and t.validation_step_end is LightningModule.validation_step_end
+                and t.forward is LightningMNISTClassifier.forward)
+
+    def _resident(self, images: torch.Tensor, targets: torch.Tensor):
+        if self._u8 is not None and images is getattr(self, "_u8_host", None):
+            return self._u8, self._labels  # validation split of the training dataset
+        cache = self.__dict__.setdefault("_eval_sets", {})
+        key = id(images)
+        if key not in cache:
+            cache[key] = (images, images.to(self.dev).contiguous(), targets.to(self.dev, torch.int64).contiguous())
+        return cache[key][1], cache[key][2]
+
+    def eval_epoch(self, dl, n_batches: int):
+        """One validation pass over the resident dataset in ONE launch (a workgroup
+        per 32 samples, per-chunk partial sums reduced deterministically).
+        Returns ``{"val_loss", "val_accuracy"}`` device scalars -- the mean over the
+        ``n_batches`` equal-size batches, which is exactly what the eager
+        validation_step + validation_epoch_end produce -- or None when the loader
+        cannot be served from the resident data (the Trainer then runs the
+        per-batch loop)."""
+        src = _u8_source(dl.dataset)
+        if src is None or dl.batch_size is None or n_batches <= 0:
+            return None
+        images, targets, idx_map = src
+        B = int(dl.batch_size)
+        key = (id(dl), id(images), int(n_batches))
+        cached = self.__dict__.setdefault("_eval_orders", {}).get(key)
+        if cached is None:
+            order = _sampler_order(dl.sampler)
+            if idx_map is not None:
+                order = idx_map[order]
+            full = order.numel() // B
+            if full < n_batches and order.numel() % B:
+                return None  # a partial last batch: eager weights it like a full one
+            nb = min(int(n_batches), full)
+            if nb <= 0:
+                return None
+            order = order[: nb * B]
+            assert int(order.max()) < images.size(0) and int(order.min()) >= 0  # the kernel trusts indices
+            cached = (order.to(self.dev), nb)
+            self._eval_orders[key] = cached
+        order_dev, nb = cached
+        u8, labels = self._resident(images, targets)
+        n = nb * B
+        part = torch.empty((n + 31) // 32, 2, device=self.dev)
+        fused_mlp.mlp_eval(self.arena.data[: self.np], L1=self.L1, L2=self.L2, B=n, labels=labels, out=part,
+                           x_u8=u8, index=order_dev)
+        tot = part.sum(0) / n
+        return {"val_loss": tot[0], "val_accuracy": tot[1]}
 
     # --------------------------------------------------------------- state
     def sync_params_to_module(self) -> None:

@@ -66,7 +66,6 @@ from .fused_mlp import (  # noqa: E402
     mlp_param_count,
     mlp_supported,
     mlp_train_step,
-    mlp_train_step2,
     mlp_adam_,
     mlp_refresh_shadow,
     mlp_shadow_layout,

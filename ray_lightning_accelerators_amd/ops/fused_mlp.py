@@ -167,56 +167,6 @@ def mlp_refresh_shadow(params: torch.Tensor, shadow: torch.Tensor, L1: int, L2: 
         shadow[lay["w3t"]: lay["total"]].copy_(w3t.reshape(-1))
 
 
-def mlp_train_step2(
-    params: torch.Tensor,
-    grads: torch.Tensor,
-    *,
-    shadow: torch.Tensor,
-    dh1t: torch.Tensor,
-    counters: torch.Tensor,
-    L1: int,
-    L2: int,
-    B: int,
-    labels: torch.Tensor,
-    x_u8: Optional[torch.Tensor] = None,
-    x_f32: Optional[torch.Tensor] = None,
-    order: Optional[torch.Tensor] = None,
-    n_batches: int = 0,
-    exp_avg: Optional[torch.Tensor] = None,
-    exp_avg_sq: Optional[torch.Tensor] = None,
-    stats: Optional[torch.Tensor] = None,
-    accumulate_grad: bool = False,
-    apply_adam: bool = False,
-    advance_step: bool = True,
-    lr: float = 1e-3,
-    betas: Tuple[float, float] = (0.9, 0.999),
-    eps: float = 1e-8,
-    weight_decay: float = 0.0,
-    lr_tensor: Optional[torch.Tensor] = None,
-    adamw: bool = False,
-    stamps: Optional[torch.Tensor] = None,
-) -> None:
-    """v2 fused step: head kernel + 49-workgroup W1 kernel, weights read from the
-    bf16 ``shadow`` (kept current by the Adam epilogues).  Same semantics as
-    :func:`mlp_train_step`; ``counters`` has 3 slots (step, cursor, last cursor)."""
-    if use_native(params):
-        require().mlp_train_step2(
-            x_u8, x_f32, labels, order, counters, int(n_batches), int(B), int(L1), int(L2), params, grads,
-            exp_avg, exp_avg_sq, shadow, dh1t, stats, bool(accumulate_grad), bool(apply_adam), bool(advance_step),
-            float(lr), float(betas[0]), float(betas[1]), float(eps), float(weight_decay), lr_tensor, bool(adamw),
-            stamps,
-        )
-        return
-    if x_u8 is not None:
-        counters[2] = counters[1]
-    mlp_train_step(params, grads, L1=L1, L2=L2, B=B, labels=labels, x_u8=x_u8, x_f32=x_f32, order=order,
-                   counters=counters[:2], n_batches=n_batches, exp_avg=exp_avg, exp_avg_sq=exp_avg_sq, stats=stats,
-                   accumulate_grad=accumulate_grad, apply_adam=apply_adam, advance_step=advance_step, lr=lr,
-                   betas=betas, eps=eps, weight_decay=weight_decay, lr_tensor=lr_tensor, adamw=adamw)
-    if apply_adam:
-        mlp_refresh_shadow(params, shadow, L1, L2)
-
-
 MLP3_STEP, MLP3_HEAD, MLP3_TAIL_GRAD, MLP3_TAIL_ADAM, MLP3_PRIME, MLP3_STEP_DP = range(6)
 W1_TILES = IN_FEATURES // 16
 
@@ -233,6 +183,8 @@ def mlp3_buffers(L1: int, L2: int, B: int, device) -> Dict[str, torch.Tensor]:
         "yring": torch.full((2 * bp,), -1, dtype=torch.int32, device=device),
         # [0, 5) current state, [5, 10) the head's advanced copy (published by the tail)
         "counters": torch.zeros(10, dtype=torch.int64, device=device),
+        # per-head-workgroup (sum NLL, #correct, #rows, -) when the batch spans several
+        "head_part": torch.zeros(bp // 32 * 4, device=device),
     }
 
 
@@ -268,6 +220,7 @@ def mlp3_launch(
     adamw: bool = False,
     stamps: Optional[torch.Tensor] = None,
     dp_ctx: Optional[Sequence[int]] = None,
+    head_part: Optional[torch.Tensor] = None,
 ) -> None:
     """One v3 launch (GPU only).  ``kind``: MLP3_STEP (head + fused tail, world size 1),
     MLP3_HEAD / MLP3_TAIL_GRAD (gradients, before the allreduce), MLP3_TAIL_ADAM
@@ -281,7 +234,7 @@ def mlp3_launch(
         int(kind), x_u8, labels, order, counters, int(n_batches), int(B), int(L1), int(L2), params, grads, exp_avg,
         exp_avg_sq, shadow, dh1t, xring, h1pre, act, yring, stats, bool(advance_step), float(lr), float(betas[0]),
         float(betas[1]), float(eps), float(weight_decay), float(grad_scale), lr_tensor, bool(adamw), stamps,
-        [int(v) for v in (dp_ctx or ())],
+        [int(v) for v in (dp_ctx or ())], head_part,
     )
 
 
@@ -314,15 +267,25 @@ def mlp_eval(
     index: Optional[torch.Tensor] = None,
     logits: Optional[torch.Tensor] = None,
 ) -> None:
-    """Forward only: out[0] += sum NLL, out[1] += #correct; optional log-probs."""
+    """Forward only.  ``out`` [2]: out[0] += sum NLL, out[1] += #correct.  ``out``
+    [ceil(B/32), 2]: per-32-row-chunk (sum NLL, #correct), overwritten -- the GPU
+    kernel then runs one workgroup per chunk and the caller's ``out.sum(0)`` is
+    deterministic.  Optional log-probs into ``logits``."""
     if use_native(params):
         require().mlp_eval(x_u8, x_f32, labels, index, int(B), int(L1), int(L2), params, logits, out)
         return
     x, y = _gather_batch(x_u8, x_f32, labels, None, 0, B, index=index)
     with torch.no_grad():
         logp = F.log_softmax(_reference_forward(mlp_unpack(params, L1, L2), x), dim=1)
-        out[0] += F.nll_loss(logp, y, reduction="sum")
-        out[1] += (logp.argmax(dim=1) == y).sum().float()
+        nll = F.nll_loss(logp, y, reduction="none")
+        hit = (logp.argmax(dim=1) == y).float()
+        if out.dim() == 2:
+            pad = out.size(0) * 32 - B
+            out[:, 0] = F.pad(nll, (0, pad)).view(-1, 32).sum(1)
+            out[:, 1] = F.pad(hit, (0, pad)).view(-1, 32).sum(1)
+        else:
+            out[0] += nll.sum()
+            out[1] += hit.sum()
         if logits is not None:
             logits.view(B, NUM_CLASSES).copy_(logp)
 

@@ -69,7 +69,6 @@ class FusedMLPEngine:
         init_params: Optional[torch.Tensor] = None,
         stats_ring: int = 1024,
         seed: int = 0,
-        kernel_version: int = 3,
         buffers: Optional[Dict[str, torch.Tensor]] = None,
         dp_context: Optional[Sequence[int]] = None,
     ):
@@ -90,9 +89,8 @@ class FusedMLPEngine:
         self.native = self.device.type == "cuda"
         self.world_size, self.rank = int(world_size), int(rank)
         self.allreduce = allreduce
-        self.kernel_version = int(kernel_version)
         self.dp_ctx = None
-        if dp_context is not None and self.world_size > 1 and self.device.type == "cuda" and self.kernel_version == 3:
+        if dp_context is not None and self.world_size > 1 and self.device.type == "cuda":
             ctx = [int(v) for v in dp_context]
             if ctx[0] != self.world_size or ctx[1] != self.rank:
                 raise ValueError("dp_context belongs to a different (world, rank)")
@@ -121,6 +119,7 @@ class FusedMLPEngine:
         self.counters = bufs["counters"]
         self.dh1t, self.xring, self.h1pre, self.act = bufs["dh1t"], bufs["xring"], bufs["h1pre"], bufs["act"]
         self.yring = bufs["yring"]
+        self.head_part = bufs["head_part"]
         self.stats = torch.zeros(stats_ring, 4, device=self.device)
         self.seed = seed
         self.epoch = 0
@@ -250,12 +249,13 @@ class FusedMLPEngine:
         return dict(x_u8=self.x_u8, labels=self.labels, order=self.order, counters=self.counters,
                     n_batches=self.n_batches, B=self.B, L1=self.L1, L2=self.L2, params=self.params,
                     grads=self.grads, exp_avg=self.exp_avg, exp_avg_sq=self.exp_avg_sq, shadow=self.shadow,
-                    dh1t=self.dh1t, xring=self.xring, h1pre=self.h1pre, act=self.act, yring=self.yring, lr=self.lr, betas=self.betas,
+                    dh1t=self.dh1t, xring=self.xring, h1pre=self.h1pre, act=self.act, yring=self.yring,
+                    head_part=self.head_part, lr=self.lr, betas=self.betas,
                     eps=self.eps, weight_decay=self.wd, lr_tensor=self.lr_tensor)
 
     def prime(self) -> None:
         """Layer-1 pre-activations of the pending batch from the current weights."""
-        if self.native and self.kernel_version == 3:
+        if self.native:
             self.h1pre.zero_()
             fused_mlp.mlp3_launch(fused_mlp.MLP3_PRIME, **self._kw3())
         self._primed = True
@@ -267,7 +267,7 @@ class FusedMLPEngine:
             self.prime()
         if not self.native:
             self._reference_step()
-        elif self.kernel_version == 3:
+        else:
             kw = self._kw3()
             if self.world_size == 1:
                 fused_mlp.mlp3_launch(fused_mlp.MLP3_STEP, stats=self.stats, **kw)
@@ -276,29 +276,10 @@ class FusedMLPEngine:
                                       dp_ctx=self.dp_ctx, **kw)
             else:
                 fused_mlp.mlp3_launch(fused_mlp.MLP3_HEAD, stats=self.stats, **kw)
-                fused_mlp.mlp3_launch(fused_mlp.MLP3_TAIL_GRAD, **kw)
+                fused_mlp.mlp3_launch(fused_mlp.MLP3_TAIL_GRAD, stats=self.stats, **kw)  # multi-block head stats
                 if self.allreduce is not None:
                     self.allreduce(self.comm_buffer)
                 fused_mlp.mlp3_launch(fused_mlp.MLP3_TAIL_ADAM, grad_scale=1.0 / self.world_size, **kw)
-        else:
-            self._v2_step()
-
-    def _v2_step(self) -> None:
-        """Previous two-kernel step (kept for A/B comparisons); reads order buffer 0 only."""
-        fused = self.world_size == 1
-        fused_mlp.mlp_train_step2(
-            self.params, self.grads, shadow=self.shadow, dh1t=self.dh1t, counters=self.counters, L1=self.L1,
-            L2=self.L2, B=self.B, labels=self.labels, x_u8=self.x_u8, order=self.order[0],
-            n_batches=self.n_batches, exp_avg=self.exp_avg, exp_avg_sq=self.exp_avg_sq, stats=self.stats,
-            apply_adam=fused, advance_step=True, lr=self.lr, betas=self.betas, eps=self.eps,
-            weight_decay=self.wd, lr_tensor=self.lr_tensor,
-        )
-        if not fused:
-            if self.allreduce is not None:
-                self.allreduce(self.comm_buffer)
-            fused_mlp.mlp_adam_(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.shadow, L1=self.L1,
-                                L2=self.L2, lr=self.lr, step=self.counters[0:1], betas=self.betas, eps=self.eps,
-                                weight_decay=self.wd, grad_scale=1.0 / self.world_size, lr_tensor=self.lr_tensor)
 
     def _reference_step(self) -> None:
         """fp32 PyTorch step with the device kernels' batch / counter semantics."""
@@ -332,12 +313,8 @@ class FusedMLPEngine:
             self.step_in_epoch = 0
             if self._host_epochs:
                 return  # the host calls begin_epoch()
-            if self.kernel_version == 3 or not self.native:
-                # buffer (epoch + 1) % 2 was last read by the step just enqueued
-                self._fill_order(self.epoch + 1)
-            else:
-                idx = shard_indices(self.n_data, self.world_size, self.rank, self.epoch, self.seed, self.shuffle)
-                self.order[0].copy_(idx[: self.n_batches * self.B].to(self.device), non_blocking=True)
+            # buffer (epoch + 1) % 2 was last read by the step just enqueued
+            self._fill_order(self.epoch + 1)
 
     def steps_to_epoch_end(self) -> int:
         return self.n_batches - self.step_in_epoch

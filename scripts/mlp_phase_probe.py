@@ -1,6 +1,6 @@
-"""Diagnostic: per-step wall time of the fused MLP step (v2 head+W1 vs v3 pipelined
-head+tail), eager and hipGraph-replayed, plus per-phase timings of the head
-kernel from in-kernel s_memrealtime stamps (100 MHz)."""
+"""Diagnostic: per-step wall time of the fused MLP step (pipelined head + tail),
+eager and hipGraph-replayed, plus per-phase timings of the head kernel (block 0)
+and tail block 0 from in-kernel s_memrealtime stamps (100 MHz)."""
 import json
 import sys
 import time
@@ -30,31 +30,22 @@ def wall(eng, n=1000):
 
 
 for (L1, L2, B) in shapes:
-    for ver in (2, 3):
-        eng = FusedMLPEngine(L1, L2, B, lr=1e-3, device=dev, kernel_version=ver)
-        eng.set_data(x, y)
-        entry = {"eager_us_per_step": round(wall(eng), 2)}
-        eng.capture(8)
-        entry["graph8_us_per_step"] = round(wall(eng), 2)
-        st = torch.zeros(16, dtype=torch.int64, device=dev)
-        acc = torch.zeros(11, dtype=torch.float64)
-        names = (["start", "staged", "l1", "l3+softmax", "dH", "end"] if ver == 2
-                 else ["start", "h1", "l3", "dH", "end", "-", "-", "-", "tail_start", "tail_loaded", "tail_end"])
-        for _ in range(100):
-            if ver == 2:
-                fused_mlp.mlp_train_step2(eng.params, eng.grads, shadow=eng.shadow, dh1t=eng.dh1t,
-                                          counters=eng.counters, L1=L1, L2=L2, B=B, labels=eng.labels,
-                                          x_u8=eng.x_u8, order=eng.order[0], n_batches=eng.n_batches,
-                                          exp_avg=eng.exp_avg, exp_avg_sq=eng.exp_avg_sq, apply_adam=True,
-                                          lr=1e-3, stamps=st)
-            else:
-                fused_mlp.mlp3_launch(fused_mlp.MLP3_STEP, stamps=st, **eng._kw3())
-            torch.cuda.synchronize()
-            s = st[:len(names)].cpu().double()
-            acc[:len(names)] += (s - s[0]) * 10.0 / 1000.0
-        acc /= 100
-        entry["phase_end_us"] = {k: round(float(v), 2) for k, v in zip(names, acc) if k != "-"}
-        key = f"{L1}x{L2} B{B} v{ver}"
-        res[key] = entry
-        print(key, json.dumps(entry), flush=True)
+    eng = FusedMLPEngine(L1, L2, B, lr=1e-3, device=dev)
+    eng.set_data(x, y)
+    entry = {"eager_us_per_step": round(wall(eng), 2)}
+    eng.capture(8)
+    entry["graph8_us_per_step"] = round(wall(eng), 2)
+    st = torch.zeros(16, dtype=torch.int64, device=dev)
+    acc = torch.zeros(11, dtype=torch.float64)
+    names = ["start", "h1", "l3", "dH", "end", "-", "-", "-", "tail_start", "tail_loaded", "tail_end"]
+    for _ in range(100):
+        fused_mlp.mlp3_launch(fused_mlp.MLP3_STEP, stamps=st, stats=eng.stats, **eng._kw3())
+        torch.cuda.synchronize()
+        s = st[:len(names)].cpu().double()
+        acc[:len(names)] += (s - s[0]) * 10.0 / 1000.0
+    acc /= 100
+    entry["phase_end_us"] = {k: round(float(v), 2) for k, v in zip(names, acc) if k != "-"}
+    key = f"{L1}x{L2} B{B}"
+    res[key] = entry
+    print(key, json.dumps(entry), flush=True)
 json.dump(res, open('gpurun_out/mlp_phases.json', 'w'), indent=1)

@@ -1,0 +1,74 @@
+"""The benchmark entry point (``bench.py``) launches its own ranks.
+
+``python bench.py --gpus N`` must start N ranks itself -- as runtime actors,
+the RayAccelerator worker path -- and print ONE JSON line with the contract's
+fields (it used to exit rc=1 without torchrun).  On CPU the ranks
+run the engine's fp32 reference step over gloo.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIELDS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+          "vs_baseline", "dtype", "data", "config")
+
+
+def _bench(*args, env=None, timeout=300):
+    e = dict(os.environ)
+    e.update(env or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd="/tmp", env=e,
+                       capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    for k in FIELDS:
+        assert k in out, k
+    return out, p.stderr
+
+
+@pytest.mark.parametrize("launcher", ["ray", "spawn"])
+def test_bench_launches_two_cpu_ranks(launcher):
+    out, err = _bench("--device", "cpu", "--gpus", "2", "--steps", "10", "--warmup", "2", "--launcher", launcher)
+    assert out["n_gpus"] == 2 and out["steps"] == 10 and out["warmup"] == 2
+    assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 64
+    assert out["config"]["launch"] == ("ray-actors" if launcher == "ray" else "spawn")
+    assert out["value"] > 0
+    if launcher == "spawn":  # actor ranks log to the runtime session, not this stderr
+        assert "world=2" in err
+
+
+def test_bench_horovod_mode_cpu():
+    out, _ = _bench("--device", "cpu", "--gpus", "2", "--steps", "10", "--warmup", "2", "--accelerator", "horovod")
+    assert out["n_gpus"] == 2 and out["config"]["accelerator"] == "horovod"
+
+
+def test_bench_single_rank_cpu():
+    out, _ = _bench("--device", "cpu", "--steps", "10", "--warmup", "2")
+    assert out["n_gpus"] == 1 and out["vs_baseline"] is None and out["dtype"] == "fp32"
+
+
+def test_bench_via_trainer_cpu():
+    out, _ = _bench("--device", "cpu", "--gpus", "2", "--via", "trainer", "--trainer-epochs", "2", timeout=600)
+    assert out["n_gpus"] == 2 and out["config"]["accelerator"] == "RayAccelerator"
+    assert len(out["epoch_wall_s"]) == 2 and out["config"]["checkpointing"]
+    assert out["steps"] == 859  # one steady epoch of 27,500 / 32 batches per rank
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_share_gpu():
+    """The N>1 GPU path (fused xGMI tail exchange, hipGraph) with two actor ranks on
+    the box's one GPU (same-device IPC stands in for the xGMI link)."""
+    out, err = _bench("--gpus", "2", "--steps", "200", "--warmup", "50", env={"RLA_BENCH_SHARE_GPU": "1"})
+    assert out["n_gpus"] == 2 and out["config"]["route"] == "xgmi-fused", (out, err[-2000:])
+    assert out["config"]["launch"] == "ray-actors"
+
+
+@pytest.mark.gpu
+def test_bench_torch_graph_baseline():
+    out, _ = _bench("--impl", "torch-graph", "--steps", "200", "--warmup", "20")
+    assert out["n_gpus"] == 1 and out["config"]["impl"] == "torch-graph" and out["value"] > 0

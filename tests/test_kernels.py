@@ -338,15 +338,7 @@ def test_mlp_training_converges_native():
     assert last[:, 0].mean() < 1.0, last[:, 0]
 
 
-# ------------------------------------------------------- v2 (head + W1 kernels)
-def _v2_buffers(L1, L2, B, params, dev):
-    lay = fused_mlp.mlp_shadow_layout(L1, L2)
-    shadow = torch.zeros(lay["total"], dtype=torch.bfloat16, device=dev)
-    fused_mlp.mlp_refresh_shadow(params, shadow, L1, L2)
-    dh1t = torch.zeros(L1 * ((B + 31) // 32 * 32), dtype=torch.bfloat16, device=dev)
-    return shadow, dh1t
-
-
+# ------------------------------------------------------- bf16 weight shadows
 @gpu
 def test_mlp_shadow_refresh_native_matches_reference():
     dev = _dev()
@@ -363,79 +355,3 @@ def test_mlp_shadow_refresh_native_matches_reference():
         assert torch.equal(nat.cpu()[lay["w2t"]:], ref[lay["w2t"]:])
 
 
-@gpu
-@pytest.mark.parametrize("L1,L2", sorted(fused_mlp.SUPPORTED))
-@pytest.mark.parametrize("B", [32, 48, 128])
-def test_mlp2_grads_vs_emulation(L1, L2, B):
-    dev = _dev()
-    params, kw = _mlp_case(L1, L2, B, "u8", dev, seed=11)
-    grads = torch.zeros_like(params)
-    shadow, dh1t = _v2_buffers(L1, L2, B, params, dev)
-    cnt = torch.zeros(3, dtype=torch.int64, device=dev)
-    kw = {k: v for k, v in kw.items() if k != "counters"}
-    fused_mlp.mlp_train_step2(params, grads, shadow=shadow, dh1t=dh1t, counters=cnt, **kw)
-    idx = kw["order"][:B].cpu()
-    x = kw["x_u8"].cpu()[idx].float() / 255.0
-    emu = _emulate_bf16_grads(params, x, kw["labels"].cpu()[idx], L1, L2, B)
-    gn = fused_mlp.mlp_unpack(grads.cpu(), L1, L2)
-    ge = fused_mlp.mlp_unpack(emu, L1, L2)
-    errs = {k: _rel(gn[k], ge[k]) for k in gn}
-    assert all(e < 1e-2 for e in errs.values()), errs
-    assert cnt.tolist() == [1, 1, 0]
-
-
-@gpu
-@pytest.mark.parametrize("B", [17, 64, 100])
-def test_mlp2_f32_mode_vs_emulation(B):
-    dev = _dev()
-    L1, L2 = 32, 64
-    params, kw = _mlp_case(L1, L2, B, "f32", dev, seed=13)
-    grads = torch.zeros_like(params)
-    shadow, dh1t = _v2_buffers(L1, L2, B, params, dev)
-    cnt = torch.zeros(3, dtype=torch.int64, device=dev)
-    kw = {k: v for k, v in kw.items() if k != "counters"}
-    stats = torch.zeros(4, 4, device=dev)
-    fused_mlp.mlp_train_step2(params, grads, shadow=shadow, dh1t=dh1t, counters=cnt, stats=stats, **kw)
-    emu = _emulate_bf16_grads(params, kw["x_f32"].cpu(), kw["labels"].cpu(), L1, L2, B)
-    assert _rel(grads.cpu(), emu) < 1e-2
-    assert stats[0, 2].item() == B
-
-
-@gpu
-@pytest.mark.parametrize("L1,L2,B", [(32, 64, 32), (64, 128, 64), (128, 256, 128), (32, 32, 48)])
-def test_mlp2_fused_adam_matches_separate(L1, L2, B):
-    """v2 with Adam fused (world size 1) == v2 grads + mlp_adam_ (world size > 1 path)."""
-    dev = _dev()
-    params, kw = _mlp_case(L1, L2, B, "u8", dev, seed=17)
-    kw = {k: v for k, v in kw.items() if k != "counters"}
-    pa, pb = params.clone(), params.clone()
-    ma, va, mb, vb = (torch.zeros_like(params) for _ in range(4))
-    sa, da = _v2_buffers(L1, L2, B, pa, dev)
-    sb, db = _v2_buffers(L1, L2, B, pb, dev)
-    ca = torch.zeros(3, dtype=torch.int64, device=dev)
-    cb = torch.zeros(3, dtype=torch.int64, device=dev)
-    gb = torch.zeros_like(params)
-    for _ in range(3):
-        fused_mlp.mlp_train_step2(pa, torch.zeros_like(params), shadow=sa, dh1t=da, counters=ca, exp_avg=ma,
-                                  exp_avg_sq=va, apply_adam=True, lr=1e-2, **kw)
-        fused_mlp.mlp_train_step2(pb, gb, shadow=sb, dh1t=db, counters=cb, lr=1e-2, **kw)
-        fused_mlp.mlp_adam_(pb, gb, mb, vb, sb, L1=L1, L2=L2, lr=1e-2, step=cb[0:1])
-    torch.cuda.synchronize()
-    assert torch.allclose(pa, pb, atol=1e-5), (pa - pb).abs().max()
-    for p, s in ((pa, sa), (pb, sb)):
-        ref = torch.zeros_like(s)
-        fused_mlp.mlp_refresh_shadow(p, ref, L1, L2)
-        assert torch.equal(s, ref)  # epilogue-written shadows == a full refresh of the fp32 masters
-
-
-@gpu
-def test_mlp2_training_converges():
-    from ray_lightning_accelerators_amd.models.data import synthetic_mnist
-    from ray_lightning_accelerators_amd.parallel.mlp_engine import FusedMLPEngine
-
-    x, y = synthetic_mnist(4096, seed=0)
-    eng = FusedMLPEngine(32, 64, 32, lr=1e-3, device=_dev())
-    eng.set_data(x, y)
-    eng.run(300)
-    torch.cuda.synchronize()
-    assert eng.recent_stats(20)[:, 0].mean() < 0.5

@@ -163,6 +163,41 @@ def test_mlp3_fused_matches_split(L1, L2, B):
 
 
 @gpu
+@pytest.mark.parametrize("L1,L2,B", [(128, 256, 128), (32, 64, 100), (64, 128, 256)])
+def test_mlp3_multiblock_head_stats(L1, L2, B):
+    """Batches above 32 rows run one head workgroup per 32 rows; the step's loss /
+    correct / count (reduced by tail block 0 in block order) match an fp32 forward
+    of the consumed batch, and are identical across repeated runs."""
+    import torch.nn.functional as F
+
+    dev = _dev()
+    n_data = 4 * B
+    x, y = _data(n_data, seed=B)
+    runs = []
+    for _ in range(2):
+        eng = FusedMLPEngine(L1, L2, B, lr=1e-2, device=dev)
+        eng.set_data(x, y)
+        rows = []
+        for s in range(5):
+            epoch, cur = eng.epoch, eng.step_in_epoch
+            p_before = eng.params.detach().cpu().clone()
+            eng.step()
+            torch.cuda.synchronize()
+            idx = shard_indices(n_data, 1, 0, epoch, 0, True)[cur * B:(cur + 1) * B]
+            pv = fused_mlp.mlp_unpack(p_before, L1, L2)
+            h = torch.relu(F.linear(x[idx].float() / 255.0, pv["layer_1.weight"], pv["layer_1.bias"]))
+            h = torch.relu(F.linear(h, pv["layer_2.weight"], pv["layer_2.bias"]))
+            logp = F.log_softmax(F.linear(h, pv["layer_3.weight"], pv["layer_3.bias"]), dim=1)
+            st = eng.recent_stats(1)[0]
+            assert int(st[2]) == B and int(st[3]) == s + 1, st
+            assert abs(float(st[0]) - float(F.nll_loss(logp, y[idx]))) < 3e-2 * max(1.0, float(st[0])), (s, st)
+            assert abs(int(st[1]) - int((logp.argmax(1) == y[idx]).sum())) <= max(2, B // 25), (s, st)
+            rows.append(st.clone())
+        runs.append(torch.stack(rows))
+    assert torch.equal(runs[0], runs[1])
+
+
+@gpu
 def test_mlp3_graph_replay_matches_eager():
     dev = _dev()
     # 5 batches per epoch, 3 steps per graph: replays, eager remainders and
