@@ -576,30 +576,60 @@ def run_rank(args):
 class _EpochClock(Callback):
     """Callback: wall-clock of every epoch from one epoch start to the next (so an
     epoch's time includes its validation pass, checkpoint write and logging),
-    max over ranks; rank 0 writes the rows to ``path``."""
+    max over ranks, plus the per-epoch split train / validation / rest (device
+    synced at each mark); ``trace`` also marks every dispatch chunk.  Rank 0
+    writes the rows to ``path``."""
 
-    def __init__(self, path):
+    def __init__(self, path, trace=False):
         self.path = path
-        self.marks = []
+        self.trace = trace
+        self.marks = []  # (epoch, name, t)
 
-    def _mark(self, trainer):
+    def _mark(self, trainer, name):
         if trainer.on_gpu:
             torch.cuda.synchronize()
-        self.marks.append(time.perf_counter())
+        self.marks.append((trainer.current_epoch, name, time.perf_counter()))
 
     def on_train_epoch_start(self, trainer, pl_module):
-        self._mark(trainer)
+        self._mark(trainer, "epoch_start")
+
+    def on_validation_start(self, trainer, pl_module):
+        if not trainer.running_sanity_check:
+            self._mark(trainer, "val_start")
+
+    def on_validation_end(self, trainer, pl_module):
+        if not trainer.running_sanity_check:
+            self._mark(trainer, "val_end")
+
+    def on_train_chunk_end(self, trainer, pl_module, outputs, n_steps, n_samples):
+        if self.trace:
+            self._mark(trainer, "chunk_end")
 
     def on_train_end(self, trainer, pl_module):
-        self._mark(trainer)
-        secs = torch.tensor([b - a for a, b in zip(self.marks, self.marks[1:])], dtype=torch.float64)
+        self._mark(trainer, "train_end")
+        starts = [t for _, n, t in self.marks if n in ("epoch_start", "train_end")]
+        secs = torch.tensor([b - a for a, b in zip(starts, starts[1:])], dtype=torch.float64)
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             t = secs.to(trainer.accelerator_backend._comm_device())
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             secs = t.cpu()
+        split = []
+        for e in range(len(starts) - 1):
+            ev = {n: t for ep, n, t in self.marks if ep == e and n in ("val_start", "val_end")}
+            t0, t1 = starts[e], starts[e + 1]
+            vs, ve = ev.get("val_start", t1), ev.get("val_end", t1)
+            row = {"train_s": round(vs - t0, 5), "val_s": round(ve - vs, 5), "rest_s": round(t1 - ve, 5)}
+            if self.trace:
+                ch = [t for ep, n, t in self.marks if ep == e and n == "chunk_end"]
+                gaps = [b - a for a, b in zip([t0] + ch, ch)]
+                if gaps:
+                    i = max(range(len(gaps)), key=gaps.__getitem__)
+                    row.update(chunks=len(gaps), slowest_chunk_s=round(gaps[i], 5), slowest_chunk=i,
+                               median_chunk_s=round(statistics.median(gaps), 6))
+            split.append(row)
         if trainer.global_rank == 0:
             with open(self.path, "w") as f:
-                json.dump({"epoch_s": secs.tolist(), "world": trainer.world_size,
+                json.dump({"epoch_s": secs.tolist(), "split": split, "world": trainer.world_size,
                            "batches": int(trainer.num_training_batches),
                            "val_batches": [int(v) for v in trainer.num_val_batches],
                            "fused": trainer._fused is not None,
@@ -622,7 +652,7 @@ def run_trainer(args):
     gpu = args.device == "cuda"
     env = rank_env()
     out_path = tempfile.mktemp(prefix="rla-bench-", suffix=".json")
-    clock = _EpochClock(out_path)
+    clock = _EpochClock(out_path, trace=os.environ.get("RLA_BENCH_TRACE") == "1")
     model = MNISTClassifier({"layer_1": args.layer_1, "layer_2": args.layer_2, "lr": args.lr,
                              "batch_size": args.batch_size})
     root = tempfile.mkdtemp(prefix="rla-bench-trainer-")
@@ -693,6 +723,7 @@ def run_trainer(args):
             "fused_step": rows["fused"],
         },
         "epoch_wall_s": [round(v, 5) for v in epochs],
+        "epoch_split": rows["split"],
         "median_steady_epoch_samples_per_s": round(per_epoch / med, 1),
         "steady_epoch_spread": round(max(steady) / min(steady), 3),
         "fit_wall_s": round(fit_s, 2),

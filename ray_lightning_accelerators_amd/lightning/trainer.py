@@ -538,9 +538,10 @@ class Trainer:
 
     def _flush_logger(self, defer: bool = False) -> None:
         """Hand ``logged_metrics`` to the logger.  ``defer`` (multi-step dispatch):
-        device values are copied to the host asynchronously and written at the
-        next flush, so a log point does not drain the GPU queue."""
-        self._write_pending_log()
+        device values are copied to the host asynchronously and written once their
+        copy has landed -- a log point never waits for the GPU queue to drain
+        (only a backlog of more than a few unfinished snapshots does)."""
+        self._write_pending_log(block=not defer)
         if self.logger is None or not self.logged_metrics or not self.is_global_zero:
             return
         metrics = dict(self.logged_metrics)
@@ -549,16 +550,24 @@ class Trainer:
                     for k, v in metrics.items()}
             ev = torch.cuda.Event()
             ev.record()
-            self._pending_log = (snap, self.global_step, ev)
+            if self._pending_log is None:
+                self._pending_log = []
+            self._pending_log.append((snap, self.global_step, ev))
             return
         self.logger.log_metrics(metrics, step=self.global_step)
 
-    def _write_pending_log(self) -> None:
-        pending, self._pending_log = self._pending_log, None
-        if pending is not None:
-            snap, step, ev = pending
+    def _write_pending_log(self, block: bool = True) -> None:
+        """Write deferred snapshots in step order: all of them (``block``), else the
+        ones whose copy has completed, plus the oldest while more than 4 wait."""
+        pending = self._pending_log or []
+        while pending:
+            snap, step, ev = pending[0]
+            if not block and len(pending) <= 4 and not ev.query():
+                break
             ev.synchronize()
+            pending.pop(0)
             self.logger.log_metrics(snap, step=step)
+        self._pending_log = pending or None
 
     # ---------------------------------------------------------- evaluation
     def run_sanity_check(self, model: LightningModule) -> None:

@@ -329,9 +329,16 @@ class FusedMNISTStep:
                 st["step"].fill_(float(self.gs.step))
         ring = eng.stats.size(0)
         k = min(n_steps, ring)
-        # device-side slot list: a host list would be a blocking H2D copy (a sync) per chunk
-        slots = (torch.arange(k, device=self.dev) + (first + n_steps - k)) % ring
-        rows = eng.stats.index_select(0, slots)  # snapshot: the ring wraps in later chunks
+        # Snapshot the whole ring in step order (the ring wraps in later chunks) and
+        # keep the last k rows as a view.  The gather is the SAME size every chunk:
+        # a chunk-sized gather picked a different ROCm index kernel for small
+        # chunks, and loading that kernel's code object the first time one
+        # appeared stalled that epoch by ~60 ms (profiles/r2_c05).  The slot list
+        # is built on the device: a host list would be a blocking H2D copy per chunk.
+        if getattr(self, "_ring_ar", None) is None or self._ring_ar.numel() != ring:
+            self._ring_ar = torch.arange(ring, device=self.dev)
+        slots = (self._ring_ar + (first + n_steps)) % ring
+        rows = eng.stats.index_select(0, slots)[ring - k:]
         last = rows[-1]
         self.model.log("ptl/train_loss", last[0])
         self.model.log("ptl/train_accuracy", last[1] / last[2].clamp(min=1))

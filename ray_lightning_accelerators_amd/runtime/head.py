@@ -7,7 +7,13 @@ Responsibilities (reference call sites in SURVEY.md §2.2 U17):
     set to the allocated GPU (one whole GPU per training worker, reference
     ray_ddp.py:94-96) and ``RLA_NODE_IP`` set to the node's address;
   * the actor table (ALIVE / DEAD) behind ``runtime.actors()``;
-  * killing actors and noticing workers that die (fail-fast).
+  * killing actors and noticing workers that die (fail-fast, SURVEY.md §5.3);
+  * a pool of PRE-STARTED worker processes (``RLA_WORKER_POOL``, default 2):
+    interpreters that already imported torch but never touched a GPU wait for
+    an actor assignment (env incl. HIP_VISIBLE_DEVICES, cwd, log file), so an
+    actor starts in milliseconds instead of paying interpreter + torch import
+    (~2 s) -- the dominant cost of short Tune trials (Ray keeps a worker pool
+    for the same reason).
 
 The head never imports torch and never touches a GPU, so it can fork workers
 safely even when the driver process has already initialised HIP.
@@ -80,6 +86,51 @@ class Head:
         self.actors: Dict[str, ActorRecord] = {}
         self.listener, self.address = P.make_listener(session_dir, authkey, "head")
         self.stopping = False
+        # pre-started workers: pid -> Popen while starting, then (Popen, conn) when ready
+        self.pool_target = max(0, int(os.environ.get("RLA_WORKER_POOL", "2")))
+        self.pool_starting: Dict[int, subprocess.Popen] = {}
+        self.pool_ready: List = []
+        self.pool_lock = threading.Lock()
+
+    # ------------------------------------------------------------ worker pool
+    def _pool_env(self) -> Dict[str, str]:
+        env = dict(os.environ)
+        env[P.ENV_HEAD] = self.address
+        env[P.ENV_AUTH] = self.authkey.hex()
+        env[P.ENV_SESSION_DIR] = self.session_dir
+        env[P.ENV_SYS_PATH] = self.sys_path
+        env["PYTHONUNBUFFERED"] = "1"
+        env.pop(P.ENV_ACTOR_ID, None)
+        return env
+
+    def refill_pool(self) -> None:
+        if self.stopping:
+            return
+        with self.pool_lock:
+            missing = self.pool_target - len(self.pool_ready) - len(self.pool_starting)
+            for _ in range(max(0, missing)):
+                log = open(os.path.join(self.log_dir, "pool.log"), "ab")
+                proc = subprocess.Popen([sys.executable, "-m", "ray_lightning_accelerators_amd.runtime.worker", "--pool"],
+                                        env=self._pool_env(), stdout=log, stderr=subprocess.STDOUT,
+                                        start_new_session=True)
+                log.close()
+                self.pool_starting[proc.pid] = proc
+
+    def _take_pooled(self):
+        """An idle pre-started worker (its Popen and the connection it waits on), or None."""
+        with self.pool_lock:
+            while self.pool_ready:
+                proc, conn = self.pool_ready.pop(0)
+                if proc.poll() is None:
+                    return proc, conn
+        return None
+
+    @staticmethod
+    def _poolable(msg: dict) -> bool:
+        # interpreter-start settings cannot be applied to a running process
+        env = msg.get("env") or {}
+        return msg.get("capture_output", True) and not any(
+            k.startswith(("PYTHON", "LD_", "MALLOC")) for k in env)
 
     # ---------------------------------------------------------- scheduling
     def _place(self, req: Dict[str, float], node_ip: Optional[str]) -> Optional[Node]:
@@ -143,12 +194,29 @@ class Head:
         # workers on 8 CPUs ran 64 ms/step instead of ~2 ms)
         if "OMP_NUM_THREADS" not in (msg.get("env") or {}):
             env["OMP_NUM_THREADS"] = str(max(1, int(req.get("CPU", 1) or 1)))
-        log = open(os.path.join(self.log_dir, f"worker-{actor_id[:8]}.log"), "ab")
-        cmd = [sys.executable, "-m", "ray_lightning_accelerators_amd.runtime.worker"]
-        proc = subprocess.Popen(cmd, env=env, stdout=log if msg.get("capture_output", True) else None,
-                                stderr=subprocess.STDOUT if msg.get("capture_output", True) else None,
-                                cwd=msg.get("cwd") or os.getcwd(), start_new_session=True)
-        log.close()
+        log_path = os.path.join(self.log_dir, f"worker-{actor_id[:8]}.log")
+        pooled = self._take_pooled() if self._poolable(msg) else None
+        proc = None
+        if pooled is not None:
+            proc, conn = pooled
+            # the actor-specific part of the environment (a pooled process already
+            # carries the head's); applied before the worker touches any GPU
+            delta = {k: v for k, v in env.items() if os.environ.get(k) != v}
+            unset = [k for k in os.environ if k not in env]
+            try:
+                conn.send({"op": "assign", "env": delta, "unset": unset, "cwd": msg.get("cwd") or os.getcwd(),
+                           "log": log_path})
+                conn.close()
+            except (OSError, EOFError):
+                proc = None
+            threading.Thread(target=self.refill_pool, daemon=True).start()
+        if proc is None:
+            log = open(log_path, "ab")
+            cmd = [sys.executable, "-m", "ray_lightning_accelerators_amd.runtime.worker"]
+            proc = subprocess.Popen(cmd, env=env, stdout=log if msg.get("capture_output", True) else None,
+                                    stderr=subprocess.STDOUT if msg.get("capture_output", True) else None,
+                                    cwd=msg.get("cwd") or os.getcwd(), start_new_session=True)
+            log.close()
         rec.proc = proc
         rec.pid = proc.pid
         # wait for the worker to register its listener
@@ -210,6 +278,15 @@ class Head:
             try:
                 if op == "create_actor":
                     reply = self.create_actor(msg)
+                elif op == "pool_ready":
+                    # a pre-started worker: keep its connection for the assignment
+                    with self.pool_lock:
+                        proc = self.pool_starting.pop(int(msg["pid"]), None)
+                        if proc is not None and not self.stopping:
+                            self.pool_ready.append((proc, conn))
+                            return
+                    conn.close()
+                    return
                 elif op == "register":
                     rec = self.actors.get(msg["actor_id"])
                     if rec is not None:
@@ -270,6 +347,14 @@ class Head:
         for rec in list(self.actors.values()):
             if rec.state != "DEAD":
                 self._kill(rec, "runtime shutdown")
+        with self.pool_lock:
+            idle = [p for p, _ in self.pool_ready] + list(self.pool_starting.values())
+            self.pool_ready, self.pool_starting = [], {}
+        for proc in idle:
+            try:
+                os.killpg(proc.pid, signal.SIGKILL)
+            except (ProcessLookupError, PermissionError):
+                pass
         try:
             self.listener.close()
         except OSError:
@@ -278,6 +363,7 @@ class Head:
 
     def serve(self, ready_fd: Optional[int]) -> None:
         threading.Thread(target=self.monitor, daemon=True).start()
+        threading.Thread(target=self.refill_pool, daemon=True).start()
         if ready_fd is not None:
             os.write(ready_fd, (self.address + "\n").encode())
             os.close(ready_fd)

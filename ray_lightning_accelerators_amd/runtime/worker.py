@@ -97,11 +97,43 @@ class WorkerServer:
             threading.Thread(target=self._serve_conn, args=(P.SafeConn(c),), daemon=True).start()
 
 
+def _wait_for_assignment() -> None:
+    """Pre-started pool worker: import the heavy modules now (never touching a
+    GPU), then block until the head assigns an actor; apply its environment
+    (HIP_VISIBLE_DEVICES, actor id, ...), working directory and log file."""
+    import torch  # noqa: F401 - the import is the point: it is what a pooled worker saves
+    import torch.distributed  # noqa: F401
+
+    head = P.connect(os.environ[P.ENV_HEAD], bytes.fromhex(os.environ[P.ENV_AUTH]))
+    head.send({"op": "pool_ready", "pid": os.getpid()})
+    try:
+        msg = head.recv()
+    except (EOFError, OSError):
+        os._exit(0)  # head gone: nobody will ever assign this worker
+    head.close()
+    for k in msg.get("unset", []):
+        os.environ.pop(k, None)
+    os.environ.update(msg.get("env") or {})
+    os.chdir(msg.get("cwd") or os.getcwd())
+    fd = os.open(msg["log"], os.O_WRONLY | os.O_CREAT | os.O_APPEND, 0o644)
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os.dup2(fd, 1)
+    os.dup2(fd, 2)
+    os.close(fd)
+    n = os.environ.get("OMP_NUM_THREADS")
+    if n and n.isdigit():
+        torch.set_num_threads(int(n))  # libgomp read the head's value at import
+
+
 def main() -> None:
+    pooled = "--pool" in sys.argv[1:]
     extra = os.environ.get(P.ENV_SYS_PATH, "")
     for p in reversed([x for x in extra.split(os.pathsep) if x]):
         if p not in sys.path:
             sys.path.insert(0, p)
+    if pooled:
+        _wait_for_assignment()
     from . import client
 
     client._mark_worker()

@@ -15,7 +15,7 @@ from ray_lightning_accelerators_amd.parallel.mlp_engine import FusedMLPEngine  #
 dev = torch.device('cuda', 0)
 res = {}
 x, y = synthetic_mnist(8192, seed=0)
-shapes = [(32, 64, 32), (32, 64, 64), (64, 128, 64), (128, 256, 128)]
+shapes = [(32, 64, 32), (128, 256, 32), (64, 128, 64), (128, 256, 128)]
 if len(sys.argv) > 1 and sys.argv[1] == "quick":
     shapes = shapes[:1]
 

@@ -194,3 +194,40 @@ def test_executor_accelerator_pickling_drops_handles(rt):
     clone = cloudpickle.loads(cloudpickle.dumps(acc))
     assert clone.workers == []
     ray.kill(acc.workers[0])
+
+
+@ray.remote
+class _Probe:
+    def info(self):
+        import sys
+
+        return {"torch_preloaded": "torch" in sys.modules, "vis": os.environ.get("HIP_VISIBLE_DEVICES"),
+                "actor": os.environ.get("RLA_ACTOR_ID"), "cwd": os.getcwd(), "pid": os.getpid(),
+                "omp": os.environ.get("OMP_NUM_THREADS")}
+
+
+def test_prestarted_worker_pool_assigns_actor_env():
+    """Actors start on pre-started pool workers (torch already imported, no GPU
+    touched) and still get their own GPU pinning, actor id, cwd and thread count."""
+    ray.init(num_cpus=4, num_gpus=0, _nodes=[{"ip": "127.0.0.1", "num_cpus": 4, "num_gpus": 2,
+                                               "gpu_ids": ["0", "1"]}])
+    try:
+        time.sleep(8.0)  # the head pre-starts RLA_WORKER_POOL (default 2) workers at init
+        t0 = time.perf_counter()
+        a = _Probe.options(num_cpus=2, num_gpus=1).remote()
+        b = _Probe.options(num_cpus=1, num_gpus=1).remote()
+        ia, ib = ray.get([a.info.remote(), b.info.remote()])
+        dt = time.perf_counter() - t0
+        assert ia["torch_preloaded"] and ib["torch_preloaded"], (ia, ib)
+        assert {ia["vis"], ib["vis"]} == {"0", "1"}
+        assert ia["actor"] != ib["actor"] and ia["pid"] != ib["pid"]
+        assert ia["omp"] == "2" and ib["omp"] == "1"
+        assert ia["cwd"] == os.getcwd()
+        assert dt < 5.0, dt  # no interpreter + torch start on the critical path
+        # the pool refills: a third actor is also served from it
+        time.sleep(8.0)
+        c = _Probe.options(num_cpus=1).remote()
+        ic = ray.get(c.info.remote())
+        assert ic["torch_preloaded"] and ic["vis"] == "", ic
+    finally:
+        ray.shutdown()

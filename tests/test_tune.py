@@ -102,7 +102,7 @@ class _GpuProbe:
 
 def _packing_trainable(config):
     workers = [ray.remote(_GpuProbe).options(num_cpus=1, num_gpus=1).remote() for _ in range(2)]
-    out = ray.get([w.hold.remote(2.0) for w in workers])
+    out = ray.get([w.hold.remote(6.0) for w in workers])  # > worst-case worker start skew
     for w in workers:
         ray.kill(w)
     tune.report(devices=",".join(d for d, _, _ in out), start=min(s for _, s, _ in out),
