@@ -35,6 +35,7 @@ from .. import runtime as ray
 from ..lightning.accelerators import DataParallelAccelerator
 from ..lightning.utilities import log
 from ..session import init_session, shutdown_session
+from ..utils.timeline import mark
 from ..util import Queue, process_results
 
 
@@ -117,6 +118,7 @@ class RayAccelerator(DataParallelAccelerator):
         assert self.trainer is not None, "trainer must be attached before setup()"
         self.trainer.use_ddp = True
         self.trainer.model = model
+        mark("ddp_setup")
         self.workers = [self._create_worker() for _ in range(self.num_workers)]
         if self.init_hook:
             ray.get([w.execute.remote(self.init_hook) for w in self.workers])
@@ -178,7 +180,9 @@ class RayAccelerator(DataParallelAccelerator):
         self.global_to_local = self.get_local_ranks()
         trainer = self.trainer
         assert trainer is not None
+        mark("ddp_train_begin")
         trainer_ref = ray.put(trainer)
+        mark("trainer_put")
         self.trainer = None  # do not pickle the trainer twice
         queue = None
         if _tune_session_enabled():
@@ -195,6 +199,7 @@ class RayAccelerator(DataParallelAccelerator):
             self.trainer = trainer
             if queue is not None:
                 queue.shutdown()
+        mark("ddp_results")
         results, best_path, state_dict = results[0]
         trainer.model.load_state_dict(state_dict)
         if trainer.checkpoint_callback is not None:
@@ -203,6 +208,7 @@ class RayAccelerator(DataParallelAccelerator):
 
     # ----------------------------------------------------------- worker side
     def train_remote(self, trainer, global_rank: int, queue=None):
+        mark("worker_train_remote", rank=global_rank)
         assert isinstance(self, RayAccelerator)
         self.trainer = trainer
         trainer.accelerator_backend = self
@@ -231,7 +237,8 @@ class RayAccelerator(DataParallelAccelerator):
             kw = {}
             if self.use_gpu:
                 torch.cuda.set_device(0)
-                if backend == "nccl":
+                if backend == "nccl" and world_size > 1:
+                    # eager RCCL communicator; a world of 1 never runs a collective
                     kw["device_id"] = torch.device("cuda", 0)
             dist.init_process_group(backend=backend, init_method=self.ddp_address, rank=global_rank,
                                     world_size=world_size, **kw)

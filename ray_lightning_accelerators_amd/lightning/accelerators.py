@@ -16,7 +16,14 @@ import torch
 import torch.distributed as dist
 
 from ..config import RLAConfig, get_config, log_config, set_config
+from ..utils.timeline import mark
 from .utilities import log, move_to_device, rank_zero_only_state, seed_everything
+
+
+def _dist_active() -> bool:
+    """A process group with more than one rank (a world of 1 needs no collective --
+    and an RCCL group of 1 would create its communicator, ~1 s, on the first one)."""
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
 class Accelerator:
@@ -148,18 +155,18 @@ class Accelerator:
         return {}
 
     def barrier(self, name: Optional[str] = None) -> None:
-        if dist.is_available() and dist.is_initialized():
+        if _dist_active():
             dist.barrier()
 
     def broadcast(self, obj: Any, src: int = 0) -> Any:
-        if not (dist.is_available() and dist.is_initialized()):
+        if not _dist_active():
             return obj
         box = [obj]
         dist.broadcast_object_list(box, src=src)
         return box[0]
 
     def sync_tensor(self, tensor: torch.Tensor, group=None, reduce_op: Any = "mean") -> torch.Tensor:
-        if not (dist.is_available() and dist.is_initialized()):
+        if not _dist_active():
             return tensor
         t = tensor.clone().to(self._comm_device())
         op = str(reduce_op).lower()
@@ -174,7 +181,7 @@ class Accelerator:
         return t.to(tensor.device)
 
     def all_gather(self, tensor: torch.Tensor) -> torch.Tensor:
-        if not (dist.is_available() and dist.is_initialized()):
+        if not _dist_active():
             return tensor.unsqueeze(0)
         t = tensor.to(self._comm_device())
         out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
@@ -182,7 +189,7 @@ class Accelerator:
         return torch.stack(out).to(tensor.device)
 
     def early_stopping_should_stop(self, should_stop: bool) -> bool:
-        if not (dist.is_available() and dist.is_initialized()):
+        if not _dist_active():
             return should_stop
         t = torch.tensor([1.0 if should_stop else 0.0], device=self._comm_device())
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
@@ -267,9 +274,12 @@ class DataParallelAccelerator(Accelerator):
             seed_everything(int(os.environ["PL_GLOBAL_SEED"]))
         self.set_world_ranks(process_idx)
         rank_zero_only_state.rank = t.global_rank
+        mark("pg_init_begin", rank=t.global_rank)
         self.init_ddp_connection(t.global_rank, t.world_size)
+        mark("pg_init_end", rank=t.global_rank)
         log_config(t.global_rank, self.config)
         self.init_device(process_idx, t.global_rank == 0)
+        mark("device_ready", rank=t.global_rank)
         if t.sync_batchnorm and t.world_size > 1 and dist.is_initialized():
             # PL: Trainer(sync_batchnorm=True) -> BN statistics all-reduced across ranks
             # (fused BN+ReLU layers stay fused and all-reduce their per-channel sums)
@@ -277,8 +287,11 @@ class DataParallelAccelerator(Accelerator):
 
             convert_sync_batchnorm(model)
         self.model_to_device(model)
+        mark("model_on_device", rank=t.global_rank)
         results = t._run(model)
+        mark("run_end", rank=t.global_rank)
         self.transfer_distrib_spawn_state_on_fit_end(model, results)
+        mark("state_handed_back", rank=t.global_rank)
         return results
 
     def transfer_distrib_spawn_state_on_fit_end(self, model, results) -> None:

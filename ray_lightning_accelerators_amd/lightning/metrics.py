@@ -65,7 +65,7 @@ class Accuracy(Metric):
 
     def compute(self) -> torch.Tensor:
         c, t = self.correct.clone(), self.total.clone()
-        if dist.is_available() and dist.is_initialized():
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             dev = c.device
             buf = torch.stack([c, t])
             if dist.get_backend() == "nccl":

@@ -31,6 +31,7 @@ from .utilities import atomic_save, load_checkpoint, log, move_to_device, rank_z
 from ..config import get_config
 from ..utils.faults import maybe_inject as maybe_inject_fault
 from ..utils.profiling import resolve_profiler
+from ..utils.timeline import mark
 
 PL_COMPAT_VERSION = "1.1.7"
 
@@ -351,11 +352,15 @@ class Trainer:
 
         acc = resolve_accelerator(self)
         acc.trainer = self
+        mark("fit_setup_begin")
         acc.setup(model)
+        mark("fit_setup_end")
         try:
             results = acc.train()
         finally:
+            mark("fit_teardown_begin")
             acc.teardown()
+            mark("fit_teardown_end")
         return results
 
     # -------------------------------------------------- worker-side entry
@@ -378,16 +383,22 @@ class Trainer:
         model.trainer = self
         self.model = model
         self.call_setup_hook(model)
+        mark("setup_hook_done", rank=self.global_rank)
         self._prepare_dataloaders(model)
+        mark("dataloaders_ready", rank=self.global_rank)
         if self.testing:
             self.optimizers, self.lr_schedulers = [], []
             results = self.run_test()
             model.teardown("test")
             return results
         opts, scheds = _normalize_optimizers(model.configure_optimizers())
+        mark("configure_optimizers_done", rank=self.global_rank)
         self.optimizers, self.lr_schedulers = self.accelerator_backend.setup_optimizers(model, opts, scheds)
+        mark("optimizers_ready", rank=self.global_rank)
         self.accelerator_backend.configure_ddp(model)
+        mark("ddp_configured", rank=self.global_rank)
         self._fused = self._maybe_fused(model)
+        mark("fused_step_ready", rank=self.global_rank)
         if self.resume_from_checkpoint and os.path.exists(self.resume_from_checkpoint):
             self.checkpoint_connector.restore(self.resume_from_checkpoint, on_gpu=self.on_gpu)
         self.run_train()
@@ -679,6 +690,7 @@ class Trainer:
             if self.is_global_zero and model.hparams:
                 self.logger.log_hyperparams(model.hparams)
         self.run_sanity_check(model)
+        mark("sanity_check_done", rank=self.global_rank)
         self.call_hook("on_train_start")
         # Everything alive now (torch, the model, the data) is long-lived: move it
         # out of the cyclic GC's generations, so a full collection during the
@@ -715,6 +727,7 @@ class Trainer:
         sampler = getattr(dl, "sampler", None)
         if hasattr(sampler, "set_epoch"):
             sampler.set_epoch(self.current_epoch)
+        mark("epoch_start", rank=self.global_rank, epoch=self.current_epoch)
         self.call_hook("on_epoch_start")
         self.call_hook("on_train_epoch_start")
         epoch_outputs: List[Any] = []

@@ -10,8 +10,11 @@ in the dataset's ``__getitem__`` on CPU or inside the fused kernel on GPU.
 from __future__ import annotations
 
 import math
+import os
+import tempfile
 from typing import Optional, Tuple
 
+import numpy as np
 import torch
 from torch.utils.data import Dataset
 
@@ -31,8 +34,53 @@ def _prototypes(seed: int = 0) -> torch.Tensor:
     return protos
 
 
+_CACHE_VERSION = 1
+_memo = {}
+
+
+def _cache_dir() -> str:
+    return os.environ.get("RLA_DATA_CACHE") or os.path.join(tempfile.gettempdir(), "rla-synthetic-mnist")
+
+
 def synthetic_mnist(n: int, seed: int = 0, noise: float = 0.1, jitter: int = 1) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Return (images uint8 [n, 784], labels int64 [n])."""
+    """Return (images uint8 [n, 784], labels int64 [n]).
+
+    Generated once per machine: the arrays are cached as ``.npy`` files (the
+    stand-in for the reference's MNIST download into ``data_dir``), so every
+    later Tune trial / training worker loads 47 MB in tens of milliseconds
+    instead of regenerating it (~2.5 s single-threaded, which dominated the
+    start-up of short trials).  ``RLA_DATA_CACHE=0`` disables the disk cache."""
+    key = (n, seed, float(noise), jitter)
+    if key in _memo:
+        x, y = _memo[key]
+        return x.clone(), y.clone()
+    use_disk = os.environ.get("RLA_DATA_CACHE", "") != "0"
+    stem = os.path.join(_cache_dir(), f"v{_CACHE_VERSION}_n{n}_s{seed}_z{noise:g}_j{jitter}")
+    if use_disk:
+        try:
+            x = torch.from_numpy(np.load(stem + "_x.npy"))
+            y = torch.from_numpy(np.load(stem + "_y.npy"))
+            if x.shape == (n, IMG * IMG) and y.shape == (n,):
+                _memo[key] = (x, y)
+                return x.clone(), y.clone()
+        except (OSError, ValueError):
+            pass
+    x, y = _generate(n, seed, noise, jitter)
+    _memo[key] = (x, y)
+    if use_disk:
+        try:  # atomic publish: concurrent trials may race to write the same arrays
+            os.makedirs(_cache_dir(), exist_ok=True)
+            for suffix, arr in (("_x.npy", x), ("_y.npy", y)):
+                tmp = f"{stem}{suffix}.{os.getpid()}.tmp"
+                with open(tmp, "wb") as f:
+                    np.save(f, arr.numpy())
+                os.replace(tmp, stem + suffix)
+        except OSError:
+            pass
+    return x.clone(), y.clone()
+
+
+def _generate(n: int, seed: int, noise: float, jitter: int) -> Tuple[torch.Tensor, torch.Tensor]:
     g = torch.Generator().manual_seed(seed)
     protos = _prototypes(0)  # class definitions are shared by every split
     labels = torch.randint(0, 10, (n,), generator=g)

@@ -369,14 +369,19 @@ class ActorClass:
         handle = ActorHandle(None, addr_fut, meta)
 
         def create_actor():
+            from ..utils.timeline import mark
+
             try:
+                mark("actor_create", cls=self._cls.__name__)
                 reply = rt.head_call_new_conn(create)
                 if not reply.get("ok"):
                     raise RuntimeError(f"actor creation failed: {reply.get('error')}\n{reply.get('log', '')}")
+                mark("actor_registered", cls=self._cls.__name__, actor_pid=reply.get("pid"))
                 conn = rt.conn_for(reply["address"])
                 init = conn.submit({"kind": "init", "cls": cls_payload, "payload": init_payload,
                                     "max_concurrency": opts.get("max_concurrency", 1)})
                 init.result()  # constructor errors surface on every later call
+                mark("actor_ready", cls=self._cls.__name__)
                 addr_fut.set_result(reply)
             except BaseException as e:  # noqa: BLE001
                 addr_fut.set_exception(e)

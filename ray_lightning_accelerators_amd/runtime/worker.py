@@ -104,6 +104,14 @@ def _wait_for_assignment() -> None:
     import torch  # noqa: F401 - the import is the point: it is what a pooled worker saves
     import torch.distributed  # noqa: F401
 
+    # the first optimizer construction imports torch._dynamo (~1 s); the framework's
+    # pure-Python layers are what every training worker unpickles next (no GPU call)
+    torch.optim.Adam([torch.nn.Parameter(torch.zeros(1))])
+    import ray_lightning_accelerators_amd.accelerators.ray_ddp  # noqa: F401
+    import ray_lightning_accelerators_amd.lightning  # noqa: F401
+    import ray_lightning_accelerators_amd.models.datamodules  # noqa: F401
+    import ray_lightning_accelerators_amd.tune  # noqa: F401
+
     head = P.connect(os.environ[P.ENV_HEAD], bytes.fromhex(os.environ[P.ENV_AUTH]))
     head.send({"op": "pool_ready", "pid": os.getpid()})
     try:

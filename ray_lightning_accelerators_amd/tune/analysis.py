@@ -8,7 +8,6 @@ import math
 import os
 from typing import Any, Dict, List, Optional
 
-import pandas as pd
 
 
 class Trial:
@@ -162,18 +161,20 @@ class ExperimentAnalysis:
         return {t.trial_id: t.last_result for t in self.trials}
 
     @property
-    def results_df(self) -> pd.DataFrame:
+    def results_df(self) -> "pd.DataFrame":
         rows = []
         for t in self.trials:
             if t.last_result is None:
                 continue
             rows.append(_flatten(t.last_result, "") | {})
+        import pandas as pd  # lazy: 0.6 s of import that trial / training workers never need
+
         df = pd.DataFrame([_flatten_config(r) for r in rows])
         if "trial_id" in df.columns:
             df = df.set_index("trial_id", drop=False)
         return df
 
-    def dataframe(self, metric: Optional[str] = None, mode: Optional[str] = None) -> pd.DataFrame:
+    def dataframe(self, metric: Optional[str] = None, mode: Optional[str] = None) -> "pd.DataFrame":
         rows = []
         for t in self.trials:
             if not t.results:
@@ -186,9 +187,13 @@ class ExperimentAnalysis:
             row = _flatten_config(_flatten(r))
             row["logdir"] = t.logdir
             rows.append(row)
+        import pandas as pd
+
         return pd.DataFrame(rows)
 
-    def trial_dataframes(self) -> Dict[str, pd.DataFrame]:
+    def trial_dataframes(self) -> Dict[str, "pd.DataFrame"]:
+        import pandas as pd
+
         return {t.logdir: pd.DataFrame([_flatten_config(_flatten(r)) for r in t.results]) for t in self.trials}
 
     def stats(self) -> Dict[str, Any]:

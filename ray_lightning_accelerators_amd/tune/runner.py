@@ -37,11 +37,15 @@ class _TrialActor:
         if log_to_file:
             sys.stdout = open(os.path.join(trial_dir, "stdout"), "a", buffering=1)
             sys.stderr = open(os.path.join(trial_dir, "stderr"), "a", buffering=1)
+        from ..utils.timeline import mark
+
+        mark("trial_start", trial=trial_id)
         tsession.init_trial_session(trial_id, trial_dir, config, report_queue, experiment_id)
         try:
             fn(config)
         finally:
             tsession.shutdown_trial_session()
+            mark("trial_end", trial=trial_id)
         return {"ok": True}
 
 
