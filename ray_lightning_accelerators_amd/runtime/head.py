@@ -8,7 +8,8 @@ Responsibilities (reference call sites in SURVEY.md §2.2 U17):
     ray_ddp.py:94-96) and ``RLA_NODE_IP`` set to the node's address;
   * the actor table (ALIVE / DEAD) behind ``runtime.actors()``;
   * killing actors and noticing workers that die (fail-fast, SURVEY.md §5.3);
-  * a pool of PRE-STARTED worker processes (``RLA_WORKER_POOL``, default 4):
+  * a pool of PRE-STARTED worker processes (``RLA_WORKER_POOL``, default half
+    the CPUs, 2..8):
     interpreters that already imported torch but never touched a GPU wait for
     an actor assignment (env incl. HIP_VISIBLE_DEVICES, cwd, log file), so an
     actor starts in milliseconds instead of paying interpreter + torch import
@@ -87,7 +88,11 @@ class Head:
         self.listener, self.address = P.make_listener(session_dir, authkey, "head")
         self.stopping = False
         # pre-started workers: pid -> Popen while starting, then (Popen, conn) when ready
-        self.pool_target = max(0, int(os.environ.get("RLA_WORKER_POOL", "4")))
+        # default: half the cluster's CPUs, 2..8 (a Tune trial consumes ~3 processes:
+        # trial, training worker(s), report queue)
+        cpus = int(sum(n.total.get("CPU", 0) for n in nodes))
+        default_pool = min(8, max(2, cpus // 2))
+        self.pool_target = max(0, int(os.environ.get("RLA_WORKER_POOL", str(default_pool))))
         self.pool_starting: Dict[int, subprocess.Popen] = {}
         self.pool_ready: List = []
         self.pool_lock = threading.Lock()

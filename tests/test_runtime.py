@@ -212,7 +212,7 @@ def test_prestarted_worker_pool_assigns_actor_env():
     ray.init(num_cpus=4, num_gpus=0, _nodes=[{"ip": "127.0.0.1", "num_cpus": 4, "num_gpus": 2,
                                                "gpu_ids": ["0", "1"]}])
     try:
-        time.sleep(8.0)  # the head pre-starts RLA_WORKER_POOL (default 4) workers at init
+        time.sleep(8.0)  # the head pre-starts RLA_WORKER_POOL (default: 2 for 4 CPUs) workers at init
         t0 = time.perf_counter()
         a = _Probe.options(num_cpus=2, num_gpus=1).remote()
         b = _Probe.options(num_cpus=1, num_gpus=1).remote()
