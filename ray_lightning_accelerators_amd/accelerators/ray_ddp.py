@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import os
 import socket
+import sys
 from collections import defaultdict
 from typing import Callable, List, Optional
 
@@ -47,6 +48,12 @@ class RayExecutor:
         os.environ[key] = value
 
     def set_env_vars(self, env: dict) -> None:
+        vis = [k for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES")
+               if k in env and str(env[k]) != os.environ.get(k)]
+        if vis and "torch" in sys.modules and sys.modules["torch"].cuda.is_initialized():
+            # the HIP runtime read the device list at initialisation: a late change
+            # would be silently ignored and ranks would land on the wrong GPU
+            raise RuntimeError(f"{vis} changed after this worker initialised HIP")
         os.environ.update({k: str(v) for k, v in env.items()})
 
     def get_node_ip(self) -> str:

@@ -82,7 +82,14 @@ struct Cfg3 {
   static constexpr size_t oY = odZT + (size_t)16 * TS * 2;
   static constexpr size_t oMisc = oY + (size_t)BC * 4;
   static constexpr size_t oBias = oMisc + 64;
-  static constexpr size_t total = oBias + (((size_t)(L1 + L2 + 16) * 4 + 15) / 16) * 16;
+  // K-split partial sums (fp32), reduced in fixed group order: layer 3 [KG3][BC][16],
+  // dH1 [KG1][BC][L1]
+  static constexpr int KS3 = L2 / 32, KG3 = KS3 < 4 ? KS3 : 4;
+  static constexpr int KSH = L2 / 32, KG1A = 8 / TN1, KG1 = KSH < KG1A ? KSH : KG1A;
+  static constexpr size_t oPart = oBias + (((size_t)(L1 + L2 + 16) * 4 + 15) / 16) * 16;
+  static constexpr size_t szPart3 = KG3 > 1 ? (size_t)KG3 * BC * 16 * 4 : 0;
+  static constexpr size_t szPart1 = KG1 > 1 ? (size_t)KG1 * BC * L1 * 4 : 0;
+  static constexpr size_t total = oPart + (szPart3 > szPart1 ? szPart3 : szPart1);
 };
 
 template <int BC, int L1, int L2>
@@ -181,9 +188,18 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
     for (int i = tid; i < BC * L1 / 2; i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
   }
   const float invB = 1.f / (float)a.B;
-  constexpr int KS2 = L1 / 32, KS3 = L2 / 32, KSH = L2 / 32;
-  constexpr int P3 = KS3 < 4 ? KS3 : 4;
-  constexpr int PH = KSH < 4 ? KSH : 4;
+  constexpr int KS2 = L1 / 32, KS3 = C::KS3, KSH = C::KSH;
+  constexpr int MT = C::MT;
+  // Wave work maps (8 waves).  Layer 2 / dH2: wave w owns output column tiles
+  // nt = w + 8j (j < NTW2) for BOTH row tiles, so each weight fragment feeds MT
+  // MFMAs.  Layer 3: (row tile, K group) per wave, KG3 groups of KPG3 k-steps.
+  // dH1: (column tile, K group) per wave, KG1 groups of KPG1 k-steps.  K-split
+  // partials are summed in fixed group order through LDS -> deterministic.
+  constexpr int NTW2 = (C::TN2 + kWaves - 1) / kWaves;
+  constexpr int KG3 = C::KG3, KPG3 = KS3 / KG3;
+  constexpr int KG1 = C::KG1, KPG1 = KSH / KG1;
+  static_assert(MT * KG3 <= kWaves && C::TN1 * KG1 <= kWaves, "wave maps");
+  float* sPart = (float*)(smem + C::oPart);
 
   // LDS [rows][TS] -> act rows [dst_row][Bp] at columns [row0, row0 + BC) (< Bp)
   auto copy_rows = [&](const __bf16* src, int nrows, int dst_row, int row0) {
@@ -198,30 +214,31 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
   {
     const int row0 = c * BC;
 
-    // ---- batch-independent weight fragments, issued first ----
-    bf16x8 w2f[KS2];
-    {
-      const int nt = w / C::MT;
+    // ---- every weight fragment this wave needs, issued before anything waits ----
+    // (one L2 round trip in total instead of one per tile / k-step)
+    bf16x8 w2f[NTW2][KS2];
+    bf16x8 w3tf[NTW2];
+#pragma unroll
+    for (int j = 0; j < NTW2; ++j) {
+      const int nt = w + kWaves * j;
+      const bool ok = nt < C::TN2;
 #pragma unroll
       for (int ks = 0; ks < KS2; ++ks)
-        w2f[ks] = (w < C::MT * C::TN2) ? ld8(SH + O::W2 + (int64_t)(nt * 16 + r16) * L1 + ks * 32 + 8 * g) : zero8();
+        w2f[j][ks] = ok ? ld8(SH + O::W2 + (int64_t)(nt * 16 + r16) * L1 + ks * 32 + 8 * g) : zero8();
+      w3tf[j] = (ok && g < 2) ? ld8(SH + O::W3T + (int64_t)(nt * 16 + r16) * 16 + 8 * g) : zero8();
     }
-    bf16x8 w3f[P3];
+    const int mt3 = w % MT, kg3 = w / MT;
+    bf16x8 w3f[KPG3];
 #pragma unroll
-    for (int ks = 0; ks < P3; ++ks)
-      w3f[ks] = (w < C::MT && r16 < kNC) ? ld8(SH + O::W3 + (int64_t)r16 * L2 + ks * 32 + 8 * g) : zero8();
-    bf16x8 w3tf;
-    {
-      const int nt = w / C::MT;
-      w3tf = (w < C::MT * C::TN2 && g < 2) ? ld8(SH + O::W3T + (int64_t)(nt * 16 + r16) * 16 + 8 * g) : zero8();
-    }
-    bf16x8 w2tf[PH];
-    {
-      const int ct = w / C::MT;
+    for (int i = 0; i < KPG3; ++i)
+      w3f[i] = (kg3 < KG3 && r16 < kNC) ? ld8(SH + O::W3 + (int64_t)r16 * L2 + (kg3 * KPG3 + i) * 32 + 8 * g)
+                                        : zero8();
+    const int ct1 = w % C::TN1, kg1 = w / C::TN1;
+    bf16x8 w2tf[KPG1];
 #pragma unroll
-      for (int ks = 0; ks < PH; ++ks)
-        w2tf[ks] = (w < C::MT * C::TN1) ? ld8(SH + O::W2T + (int64_t)(ct * 16 + r16) * L2 + ks * 32 + 8 * g) : zero8();
-    }
+    for (int i = 0; i < KPG1; ++i)
+      w2tf[i] = (kg1 < KG1) ? ld8(SH + O::W2T + (int64_t)(ct1 * 16 + r16) * L2 + (kg1 * KPG1 + i) * 32 + 8 * g)
+                            : zero8();
     // Labels and H1pre of BOTH ring slots are loaded before the barrier and
     // selected after it: none of these loads waits for the counters read.
     constexpr int NQ = (BC * L1 / 4 + kThreads - 1) / kThreads;
@@ -273,47 +290,59 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
     if (a.stamps && tid == 0 && c == 0) a.stamps[1] = __builtin_amdgcn_s_memrealtime();
     copy_rows(sH1T, L1, A::H1T, row0);
 
-    // ---------------- layer 2 ----------------
-    for (int tile = w; tile < C::MT * C::TN2; tile += kWaves) {
-      const int mt = tile % C::MT, nt = tile / C::MT;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    // ---------------- layer 2: H2 = relu(H1 W2^T + b2) ----------------
 #pragma unroll
-      for (int ks = 0; ks < KS2; ++ks) {
-        const bf16x8 bfrag = (tile == w) ? w2f[ks] : ld8(SH + O::W2 + (int64_t)(nt * 16 + r16) * L1 + ks * 32 + 8 * g);
-        acc = mfma16(ld8(sH1 + (mt * 16 + r16) * C::H1S + ks * 32 + 8 * g), bfrag, acc);
-      }
+    for (int j = 0; j < NTW2; ++j) {
+      const int nt = w + kWaves * j;
+      if (nt >= C::TN2) continue;
       const int n = nt * 16 + r16;
       const float bias = sBias[L1 + n];
-      bf16x4 t4;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const __bf16 h = relu_bf(acc[i] + bias);
-        sH2[(mt * 16 + 4 * g + i) * C::H2S + n] = h;
-        t4[i] = h;
+      for (int mt = 0; mt < MT; ++mt) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS2; ++ks)
+          acc = mfma16(ld8(sH1 + (mt * 16 + r16) * C::H1S + ks * 32 + 8 * g), w2f[j][ks], acc);
+        bf16x4 t4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const __bf16 h = relu_bf(acc[i] + bias);
+          sH2[(mt * 16 + 4 * g + i) * C::H2S + n] = h;
+          t4[i] = h;
+        }
+        if (row0 + mt * 16 < Bp)
+          *reinterpret_cast<bf16x4*>(ACT + (int64_t)(A::H2T + n) * Bp + row0 + mt * 16 + 4 * g) = t4;
       }
-      if (row0 + mt * 16 < Bp)
-        *reinterpret_cast<bf16x4*>(ACT + (int64_t)(A::H2T + n) * Bp + row0 + mt * 16 + 4 * g) = t4;
     }
     __syncthreads();
 
-    // ---------------- layer 3 (logits) ----------------
-    if (w < C::MT) {
-      const int mt = w;
+    // ---------------- layer 3 (logits), K split over waves ----------------
+    if (kg3 < KG3) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < KS3; ++ks) {
-        bf16x8 bfrag;
-        if (ks < P3) bfrag = w3f[ks < P3 ? ks : 0];
-        else bfrag = (r16 < kNC) ? ld8(SH + O::W3 + (int64_t)r16 * L2 + ks * 32 + 8 * g) : zero8();
-        acc = mfma16(ld8(sH2 + (mt * 16 + r16) * C::H2S + ks * 32 + 8 * g), bfrag, acc);
-      }
+      for (int i = 0; i < KPG3; ++i)
+        acc = mfma16(ld8(sH2 + (mt3 * 16 + r16) * C::H2S + (kg3 * KPG3 + i) * 32 + 8 * g), w3f[i], acc);
       if (r16 < kNC) {
-        const float bias = sBias[L1 + L2 + r16];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) sZ[(mt * 16 + 4 * g + i) * 16 + r16] = acc[i] + bias;
+        for (int i = 0; i < 4; ++i) {
+          const int e = (mt3 * 16 + 4 * g + i) * 16 + r16;
+          if constexpr (KG3 == 1) sZ[e] = acc[i] + sBias[L1 + L2 + r16];
+          else sPart[kg3 * BC * 16 + e] = acc[i];
+        }
       }
     }
     __syncthreads();
+    if constexpr (KG3 > 1) {
+      for (int e = tid; e < BC * 16; e += kThreads) {
+        const int j = e & 15;
+        if (j >= kNC) continue;
+        float z = 0.f;
+#pragma unroll
+        for (int k = 0; k < KG3; ++k) z += sPart[k * BC * 16 + e];
+        sZ[e] = z + sBias[L1 + L2 + j];
+      }
+      __syncthreads();
+    }
     if (a.stamps && tid == 0 && c == 0) a.stamps[2] = __builtin_amdgcn_s_memrealtime();
 
     // ---------------- log_softmax / NLL / accuracy / dZ (one row per lane) -------------
@@ -370,42 +399,70 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
     __syncthreads();
     copy_rows(sdZT, 16, A::DZT, row0);
 
-    // ---------------- dH2 = (dZ W3) * (H2 > 0) ----------------
-    for (int tile = w; tile < C::MT * C::TN2; tile += kWaves) {
-      const int mt = tile % C::MT, nt = tile / C::MT, n = nt * 16 + r16;
-      const bf16x8 bfrag = (tile == w) ? w3tf : ((g < 2) ? ld8(SH + O::W3T + (int64_t)n * 16 + 8 * g) : zero8());
-      const f32x4 acc = mfma16(ld8(sdZ + (mt * 16 + r16) * kDZS + 8 * g), bfrag, f32x4{0.f, 0.f, 0.f, 0.f});
-      bf16x4 t4;
+    // ---------------- dH2 = (dZ W3) * (H2 > 0), in place over H2 ----------------
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        __bf16* hp = sH2 + (mt * 16 + 4 * g + i) * C::H2S + n;
-        const __bf16 d = ((float)(*hp) > 0.f) ? (__bf16)acc[i] : (__bf16)0.f;
-        *hp = d;
-        t4[i] = d;
+    for (int j = 0; j < NTW2; ++j) {
+      const int nt = w + kWaves * j;
+      if (nt >= C::TN2) continue;
+      const int n = nt * 16 + r16;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const f32x4 acc = mfma16(ld8(sdZ + (mt * 16 + r16) * kDZS + 8 * g), w3tf[j], f32x4{0.f, 0.f, 0.f, 0.f});
+        bf16x4 t4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          __bf16* hp = sH2 + (mt * 16 + 4 * g + i) * C::H2S + n;
+          const __bf16 d = ((float)(*hp) > 0.f) ? (__bf16)acc[i] : (__bf16)0.f;
+          *hp = d;
+          t4[i] = d;
+        }
+        if (row0 + mt * 16 < Bp)
+          *reinterpret_cast<bf16x4*>(ACT + (int64_t)(A::DH2T + n) * Bp + row0 + mt * 16 + 4 * g) = t4;
       }
-      if (row0 + mt * 16 < Bp)
-        *reinterpret_cast<bf16x4*>(ACT + (int64_t)(A::DH2T + n) * Bp + row0 + mt * 16 + 4 * g) = t4;
     }
     __syncthreads();
 
-    // ---------------- dH1 = (dH2 W2) * (H1 > 0) -> dh1t ----------------
-    for (int tile = w; tile < C::MT * C::TN1; tile += kWaves) {
-      const int mt = tile % C::MT, ct = tile / C::MT, m = ct * 16 + r16;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    // ---------------- dH1 = (dH2 W2) * (H1 > 0) -> dh1t, K split over waves ----------------
+    if (kg1 < KG1) {
+      const int m = ct1 * 16 + r16;
 #pragma unroll
-      for (int ks = 0; ks < KSH; ++ks) {
-        bf16x8 bfrag;
-        if (tile == w && ks < PH) bfrag = w2tf[ks < PH ? ks : 0];
-        else bfrag = ld8(SH + O::W2T + (int64_t)m * L2 + ks * 32 + 8 * g);
-        acc = mfma16(ld8(sH2 + (mt * 16 + r16) * C::H2S + ks * 32 + 8 * g), bfrag, acc);
-      }
-      bf16x4 t4;
+      for (int mt = 0; mt < MT; ++mt) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const __bf16 hv = sH1[(mt * 16 + 4 * g + i) * C::H1S + m];
-        t4[i] = ((float)hv > 0.f) ? (__bf16)acc[i] : (__bf16)0.f;
+        for (int i = 0; i < KPG1; ++i)
+          acc = mfma16(ld8(sH2 + (mt * 16 + r16) * C::H2S + (kg1 * KPG1 + i) * 32 + 8 * g), w2tf[i], acc);
+        if constexpr (KG1 == 1) {
+          bf16x4 t4;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const __bf16 hv = sH1[(mt * 16 + 4 * g + i) * C::H1S + m];
+            t4[i] = ((float)hv > 0.f) ? (__bf16)acc[i] : (__bf16)0.f;
+          }
+          if (row0 + mt * 16 < Bp)
+            *reinterpret_cast<bf16x4*>(DH1T + (int64_t)m * Bp + row0 + mt * 16 + 4 * g) = t4;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sPart[(kg1 * BC + mt * 16 + 4 * g + i) * L1 + m] = acc[i];
+        }
       }
-      if (row0 + mt * 16 < Bp) *reinterpret_cast<bf16x4*>(DH1T + (int64_t)m * Bp + row0 + mt * 16 + 4 * g) = t4;
+    }
+    if constexpr (KG1 > 1) {
+      __syncthreads();
+      // fixed-order reduction of the K groups; 4 consecutive rows per item (one bf16x4 store)
+      for (int e = tid; e < L1 * (BC / 4); e += kThreads) {
+        const int m = e % L1, q = e / L1;
+        bf16x4 t4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int b = 4 * q + i;
+          float v = 0.f;
+#pragma unroll
+          for (int k = 0; k < KG1; ++k) v += sPart[(k * BC + b) * L1 + m];
+          const __bf16 hv = sH1[b * C::H1S + m];
+          t4[i] = ((float)hv > 0.f) ? (__bf16)v : (__bf16)0.f;
+        }
+        if (row0 + 4 * q < Bp) *reinterpret_cast<bf16x4*>(DH1T + (int64_t)m * Bp + row0 + 4 * q) = t4;
+      }
     }
     __syncthreads();
     if (a.stamps && tid == 0 && c == 0) a.stamps[3] = __builtin_amdgcn_s_memrealtime();

@@ -115,6 +115,53 @@ def test_multi_host_topology():
     assert all(e["HOROVOD_SIZE"] == 4 and e["HOROVOD_LOCAL_SIZE"] == 2 for e in envs)
 
 
+def _hip_state():
+    import os
+
+    import torch as t
+
+    return os.environ.get("HIP_VISIBLE_DEVICES"), t.cuda.is_initialized()
+
+
+def test_gpu_slots_share_host_devices_before_hip_init():
+    """Horovod-on-Ray semantics: every slot of a host sees ALL the host's GPUs and
+    picks its own with hvd.local_rank().  The runtime starts each slot pinned to one
+    device; the executor widens the visibility -- which only works while HIP is
+    still uninitialised in that worker."""
+    ray.init(num_cpus=4, _nodes=[{"ip": "127.0.0.1", "num_cpus": 4, "num_gpus": 2, "gpu_ids": ["0", "1"]}])
+    try:
+        ex = HorovodRayExecutor(num_hosts=1, num_slots=2, use_gpu=True)
+        ex.start()
+        states = ex.execute(lambda *_: _hip_state())
+        envs = ex.envs
+        ex.shutdown()
+    finally:
+        ray.shutdown()
+    assert [s[0] for s in states] == ["0,1", "0,1"]
+    assert not any(s[1] for s in states), states
+    assert [e["HOROVOD_LOCAL_RANK"] for e in envs] == [0, 1]
+
+
+def test_visibility_change_after_hip_init_is_refused():
+    """A visibility change in a worker that already initialised HIP is refused loudly."""
+    from ray_lightning_accelerators_amd.accelerators.ray_ddp import RayExecutor
+
+    ex = RayExecutor._cls() if hasattr(RayExecutor, "_cls") else None
+    if ex is None:
+        pytest.skip("executor class not reachable")
+    import sys
+    import types
+
+    fake_torch = types.SimpleNamespace(cuda=types.SimpleNamespace(is_initialized=lambda: True))
+    real = sys.modules.get("torch")
+    sys.modules["torch"] = fake_torch
+    try:
+        with pytest.raises(RuntimeError, match="initialised HIP"):
+            ex.set_env_vars({"HIP_VISIBLE_DEVICES": "7"})
+    finally:
+        sys.modules["torch"] = real
+
+
 # ------------------------------------------------------------------ GPU (reference test_horovod.py:85-140)
 @pytest.fixture
 def ray_start_gpus():
