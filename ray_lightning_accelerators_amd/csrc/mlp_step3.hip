@@ -84,8 +84,10 @@ struct Cfg3 {
   static constexpr size_t oBias = oMisc + 64;
   // K-split partial sums (fp32), reduced in fixed group order: layer 3 [KG3][BC][16],
   // dH1 [KG1][BC][L1]
-  static constexpr int KS3 = L2 / 32, KG3 = KS3 < 4 ? KS3 : 4;
-  static constexpr int KSH = L2 / 32, KG1A = 8 / TN1, KG1 = KSH < KG1A ? KSH : KG1A;
+  // K splits only where a wave would chain >= 4 k-steps (L2 >= 128); below that
+  // the unsplit maps below were measured faster (profiles/r2_c11)
+  static constexpr int KS3 = L2 / 32, KG3 = KS3 >= 4 ? 4 : 1;
+  static constexpr int KSH = L2 / 32, KG1A = 8 / TN1, KG1 = KSH < 4 ? 1 : (KSH < KG1A ? KSH : KG1A);
   static constexpr size_t oPart = oBias + (((size_t)(L1 + L2 + 16) * 4 + 15) / 16) * 16;
   static constexpr size_t szPart3 = KG3 > 1 ? (size_t)KG3 * BC * 16 * 4 : 0;
   static constexpr size_t szPart1 = KG1 > 1 ? (size_t)KG1 * BC * L1 * 4 : 0;
@@ -134,7 +136,11 @@ __device__ __forceinline__ void gather_tile(const MLP3Args& a, int kt, int64_t o
 // Head kernel (blocks [0, nchunks): one 8-wave workgroup per BC batch rows;
 // blocks [nchunks, nchunks + 49): next-batch gather)
 // ---------------------------------------------------------------------------
-template <int BC, int L1, int L2>
+// MULTI = false (B <= 32): ONE row block, its index and the block-role branch
+// compile-time constants -- the runtime form (row block = blockIdx.x, branch on
+// a kernarg-derived chunk count) measured 0.7 us slower per step at the
+// default 32-64 / batch-32 config (profiles/r2_c11, A/B on one box).
+template <int BC, int L1, int L2, bool MULTI>
 __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
   using C = Cfg3<BC, L1, L2>;
   using O = Off<L1, L2>;
@@ -154,14 +160,14 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
   const __bf16* SH = reinterpret_cast<const __bf16*>(a.shadow);
   const float* P = a.params;
 
-  const int nchunks = (a.B + BC - 1) / BC;
+  const int nchunks = MULTI ? (a.B + BC - 1) / BC : 1;
   if ((int)blockIdx.x >= nchunks) {  // the NEXT batch's tiles, for this step's tail (xring / yring slot ^ 1)
     int64_t nc = a.counters[1] + 1, nob = a.counters[4];
     if (nc >= a.n_batches) { nc = 0; nob ^= 1; }
     gather_tile(a, (int)blockIdx.x - nchunks, nob, nc, a.counters[3] ^ 1, kThreads);
     return;
   }
-  const int c = blockIdx.x;  // this workgroup's batch rows [c * BC, c * BC + BC)
+  const int c = MULTI ? (int)blockIdx.x : 0;  // this workgroup's batch rows [c * BC, c * BC + BC)
 
   // device counters: uniform scalar loads, no LDS broadcast round trip
   const int64_t t = a.counters[0] + 1;
@@ -195,7 +201,14 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
   // MFMAs.  Layer 3: (row tile, K group) per wave, KG3 groups of KPG3 k-steps.
   // dH1: (column tile, K group) per wave, KG1 groups of KPG1 k-steps.  K-split
   // partials are summed in fixed group order through LDS -> deterministic.
-  constexpr int NTW2 = (C::TN2 + kWaves - 1) / kWaves;
+  // narrow layer 2 (TN2 * MT <= 8 tiles): one (column, row) tile per wave instead,
+  // so all 8 waves work (measured faster at 32-64 than column-per-wave)
+  constexpr bool ROW2 = C::TN2 * MT <= kWaves;
+  constexpr int NTW2 = ROW2 ? 1 : (C::TN2 + kWaves - 1) / kWaves;
+  constexpr int MTW2 = ROW2 ? 1 : MT;  // row tiles per wave in layer 2 / dH2
+  const int nt_base = ROW2 ? w % C::TN2 : w;
+  const int mt_base = ROW2 ? w / C::TN2 : 0;
+  const bool l2_active = ROW2 ? (w < C::TN2 * MT) : true;
   constexpr int KG3 = C::KG3, KPG3 = KS3 / KG3;
   constexpr int KG1 = C::KG1, KPG1 = KSH / KG1;
   static_assert(MT * KG3 <= kWaves && C::TN1 * KG1 <= kWaves, "wave maps");
@@ -214,31 +227,6 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
   {
     const int row0 = c * BC;
 
-    // ---- every weight fragment this wave needs, issued before anything waits ----
-    // (one L2 round trip in total instead of one per tile / k-step)
-    bf16x8 w2f[NTW2][KS2];
-    bf16x8 w3tf[NTW2];
-#pragma unroll
-    for (int j = 0; j < NTW2; ++j) {
-      const int nt = w + kWaves * j;
-      const bool ok = nt < C::TN2;
-#pragma unroll
-      for (int ks = 0; ks < KS2; ++ks)
-        w2f[j][ks] = ok ? ld8(SH + O::W2 + (int64_t)(nt * 16 + r16) * L1 + ks * 32 + 8 * g) : zero8();
-      w3tf[j] = (ok && g < 2) ? ld8(SH + O::W3T + (int64_t)(nt * 16 + r16) * 16 + 8 * g) : zero8();
-    }
-    const int mt3 = w % MT, kg3 = w / MT;
-    bf16x8 w3f[KPG3];
-#pragma unroll
-    for (int i = 0; i < KPG3; ++i)
-      w3f[i] = (kg3 < KG3 && r16 < kNC) ? ld8(SH + O::W3 + (int64_t)r16 * L2 + (kg3 * KPG3 + i) * 32 + 8 * g)
-                                        : zero8();
-    const int ct1 = w % C::TN1, kg1 = w / C::TN1;
-    bf16x8 w2tf[KPG1];
-#pragma unroll
-    for (int i = 0; i < KPG1; ++i)
-      w2tf[i] = (kg1 < KG1) ? ld8(SH + O::W2T + (int64_t)(ct1 * 16 + r16) * L2 + (kg1 * KPG1 + i) * 32 + 8 * g)
-                            : zero8();
     // Labels and H1pre of BOTH ring slots are loaded before the barrier and
     // selected after it: none of these loads waits for the counters read.
     constexpr int NQ = (BC * L1 / 4 + kThreads - 1) / kThreads;
@@ -263,6 +251,36 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
       const int y0 = ok ? a.yring[row0 + tid] : -1, y1 = ok ? a.yring[Bp + row0 + tid] : -1;
       sY[tid] = slot ? y1 : y0;  // staged by the previous head launch; -1 past B
     }
+    // ---- every weight fragment this wave needs, issued right behind the H1pre /
+    // label loads the first barrier waits for (the in-order vmcnt lets the
+    // fragments stay in flight across it): one L2 round trip in total ----
+    bf16x8 w2f[NTW2][KS2];
+    bf16x8 w3tf[NTW2];
+#pragma unroll
+    for (int j = 0; j < NTW2; ++j) {
+      const int nt = nt_base + kWaves * j;
+      const bool ok = l2_active && nt < C::TN2;
+#pragma unroll
+      for (int ks = 0; ks < KS2; ++ks)
+        w2f[j][ks] = ok ? ld8(SH + O::W2 + (int64_t)(nt * 16 + r16) * L1 + ks * 32 + 8 * g) : zero8();
+      w3tf[j] = (ok && g < 2) ? ld8(SH + O::W3T + (int64_t)(nt * 16 + r16) * 16 + 8 * g) : zero8();
+    }
+    const int mt3 = w % MT, kg3 = w / MT;
+    bf16x8 w3f[KPG3];
+#pragma unroll
+    for (int i = 0; i < KPG3; ++i)
+      w3f[i] = (kg3 < KG3 && r16 < kNC) ? ld8(SH + O::W3 + (int64_t)r16 * L2 + (kg3 * KPG3 + i) * 32 + 8 * g)
+                                        : zero8();
+    // dH1 with a short K (KG1 == 1) and few tiles: one (column, row) tile per wave
+    constexpr bool ROW1 = KG1 == 1 && C::TN1 * MT <= kWaves;
+    constexpr int MTW1 = ROW1 ? 1 : MT;
+    const int ct1 = w % C::TN1, kg1 = ROW1 ? (w < C::TN1 * MT ? 0 : 1) : w / C::TN1;
+    const int mt1_base = ROW1 ? w / C::TN1 : 0;
+    bf16x8 w2tf[KPG1];
+#pragma unroll
+    for (int i = 0; i < KPG1; ++i)
+      w2tf[i] = (kg1 < KG1) ? ld8(SH + O::W2T + (int64_t)(ct1 * 16 + r16) * L2 + (kg1 * KPG1 + i) * 32 + 8 * g)
+                            : zero8();
     __syncthreads();  // sBias ready
 
     // ---- H1 = relu(H1pre + b1); H1pre chunk is contiguous in fragment order ----
@@ -293,12 +311,13 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
     // ---------------- layer 2: H2 = relu(H1 W2^T + b2) ----------------
 #pragma unroll
     for (int j = 0; j < NTW2; ++j) {
-      const int nt = w + kWaves * j;
-      if (nt >= C::TN2) continue;
+      const int nt = nt_base + kWaves * j;
+      if (!l2_active || nt >= C::TN2) continue;
       const int n = nt * 16 + r16;
       const float bias = sBias[L1 + n];
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
+      for (int mi = 0; mi < MTW2; ++mi) {
+        const int mt = mt_base + mi;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < KS2; ++ks)
@@ -402,11 +421,12 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
     // ---------------- dH2 = (dZ W3) * (H2 > 0), in place over H2 ----------------
 #pragma unroll
     for (int j = 0; j < NTW2; ++j) {
-      const int nt = w + kWaves * j;
-      if (nt >= C::TN2) continue;
+      const int nt = nt_base + kWaves * j;
+      if (!l2_active || nt >= C::TN2) continue;
       const int n = nt * 16 + r16;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
+      for (int mi = 0; mi < MTW2; ++mi) {
+        const int mt = mt_base + mi;
         const f32x4 acc = mfma16(ld8(sdZ + (mt * 16 + r16) * kDZS + 8 * g), w3tf[j], f32x4{0.f, 0.f, 0.f, 0.f});
         bf16x4 t4;
 #pragma unroll
@@ -426,7 +446,8 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
     if (kg1 < KG1) {
       const int m = ct1 * 16 + r16;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
+      for (int mi = 0; mi < MTW1; ++mi) {
+        const int mt = mt1_base + mi;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < KPG1; ++i)
@@ -711,6 +732,25 @@ __device__ __forceinline__ void small_adam_flat(const MLP3Args& a, const AdamSca
   }
 }
 
+// Multi-block head (B > 32): its per-block (sum NLL, #correct, #rows), summed in
+// block order into the stats ring.  Run by one lane of the tail's LAST block at
+// the END of its work: placed at the tail's start, this branch cost the default
+// step ~0.7 us (it delayed the issue of every block's initial loads).
+__device__ __forceinline__ void tail_head_stats(const MLP3Args& a, const int64_t* cn) {
+  float l = 0.f, k = 0.f, n = 0.f;
+  for (int cb = 0; cb < (a.B + kHeadRows - 1) / kHeadRows; ++cb) {
+    l += a.head_part[cb * 4 + 0];
+    k += a.head_part[cb * 4 + 1];
+    n += a.head_part[cb * 4 + 2];
+  }
+  const int64_t t = cn[0];
+  float* st = a.stats + (int)((t - 1) % (a.stats_ring > 0 ? a.stats_ring : 1)) * 4;
+  st[0] = l / (float)a.B;
+  st[1] = k;
+  st[2] = n;
+  st[3] = (float)t;
+}
+
 template <int L1, int L2>
 __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, int mode) {
   constexpr int TN1 = L1 / 16;
@@ -729,21 +769,6 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
   // block 0 publishes it as the current state for the next head
   const int64_t* cn = a.counters + kCnt;
   if (blockIdx.x == 0 && tid < kCnt) a.counters[tid] = cn[tid];
-  if (blockIdx.x == 0 && tid == 0 && a.stats && a.B > kHeadRows && do_grad) {
-    // multi-block head: its per-block (sum NLL, #correct, #rows), summed in block order
-    float l = 0.f, k = 0.f, n = 0.f;
-    for (int cb = 0; cb < (a.B + kHeadRows - 1) / kHeadRows; ++cb) {
-      l += a.head_part[cb * 4 + 0];
-      k += a.head_part[cb * 4 + 1];
-      n += a.head_part[cb * 4 + 2];
-    }
-    const int64_t t = cn[0];
-    float* st = a.stats + (int)((t - 1) % (a.stats_ring > 0 ? a.stats_ring : 1)) * 4;
-    st[0] = l / (float)a.B;
-    st[1] = k;
-    st[2] = n;
-    st[3] = (float)t;
-  }
   if (tid == 0 && do_adam) {
     const int64_t t = cn[0];  // already advanced by the head kernel
     adam_scalars(sh_o, t, a.lr_ptr ? a.lr_ptr[0] : a.lr, a.beta1, a.beta2, a.eps, a.weight_decay, a.adamw);
@@ -771,6 +796,7 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
         if (r.valid[i]) r.v[i] = dp_sum1(a, dslot, r.gi[i]) * scale;
     }
     small_finalize<L1, L2>(a, mode != kGrad, r, sh_o);
+    if (blockIdx.x == gridDim.x - 1 && tid == 0 && a.stats && a.B > kHeadRows) tail_head_stats(a, cn);
     return;
   }
   const int kt = blockIdx.x;
@@ -907,7 +933,10 @@ int dispatch3(const MLP3Args& a, int kind, hipStream_t stream) {
     // one workgroup per 32 batch rows (concurrent), then the 49 gather blocks
     const int nchunks = (a.B + kHeadRows - 1) / kHeadRows;
     if (nchunks > 1 && !a.head_part) return -4;
-    hipLaunchKernelGGL((mlp3_head_kernel<kHeadRows, L1, L2>), dim3(nchunks + kTiles), dim3(kThreads), 0, stream, a);
+    if (nchunks > 1)
+      hipLaunchKernelGGL((mlp3_head_kernel<kHeadRows, L1, L2, true>), dim3(nchunks + kTiles), dim3(kThreads), 0, stream, a);
+    else
+      hipLaunchKernelGGL((mlp3_head_kernel<kHeadRows, L1, L2, false>), dim3(1 + kTiles), dim3(kThreads), 0, stream, a);
   }
   int mode = -1, grid = kTiles;
   if (kind == kMLP3Step) { mode = kFused; grid += SmallTasks<L1, L2>::NBLK; }

@@ -7,7 +7,7 @@ import time
 
 import torch
 
-sys.path.insert(0, '.')
+sys.path.insert(0, ".")
 from ray_lightning_accelerators_amd.models.data import synthetic_mnist  # noqa: E402
 from ray_lightning_accelerators_amd.ops import fused_mlp  # noqa: E402
 from ray_lightning_accelerators_amd.parallel.mlp_engine import FusedMLPEngine  # noqa: E402
