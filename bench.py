@@ -59,6 +59,7 @@ if ROOT not in sys.path:
 from ray_lightning_accelerators_amd.lightning.callbacks import Callback  # noqa: E402
 
 METRIC = "samples/sec (whole node) + DDP scaling eff, MNISTClassifier at 1/2/4/8 workers"
+BENCH_SPIN = 1 << 22  # xGMI poll bound in the bench (~seconds)
 RESNET_METRIC = "images/sec (whole node), ResNet-50 synthetic ImageNet 224px"
 # Stock PyTorch-ROCm on one MI355X at the default 784-32-64-10 / batch-32 config
 # (BASELINE.md "Our MI355X measurements"; the reference publishes no numbers).
@@ -191,8 +192,12 @@ def make_native(args, world, rank, dev, x, y, force_split=False):
         comm = None
         if args.comm != "torch" and dev.type == "cuda":
             # one 109-532 KiB bucket per step: the one-shot area covers it, no two-shot region
+            # bench poll bound ~seconds: a step that waits longer for a peer is broken,
+            # and the post-capture check below must see it quickly (Trainer runs keep
+            # the config's minutes-long bound for peers busy writing checkpoints)
             comm = get_native_comm(use_xgmi=args.comm in ("auto", "xgmi"),
-                                   use_rccl=dist.get_backend() == "nccl", twoshot_bytes=0)
+                                   use_rccl=dist.get_backend() == "nccl", twoshot_bytes=0,
+                                   spin_limit=BENCH_SPIN)
         if comm is not None:
             log(rank, comm.describe())
             assert comm.world == world
@@ -492,12 +497,14 @@ def run_rank(args):
     if rn and args.bucket_sweep:
         sweep = [float(v) for v in args.bucket_sweep.split(",") if v]
     run, last_loss, checksum, info = maker(args, world, rank, dev, x, y)
-    run(args.warmup)
     if world > 1 and args.impl == "native" and not rn:
-        # self-check of the fused xGMI exchange before anything is timed
+        # self-check of the xGMI data path before anything is timed: the capture ran
+        # one real step; a few more, then the error word and replica equality
+        run(min(args.warmup, 8))
+        sync(dev)
         if not (comm_healthy(world) and replicas_agree(world, checksum)):
             run, last_loss, checksum, info = degrade_to_split(args, world, rank, dev, x, y)
-            run(args.warmup)
+    run(args.warmup)
     log(rank, f"world={world} route={info.get('route')} device={dev}")
     elapsed = timed(run, args.steps, world, dev)
     curve = None

@@ -31,6 +31,8 @@ from ..config import get_config
 
 _mod = None
 _mod_err: Optional[BaseException] = None
+# poll bound of the start-up validation collectives (~seconds with s_sleep polling)
+VALIDATION_SPIN = 1 << 22
 
 
 def native_comm_module():
@@ -125,13 +127,17 @@ class NativeCommunicator:
                 ok = False
         if not _agree(ok, group):
             return
-        if spin_limit is not None:
-            self._c.set_spin_limit(int(spin_limit))
         if validate:
+            # short bounded polls while validating: every rank launches right after a
+            # barrier, so a broken link shows up in seconds, not after the (minutes-
+            # long) training bound
+            self._c.set_spin_limit(min(int(spin_limit or VALIDATION_SPIN), VALIDATION_SPIN))
             ok = self._validate_xgmi(group)
             if not _agree(ok, group):
                 self._drop_failed_path(0, "xGMI one-shot", group)
                 return
+        if spin_limit is not None:
+            self._c.set_spin_limit(int(spin_limit))
         self.xgmi = True
 
     def _drop_failed_path(self, which: int, name: str, group) -> None:
@@ -195,13 +201,14 @@ class NativeCommunicator:
                 ok = False
         if not _agree(ok, group):
             return
-        if spin_limit is not None:
-            self._c.set_spin_limit(int(spin_limit))
         if validate:
+            self._c.set_spin_limit(min(int(spin_limit or VALIDATION_SPIN), VALIDATION_SPIN))
             ok = self._validate_twoshot(group)
             if not _agree(ok, group):
                 self._drop_failed_path(1, "xGMI two-shot", group)
                 return
+        if spin_limit is not None:
+            self._c.set_spin_limit(int(spin_limit))
         self.twoshot = True
 
     def _validate_twoshot(self, group) -> bool:

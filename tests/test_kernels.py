@@ -242,6 +242,7 @@ def test_mlp_grads_native_vs_fp32(L1, L2, B):
     views_n = fused_mlp.mlp_unpack(grads.cpu(), L1, L2)
     views_r = fused_mlp.mlp_unpack(ref_g, L1, L2)
     errs = {name: _rel(views_n[name], views_r[name]) for name in views_n}
+    print(f"MLP_FP32_ERR {L1} {L2} {B} " + " ".join(f"{k}={v:.4f}" for k, v in errs.items()))
     assert all(e < 0.2 for e in errs.values()), errs  # bf16 compute vs fp32
     idx = kw["order"][:B].cpu()
     x = kw["x_u8"].cpu()[idx].float() / 255.0
