@@ -243,7 +243,14 @@ def test_mlp_grads_native_vs_fp32(L1, L2, B):
     views_r = fused_mlp.mlp_unpack(ref_g, L1, L2)
     errs = {name: _rel(views_n[name], views_r[name]) for name in views_n}
     print(f"MLP_FP32_ERR {L1} {L2} {B} " + " ".join(f"{k}={v:.4f}" for k, v in errs.items()))
-    assert all(e < 0.2 for e in errs.values()), errs  # bf16 compute vs fp32
+    # bf16 operands (X, H1, H2, dZ, dH2, dH1) vs an fp32 pipeline: measured at most 0.10
+    # norm-wise over every SUPPORTED x B case (profiles/r2_c12/mlp_fp32_err.log), so
+    # 0.12 here; plus direction (cosine) -- the tight check follows against the
+    # bf16-rounding emulation below
+    assert all(e < 0.12 for e in errs.values()), errs
+    cos = {n: float(F.cosine_similarity(views_n[n].reshape(1, -1).float(), views_r[n].reshape(1, -1).float()))
+           for n in views_n}
+    assert all(c > 0.99 for c in cos.values()), cos
     idx = kw["order"][:B].cpu()
     x = kw["x_u8"].cpu()[idx].float() / 255.0
     emu = _emulate_bf16_grads(params, x, kw["labels"].cpu()[idx], L1, L2, B)
@@ -270,7 +277,7 @@ def test_mlp_ragged_batch_f32(B):
     fused_mlp.mlp_train_step(params.cpu(), ref_g, stats=ref_stats, **cpu_kw)
     emu = _emulate_bf16_grads(params, kw["x_f32"].cpu(), kw["labels"].cpu(), L1, L2, B)
     assert _rel(grads.cpu(), emu) < 1e-2
-    assert _rel(grads.cpu(), ref_g) < 0.2
+    assert _rel(grads.cpu(), ref_g) < 0.12
     s, rs = stats.cpu()[0], ref_stats[0]
     assert abs(s[0] - rs[0]) < 2e-2 * max(1.0, abs(rs[0]))   # mean loss
     assert abs(s[1] - rs[1]) <= 2                            # correct count
