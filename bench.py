@@ -460,15 +460,17 @@ def make_resnet(args, world, rank, dev, x, y, bucket_mb=None):
 
 # ------------------------------------------------------------ measurement
 def timed(run, steps, world, dev) -> float:
-    """EXACTLY ``steps`` steps between barrier + device sync on both sides; the
-    slowest rank's time."""
+    """EXACTLY ``steps`` steps, bracketed by barrier + device sync on both sides;
+    each rank's clock stops at its own sync (before the closing barrier, whose
+    ~50-100 us collective would otherwise be billed to a 20-step window), and the
+    slowest rank's time is reported."""
     barrier(world)
     sync(dev)
     t0 = time.perf_counter()
     run(steps)
     sync(dev)
-    barrier(world)
     elapsed = time.perf_counter() - t0
+    barrier(world)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64,
                          device=dev if dist.get_backend() == "nccl" else "cpu")

@@ -132,6 +132,13 @@ __device__ __forceinline__ void gather_tile(const MLP3Args& a, int kt, int64_t o
     for (int b = tid; b < Bp; b += nthreads) a.yring[dst_slot * Bp + b] = b < B ? (int)a.labels[idx[b]] : -1;
 }
 
+// Diagnostic stamp (probe builds only pass a.stamps): latest end over many blocks.
+__device__ __forceinline__ void stamp_max(const MLP3Args& a, int k) {
+  if (a.stamps && threadIdx.x == 0)
+    atomicMax(reinterpret_cast<unsigned long long*>(a.stamps + k),
+              (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
 // ---------------------------------------------------------------------------
 // Head kernel (blocks [0, nchunks): one 8-wave workgroup per BC batch rows;
 // blocks [nchunks, nchunks + 49): next-batch gather)
@@ -165,6 +172,7 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
     int64_t nc = a.counters[1] + 1, nob = a.counters[4];
     if (nc >= a.n_batches) { nc = 0; nob ^= 1; }
     gather_tile(a, (int)blockIdx.x - nchunks, nob, nc, a.counters[3] ^ 1, kThreads);
+    stamp_max(a, 5);
     return;
   }
   const int c = MULTI ? (int)blockIdx.x : 0;  // this workgroup's batch rows [c * BC, c * BC + BC)
@@ -769,19 +777,29 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
   // block 0 publishes it as the current state for the next head
   const int64_t* cn = a.counters + kCnt;
   if (blockIdx.x == 0 && tid < kCnt) a.counters[tid] = cn[tid];
-  if (tid == 0 && do_adam) {
-    const int64_t t = cn[0];  // already advanced by the head kernel
-    adam_scalars(sh_o, t, a.lr_ptr ? a.lr_ptr[0] : a.lr, a.beta1, a.beta2, a.eps, a.weight_decay, a.adamw);
-  }
+  // Adam's step scalars need the step counter (a load) and two double-precision
+  // pows: issued here, computed by lane 0 only AFTER its block's own loads are in
+  // flight -- computed first, they delayed wave 0's loads (and the block) by a
+  // full round trip plus the pows.
+  const int64_t t_step = cn[0];  // already advanced by the head kernel
+  const float lr_now = a.lr_ptr ? a.lr_ptr[0] : a.lr;
+  auto scalars = [&]() {
+    if (tid == 0 && do_adam)
+      adam_scalars(sh_o, t_step, lr_now, a.beta1, a.beta2, a.eps, a.weight_decay, a.adamw);
+  };
   if ((int)blockIdx.x >= kTiles) {  // small parameters (block-uniform branch)
-    __syncthreads();
     const int sblk = (int)blockIdx.x - kTiles;
     if (mode == kAdam) {
+      scalars();
+      __syncthreads();
       small_adam_flat<L1, L2>(a, sh_o, sblk, (int)gridDim.x - kTiles);
+      stamp_max(a, 11);
       return;
     }
     SmallRes r;
     small_compute<L1, L2>(a, mode != kGrad, sblk * TN1 + ct, r);
+    scalars();
+    __syncthreads();
     if (mode == kFusedDP) {
       __shared__ uint32_t sh_dgen;
       __shared__ int sh_dfail;
@@ -797,6 +815,7 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
     }
     small_finalize<L1, L2>(a, mode != kGrad, r, sh_o);
     if (blockIdx.x == gridDim.x - 1 && tid == 0 && a.stats && a.B > kHeadRows) tail_head_stats(a, cn);
+    stamp_max(a, 11);
     return;
   }
   const int kt = blockIdx.x;
@@ -855,6 +874,7 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
       *reinterpret_cast<bf16x8*>(xr_next + b * 16 + 8) = hi;
     }
   }
+  scalars();
   __syncthreads();
   if (a.stamps && kt == 0 && tid == 0) a.stamps[9] = __builtin_amdgcn_s_memrealtime();
 
@@ -921,6 +941,7 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
     }
   }
   if (a.stamps && kt == 0 && tid == 0) a.stamps[10] = __builtin_amdgcn_s_memrealtime();
+  stamp_max(a, 11);
 }
 
 template <int L1, int L2>

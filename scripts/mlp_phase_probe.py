@@ -36,9 +36,11 @@ for (L1, L2, B) in shapes:
     eng.capture(8)
     entry["graph8_us_per_step"] = round(wall(eng), 2)
     st = torch.zeros(16, dtype=torch.int64, device=dev)
-    acc = torch.zeros(11, dtype=torch.float64)
-    names = ["start", "h1", "l3", "dH", "end", "-", "-", "-", "tail_start", "tail_loaded", "tail_end"]
+    acc = torch.zeros(12, dtype=torch.float64)
+    names = ["start", "h1", "l3", "dH", "end", "gather_end", "-", "-", "tail_start", "tail_loaded", "tail_end",
+             "tail_all_end"]
     for _ in range(100):
+        st.zero_()
         fused_mlp.mlp3_launch(fused_mlp.MLP3_STEP, stamps=st, stats=eng.stats, **eng._kw3())
         torch.cuda.synchronize()
         s = st[:len(names)].cpu().double()
