@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--epochs", type=int, default=2)
     ap.add_argument("--use-gpu", type=int, default=1)
     ap.add_argument("--gpus", type=int, default=None, help="GPUs the runtime may pack trials onto")
+    ap.add_argument("--share-gpu", type=int, default=0,
+                    help="rehearsal: a virtual N-GPU ledger whose devices all map to GPU 0 (config 4's 4 trials x "
+                         "2 workers on a 1-GPU box; gloo process groups, xGMI protocol over same-device IPC)")
     args = ap.parse_args()
     gpu = bool(args.use_gpu)
     if gpu:
@@ -41,7 +44,14 @@ def main():
     else:
         n_gpus = 0
     os.environ.setdefault("TUNE_RESULTS_DIR", tempfile.mkdtemp())
-    ray.init(num_cpus=max(16, (args.workers + 1) * args.trials), num_gpus=n_gpus)  # the box's 16-CPU share
+    ncpu = max(16, (args.workers + 1) * args.trials)  # the box's 16-CPU share
+    if gpu and args.share_gpu:
+        n_gpus = args.share_gpu
+        os.environ["RLA_PG_BACKEND"] = "gloo"  # RCCL refuses two ranks on one device
+        ray.init(num_cpus=ncpu, _nodes=[{"ip": "127.0.0.1", "num_cpus": ncpu, "num_gpus": n_gpus,
+                                         "gpu_ids": ["0"] * n_gpus, "resources": {}}])
+    else:
+        ray.init(num_cpus=ncpu, num_gpus=n_gpus)
     time.sleep(args.warm)  # a long-lived cluster has its worker pool warm; 0 = cold start counted
     t0 = time.perf_counter()
     try:
@@ -56,7 +66,7 @@ def main():
         "metric": "Tune sweep trials/hour (tune_mnist, RayAccelerator workers)",
         "value": round(args.trials / wall * 3600.0, 1), "unit": "trials/hour", "trials": args.trials,
         "workers_per_trial": args.workers, "gpus": n_gpus, "epochs_per_trial": args.epochs,
-        "wall_s": round(wall, 2), "pool_warm_s": args.warm, "s_per_trial": round(wall / args.trials, 2), "reports_per_trial": iters,
+        "wall_s": round(wall, 2), "pool_warm_s": args.warm, "virtual_gpus_on_one": args.share_gpu, "s_per_trial": round(wall / args.trials, 2), "reports_per_trial": iters,
         "best_config": analysis.best_config, "data": "synthetic"}), flush=True)
 
 
