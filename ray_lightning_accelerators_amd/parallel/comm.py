@@ -21,6 +21,7 @@ Safety rules (a wrong collective can hang 8 GPUs):
 from __future__ import annotations
 
 import importlib
+import logging
 import os
 from typing import Callable, Optional
 
@@ -108,6 +109,9 @@ class NativeCommunicator:
         self._c.set_route_limits(one_max, two_max)
         if watchdog_ms > 0:
             self._c.start_watchdog(watchdog_ms)
+        if self.rank == 0:
+            # the data-plane decision of this job, once
+            logging.getLogger("ray_lightning_accelerators_amd.comm").info("bring-up: %s", self.describe())
 
     # ------------------------------------------------------------- xGMI
     def _setup_xgmi(self, xgmi_bytes, validate, spin_limit, group):
