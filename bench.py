@@ -230,15 +230,20 @@ def make_native(args, world, rank, dev, x, y, force_split=False):
 
         route = f"split-{get_native_comm(create=False).route(eng.comm_buffer)}"  # oneshot / rccl / torch
     graphed = False
-    if args.graph_steps > 0 and dev.type == "cuda" and route not in ("split-c10d-gloo", "split-torch"):
-        graphed = eng.capture(args.graph_steps)
-        if not graphed:
+    gsteps = graph_steps_for(args.graph_steps, args.steps)
+    if gsteps > 0 and dev.type == "cuda" and route not in ("split-c10d-gloo", "split-torch"):
+        graphed = eng.capture(gsteps)
+        if graphed:
+            # one replay before anything is counted: the first launch of an
+            # instantiated graph uploads it (tens of us, once) -- part of capture
+            eng.run(gsteps)
+        else:
             log(rank, "hipGraph capture failed; running eager launches")
 
     def replica_checksum():
         return float(eng.params.double().sum()) + 1e-3 * float(eng.params.double().abs().sum())
 
-    info = {"route": route, "hip_graph_steps": args.graph_steps if graphed else 0}
+    info = {"route": route, "hip_graph_steps": gsteps if graphed else 0}
     return eng.run, (lambda: float(eng.recent_stats(20)[:, 0].mean())), replica_checksum, info
 
 
@@ -262,6 +267,18 @@ def degrade_to_split(args, world, rank, dev, x, y):
         barrier(world)
     log(rank, "fused xGMI data path failed its warm-up check; re-running on the split RCCL path")
     return make_native(args, world, rank, dev, x, y, force_split=True)
+
+
+def graph_steps_for(requested: int, steps: int) -> int:
+    """Steps per captured graph: the largest size <= max(requested, 16) that divides
+    the timed step count, so the timed window is whole replays (a 20-step window
+    with 8-step graphs would end in 4 eager steps)."""
+    if requested <= 0:
+        return 0
+    for g in range(max(requested, 16), 0, -1):
+        if steps % g == 0 and g <= max(requested, 16):
+            return g if g >= min(requested, 4) else requested
+    return requested
 
 
 def replicas_agree(world, checksum) -> bool:
