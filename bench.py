@@ -270,13 +270,15 @@ def degrade_to_split(args, world, rank, dev, x, y):
 
 
 def graph_steps_for(requested: int, steps: int) -> int:
-    """Steps per captured graph: the largest size <= max(requested, 16) that divides
+    """Steps per captured graph: the largest size <= max(requested, 32) that divides
     the timed step count, so the timed window is whole replays (a 20-step window
-    with 8-step graphs would end in 4 eager steps)."""
+    with 8-step graphs would end in 4 eager steps, and every replay's host launch
+    is paid once up front)."""
     if requested <= 0:
         return 0
-    for g in range(max(requested, 16), 0, -1):
-        if steps % g == 0 and g <= max(requested, 16):
+    cap = max(requested, 32)
+    for g in range(cap, 0, -1):
+        if steps % g == 0:
             return g if g >= min(requested, 4) else requested
     return requested
 
