@@ -305,11 +305,24 @@ class FusedMNISTStep:
         """Most steps one :meth:`train_chunk` can report per-step losses for."""
         return int(self.stats.size(0))  # the engine's stats ring has this size
 
-    def train_chunk(self, n_steps: int, graph_steps: int = 8):
+    def _graph_steps(self) -> int:
+        """Steps per captured graph: the Trainer cuts dispatches at multiples of
+        ``log_every_n_steps``, so the largest divisor of it up to 32 (25 for the
+        default 50) makes a typical chunk whole replays (with 8-step graphs a
+        50-step chunk was 6 replays + 2 eager steps)."""
+        every = max(1, int(getattr(self.trainer, "log_every_n_steps", 50) or 50))
+        for g in range(min(32, every), 3, -1):
+            if every % g == 0:
+                return g
+        return 8
+
+    def train_chunk(self, n_steps: int, graph_steps: Optional[int] = None):
         """``n_steps`` consecutive resident-mode steps in one dispatch (hipGraph
         replays of ``graph_steps`` steps each, captured once per epoch); the
         Trainer uses it when nothing observes individual batches.  Returns the
         per-step ``{"loss"}`` outputs (rows of one device gather, no host sync)."""
+        if graph_steps is None:
+            graph_steps = self._graph_steps()
         eng = self.eng
         self._sync_lr()
         g = self.opt.param_groups[0]
