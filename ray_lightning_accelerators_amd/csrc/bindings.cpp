@@ -4,6 +4,7 @@
 // before launching: a hand-written kernel must never see a shape it was not
 // built for (an out-of-bounds access can reset every GPU of the host).
 #include <torch/extension.h>
+#include <cstdlib>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
@@ -249,6 +250,8 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
     a.dp_gen = reinterpret_cast<uint32_t*>(dp_ctx[4]);
     a.dp_err = reinterpret_cast<int*>(dp_ctx[5]);
     for (int r = 0; r < a.dp_world; ++r) a.dp_regions[r] = reinterpret_cast<char*>(dp_ctx[6 + r]);
+    const char* fence = std::getenv("RLA_DP_FENCE");  // "all": every wave fences (previous form)
+    a.dp_lite = (fence && std::string(fence) == "all") ? 0 : 1;
   }
   TORCH_CHECK(rla::launch_mlp3(a, (int)kind, cur_stream(params)) == 0, "fused MLP v3 launch failed");
 }

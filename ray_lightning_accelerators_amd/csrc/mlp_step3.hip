@@ -676,6 +676,42 @@ __device__ __forceinline__ int dp_begin(const MLP3Args& a, uint32_t* sh_gen) {
 }
 
 __device__ __forceinline__ void dp_signal_and_wait(const MLP3Args& a, uint32_t gen, int slot, int* sh_fail) {
+  if (a.dp_lite) {
+    // One wave fences (guide's producer/consumer form, system scope): every wave
+    // drains its pushes, the block barrier orders them before wave 0's release
+    // fence and flag stores; wave 0 polls, ONE acquire, barrier, then everyone
+    // reads.  The all-threads form below paid a system fence per wave, twice.
+    const int tid = threadIdx.x, blk = blockIdx.x;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid < 64) {
+      if (tid == 0) *sh_fail = 0;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (tid < a.dp_world)
+        __hip_atomic_store(dp_flag(a.dp_regions[tid], slot, blk, a.dp_rank), gen, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      if (tid < a.dp_world) {
+        uint32_t* f = dp_flag(a.dp_regions[a.dp_rank], slot, blk, tid);
+        int64_t spins = 0;
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != gen) {
+          if (++spins > a.dp_spin) {
+            *sh_fail = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (tid == 0) {
+      a.dp_gen[blk] = gen;
+      if (*sh_fail) __hip_atomic_store(a.dp_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    return;
+  }
   __threadfence_system();
   __syncthreads();
   const int tid = threadIdx.x, blk = blockIdx.x;

@@ -72,3 +72,16 @@ def test_bench_two_ranks_share_gpu():
 def test_bench_torch_graph_baseline():
     out, _ = _bench("--impl", "torch-graph", "--steps", "200", "--warmup", "20")
     assert out["n_gpus"] == 1 and out["config"]["impl"] == "torch-graph" and out["value"] > 0
+
+
+def test_graph_steps_divide_the_timed_window():
+    import importlib
+    import sys
+
+    sys.path.insert(0, ROOT)
+    bench = importlib.import_module("bench")
+    assert bench.graph_steps_for(8, 20) == 20  # one replay covers the driver's 20-step window
+    assert bench.graph_steps_for(8, 2000) == 25
+    assert 2000 % bench.graph_steps_for(8, 2000) == 0
+    assert bench.graph_steps_for(8, 2003) == 8  # prime window: fall back to the requested size
+    assert bench.graph_steps_for(0, 20) == 0  # eager launches requested
