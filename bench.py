@@ -210,7 +210,7 @@ def make_native(args, world, rank, dev, x, y, force_split=False):
             if args.dp == "fused" and not force_split:
                 from ray_lightning_accelerators_amd.ops.fused_mlp import mlp_param_count
 
-                dp_ctx = comm.dp_context(mlp_param_count(args.layer_1, args.layer_2))
+                dp_ctx = comm.dp_context(2 * mlp_param_count(args.layer_1, args.layer_2))  # granule area
             route = "xgmi-fused" if dp_ctx else "split-native"
         else:
             def allreduce(t):

@@ -250,8 +250,13 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
     a.dp_gen = reinterpret_cast<uint32_t*>(dp_ctx[4]);
     a.dp_err = reinterpret_cast<int*>(dp_ctx[5]);
     for (int r = 0; r < a.dp_world; ++r) a.dp_regions[r] = reinterpret_cast<char*>(dp_ctx[6 + r]);
-    const char* fence = std::getenv("RLA_DP_FENCE");  // "all": every wave fences (previous form)
-    a.dp_lite = (fence && std::string(fence) == "all") ? 0 : 1;
+    // exchange protocol: "granule" (default: tagged 8-byte words, no fences; needs a
+    // receive area of 2 floats per parameter), "wave" (flags, one wave fences),
+    // "all" (flags, every wave fences)
+    const char* proto = std::getenv("RLA_DP_PROTO");
+    const std::string pr = proto ? proto : "granule";
+    a.dp_lite = pr == "all" ? 0 : (pr == "wave" ? 1 : 2);
+    if (a.dp_lite == 2 && a.dp_stride < 2 * np) a.dp_lite = 1;  // area too small for granules
   }
   TORCH_CHECK(rla::launch_mlp3(a, (int)kind, cur_stream(params)) == 0, "fused MLP v3 launch failed");
 }

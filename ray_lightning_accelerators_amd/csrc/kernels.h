@@ -181,7 +181,7 @@ struct MLP3Args {
   int64_t dp_stride;        // floats per (slot, rank) receive area (>= param count)
   int64_t dp_spin;          // poll bound
   int dp_rank, dp_world;
-  int dp_lite;              // 1: one wave fences per block exchange (RLA_DP_FENCE=wave, default)
+  int dp_lite;              // exchange protocol: 2 tagged granules (default), 1 flags + one fencing wave, 0 flags + all waves
 };
 enum MLP3Kind { kMLP3Step = 0, kMLP3Head = 1, kMLP3TailGrad = 2, kMLP3TailAdam = 3, kMLP3Prime = 4,
                 kMLP3StepDP = 5 };

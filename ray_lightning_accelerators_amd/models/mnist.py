@@ -207,7 +207,7 @@ class FusedMNISTStep:
 
             comm = get_native_comm()  # every rank reaches here together (first epoch)
             if comm is not None:
-                dp_ctx = comm.dp_context(self.np)
+                dp_ctx = comm.dp_context(2 * self.np)  # tagged-granule receive area
         eng = FusedMLPEngine(self.L1, self.L2, B, lr=float(g["lr"]), betas=tuple(g["betas"]), eps=g["eps"],
                              weight_decay=g["weight_decay"], device=self.dev, world_size=self.world,
                              rank=self.trainer.global_rank, allreduce=self._allreduce, buffers=bufs,

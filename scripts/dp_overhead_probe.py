@@ -1,6 +1,7 @@
 """Diagnostic: intrinsic cost of the fused data-parallel tail's in-kernel exchange
-protocol on ONE GPU.  A world-1 aux region (push to self, system fences, flag,
-poll, fixed-order sum) is driven by the StepDP kernel and timed against the
+protocol on ONE GPU.  A world-1 aux region (push to self, then tagged-granule polls
+-- or, with RLA_DP_PROTO=wave|all, system fences + flags --
+and a fixed-order sum) is driven by the StepDP kernel and timed against the
 plain fused step, both replayed from hipGraphs -- a lower bound of what the
 exchange adds per step at N > 1 (where the pushes also cross xGMI)."""
 import sys
@@ -18,7 +19,7 @@ dev = torch.device("cuda", 0)
 x, y = synthetic_mnist(55000, seed=0)
 mod = native_comm_module()
 c = mod.Communicator(0, 1, 0)
-c.aux_open([c.aux_handle(fused_mlp.mlp_param_count(32, 64))])
+c.aux_open([c.aux_handle(2 * fused_mlp.mlp_param_count(32, 64))])  # granule area
 ctx = [int(v) for v in c.aux_context()]
 
 

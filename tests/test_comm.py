@@ -345,7 +345,7 @@ def _gpu_worker(rank, world, port, q, mode):
             g = torch.Generator().manual_seed(7)
             xs = torch.randint(0, 256, (2048, 784), dtype=torch.uint8, generator=g)
             ys = torch.randint(0, 10, (2048,), generator=g)
-            ctx = comm.dp_context(27882)
+            ctx = comm.dp_context(2 * 27882)  # tagged-granule receive area
             res["dp_ctx"] = ctx is not None
 
             def make(dp):
@@ -466,7 +466,10 @@ def test_xgmi_dead_peer_times_out_instead_of_hanging():
 
 
 @gpu
-def test_fused_dp_mlp_step_matches_split_allreduce():
+@pytest.mark.parametrize("proto", ["granule", "wave"])
+def test_fused_dp_mlp_step_matches_split_allreduce(proto, monkeypatch):
+    # granule: tagged 8-byte words, no fences (default); wave: flags + one fencing wave
+    monkeypatch.setenv("RLA_DP_PROTO", proto)
     out = _run_gpu("mlp_dp")
     for r, res in out.items():
         assert res["dp_ctx"] and res["dp_mode"], (r, res)
