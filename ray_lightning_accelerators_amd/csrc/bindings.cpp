@@ -173,8 +173,9 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
           Tensor dh1t, Tensor xring, Tensor h1pre, Tensor act, Tensor yring, optional<Tensor> stats,
           bool advance_step, double lr,
           double beta1, double beta2, double eps, double weight_decay, double grad_scale, optional<Tensor> lr_t,
-          bool adamw, optional<Tensor> stamps, std::vector<int64_t> dp_ctx, optional<Tensor> head_part) {
-  TORCH_CHECK(kind >= 0 && kind <= 5, "mlp3: bad kind ", kind);
+          bool adamw, optional<Tensor> stamps, std::vector<int64_t> dp_ctx, optional<Tensor> head_part,
+          optional<Tensor> hand) {
+  TORCH_CHECK(kind >= 0 && kind <= 6, "mlp3: bad kind ", kind);
   TORCH_CHECK(rla::mlp_supported((int)L1, (int)L2), "no fused MLP kernel for layer sizes ", L1, "/", L2);
   TORCH_CHECK(B >= 1 && B <= 256, "fused MLP step supports 1 <= batch <= 256");
   const int64_t np = mlp_param_count(L1, L2);
@@ -229,6 +230,14 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
   a.stats_ring = a.stats ? (int)(stats->numel() / 4) : 0;
   a.head_part = ptr_or_null<float>(head_part, "head_part", at::kFloat, (Bp / 32) * 4);
   TORCH_CHECK(B <= 32 || a.head_part != nullptr, "mlp3: batches above 32 rows need head_part [ceil(B/32), 4]");
+  if (kind == rla::kMLP3Step1) {
+    TORCH_CHECK(B <= 32, "the one-launch step handles batches of up to 32 rows");
+    TORCH_CHECK(counters.numel() >= 16, "the one-launch step needs counters of >= 16 int64 (launch sequence)");
+    a.hand = reinterpret_cast<unsigned long long*>(
+        ptr_or_null<int64_t>(hand, "hand", at::kLong, rla::mlp3_hand_words((int)L1, (int)L2)));
+    TORCH_CHECK(a.hand != nullptr, "the one-launch step needs the hand-off buffer `hand`");
+    a.hand_spin = 1 << 20;
+  }
   a.apply_adam = kind == rla::kMLP3Step;
   a.advance_step = advance_step;
   a.lr = (float)lr; a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.eps = (float)eps;
@@ -470,7 +479,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("adamw"), py::arg("stamps") = py::none());
   m.def("mlp_eval", &mlp_eval, "fused MNIST-MLP forward + NLL/accuracy");
   m.def("mlp3", &mlp3, "fused MNIST-MLP step v3 (pipelined layer 1): kind 0 step, 1 head, 2 tail-grad, "
-        "3 tail-adam, 4 prime");
+        "3 tail-adam, 4 prime, 5 step with the in-kernel xGMI exchange, 6 one-launch step (B <= 32)");
+  m.def("mlp3_hand_words", [](int64_t l1, int64_t l2) { return rla::mlp3_hand_words((int)l1, (int)l2); });
   m.def("mlp_adam", &mlp_adam, "MLP arena Adam + bf16 shadow refresh (update=False: refresh only)");
   m.def("mlp_shadow_size", [](int64_t l1, int64_t l2) { return rla::mlp_shadow_layout((int)l1, (int)l2).total; });
   m.def("mlp_supported", [](int64_t a, int64_t b) { return rla::mlp_supported((int)a, (int)b); });

@@ -151,7 +151,8 @@ struct MLP3Args {
   const int64_t* labels;    // [N_data]
   const int64_t* order;     // [2][order_stride]: two epochs' sample orders
   int64_t order_stride;     // n_batches * B
-  int64_t* counters;        // [10]: (step, next cursor, consumed cursor, ring slot, order buffer) x {current, next}
+  int64_t* counters;        // [10]: (step, next cursor, consumed cursor, ring slot, order buffer) x {current, next};
+                            // [10] launch sequence number of the one-launch step (counters of >= 16)
   int64_t n_batches;
   int B, L1, L2;
   float* params;
@@ -182,9 +183,13 @@ struct MLP3Args {
   int64_t dp_spin;          // poll bound
   int dp_rank, dp_world;
   int dp_lite;              // exchange protocol: 2 tagged granules (default), 1 flags + one fencing wave, 0 flags + all waves
+  // one-launch step (kMLP3Step1): in-launch hand-off words (mlp_step3.hip) and their poll bound
+  unsigned long long* hand;
+  int64_t hand_spin;
 };
 enum MLP3Kind { kMLP3Step = 0, kMLP3Head = 1, kMLP3TailGrad = 2, kMLP3TailAdam = 3, kMLP3Prime = 4,
-                kMLP3StepDP = 5 };
+                kMLP3StepDP = 5, kMLP3Step1 = 6 };
+int64_t mlp3_hand_words(int L1, int L2);  // int64 words of the one-launch step's hand-off buffer
 int launch_mlp3(const MLP3Args& a, int kind, hipStream_t stream);
 int mlp3_act_rows(int L1, int L2);
 

@@ -36,15 +36,18 @@ __device__ __forceinline__ void adam_scalars(AdamScal& o, int64_t t, float lr, f
   o.beta1 = b1; o.beta2 = b2; o.eps = eps; o.wd = wd; o.adamw = adamw;
 }
 
+// Explicit FMAs and no compiler contraction: every kernel that inlines this (tail
+// epilogues, the one-launch step's tiles, the arena Adam) computes the same bits.
 __device__ __forceinline__ float adam1(float p, float g, float& m, float& v, const AdamScal& o) {
+#pragma clang fp contract(off)
   if (o.wd != 0.f) {
     if (o.adamw) p = p * (1.f - o.lr * o.wd);
-    else g = g + o.wd * p;
+    else g = fmaf(o.wd, p, g);
   }
-  m = m + (1.f - o.beta1) * (g - m);
-  v = v * o.beta2 + (1.f - o.beta2) * (g * g);
+  m = fmaf(1.f - o.beta1, g - m, m);
+  v = fmaf(1.f - o.beta2, g * g, v * o.beta2);
   const float denom = sqrtf(v) / o.bc2_sqrt + o.eps;
-  return p + (-o.step_size) * (m / denom);
+  return fmaf(-o.step_size, m / denom, p);
 }
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;

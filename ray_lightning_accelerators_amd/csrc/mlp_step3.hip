@@ -140,6 +140,66 @@ __device__ __forceinline__ void stamp_max(const MLP3Args& a, int k) {
 }
 
 // ---------------------------------------------------------------------------
+// In-launch hand-off of the one-launch step (mlp3_one_kernel): bf16 pairs in
+// 8-byte {payload, tag} granules, each written by ONE agent-scope (sc1,
+// write-through) store and read by agent-scope (sc1) loads until the tag is this
+// launch's sequence number -- no flag, no fence (the guide's granule hand-off,
+// ~0.8-1 us against ~1.5 us for a dependent kernel boundary; more importantly the
+// consumers' own loads and gathers overlap the head instead of following it).
+// `hand` (int64 words): [kHandAck] blocks' state-read acknowledgements, [kHandErr]
+// poll-timeout word, [kHandDone] the head's weights-read-done granule, then dH1^T
+// ([L1][32] -> 16 granules a row) and the act rows ([ROWS][32]).
+// ---------------------------------------------------------------------------
+constexpr int kSeq = 10;  // counters[10]: launch sequence number of the one-launch step (granule tag)
+constexpr int kHandAck = 0, kHandErr = 16, kHandDone = 32, kHandDH1 = 48;
+__host__ __device__ constexpr int64_t hand_act_base(int L1) { return kHandDH1 + (int64_t)L1 * 16; }
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void hand_put4(unsigned long long* g, bf16x4 v, uint32_t tag) {
+  const u32x2 u = __builtin_bit_cast(u32x2, v);
+  const unsigned long long hi = (unsigned long long)tag << 32;
+  __hip_atomic_store(g, hi | u[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(g + 1, hi | u[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void hand_put8(unsigned long long* g, bf16x8 v, uint32_t tag) {
+  const u32x4 u = __builtin_bit_cast(u32x4, v);
+  const unsigned long long hi = (unsigned long long)tag << 32;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) __hip_atomic_store(g + i, hi | u[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 8 bf16 (4 granules) once all carry `tag`; *fail on a poll timeout
+__device__ __forceinline__ bf16x8 hand_get8(unsigned long long* g, uint32_t tag, int64_t spin, int* fail) {
+  unsigned long long w[4];
+  int64_t n = 0;
+  while (true) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint32_t)(w[0] >> 32) == tag && (uint32_t)(w[1] >> 32) == tag && (uint32_t)(w[2] >> 32) == tag &&
+        (uint32_t)(w[3] >> 32) == tag)
+      break;
+    if (++n > spin) {
+      *fail = 1;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  const u32x4 u = {(uint32_t)w[0], (uint32_t)w[1], (uint32_t)w[2], (uint32_t)w[3]};
+  return __builtin_bit_cast(bf16x8, u);
+}
+__device__ __forceinline__ void hand_wait(unsigned long long* g, uint32_t tag, int64_t spin, int* fail) {
+  int64_t n = 0;
+  while ((uint32_t)(__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) != tag) {
+    if (++n > spin) {
+      *fail = 1;
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Head kernel (blocks [0, nchunks): one 8-wave workgroup per BC batch rows;
 // blocks [nchunks, nchunks + 49): next-batch gather)
 // ---------------------------------------------------------------------------
@@ -147,12 +207,17 @@ __device__ __forceinline__ void stamp_max(const MLP3Args& a, int k) {
 // compile-time constants -- the runtime form (row block = blockIdx.x, branch on
 // a kernarg-derived chunk count) measured 0.7 us slower per step at the
 // default 32-64 / batch-32 config (profiles/r2_c11, A/B on one box).
-template <int BC, int L1, int L2, bool MULTI>
-__global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
+//
+// GRAN = true: the head of the one-launch step (mlp3_one_kernel, B <= 32): the
+// transposed activations / deltas go to the SAME launch's tile and small blocks
+// as tagged granules (hand_put*), H1pre's other slot is zeroed write-through, and
+// the state advance waits until every other block has read the current state.
+template <int BC, int L1, int L2, bool MULTI, bool GRAN>
+__device__ __forceinline__ void head_body(const MLP3Args& a, char* smem) {
   using C = Cfg3<BC, L1, L2>;
   using O = Off<L1, L2>;
   using A = Act<L1, L2>;
-  __shared__ __attribute__((aligned(16))) char smem[C::total];
+  static_assert(!GRAN || (!MULTI && BC == 32), "one-launch head: one 32-row block");
   __bf16* sH1 = (__bf16*)(smem + C::oH1);
   __bf16* sH1T = (__bf16*)(smem + C::oH1T);
   __bf16* sH2 = (__bf16*)(smem + C::oH2);
@@ -168,13 +233,6 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
   const float* P = a.params;
 
   const int nchunks = MULTI ? (a.B + BC - 1) / BC : 1;
-  if ((int)blockIdx.x >= nchunks) {  // the NEXT batch's tiles, for this step's tail (xring / yring slot ^ 1)
-    int64_t nc = a.counters[1] + 1, nob = a.counters[4];
-    if (nc >= a.n_batches) { nc = 0; nob ^= 1; }
-    gather_tile(a, (int)blockIdx.x - nchunks, nob, nc, a.counters[3] ^ 1, kThreads);
-    stamp_max(a, 5);
-    return;
-  }
   const int c = MULTI ? (int)blockIdx.x : 0;  // this workgroup's batch rows [c * BC, c * BC + BC)
 
   // device counters: uniform scalar loads, no LDS broadcast round trip
@@ -185,6 +243,9 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
   const int Bp = (a.B + 31) / 32 * 32;
   __bf16* ACT = reinterpret_cast<__bf16*>(a.act);
   __bf16* DH1T = reinterpret_cast<__bf16*>(a.dh1t);
+  const uint32_t tag = GRAN ? (uint32_t)(a.counters[kSeq] + 1) : 0u;
+  unsigned long long* HG_DH1 = a.hand + kHandDH1;
+  unsigned long long* HG_ACT = a.hand + hand_act_base(L1);
 
   constexpr int NBIAS = L1 + L2 + kNC;
   if (tid < NBIAS) {
@@ -197,7 +258,14 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
   }
   // the tail of this step accumulates the next step's H1pre into the other slot;
   // in fragment order this block's rows are one contiguous BC * L1 range
-  {
+  if constexpr (GRAN) {
+    // write-through: this launch's tile blocks add into these words (memory-side
+    // atomics) once they hold the dH1 granules, published after every wave's
+    // vmcnt(0) wait below
+    unsigned long long* z = reinterpret_cast<unsigned long long*>(a.h1pre + (slot ^ 1) * (int64_t)Bp * L1);
+    for (int i = tid; i < BC * L1; i += kThreads)
+      __hip_atomic_store(z + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
     uint4* z = reinterpret_cast<uint4*>(a.h1pre + (slot ^ 1) * (int64_t)Bp * L1 + (int64_t)c * BC * L1);
     for (int i = tid; i < BC * L1 / 2; i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
   }
@@ -227,7 +295,8 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
     constexpr int CPR = BC / 8;
     for (int e = tid; e < nrows * CPR; e += kThreads) {
       const int r = e / CPR, col = (e - r * CPR) * 8;
-      if (row0 + col < Bp)
+      if constexpr (GRAN) hand_put8(HG_ACT + (dst_row + r) * 16 + col / 2, ld8(src + r * C::TS + col), tag);
+      else if (row0 + col < Bp)
         *reinterpret_cast<bf16x8*>(ACT + (int64_t)(dst_row + r) * Bp + row0 + col) = ld8(src + r * C::TS + col);
     }
   };
@@ -337,7 +406,8 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
           sH2[(mt * 16 + 4 * g + i) * C::H2S + n] = h;
           t4[i] = h;
         }
-        if (row0 + mt * 16 < Bp)
+        if constexpr (GRAN) hand_put4(HG_ACT + (A::H2T + n) * 16 + (mt * 16 + 4 * g) / 2, t4, tag);
+        else if (row0 + mt * 16 < Bp)
           *reinterpret_cast<bf16x4*>(ACT + (int64_t)(A::H2T + n) * Bp + row0 + mt * 16 + 4 * g) = t4;
       }
     }
@@ -444,11 +514,23 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
           *hp = d;
           t4[i] = d;
         }
-        if (row0 + mt * 16 < Bp)
+        if constexpr (GRAN) hand_put4(HG_ACT + (A::DH2T + n) * 16 + (mt * 16 + 4 * g) / 2, t4, tag);
+        else if (row0 + mt * 16 < Bp)
           *reinterpret_cast<bf16x4*>(ACT + (int64_t)(A::DH2T + n) * Bp + row0 + mt * 16 + 4 * g) = t4;
       }
     }
-    __syncthreads();
+    if constexpr (GRAN) {
+      // every wave's stores (the write-through H1pre zeroing above all) have
+      // completed, and every weight / bias load of this launch has returned: the
+      // `done` granule lets the small blocks overwrite weights and biases
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0)
+        __hip_atomic_store(a.hand + kHandDone, (unsigned long long)tag << 32, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __syncthreads();
+    }
 
     // ---------------- dH1 = (dH2 W2) * (H1 > 0) -> dh1t, K split over waves ----------------
     if (kg1 < KG1) {
@@ -467,7 +549,8 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
             const __bf16 hv = sH1[(mt * 16 + 4 * g + i) * C::H1S + m];
             t4[i] = ((float)hv > 0.f) ? (__bf16)acc[i] : (__bf16)0.f;
           }
-          if (row0 + mt * 16 < Bp)
+          if constexpr (GRAN) hand_put4(HG_DH1 + m * 16 + (mt * 16 + 4 * g) / 2, t4, tag);
+          else if (row0 + mt * 16 < Bp)
             *reinterpret_cast<bf16x4*>(DH1T + (int64_t)m * Bp + row0 + mt * 16 + 4 * g) = t4;
         } else {
 #pragma unroll
@@ -490,7 +573,8 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
           const __bf16 hv = sH1[b * C::H1S + m];
           t4[i] = ((float)hv > 0.f) ? (__bf16)v : (__bf16)0.f;
         }
-        if (row0 + 4 * q < Bp) *reinterpret_cast<bf16x4*>(DH1T + (int64_t)m * Bp + row0 + 4 * q) = t4;
+        if constexpr (GRAN) hand_put4(HG_DH1 + m * 16 + 2 * q, t4, tag);
+        else if (row0 + 4 * q < Bp) *reinterpret_cast<bf16x4*>(DH1T + (int64_t)m * Bp + row0 + 4 * q) = t4;
       }
     }
     __syncthreads();
@@ -504,7 +588,23 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
   }
   if (tid == 0 && c == 0) {
     // the advanced state goes to the NEXT copy: this launch's gather blocks are
-    // still reading the current one (the tail publishes it, see mlp3_tail_kernel)
+    // still reading the current one (the tail publishes it, see mlp3_tail_kernel).
+    // One launch: both copies, once every other block has acknowledged its read
+    // of the current state (its ack add depends on the loaded values).
+    if constexpr (GRAN) {
+      const long long others = (long long)gridDim.x - 1;
+      long long* ack = reinterpret_cast<long long*>(a.hand + kHandAck);
+      int64_t spins = 0;
+      while (__hip_atomic_load(ack, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < others) {
+        if (++spins > a.hand_spin) {
+          __hip_atomic_store(a.hand + kHandErr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      __hip_atomic_fetch_add(ack, -others, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      a.counters[kSeq] = (int64_t)tag;
+    }
     int64_t* cn = a.counters + kCnt;
     cn[0] = a.advance_step ? t : t - 1;
     cn[2] = cursor;
@@ -513,6 +613,8 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
     cn[1] = nc;
     cn[4] = nob;
     cn[3] = slot ^ 1;
+    if constexpr (GRAN)
+      for (int k = 0; k < kCnt; ++k) a.counters[k] = cn[k];
     if (a.stats && nchunks == 1) {
       const int s = (int)((t - 1) % (a.stats_ring > 0 ? a.stats_ring : 1));
       float* st = a.stats + s * 4;
@@ -523,6 +625,20 @@ __global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
     }
     if (a.stamps) a.stamps[4] = __builtin_amdgcn_s_memrealtime();
   }
+}
+
+template <int BC, int L1, int L2, bool MULTI>
+__global__ __launch_bounds__(kThreads) void mlp3_head_kernel(MLP3Args a) {
+  __shared__ __attribute__((aligned(16))) char smem[Cfg3<BC, L1, L2>::total];
+  const int nchunks = MULTI ? (a.B + BC - 1) / BC : 1;
+  if ((int)blockIdx.x >= nchunks) {  // the NEXT batch's tiles, for this step's tail (xring / yring slot ^ 1)
+    int64_t nc = a.counters[1] + 1, nob = a.counters[4];
+    if (nc >= a.n_batches) { nc = 0; nob ^= 1; }
+    gather_tile(a, (int)blockIdx.x - nchunks, nob, nc, a.counters[3] ^ 1, kThreads);
+    stamp_max(a, 5);
+    return;
+  }
+  head_body<BC, L1, L2, MULTI, false>(a, smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -550,14 +666,18 @@ struct SmallRes {
   int rowv, colv;
 };
 
-template <int L1, int L2>
-__device__ __forceinline__ void small_compute(const MLP3Args& a, bool prefetch_adam, int task, SmallRes& r) {
+// GRAN: the operands come from the one-launch head's granules (Bp = 32) instead of act / dh1t
+template <int L1, int L2, bool GRAN = false>
+__device__ __forceinline__ void small_compute(const MLP3Args& a, bool prefetch_adam, int task, SmallRes& r,
+                                              uint32_t tag = 0, int* fail = nullptr) {
   using O = Off<L1, L2>;
   using A = Act<L1, L2>;
   using S = SmallTasks<L1, L2>;
   const int lane = threadIdx.x & 63, r16 = lane & 15, g = lane >> 4;
   const int Bp = (a.B + 31) / 32 * 32;
   const __bf16* ACT = reinterpret_cast<const __bf16*>(a.act);
+  unsigned long long* HG_ACT = a.hand + hand_act_base(L1);
+  int arow_i = 0, brow_i = 0;  // act rows of the two MFMA operands (GRAN)
   r.kind = -1;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -572,8 +692,10 @@ __device__ __forceinline__ void small_compute(const MLP3Args& a, bool prefetch_a
       r.kind = 0;
       r.rowv = nt * 16 + 4 * g;
       r.colv = ct * 16 + r16;
-      arow = ACT + (int64_t)(A::DH2T + nt * 16 + r16) * Bp;
-      brow = ACT + (int64_t)(A::H1T + ct * 16 + r16) * Bp;
+      arow_i = A::DH2T + nt * 16 + r16;
+      brow_i = A::H1T + ct * 16 + r16;
+      arow = ACT + (int64_t)arow_i * Bp;
+      brow = ACT + (int64_t)brow_i * Bp;
 #pragma unroll
       for (int i = 0; i < 4; ++i) { r.gi[i] = O::W2 + (int64_t)(r.rowv + i) * L1 + r.colv; r.valid[i] = true; }
     } else {  // dW3[j][n] = sum_b dZ[b][j] H2[b][n]
@@ -581,8 +703,10 @@ __device__ __forceinline__ void small_compute(const MLP3Args& a, bool prefetch_a
       r.kind = 1;
       r.rowv = 4 * g;
       r.colv = nt * 16 + r16;
-      arow = ACT + (int64_t)(A::DZT + r16) * Bp;
-      brow = ACT + (int64_t)(A::H2T + nt * 16 + r16) * Bp;
+      arow_i = A::DZT + r16;
+      brow_i = A::H2T + nt * 16 + r16;
+      arow = ACT + (int64_t)arow_i * Bp;
+      brow = ACT + (int64_t)brow_i * Bp;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         r.valid[i] = (r.rowv + i) < kNC;
@@ -595,9 +719,14 @@ __device__ __forceinline__ void small_compute(const MLP3Args& a, bool prefetch_a
         r.pv[i] = a.params[r.gi[i]]; r.mv[i] = a.exp_avg[r.gi[i]]; r.vv[i] = a.exp_avg_sq[r.gi[i]];
       }
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int ks = 0; ks < Bp / 32; ++ks) {
-      const int b0 = ks * 32 + 8 * g;
-      acc = mfma16(ld8(arow + b0), ld8(brow + b0), acc);
+    if constexpr (GRAN) {
+      const bf16x8 bv = hand_get8(HG_ACT + brow_i * 16 + 4 * g, tag, a.hand_spin, fail);  // H1^T / H2^T: earlier
+      acc = mfma16(hand_get8(HG_ACT + arow_i * 16 + 4 * g, tag, a.hand_spin, fail), bv, acc);
+    } else {
+      for (int ks = 0; ks < Bp / 32; ++ks) {
+        const int b0 = ks * 32 + 8 * g;
+        acc = mfma16(ld8(arow + b0), ld8(brow + b0), acc);
+      }
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) r.v[i] = acc[i];
@@ -605,13 +734,35 @@ __device__ __forceinline__ void small_compute(const MLP3Args& a, bool prefetch_a
     const int e = (task - S::NTILE) * 64 + lane;
     if (e >= S::NBIAS) return;
     const __bf16* row;
-    if (e < L1) { row = reinterpret_cast<const __bf16*>(a.dh1t) + (int64_t)e * Bp; r.gi[0] = O::B1 + e; }
-    else if (e < L1 + L2) { row = ACT + (int64_t)(A::DH2T + e - L1) * Bp; r.gi[0] = O::B2 + (e - L1); }
-    else { row = ACT + (int64_t)(A::DZT + e - L1 - L2) * Bp; r.gi[0] = O::B3 + (e - L1 - L2); }
+    unsigned long long* rowg;
+    if (e < L1) {
+      row = reinterpret_cast<const __bf16*>(a.dh1t) + (int64_t)e * Bp;
+      rowg = a.hand + kHandDH1 + e * 16;
+      r.gi[0] = O::B1 + e;
+    } else if (e < L1 + L2) {
+      row = ACT + (int64_t)(A::DH2T + e - L1) * Bp;
+      rowg = HG_ACT + (A::DH2T + e - L1) * 16;
+      r.gi[0] = O::B2 + (e - L1);
+    } else {
+      row = ACT + (int64_t)(A::DZT + e - L1 - L2) * Bp;
+      rowg = HG_ACT + (A::DZT + e - L1 - L2) * 16;
+      r.gi[0] = O::B3 + (e - L1 - L2);
+    }
     r.kind = 2;
     r.valid[0] = true;
     if (prefetch_adam) { r.pv[0] = a.params[r.gi[0]]; r.mv[0] = a.exp_avg[r.gi[0]]; r.vv[0] = a.exp_avg_sq[r.gi[0]]; }
     float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if constexpr (GRAN) {
+      bf16x8 v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = hand_get8(rowg + 4 * q, tag, a.hand_spin, fail);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s8[j] += (float)v[q][j];
+      r.v[0] = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
+      return;
+    }
     // 32 rows per group: four independent 16-byte loads in flight before any add
     // (a one-load-per-iteration loop made this wave the tail kernel's straggler)
     for (int b0 = 0; b0 < Bp; b0 += 32) {
@@ -1053,8 +1204,173 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
   stamp_max(a, 11);
 }
 
+// ---------------------------------------------------------------------------
+// One-launch step (kind Step1; world size 1, B <= 32): block 0 runs the head,
+// blocks [1, 50) the W1 tiles, the rest the small parameters (one task per wave),
+// all in ONE launch.  The tile / small blocks issue everything that does not
+// depend on this step's head at once -- Adam state, W1 / X[t] tiles, the next
+// batch's gather (u8 -> bf16, parked in xring / yring), Adam scalars -- and then
+// poll the head's granules, so the two-launch step's kernel boundary and the
+// tail's load phase leave the critical path.  Same arithmetic, operand order and
+// device state as head + tail (bitwise-identical steps; tests/test_mlp3.py).
+//
+// State: every non-head block reads counters[0..5) + the sequence number once,
+// then acknowledges with an agent atomic whose operand depends on the loaded
+// values; the head rewrites the state (both copies) only after all
+// acknowledgements, so no block can see a half-advanced state.
+// ---------------------------------------------------------------------------
+template <int L1, int L2>
+struct One {
+  static constexpr int NTASK = SmallTasks<L1, L2>::NTASK;
+  static constexpr int NSMALL = (NTASK + kWaves - 1) / kWaves;
+  static constexpr size_t tile_lds = (size_t)(2 * 32 + L1) * kXSS * 2 + 64;
+  static constexpr size_t head_lds = Cfg3<32, L1, L2>::total;
+  static constexpr size_t lds = head_lds > tile_lds ? head_lds : tile_lds;
+};
+
+template <int L1, int L2>
+__device__ __forceinline__ void one_tile(const MLP3Args& a, int kt, char* smem) {
+  constexpr int TN1 = L1 / 16, Bp = 32;
+  __bf16* sX = reinterpret_cast<__bf16*>(smem);
+  __bf16* sXn = sX + Bp * kXSS;
+  __bf16* sW = sXn + Bp * kXSS;
+  AdamScal* sh_o = reinterpret_cast<AdamScal*>(sW + L1 * kXSS);
+  const int tid = threadIdx.x, lane = tid & 63, ct = tid >> 6, r16 = lane & 15, g = lane >> 4;
+  const bool mw = ct < TN1;  // waves owning a 16-neuron column of the tile
+  if (a.stamps && kt == 0 && tid == 0) a.stamps[8] = __builtin_amdgcn_s_memrealtime();
+  const int64_t c0 = a.counters[0], cursor = a.counters[1], slot = a.counters[3], ob = a.counters[4];
+  const int64_t seq = a.counters[kSeq];
+  if (tid == 0) {
+    const long long inc = ((c0 | cursor | slot | ob | seq) >= 0) ? 1 : 2;  // operand depends on every load
+    __hip_atomic_fetch_add(reinterpret_cast<long long*>(a.hand + kHandAck), inc, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const uint32_t tag = (uint32_t)(seq + 1);
+  const int B = a.B;
+  const int m = ct * 16 + r16, pix = kt * 16 + 4 * g;
+  const int64_t gidx = (int64_t)m * kD + pix;
+  F4 p4{}, m4{}, v4{};
+  if (mw) {
+    p4 = *reinterpret_cast<const F4*>(a.params + gidx);
+    m4 = *reinterpret_cast<const F4*>(a.exp_avg + gidx);
+    v4 = *reinterpret_cast<const F4*>(a.exp_avg_sq + gidx);
+  }
+  const float lr_now = a.lr_ptr ? a.lr_ptr[0] : a.lr;
+  __bf16* XR = reinterpret_cast<__bf16*>(a.xring);
+  constexpr int64_t tile_elems = (int64_t)Bp * 16;
+  // X[t] (parked by the previous step) -> sX; X[t+1] gathered -> sXn + xring[slot ^ 1]
+  if (tid < Bp) {
+    const __bf16* cur = XR + (slot * kTiles + kt) * tile_elems + tid * 16;
+    *reinterpret_cast<bf16x8*>(sX + tid * kXSS) = ld8(cur);
+    *reinterpret_cast<bf16x8*>(sX + tid * kXSS + 8) = ld8(cur + 8);
+  } else if (tid < 2 * Bp) {
+    const int b = tid - Bp;
+    int64_t nc = cursor + 1, nob = ob;
+    if (nc >= a.n_batches) { nc = 0; nob ^= 1; }
+    const int64_t* idx = a.order + nob * a.order_stride + nc * B;
+    bf16x8 lo = zero8(), hi = zero8();
+    int y = -1;
+    if (b < B) {
+      const int64_t s = idx[b];
+      u8x16_to_bf16(*reinterpret_cast<const uint4*>(a.x_u8 + s * kD + kt * 16), lo, hi);
+      if (kt == 0) y = (int)a.labels[s];
+    }
+    *reinterpret_cast<bf16x8*>(sXn + b * kXSS) = lo;
+    *reinterpret_cast<bf16x8*>(sXn + b * kXSS + 8) = hi;
+    __bf16* nx = XR + ((slot ^ 1) * kTiles + kt) * tile_elems + b * 16;
+    *reinterpret_cast<bf16x8*>(nx) = lo;
+    *reinterpret_cast<bf16x8*>(nx + 8) = hi;
+    if (kt == 0) a.yring[(slot ^ 1) * Bp + b] = y;
+  }
+  if (tid == 0) adam_scalars(*sh_o, a.advance_step ? c0 + 1 : c0, lr_now, a.beta1, a.beta2, a.eps, a.weight_decay,
+                             a.adamw);
+  __syncthreads();
+  if (a.stamps && kt == 0 && tid == 0) a.stamps[9] = __builtin_amdgcn_s_memrealtime();
+  stamp_max(a, 5);
+
+  int fail = 0;
+  bf16x4 w4;
+  if (mw) {
+    // dW1 tile: D[pixel pix+i][neuron m] = sum_b X[b][pix+i] dH1[b][m]
+    const int q = r16 >> 2, pp = r16 & 3;
+    const bf16x4 lo = tr_read(sX + (8 * g + q) * kXSS + 4 * pp);
+    const bf16x4 hi = tr_read(sX + (8 * g + 4 + q) * kXSS + 4 * pp);
+    const bf16x8 afrag = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    const bf16x8 bfrag = hand_get8(a.hand + kHandDH1 + m * 16 + 4 * g, tag, a.hand_spin, &fail);
+    const f32x4 acc = mfma16(afrag, bfrag, f32x4{0.f, 0.f, 0.f, 0.f});
+    const AdamScal o = *sh_o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      p4.v[i] = adam1(p4.v[i], acc[i], m4.v[i], v4.v[i], o);
+      w4[i] = (__bf16)p4.v[i];
+    }
+    *reinterpret_cast<F4*>(a.params + gidx) = p4;
+    *reinterpret_cast<F4*>(a.exp_avg + gidx) = m4;
+    *reinterpret_cast<F4*>(a.exp_avg_sq + gidx) = v4;
+    *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.shadow) + gidx) = w4;
+    *reinterpret_cast<bf16x4*>(sW + m * kXSS + 4 * g) = w4;
+  }
+  __syncthreads();
+  if (mw) {
+    // next step's layer-1 partial: H1pre[b][m] += sum_{16 px} X'[b][px] W1[m][px]
+    unsigned long long* h1 = reinterpret_cast<unsigned long long*>(a.h1pre + (slot ^ 1) * (int64_t)Bp * L1);
+    const bf16x8 bfrag = (g < 2) ? ld8(sW + (ct * 16 + r16) * kXSS + 8 * g) : zero8();
+#pragma unroll
+    for (int mt = 0; mt < Bp / 16; ++mt) {
+      const bf16x8 afrag = (g < 2) ? ld8(sXn + (mt * 16 + r16) * kXSS + 8 * g) : zero8();
+      const f32x4 d = mfma16(afrag, bfrag, f32x4{0.f, 0.f, 0.f, 0.f});
+      unsigned long long* dst = h1 + (int64_t)((mt * TN1 + ct) * 4) * 64 + lane;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) atomicAdd(dst + i * 64, f32_to_fixed(d[i]));
+    }
+  }
+  if (fail) __hip_atomic_store(a.hand + kHandErr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a.stamps && kt == 0 && tid == 0) a.stamps[10] = __builtin_amdgcn_s_memrealtime();
+  stamp_max(a, 11);
+}
+
+template <int L1, int L2>
+__device__ __forceinline__ void one_small(const MLP3Args& a, int sblk, char* smem) {
+  AdamScal* sh_o = reinterpret_cast<AdamScal*>(smem);
+  const int tid = threadIdx.x;
+  const int64_t c0 = a.counters[0], seq = a.counters[kSeq];
+  if (tid == 0) {
+    const long long inc = ((c0 | seq) >= 0) ? 1 : 2;
+    __hip_atomic_fetch_add(reinterpret_cast<long long*>(a.hand + kHandAck), inc, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const uint32_t tag = (uint32_t)(seq + 1);
+  const float lr_now = a.lr_ptr ? a.lr_ptr[0] : a.lr;
+  int fail = 0;
+  SmallRes r;
+  small_compute<L1, L2, true>(a, true, sblk * kWaves + (tid >> 6), r, tag, &fail);
+  if (tid == 0) adam_scalars(*sh_o, a.advance_step ? c0 + 1 : c0, lr_now, a.beta1, a.beta2, a.eps, a.weight_decay,
+                             a.adamw);
+  __syncthreads();
+  // the head has read every weight / bias of this step before `done`
+  if (r.kind >= 0) hand_wait(a.hand + kHandDone, tag, a.hand_spin, &fail);
+  small_finalize<L1, L2>(a, true, r, *sh_o);
+  if (fail) __hip_atomic_store(a.hand + kHandErr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  stamp_max(a, 11);
+}
+
+template <int L1, int L2>
+__global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
+  __shared__ __attribute__((aligned(16))) char smem[One<L1, L2>::lds];
+  const int b = blockIdx.x;
+  if (b == 0) head_body<32, L1, L2, false, true>(a, smem);
+  else if (b <= kTiles) one_tile<L1, L2>(a, b - 1, smem);
+  else one_small<L1, L2>(a, b - 1 - kTiles, smem);
+}
+
 template <int L1, int L2>
 int dispatch3(const MLP3Args& a, int kind, hipStream_t stream) {
+  if (kind == kMLP3Step1) {
+    if (a.B > 32 || !a.hand) return -5;
+    hipLaunchKernelGGL((mlp3_one_kernel<L1, L2>), dim3(1 + kTiles + One<L1, L2>::NSMALL), dim3(kThreads), 0, stream,
+                       a);
+    return 0;
+  }
   constexpr int NT = 64 * (L1 / 16);
   if (kind == kMLP3StepDP && (a.dp_world < 1 || a.dp_world > kXgmiMaxRanks || !a.dp_gen || !a.dp_err ||
                               a.dp_stride < Off<L1, L2>::NP || kTiles + SmallTasks<L1, L2>::NBLK > kDpMaxBlocks))
@@ -1088,6 +1404,7 @@ static_assert(fits3<kHeadRows, 128, 256>(), "v3 head LDS budget");
 }  // namespace
 
 int mlp3_act_rows(int L1, int L2) { return L1 + 2 * L2 + 16; }
+int64_t mlp3_hand_words(int L1, int L2) { return hand_act_base(L1) + (int64_t)(L1 + 2 * L2 + 16) * 16; }
 
 int launch_mlp3(const MLP3Args& a, int kind, hipStream_t stream) {
   if (a.B > kBMax || a.B < 1) return -2;

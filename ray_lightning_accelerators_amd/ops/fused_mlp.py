@@ -167,7 +167,13 @@ def mlp_refresh_shadow(params: torch.Tensor, shadow: torch.Tensor, L1: int, L2: 
         shadow[lay["w3t"]: lay["total"]].copy_(w3t.reshape(-1))
 
 
-MLP3_STEP, MLP3_HEAD, MLP3_TAIL_GRAD, MLP3_TAIL_ADAM, MLP3_PRIME, MLP3_STEP_DP = range(6)
+MLP3_STEP, MLP3_HEAD, MLP3_TAIL_GRAD, MLP3_TAIL_ADAM, MLP3_PRIME, MLP3_STEP_DP, MLP3_STEP1 = range(7)
+ONE_LAUNCH_MAX_B = 32  # MLP3_STEP1: one head workgroup
+
+
+def mlp3_hand_words(L1: int, L2: int) -> int:
+    """int64 words of the one-launch step's in-launch hand-off buffer (csrc/mlp_step3.hip)."""
+    return 48 + (L1 + L1 + 2 * L2 + 16) * 16
 W1_TILES = IN_FEATURES // 16
 
 
@@ -181,8 +187,11 @@ def mlp3_buffers(L1: int, L2: int, B: int, device) -> Dict[str, torch.Tensor]:
         "h1pre": torch.zeros(2 * bp * L1, dtype=torch.int64, device=device),
         "act": torch.zeros((L1 + 2 * L2 + 16) * bp, dtype=torch.bfloat16, device=device),
         "yring": torch.full((2 * bp,), -1, dtype=torch.int32, device=device),
-        # [0, 5) current state, [5, 10) the head's advanced copy (published by the tail)
-        "counters": torch.zeros(10, dtype=torch.int64, device=device),
+        # [0, 5) current state, [5, 10) the head's advanced copy (published by the tail),
+        # [10] the one-launch step's launch sequence number (its hand-off tag)
+        "counters": torch.zeros(16, dtype=torch.int64, device=device),
+        # one-launch step: acknowledgement / error words + tagged granules (head -> tiles)
+        "hand": torch.zeros(mlp3_hand_words(L1, L2), dtype=torch.int64, device=device),
         # per-head-workgroup (sum NLL, #correct, #rows, -) when the batch spans several
         "head_part": torch.zeros(bp // 32 * 4, device=device),
     }
@@ -221,6 +230,7 @@ def mlp3_launch(
     stamps: Optional[torch.Tensor] = None,
     dp_ctx: Optional[Sequence[int]] = None,
     head_part: Optional[torch.Tensor] = None,
+    hand: Optional[torch.Tensor] = None,
 ) -> None:
     """One v3 launch (GPU only).  ``kind``: MLP3_STEP (head + fused tail, world size 1),
     MLP3_HEAD / MLP3_TAIL_GRAD (gradients, before the allreduce), MLP3_TAIL_ADAM
@@ -228,13 +238,15 @@ def mlp3_launch(
     (layer-1 pre-activations of the pending batch from the current weights; the
     caller zeroes ``h1pre`` first), MLP3_STEP_DP (head + tail whose Adam epilogue
     sums the gradient tiles of all ranks over xGMI itself; ``dp_ctx`` is
-    ``NativeCommunicator.dp_context``).  ``order`` is [2, n_batches * B]: the current
-    and the next epoch's sample order (counters[4] selects)."""
+    ``NativeCommunicator.dp_context``), MLP3_STEP1 (the whole step in ONE launch,
+    world size 1, B <= 32: the tail's blocks run beside the head and take its
+    activations as tagged granules from ``hand``).  ``order`` is [2, n_batches * B]:
+    the current and the next epoch's sample order (counters[4] selects)."""
     require().mlp3(
         int(kind), x_u8, labels, order, counters, int(n_batches), int(B), int(L1), int(L2), params, grads, exp_avg,
         exp_avg_sq, shadow, dh1t, xring, h1pre, act, yring, stats, bool(advance_step), float(lr), float(betas[0]),
         float(betas[1]), float(eps), float(weight_decay), float(grad_scale), lr_tensor, bool(adamw), stamps,
-        [int(v) for v in (dp_ctx or ())], head_part,
+        [int(v) for v in (dp_ctx or ())], head_part, hand,
     )
 
 

@@ -28,6 +28,7 @@ oracle of the GPU tests) with identical batch order and optimizer semantics.
 from __future__ import annotations
 
 import math
+import os
 from typing import Callable, Dict, Optional, Sequence
 
 import torch
@@ -120,6 +121,10 @@ class FusedMLPEngine:
         self.dh1t, self.xring, self.h1pre, self.act = bufs["dh1t"], bufs["xring"], bufs["h1pre"], bufs["act"]
         self.yring = bufs["yring"]
         self.head_part = bufs["head_part"]
+        self.hand = bufs["hand"]
+        # world size 1, B <= 32: the whole step as ONE launch (RLA_MLP_ONE_LAUNCH=0: head + tail)
+        self.one_launch = (self.B <= fused_mlp.ONE_LAUNCH_MAX_B
+                           and os.environ.get("RLA_MLP_ONE_LAUNCH", "1") != "0")
         self.stats = torch.zeros(stats_ring, 4, device=self.device)
         self.seed = seed
         self.epoch = 0
@@ -136,6 +141,12 @@ class FusedMLPEngine:
     def _publish_counters(self) -> None:
         """Host edits of the device state go to both copies (current / advanced)."""
         self.counters[5:10].copy_(self.counters[0:5])
+
+    def check(self) -> None:
+        """Raise if a one-launch step's in-launch hand-off ever timed out (a block
+        polled past its bound: the step it belongs to is not trustworthy)."""
+        if self.native and int(self.hand[16].item()) != 0:
+            raise RuntimeError("fused MLP one-launch step: an in-launch hand-off timed out")
 
     def set_step(self, step: int) -> None:
         self.counters[0] = int(step)
@@ -250,7 +261,7 @@ class FusedMLPEngine:
                     n_batches=self.n_batches, B=self.B, L1=self.L1, L2=self.L2, params=self.params,
                     grads=self.grads, exp_avg=self.exp_avg, exp_avg_sq=self.exp_avg_sq, shadow=self.shadow,
                     dh1t=self.dh1t, xring=self.xring, h1pre=self.h1pre, act=self.act, yring=self.yring,
-                    head_part=self.head_part, lr=self.lr, betas=self.betas,
+                    head_part=self.head_part, hand=self.hand, lr=self.lr, betas=self.betas,
                     eps=self.eps, weight_decay=self.wd, lr_tensor=self.lr_tensor)
 
     def prime(self) -> None:
@@ -270,7 +281,8 @@ class FusedMLPEngine:
         else:
             kw = self._kw3()
             if self.world_size == 1:
-                fused_mlp.mlp3_launch(fused_mlp.MLP3_STEP, stats=self.stats, **kw)
+                kind = fused_mlp.MLP3_STEP1 if self.one_launch else fused_mlp.MLP3_STEP
+                fused_mlp.mlp3_launch(kind, stats=self.stats, **kw)
             elif self.dp_ctx is not None:
                 fused_mlp.mlp3_launch(fused_mlp.MLP3_STEP_DP, stats=self.stats, grad_scale=1.0 / self.world_size,
                                       dp_ctx=self.dp_ctx, **kw)

@@ -197,6 +197,52 @@ def test_mlp3_multiblock_head_stats(L1, L2, B):
     assert torch.equal(runs[0], runs[1])
 
 
+def _one_vs_two(L1, L2, B, kinds, n_steps, seed=3):
+    """Engine A runs the one-launch step (or the per-step kinds given), B the
+    two-launch step; every state tensor must match bit for bit."""
+    dev = _dev()
+    x, y = _data(2 * B + B // 2 + 3, seed=seed)
+    a = FusedMLPEngine(L1, L2, B, lr=1e-2, device=dev)
+    b = FusedMLPEngine(L1, L2, B, lr=1e-2, device=dev)
+    b.one_launch = False
+    a.set_data(x, y)
+    b.set_data(x, y)
+    for s in range(n_steps):
+        a.one_launch = kinds(s)
+        a.step()
+        b.step()
+    torch.cuda.synchronize()
+    a.check()
+    assert int(a.hand[0]) == 0  # every launch's acknowledgements consumed
+    assert torch.equal(a.counters[:10].cpu(), b.counters[:10].cpu()), (a.counters, b.counters)
+    w1 = L1 * 784
+    for k in ("params", "exp_avg", "exp_avg_sq", "shadow", "stats", "h1pre", "xring"):
+        pa, pb = getattr(a, k).float(), getattr(b, k).float()
+        if k in ("params", "exp_avg", "exp_avg_sq"):
+            bad = (pa != pb).nonzero().flatten().cpu()
+            assert bad.numel() == 0, (k, bad.numel(), int((bad < w1).sum()), bad[:8].tolist(),
+                                      (pa - pb).abs().max().item())
+        _assert_same(pa, pb)
+    return a
+
+
+@gpu
+@pytest.mark.parametrize("L1,L2,B", [(32, 64, 32), (32, 32, 20), (128, 256, 32), (64, 128, 1), (128, 64, 17)])
+def test_mlp3_one_launch_matches_two_launch(L1, L2, B):
+    """The one-launch step (tiles / small blocks beside the head, granule hand-off)
+    is the same computation as head + tail: bitwise-equal over 2+ epochs."""
+    a = _one_vs_two(L1, L2, B, lambda s: True, 7)
+    assert int(a.counters[10]) == 7  # one sequence number per one-launch step
+
+
+@gpu
+def test_mlp3_one_launch_interleaves_with_two_launch():
+    """The device state between steps is the same for both forms, so they mix
+    freely (graph remainders, fallbacks): alternate them every step / every other."""
+    _one_vs_two(32, 64, 32, lambda s: s % 2 == 0, 9)
+    _one_vs_two(64, 128, 24, lambda s: s % 3 != 1, 9, seed=4)
+
+
 @gpu
 def test_mlp3_graph_replay_matches_eager():
     dev = _dev()
