@@ -132,6 +132,14 @@ __device__ __forceinline__ void gather_tile(const MLP3Args& a, int kt, int64_t o
     for (int b = tid; b < Bp; b += nthreads) a.yring[dst_slot * Bp + b] = b < B ? (int)a.labels[idx[b]] : -1;
 }
 
+// Step state read through the constant address space (scalar loads, lgkmcnt): a
+// step's kernels write the counters only after every reader of the launch is
+// done with them (head: at its end; one-launch: after all blocks' acks), and a
+// vector load here made the compiler wait on vmcnt ahead of independent loads.
+__device__ __forceinline__ int64_t ld_state(const int64_t* p, int i) {
+  return ((const __attribute__((address_space(4))) int64_t*)(p))[i];
+}
+
 // Diagnostic stamp (probe builds only pass a.stamps): latest end over many blocks.
 __device__ __forceinline__ void stamp_max(const MLP3Args& a, int k) {
   if (a.stamps && threadIdx.x == 0)
@@ -139,65 +147,12 @@ __device__ __forceinline__ void stamp_max(const MLP3Args& a, int k) {
               (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
-// ---------------------------------------------------------------------------
-// In-launch hand-off of the one-launch step (mlp3_one_kernel): bf16 pairs in
-// 8-byte {payload, tag} granules, each written by ONE agent-scope (sc1,
-// write-through) store and read by agent-scope (sc1) loads until the tag is this
-// launch's sequence number -- no flag, no fence (the guide's granule hand-off,
-// ~0.8-1 us against ~1.5 us for a dependent kernel boundary; more importantly the
-// consumers' own loads and gathers overlap the head instead of following it).
-// `hand` (int64 words): [kHandAck] blocks' state-read acknowledgements, [kHandErr]
-// poll-timeout word, [kHandDone] the head's weights-read-done granule, then dH1^T
-// ([L1][32] -> 16 granules a row) and the act rows ([ROWS][32]).
-// ---------------------------------------------------------------------------
-constexpr int kSeq = 10;  // counters[10]: launch sequence number of the one-launch step (granule tag)
-constexpr int kHandAck = 0, kHandErr = 16, kHandDone = 32, kHandDH1 = 48;
-__host__ __device__ constexpr int64_t hand_act_base(int L1) { return kHandDH1 + (int64_t)L1 * 16; }
-
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ void hand_put4(unsigned long long* g, bf16x4 v, uint32_t tag) {
-  const u32x2 u = __builtin_bit_cast(u32x2, v);
-  const unsigned long long hi = (unsigned long long)tag << 32;
-  __hip_atomic_store(g, hi | u[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(g + 1, hi | u[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void hand_put8(unsigned long long* g, bf16x8 v, uint32_t tag) {
-  const u32x4 u = __builtin_bit_cast(u32x4, v);
-  const unsigned long long hi = (unsigned long long)tag << 32;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) __hip_atomic_store(g + i, hi | u[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// 8 bf16 (4 granules) once all carry `tag`; *fail on a poll timeout
-__device__ __forceinline__ bf16x8 hand_get8(unsigned long long* g, uint32_t tag, int64_t spin, int* fail) {
-  unsigned long long w[4];
-  int64_t n = 0;
-  while (true) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((uint32_t)(w[0] >> 32) == tag && (uint32_t)(w[1] >> 32) == tag && (uint32_t)(w[2] >> 32) == tag &&
-        (uint32_t)(w[3] >> 32) == tag)
-      break;
-    if (++n > spin) {
-      *fail = 1;
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  const u32x4 u = {(uint32_t)w[0], (uint32_t)w[1], (uint32_t)w[2], (uint32_t)w[3]};
-  return __builtin_bit_cast(bf16x8, u);
-}
-__device__ __forceinline__ void hand_wait(unsigned long long* g, uint32_t tag, int64_t spin, int* fail) {
-  int64_t n = 0;
-  while ((uint32_t)(__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) != tag) {
-    if (++n > spin) {
-      *fail = 1;
-      return;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
+// One-launch step bookkeeping (mlp3_one_kernel): counters[kSeq] counts its
+// launches; hand[kHandAck] accumulates one acknowledgement per block per launch
+// (monotonic: launch `seq` is complete at (seq + 1) * gridDim.x); hand[kHandErr]
+// is set when a bounded wait expires.
+constexpr int kSeq = 10;
+constexpr int kHandAck = 0, kHandErr = 16, kHandWords = 32;
 
 // ---------------------------------------------------------------------------
 // Head kernel (blocks [0, nchunks): one 8-wave workgroup per BC batch rows;
@@ -208,16 +163,18 @@ __device__ __forceinline__ void hand_wait(unsigned long long* g, uint32_t tag, i
 // a kernarg-derived chunk count) measured 0.7 us slower per step at the
 // default 32-64 / batch-32 config (profiles/r2_c11, A/B on one box).
 //
-// GRAN = true: the head of the one-launch step (mlp3_one_kernel, B <= 32): the
-// transposed activations / deltas go to the SAME launch's tile and small blocks
-// as tagged granules (hand_put*), H1pre's other slot is zeroed write-through, and
-// the state advance waits until every other block has read the current state.
-template <int BC, int L1, int L2, bool MULTI, bool GRAN>
+// REP = true: the serial chain as replicated by EVERY block of the one-launch
+// step (mlp3_one_kernel, B <= 32): nothing goes to global memory, the transposed
+// activations / deltas stay in this block's LDS (H1^T, dZ^T and the extra
+// H2^T / dH2^T / dH1^T images at OneLds offsets) for the block's own tail role;
+// no H1pre zeroing (invariant: the slot the tiles accumulate into is zero at a
+// step's start), no state advance (block 0 does it after every block's ack).
+template <int BC, int L1, int L2, bool MULTI, bool REP>
 __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem) {
   using C = Cfg3<BC, L1, L2>;
   using O = Off<L1, L2>;
   using A = Act<L1, L2>;
-  static_assert(!GRAN || (!MULTI && BC == 32), "one-launch head: one 32-row block");
+  static_assert(!REP || (!MULTI && BC == 32), "one-launch head: one 32-row block");
   __bf16* sH1 = (__bf16*)(smem + C::oH1);
   __bf16* sH1T = (__bf16*)(smem + C::oH1T);
   __bf16* sH2 = (__bf16*)(smem + C::oH2);
@@ -234,38 +191,40 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem) {
 
   const int nchunks = MULTI ? (a.B + BC - 1) / BC : 1;
   const int c = MULTI ? (int)blockIdx.x : 0;  // this workgroup's batch rows [c * BC, c * BC + BC)
+  const bool stamp_ok = a.stamps && tid == 0 && c == 0 && (!REP || blockIdx.x == 0);
 
   // device counters: uniform scalar loads, no LDS broadcast round trip
-  const int64_t t = a.counters[0] + 1;
-  const int64_t cursor = a.counters[1];
-  const int64_t slot = a.counters[3];
-  const int64_t ob = a.counters[4];
+  const int64_t t = ld_state(a.counters, 0) + 1;
+  const int64_t cursor = ld_state(a.counters, 1);
+  const int64_t slot = ld_state(a.counters, 3);
+  const int64_t ob = ld_state(a.counters, 4);
   const int Bp = (a.B + 31) / 32 * 32;
   __bf16* ACT = reinterpret_cast<__bf16*>(a.act);
   __bf16* DH1T = reinterpret_cast<__bf16*>(a.dh1t);
-  const uint32_t tag = GRAN ? (uint32_t)(a.counters[kSeq] + 1) : 0u;
-  unsigned long long* HG_DH1 = a.hand + kHandDH1;
-  unsigned long long* HG_ACT = a.hand + hand_act_base(L1);
+  // REP: LDS images of H2^T / dH2^T / dH1^T ([rows][TS] bf16) after the head's own region
+  __bf16* sH2T = (__bf16*)(smem + C::total);
+  __bf16* sDH2T = sH2T + L2 * C::TS;
+  __bf16* sDH1T = sDH2T + L2 * C::TS;
 
+  // Every load of the head's inputs is issued unconditionally (invalid lanes read
+  // a clamped in-bounds address and select zero afterwards) and LDS is written
+  // only after the last load is in flight: a load in a divergent branch, or an
+  // LDS write of a just-loaded value ahead of the others, makes the compiler wait
+  // for it (vmcnt(0)) before issuing anything else -- a full memory round trip each.
   constexpr int NBIAS = L1 + L2 + kNC;
-  if (tid < NBIAS) {
-    const int64_t bgi = tid < L1 ? O::B1 + tid : (tid < L1 + L2 ? O::B2 + (tid - L1) : O::B3 + (tid - L1 - L2));
-    sBias[tid] = P[bgi];
+  float bias_v;
+  {
+    const int bt = tid < NBIAS ? tid : 0;
+    const int64_t bgi = bt < L1 ? O::B1 + bt : (bt < L1 + L2 ? O::B2 + (bt - L1) : O::B3 + (bt - L1 - L2));
+    bias_v = P[bgi];
   }
   if (tid == 0) {
     misc[0] = 0.f; misc[1] = 0.f; misc[2] = 0.f;
-    if (a.stamps && c == 0) a.stamps[0] = __builtin_amdgcn_s_memrealtime();
+    if (stamp_ok) a.stamps[0] = __builtin_amdgcn_s_memrealtime();
   }
   // the tail of this step accumulates the next step's H1pre into the other slot;
   // in fragment order this block's rows are one contiguous BC * L1 range
-  if constexpr (GRAN) {
-    // write-through: this launch's tile blocks add into these words (memory-side
-    // atomics) once they hold the dH1 granules, published after every wave's
-    // vmcnt(0) wait below
-    unsigned long long* z = reinterpret_cast<unsigned long long*>(a.h1pre + (slot ^ 1) * (int64_t)Bp * L1);
-    for (int i = tid; i < BC * L1; i += kThreads)
-      __hip_atomic_store(z + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
+  if constexpr (!REP) {
     uint4* z = reinterpret_cast<uint4*>(a.h1pre + (slot ^ 1) * (int64_t)Bp * L1 + (int64_t)c * BC * L1);
     for (int i = tid; i < BC * L1 / 2; i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
   }
@@ -295,8 +254,7 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem) {
     constexpr int CPR = BC / 8;
     for (int e = tid; e < nrows * CPR; e += kThreads) {
       const int r = e / CPR, col = (e - r * CPR) * 8;
-      if constexpr (GRAN) hand_put8(HG_ACT + (dst_row + r) * 16 + col / 2, ld8(src + r * C::TS + col), tag);
-      else if (row0 + col < Bp)
+      if (row0 + col < Bp)
         *reinterpret_cast<bf16x8*>(ACT + (int64_t)(dst_row + r) * Bp + row0 + col) = ld8(src + r * C::TS + col);
     }
   };
@@ -308,46 +266,45 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem) {
     // selected after it: none of these loads waits for the counters read.
     constexpr int NQ = (BC * L1 / 4 + kThreads - 1) / kThreads;
     longlong2 qs[NQ][2][2];  // [item][slot][half]
+    bool qok[NQ];
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
       const int f4 = tid + k * kThreads;
       const int mtl = (f4 * 4 >> 8) / C::TN1;
+      // rows past round_up(B, 32) exist only in the last chunk's LDS image
+      qok[k] = f4 < BC * L1 / 4 && row0 + mtl * 16 < Bp;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        qs[k][s][0] = qs[k][s][1] = make_longlong2(0, 0);
-        // rows past round_up(B, 32) exist only in the last chunk's LDS image
-        if (f4 < BC * L1 / 4 && row0 + mtl * 16 < Bp) {
-          const int64_t* src = a.h1pre + s * (int64_t)Bp * L1 + (int64_t)row0 * L1 + f4 * 4;
-          qs[k][s][0] = *reinterpret_cast<const longlong2*>(src);
-          qs[k][s][1] = *reinterpret_cast<const longlong2*>(src + 2);
-        }
+        const int64_t* src = a.h1pre + (qok[k] ? s * (int64_t)Bp * L1 + (int64_t)row0 * L1 + f4 * 4 : 0);
+        qs[k][s][0] = *reinterpret_cast<const longlong2*>(src);
+        qs[k][s][1] = *reinterpret_cast<const longlong2*>(src + 2);
       }
     }
-    if (tid < BC) {
-      const bool ok = row0 + tid < Bp;
-      const int y0 = ok ? a.yring[row0 + tid] : -1, y1 = ok ? a.yring[Bp + row0 + tid] : -1;
-      sY[tid] = slot ? y1 : y0;  // staged by the previous head launch; -1 past B
-    }
+    // labels of both ring slots (staged by the previous step; -1 past B)
+    const bool yok = tid < BC && row0 + tid < Bp;
+    const int yt = yok ? row0 + tid : 0;
+    const int y0 = a.yring[yt], y1 = a.yring[Bp + yt];
     // ---- every weight fragment this wave needs, issued right behind the H1pre /
     // label loads the first barrier waits for (the in-order vmcnt lets the
     // fragments stay in flight across it): one L2 round trip in total ----
     bf16x8 w2f[NTW2][KS2];
     bf16x8 w3tf[NTW2];
+    // clamped address + select: the load itself is never conditional
+    auto ld8z = [&](bool ok, int64_t off) { const bf16x8 v = ld8(SH + (ok ? off : 0)); return ok ? v : zero8(); };
 #pragma unroll
     for (int j = 0; j < NTW2; ++j) {
       const int nt = nt_base + kWaves * j;
       const bool ok = l2_active && nt < C::TN2;
 #pragma unroll
       for (int ks = 0; ks < KS2; ++ks)
-        w2f[j][ks] = ok ? ld8(SH + O::W2 + (int64_t)(nt * 16 + r16) * L1 + ks * 32 + 8 * g) : zero8();
-      w3tf[j] = (ok && g < 2) ? ld8(SH + O::W3T + (int64_t)(nt * 16 + r16) * 16 + 8 * g) : zero8();
+        w2f[j][ks] = ld8z(ok, O::W2 + (int64_t)(nt * 16 + r16) * L1 + ks * 32 + 8 * g);
+      w3tf[j] = ld8z(ok && g < 2, O::W3T + (int64_t)(nt * 16 + r16) * 16 + 8 * g);
     }
     const int mt3 = w % MT, kg3 = w / MT;
     bf16x8 w3f[KPG3];
 #pragma unroll
     for (int i = 0; i < KPG3; ++i)
-      w3f[i] = (kg3 < KG3 && r16 < kNC) ? ld8(SH + O::W3 + (int64_t)r16 * L2 + (kg3 * KPG3 + i) * 32 + 8 * g)
-                                        : zero8();
+      w3f[i] = ld8z(kg3 < KG3 && r16 < kNC, O::W3 + (int64_t)r16 * L2 + (kg3 * KPG3 + i) * 32 + 8 * g);
     // dH1 with a short K (KG1 == 1) and few tiles: one (column, row) tile per wave
     constexpr bool ROW1 = KG1 == 1 && C::TN1 * MT <= kWaves;
     constexpr int MTW1 = ROW1 ? 1 : MT;
@@ -356,8 +313,10 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem) {
     bf16x8 w2tf[KPG1];
 #pragma unroll
     for (int i = 0; i < KPG1; ++i)
-      w2tf[i] = (kg1 < KG1) ? ld8(SH + O::W2T + (int64_t)(ct1 * 16 + r16) * L2 + (kg1 * KPG1 + i) * 32 + 8 * g)
-                            : zero8();
+      w2tf[i] = ld8z(kg1 < KG1, O::W2T + (int64_t)(ct1 * 16 + r16) * L2 + (kg1 * KPG1 + i) * 32 + 8 * g);
+    // LDS writes last: their waits cover only the earliest loads (in-order vmcnt)
+    if (tid < NBIAS) sBias[tid] = bias_v;
+    if (tid < BC) sY[tid] = yok ? (slot ? y1 : y0) : -1;
     __syncthreads();  // sBias ready
 
     // ---- H1 = relu(H1pre + b1); H1pre chunk is contiguous in fragment order ----
@@ -366,24 +325,30 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem) {
       for (int k = 0; k < NQ; ++k) {
         const int f4 = tid + k * kThreads;
         if (f4 >= BC * L1 / 4) continue;
+        if (!qok[k]) qs[k][0][0] = qs[k][0][1] = qs[k][1][0] = qs[k][1][1] = make_longlong2(0, 0);
         const int f = f4 * 4;
         const int ln = f & 63, i = (f >> 6) & 3, blk = f >> 8;
         const int ct = blk % C::TN1, mtl = blk / C::TN1;
         const int b = mtl * 16 + 4 * (ln >> 4) + i, m = ct * 16 + (ln & 15);
-        const longlong2 lo = slot ? qs[k][1][0] : qs[k][0][0];
-        const longlong2 hi = slot ? qs[k][1][1] : qs[k][0][1];
-        const int64_t q[4] = {lo.x, lo.y, hi.x, hi.y};
-        bf16x4 h;
+        // both slots converted, the RESULT selected: selecting the loaded pairs
+        // made the compiler index qs at run time (qs in scratch, and a wait on
+        // the H1pre loads right at issue, ahead of the weight-fragment loads)
+        bf16x4 hs[2];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) h[k] = relu_bf(fixed_to_f32(q[k]) + sBias[m + k]);
+        for (int sl = 0; sl < 2; ++sl) {
+          const int64_t q[4] = {qs[k][sl][0].x, qs[k][sl][0].y, qs[k][sl][1].x, qs[k][sl][1].y};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) hs[sl][k] = relu_bf(fixed_to_f32(q[k]) + sBias[m + k]);
+        }
+        const bf16x4 h = slot ? hs[1] : hs[0];
         *reinterpret_cast<bf16x4*>(sH1 + b * C::H1S + m) = h;
 #pragma unroll
         for (int k = 0; k < 4; ++k) sH1T[(m + k) * C::TS + b] = h[k];
       }
     }
     __syncthreads();
-    if (a.stamps && tid == 0 && c == 0) a.stamps[1] = __builtin_amdgcn_s_memrealtime();
-    copy_rows(sH1T, L1, A::H1T, row0);
+    if (stamp_ok) a.stamps[1] = __builtin_amdgcn_s_memrealtime();
+    if constexpr (!REP) copy_rows(sH1T, L1, A::H1T, row0);
 
     // ---------------- layer 2: H2 = relu(H1 W2^T + b2) ----------------
 #pragma unroll
@@ -406,7 +371,7 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem) {
           sH2[(mt * 16 + 4 * g + i) * C::H2S + n] = h;
           t4[i] = h;
         }
-        if constexpr (GRAN) hand_put4(HG_ACT + (A::H2T + n) * 16 + (mt * 16 + 4 * g) / 2, t4, tag);
+        if constexpr (REP) *reinterpret_cast<bf16x4*>(sH2T + n * C::TS + mt * 16 + 4 * g) = t4;
         else if (row0 + mt * 16 < Bp)
           *reinterpret_cast<bf16x4*>(ACT + (int64_t)(A::H2T + n) * Bp + row0 + mt * 16 + 4 * g) = t4;
       }
@@ -440,7 +405,7 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem) {
       }
       __syncthreads();
     }
-    if (a.stamps && tid == 0 && c == 0) a.stamps[2] = __builtin_amdgcn_s_memrealtime();
+    if (stamp_ok) a.stamps[2] = __builtin_amdgcn_s_memrealtime();
 
     // ---------------- log_softmax / NLL / accuracy / dZ (one row per lane) -------------
     if (w < (BC + 63) / 64) {
@@ -494,7 +459,7 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem) {
       }
     }
     __syncthreads();
-    copy_rows(sdZT, 16, A::DZT, row0);
+    if constexpr (!REP) copy_rows(sdZT, 16, A::DZT, row0);
 
     // ---------------- dH2 = (dZ W3) * (H2 > 0), in place over H2 ----------------
 #pragma unroll
@@ -514,23 +479,12 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem) {
           *hp = d;
           t4[i] = d;
         }
-        if constexpr (GRAN) hand_put4(HG_ACT + (A::DH2T + n) * 16 + (mt * 16 + 4 * g) / 2, t4, tag);
+        if constexpr (REP) *reinterpret_cast<bf16x4*>(sDH2T + n * C::TS + mt * 16 + 4 * g) = t4;
         else if (row0 + mt * 16 < Bp)
           *reinterpret_cast<bf16x4*>(ACT + (int64_t)(A::DH2T + n) * Bp + row0 + mt * 16 + 4 * g) = t4;
       }
     }
-    if constexpr (GRAN) {
-      // every wave's stores (the write-through H1pre zeroing above all) have
-      // completed, and every weight / bias load of this launch has returned: the
-      // `done` granule lets the small blocks overwrite weights and biases
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0)
-        __hip_atomic_store(a.hand + kHandDone, (unsigned long long)tag << 32, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __syncthreads();
-    }
+    __syncthreads();
 
     // ---------------- dH1 = (dH2 W2) * (H1 > 0) -> dh1t, K split over waves ----------------
     if (kg1 < KG1) {
@@ -549,7 +503,7 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem) {
             const __bf16 hv = sH1[(mt * 16 + 4 * g + i) * C::H1S + m];
             t4[i] = ((float)hv > 0.f) ? (__bf16)acc[i] : (__bf16)0.f;
           }
-          if constexpr (GRAN) hand_put4(HG_DH1 + m * 16 + (mt * 16 + 4 * g) / 2, t4, tag);
+          if constexpr (REP) *reinterpret_cast<bf16x4*>(sDH1T + m * C::TS + mt * 16 + 4 * g) = t4;
           else if (row0 + mt * 16 < Bp)
             *reinterpret_cast<bf16x4*>(DH1T + (int64_t)m * Bp + row0 + mt * 16 + 4 * g) = t4;
         } else {
@@ -573,13 +527,14 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem) {
           const __bf16 hv = sH1[b * C::H1S + m];
           t4[i] = ((float)hv > 0.f) ? (__bf16)v : (__bf16)0.f;
         }
-        if constexpr (GRAN) hand_put4(HG_DH1 + m * 16 + 2 * q, t4, tag);
+        if constexpr (REP) *reinterpret_cast<bf16x4*>(sDH1T + m * C::TS + 4 * q) = t4;
         else if (row0 + 4 * q < Bp) *reinterpret_cast<bf16x4*>(DH1T + (int64_t)m * Bp + row0 + 4 * q) = t4;
       }
     }
     __syncthreads();
-    if (a.stamps && tid == 0 && c == 0) a.stamps[3] = __builtin_amdgcn_s_memrealtime();
+    if (stamp_ok) a.stamps[3] = __builtin_amdgcn_s_memrealtime();
   }
+  if constexpr (REP) return;  // loss stats stay in misc[0..3); block 0 publishes them
   if (tid == 0 && nchunks > 1) {
     // several row blocks: partial sums for tail block 0's ordered reduction
     a.head_part[c * 4 + 0] = misc[0];
@@ -589,22 +544,6 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem) {
   if (tid == 0 && c == 0) {
     // the advanced state goes to the NEXT copy: this launch's gather blocks are
     // still reading the current one (the tail publishes it, see mlp3_tail_kernel).
-    // One launch: both copies, once every other block has acknowledged its read
-    // of the current state (its ack add depends on the loaded values).
-    if constexpr (GRAN) {
-      const long long others = (long long)gridDim.x - 1;
-      long long* ack = reinterpret_cast<long long*>(a.hand + kHandAck);
-      int64_t spins = 0;
-      while (__hip_atomic_load(ack, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < others) {
-        if (++spins > a.hand_spin) {
-          __hip_atomic_store(a.hand + kHandErr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      __hip_atomic_fetch_add(ack, -others, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      a.counters[kSeq] = (int64_t)tag;
-    }
     int64_t* cn = a.counters + kCnt;
     cn[0] = a.advance_step ? t : t - 1;
     cn[2] = cursor;
@@ -613,8 +552,6 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem) {
     cn[1] = nc;
     cn[4] = nob;
     cn[3] = slot ^ 1;
-    if constexpr (GRAN)
-      for (int k = 0; k < kCnt; ++k) a.counters[k] = cn[k];
     if (a.stats && nchunks == 1) {
       const int s = (int)((t - 1) % (a.stats_ring > 0 ? a.stats_ring : 1));
       float* st = a.stats + s * 4;
@@ -666,62 +603,82 @@ struct SmallRes {
   int rowv, colv;
 };
 
-// GRAN: the operands come from the one-launch head's granules (Bp = 32) instead of act / dh1t
-template <int L1, int L2, bool GRAN = false>
+// LDS images of the one-launch block's own head pass ([rows][ts] bf16, batch-contiguous rows)
+struct RepLds {
+  const __bf16 *h1t, *h2t, *dh2t, *dzt, *dh1t;
+  int ts;
+};
+
+// REP (the one-launch step): called twice -- L == nullptr: task setup + Adam
+// prefetch only (before the block's head pass); then with L: the gradient from
+// this block's LDS images instead of act / dh1t (r keeps the first call's state)
+template <int L1, int L2, bool REP = false>
 __device__ __forceinline__ void small_compute(const MLP3Args& a, bool prefetch_adam, int task, SmallRes& r,
-                                              uint32_t tag = 0, int* fail = nullptr) {
+                                              const RepLds* L = nullptr) {
+  const bool setup = !REP || L == nullptr, compute = !REP || L != nullptr;
   using O = Off<L1, L2>;
   using A = Act<L1, L2>;
   using S = SmallTasks<L1, L2>;
   const int lane = threadIdx.x & 63, r16 = lane & 15, g = lane >> 4;
   const int Bp = (a.B + 31) / 32 * 32;
   const __bf16* ACT = reinterpret_cast<const __bf16*>(a.act);
-  unsigned long long* HG_ACT = a.hand + hand_act_base(L1);
-  int arow_i = 0, brow_i = 0;  // act rows of the two MFMA operands (GRAN)
-  r.kind = -1;
+  const __bf16 *arow_l = nullptr, *brow_l = nullptr;  // REP: LDS rows of the two MFMA operands
+  if (setup) {
+    r.kind = -1;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    r.v[i] = r.pv[i] = r.mv[i] = r.vv[i] = 0.f;
-    r.gi[i] = 0;
-    r.valid[i] = false;
+    for (int i = 0; i < 4; ++i) {
+      r.v[i] = r.pv[i] = r.mv[i] = r.vv[i] = 0.f;
+      r.gi[i] = 0;
+      r.valid[i] = false;
+    }
   }
   if (task < S::NTILE) {
     const __bf16 *arow, *brow;
     if (task < S::NT_W2) {  // dW2[n][m] = sum_b dH2[b][n] H1[b][m]
       const int nt = task % S::TN2, ct = task / S::TN2;
-      r.kind = 0;
-      r.rowv = nt * 16 + 4 * g;
-      r.colv = ct * 16 + r16;
-      arow_i = A::DH2T + nt * 16 + r16;
-      brow_i = A::H1T + ct * 16 + r16;
-      arow = ACT + (int64_t)arow_i * Bp;
-      brow = ACT + (int64_t)brow_i * Bp;
+      if (setup) {
+        r.kind = 0;
+        r.rowv = nt * 16 + 4 * g;
+        r.colv = ct * 16 + r16;
+      }
+      arow = ACT + (int64_t)(A::DH2T + nt * 16 + r16) * Bp;
+      brow = ACT + (int64_t)(A::H1T + ct * 16 + r16) * Bp;
+      if constexpr (REP) {
+        arow_l = L->dh2t + (nt * 16 + r16) * L->ts;
+        brow_l = L->h1t + (ct * 16 + r16) * L->ts;
+      }
+      if (setup)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) { r.gi[i] = O::W2 + (int64_t)(r.rowv + i) * L1 + r.colv; r.valid[i] = true; }
+        for (int i = 0; i < 4; ++i) { r.gi[i] = O::W2 + (int64_t)(r.rowv + i) * L1 + r.colv; r.valid[i] = true; }
     } else {  // dW3[j][n] = sum_b dZ[b][j] H2[b][n]
       const int nt = task - S::NT_W2;
-      r.kind = 1;
-      r.rowv = 4 * g;
-      r.colv = nt * 16 + r16;
-      arow_i = A::DZT + r16;
-      brow_i = A::H2T + nt * 16 + r16;
-      arow = ACT + (int64_t)arow_i * Bp;
-      brow = ACT + (int64_t)brow_i * Bp;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        r.valid[i] = (r.rowv + i) < kNC;
-        r.gi[i] = O::W3 + (int64_t)(r.valid[i] ? r.rowv + i : 0) * L2 + r.colv;
+      if (setup) {
+        r.kind = 1;
+        r.rowv = 4 * g;
+        r.colv = nt * 16 + r16;
       }
-    }
+      arow = ACT + (int64_t)(A::DZT + r16) * Bp;
+      brow = ACT + (int64_t)(A::H2T + nt * 16 + r16) * Bp;
+      if constexpr (REP) {
+        arow_l = L->dzt + r16 * L->ts;
+        brow_l = L->h2t + (nt * 16 + r16) * L->ts;
+      }
+      if (setup)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (prefetch_adam && r.valid[i]) {
+        for (int i = 0; i < 4; ++i) {
+          r.valid[i] = (r.rowv + i) < kNC;
+          r.gi[i] = O::W3 + (int64_t)(r.valid[i] ? r.rowv + i : 0) * L2 + r.colv;
+        }
+    }
+    if (setup && prefetch_adam)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {  // unconditional: gi is in bounds for invalid rows too (row 0)
         r.pv[i] = a.params[r.gi[i]]; r.mv[i] = a.exp_avg[r.gi[i]]; r.vv[i] = a.exp_avg_sq[r.gi[i]];
       }
+    if (!compute) return;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (GRAN) {
-      const bf16x8 bv = hand_get8(HG_ACT + brow_i * 16 + 4 * g, tag, a.hand_spin, fail);  // H1^T / H2^T: earlier
-      acc = mfma16(hand_get8(HG_ACT + arow_i * 16 + 4 * g, tag, a.hand_spin, fail), bv, acc);
+    if constexpr (REP) {
+      acc = mfma16(ld8(arow_l + 8 * g), ld8(brow_l + 8 * g), acc);  // Bp = 32: one k-step
     } else {
       for (int ks = 0; ks < Bp / 32; ++ks) {
         const int b0 = ks * 32 + 8 * g;
@@ -734,35 +691,24 @@ __device__ __forceinline__ void small_compute(const MLP3Args& a, bool prefetch_a
     const int e = (task - S::NTILE) * 64 + lane;
     if (e >= S::NBIAS) return;
     const __bf16* row;
-    unsigned long long* rowg;
     if (e < L1) {
-      row = reinterpret_cast<const __bf16*>(a.dh1t) + (int64_t)e * Bp;
-      rowg = a.hand + kHandDH1 + e * 16;
+      row = REP ? L->dh1t + e * L->ts : reinterpret_cast<const __bf16*>(a.dh1t) + (int64_t)e * Bp;
       r.gi[0] = O::B1 + e;
     } else if (e < L1 + L2) {
-      row = ACT + (int64_t)(A::DH2T + e - L1) * Bp;
-      rowg = HG_ACT + (A::DH2T + e - L1) * 16;
+      row = REP ? L->dh2t + (e - L1) * L->ts : ACT + (int64_t)(A::DH2T + e - L1) * Bp;
       r.gi[0] = O::B2 + (e - L1);
     } else {
-      row = ACT + (int64_t)(A::DZT + e - L1 - L2) * Bp;
-      rowg = HG_ACT + (A::DZT + e - L1 - L2) * 16;
+      row = REP ? L->dzt + (e - L1 - L2) * L->ts : ACT + (int64_t)(A::DZT + e - L1 - L2) * Bp;
       r.gi[0] = O::B3 + (e - L1 - L2);
     }
-    r.kind = 2;
-    r.valid[0] = true;
-    if (prefetch_adam) { r.pv[0] = a.params[r.gi[0]]; r.mv[0] = a.exp_avg[r.gi[0]]; r.vv[0] = a.exp_avg_sq[r.gi[0]]; }
-    float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if constexpr (GRAN) {
-      bf16x8 v[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = hand_get8(rowg + 4 * q, tag, a.hand_spin, fail);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s8[j] += (float)v[q][j];
-      r.v[0] = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
-      return;
+    if (setup) {
+      r.kind = 2;
+      r.valid[0] = true;
+      if (prefetch_adam) { r.pv[0] = a.params[r.gi[0]]; r.mv[0] = a.exp_avg[r.gi[0]]; r.vv[0] = a.exp_avg_sq[r.gi[0]]; }
     }
+    if (!compute) return;
+    float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+
     // 32 rows per group: four independent 16-byte loads in flight before any add
     // (a one-load-per-iteration loop made this wave the tail kernel's straggler)
     for (int b0 = 0; b0 < Bp; b0 += 32) {
@@ -1027,6 +973,14 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
   };
   if ((int)blockIdx.x >= kTiles) {  // small parameters (block-uniform branch)
     const int sblk = (int)blockIdx.x - kTiles;
+    if (mode == kFused || mode == kFusedDP || mode == kAdam) {
+      // the H1pre slot the head consumed (cn[3] ^ 1) is zero for the step after
+      // this one to accumulate into (the one-launch step relies on it)
+      const int Bp = (a.B + 31) / 32 * 32;
+      uint4* z = reinterpret_cast<uint4*>(a.h1pre + (cn[3] ^ 1) * (int64_t)Bp * a.L1);
+      const int nz = Bp * a.L1 / 2, nsb = (int)gridDim.x - kTiles;
+      for (int i = sblk * NT + tid; i < nz; i += nsb * NT) z[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
     if (mode == kAdam) {
       scalars();
       __syncthreads();
@@ -1205,168 +1159,219 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
 }
 
 // ---------------------------------------------------------------------------
-// One-launch step (kind Step1; world size 1, B <= 32): block 0 runs the head,
-// blocks [1, 50) the W1 tiles, the rest the small parameters (one task per wave),
-// all in ONE launch.  The tile / small blocks issue everything that does not
-// depend on this step's head at once -- Adam state, W1 / X[t] tiles, the next
-// batch's gather (u8 -> bf16, parked in xring / yring), Adam scalars -- and then
-// poll the head's granules, so the two-launch step's kernel boundary and the
-// tail's load phase leave the critical path.  Same arithmetic, operand order and
-// device state as head + tail (bitwise-identical steps; tests/test_mlp3.py).
+// One-launch step (kind Step1; world size 1, B <= 32).  The head's serial chain
+// (H1 -> layers 2/3 -> loss -> dH2 -> dH1, ~4 us, latency-bound on one CU) is
+// REPLICATED: every block of the launch runs it on its own CU from the same
+// inputs (bitwise-identical results: fixed reduction orders), keeps H1^T / H2^T /
+// dZ^T / dH2^T / dH1^T in its LDS and goes straight on to its own tail role --
+//   block 0          loss stats + the state advance,
+//   blocks [1, 50)   one W1 column tile each (dW1, Adam, X[t+1] gather, H1pre[t+1] partial),
+//   the rest         the small parameters (one dW2 / dW3 tile or 64 biases per wave).
+// No activation crosses a CU, so the two-launch step's kernel boundary and its
+// tail's load phase (the tile's Adam state, X tiles and the next batch's gather
+// are issued before the head pass) leave the critical path.
 //
-// State: every non-head block reads counters[0..5) + the sequence number once,
-// then acknowledges with an agent atomic whose operand depends on the loaded
-// values; the head rewrites the state (both copies) only after all
-// acknowledgements, so no block can see a half-advanced state.
+// Ordering (the only cross-block traffic): every block reads the state
+// (counters, H1pre, labels, weights) and then adds one acknowledgement to
+// hand[kHandAck] (monotonic).  Whoever overwrites something another block reads
+// -- the small blocks (weights / biases), block 0 (counters, the consumed H1pre
+// slot) -- first waits for launch `seq`'s (seq + 1) * gridDim.x acks.  The W1
+// tiles write nothing another block reads (the head reads H1pre, not W1) and
+// never wait.  Invariant kept by every step kind: the H1pre slot the tiles add
+// into (slot ^ 1) is zero when a step starts (block 0 / the two-launch tail
+// zero the consumed slot; prime zeroes both).
 // ---------------------------------------------------------------------------
 template <int L1, int L2>
 struct One {
+  using C = Cfg3<32, L1, L2>;
   static constexpr int NTASK = SmallTasks<L1, L2>::NTASK;
   static constexpr int NSMALL = (NTASK + kWaves - 1) / kWaves;
-  static constexpr size_t tile_lds = (size_t)(2 * 32 + L1) * kXSS * 2 + 64;
-  static constexpr size_t head_lds = Cfg3<32, L1, L2>::total;
-  static constexpr size_t lds = head_lds > tile_lds ? head_lds : tile_lds;
+  // after the head's region: H2^T, dH2^T, dH1^T images, then the tile's X / W1 slices + Adam scalars
+  static constexpr size_t oImg = C::total;
+  static constexpr size_t oTile = oImg + (size_t)(2 * L2 + L1) * C::TS * 2;
+  static constexpr size_t lds = oTile + (size_t)(2 * 32 + L1) * kXSS * 2 + 64;
 };
+static_assert(One<128, 256>::lds <= 160 * 1024, "one-launch LDS budget");
 
-template <int L1, int L2>
-__device__ __forceinline__ void one_tile(const MLP3Args& a, int kt, char* smem) {
-  constexpr int TN1 = L1 / 16, Bp = 32;
-  __bf16* sX = reinterpret_cast<__bf16*>(smem);
-  __bf16* sXn = sX + Bp * kXSS;
-  __bf16* sW = sXn + Bp * kXSS;
-  AdamScal* sh_o = reinterpret_cast<AdamScal*>(sW + L1 * kXSS);
-  const int tid = threadIdx.x, lane = tid & 63, ct = tid >> 6, r16 = lane & 15, g = lane >> 4;
-  const bool mw = ct < TN1;  // waves owning a 16-neuron column of the tile
-  if (a.stamps && kt == 0 && tid == 0) a.stamps[8] = __builtin_amdgcn_s_memrealtime();
-  const int64_t c0 = a.counters[0], cursor = a.counters[1], slot = a.counters[3], ob = a.counters[4];
-  const int64_t seq = a.counters[kSeq];
-  if (tid == 0) {
-    const long long inc = ((c0 | cursor | slot | ob | seq) >= 0) ? 1 : 2;  // operand depends on every load
-    __hip_atomic_fetch_add(reinterpret_cast<long long*>(a.hand + kHandAck), inc, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-  }
-  const uint32_t tag = (uint32_t)(seq + 1);
-  const int B = a.B;
-  const int m = ct * 16 + r16, pix = kt * 16 + 4 * g;
-  const int64_t gidx = (int64_t)m * kD + pix;
-  F4 p4{}, m4{}, v4{};
-  if (mw) {
-    p4 = *reinterpret_cast<const F4*>(a.params + gidx);
-    m4 = *reinterpret_cast<const F4*>(a.exp_avg + gidx);
-    v4 = *reinterpret_cast<const F4*>(a.exp_avg_sq + gidx);
-  }
-  const float lr_now = a.lr_ptr ? a.lr_ptr[0] : a.lr;
-  __bf16* XR = reinterpret_cast<__bf16*>(a.xring);
-  constexpr int64_t tile_elems = (int64_t)Bp * 16;
-  // X[t] (parked by the previous step) -> sX; X[t+1] gathered -> sXn + xring[slot ^ 1]
-  if (tid < Bp) {
-    const __bf16* cur = XR + (slot * kTiles + kt) * tile_elems + tid * 16;
-    *reinterpret_cast<bf16x8*>(sX + tid * kXSS) = ld8(cur);
-    *reinterpret_cast<bf16x8*>(sX + tid * kXSS + 8) = ld8(cur + 8);
-  } else if (tid < 2 * Bp) {
-    const int b = tid - Bp;
-    int64_t nc = cursor + 1, nob = ob;
-    if (nc >= a.n_batches) { nc = 0; nob ^= 1; }
-    const int64_t* idx = a.order + nob * a.order_stride + nc * B;
-    bf16x8 lo = zero8(), hi = zero8();
-    int y = -1;
-    if (b < B) {
-      const int64_t s = idx[b];
-      u8x16_to_bf16(*reinterpret_cast<const uint4*>(a.x_u8 + s * kD + kt * 16), lo, hi);
-      if (kt == 0) y = (int)a.labels[s];
-    }
-    *reinterpret_cast<bf16x8*>(sXn + b * kXSS) = lo;
-    *reinterpret_cast<bf16x8*>(sXn + b * kXSS + 8) = hi;
-    __bf16* nx = XR + ((slot ^ 1) * kTiles + kt) * tile_elems + b * 16;
-    *reinterpret_cast<bf16x8*>(nx) = lo;
-    *reinterpret_cast<bf16x8*>(nx + 8) = hi;
-    if (kt == 0) a.yring[(slot ^ 1) * Bp + b] = y;
-  }
-  if (tid == 0) adam_scalars(*sh_o, a.advance_step ? c0 + 1 : c0, lr_now, a.beta1, a.beta2, a.eps, a.weight_decay,
-                             a.adamw);
-  __syncthreads();
-  if (a.stamps && kt == 0 && tid == 0) a.stamps[9] = __builtin_amdgcn_s_memrealtime();
-  stamp_max(a, 5);
-
-  int fail = 0;
-  bf16x4 w4;
-  if (mw) {
-    // dW1 tile: D[pixel pix+i][neuron m] = sum_b X[b][pix+i] dH1[b][m]
-    const int q = r16 >> 2, pp = r16 & 3;
-    const bf16x4 lo = tr_read(sX + (8 * g + q) * kXSS + 4 * pp);
-    const bf16x4 hi = tr_read(sX + (8 * g + 4 + q) * kXSS + 4 * pp);
-    const bf16x8 afrag = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-    const bf16x8 bfrag = hand_get8(a.hand + kHandDH1 + m * 16 + 4 * g, tag, a.hand_spin, &fail);
-    const f32x4 acc = mfma16(afrag, bfrag, f32x4{0.f, 0.f, 0.f, 0.f});
-    const AdamScal o = *sh_o;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      p4.v[i] = adam1(p4.v[i], acc[i], m4.v[i], v4.v[i], o);
-      w4[i] = (__bf16)p4.v[i];
-    }
-    *reinterpret_cast<F4*>(a.params + gidx) = p4;
-    *reinterpret_cast<F4*>(a.exp_avg + gidx) = m4;
-    *reinterpret_cast<F4*>(a.exp_avg_sq + gidx) = v4;
-    *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.shadow) + gidx) = w4;
-    *reinterpret_cast<bf16x4*>(sW + m * kXSS + 4 * g) = w4;
-  }
-  __syncthreads();
-  if (mw) {
-    // next step's layer-1 partial: H1pre[b][m] += sum_{16 px} X'[b][px] W1[m][px]
-    unsigned long long* h1 = reinterpret_cast<unsigned long long*>(a.h1pre + (slot ^ 1) * (int64_t)Bp * L1);
-    const bf16x8 bfrag = (g < 2) ? ld8(sW + (ct * 16 + r16) * kXSS + 8 * g) : zero8();
-#pragma unroll
-    for (int mt = 0; mt < Bp / 16; ++mt) {
-      const bf16x8 afrag = (g < 2) ? ld8(sXn + (mt * 16 + r16) * kXSS + 8 * g) : zero8();
-      const f32x4 d = mfma16(afrag, bfrag, f32x4{0.f, 0.f, 0.f, 0.f});
-      unsigned long long* dst = h1 + (int64_t)((mt * TN1 + ct) * 4) * 64 + lane;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) atomicAdd(dst + i * 64, f32_to_fixed(d[i]));
+// lane 0 waits for launch `seq`'s acknowledgements, then the whole block proceeds
+__device__ __forceinline__ void one_wait_acks(const MLP3Args& a, int64_t seq, int* sh_fail) {
+  if (threadIdx.x == 0) {
+    const long long target = (long long)(seq + 1) * (long long)gridDim.x;
+    const long long* ack = reinterpret_cast<const long long*>(a.hand + kHandAck);
+    int64_t n = 0;
+    *sh_fail = 0;
+    while (__hip_atomic_load(ack, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (++n > a.hand_spin) {
+        *sh_fail = 1;
+        __hip_atomic_store(a.hand + kHandErr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
     }
   }
-  if (fail) __hip_atomic_store(a.hand + kHandErr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (a.stamps && kt == 0 && tid == 0) a.stamps[10] = __builtin_amdgcn_s_memrealtime();
-  stamp_max(a, 11);
-}
-
-template <int L1, int L2>
-__device__ __forceinline__ void one_small(const MLP3Args& a, int sblk, char* smem) {
-  AdamScal* sh_o = reinterpret_cast<AdamScal*>(smem);
-  const int tid = threadIdx.x;
-  const int64_t c0 = a.counters[0], seq = a.counters[kSeq];
-  if (tid == 0) {
-    const long long inc = ((c0 | seq) >= 0) ? 1 : 2;
-    __hip_atomic_fetch_add(reinterpret_cast<long long*>(a.hand + kHandAck), inc, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-  }
-  const uint32_t tag = (uint32_t)(seq + 1);
-  const float lr_now = a.lr_ptr ? a.lr_ptr[0] : a.lr;
-  int fail = 0;
-  SmallRes r;
-  small_compute<L1, L2, true>(a, true, sblk * kWaves + (tid >> 6), r, tag, &fail);
-  if (tid == 0) adam_scalars(*sh_o, a.advance_step ? c0 + 1 : c0, lr_now, a.beta1, a.beta2, a.eps, a.weight_decay,
-                             a.adamw);
   __syncthreads();
-  // the head has read every weight / bias of this step before `done`
-  if (r.kind >= 0) hand_wait(a.hand + kHandDone, tag, a.hand_spin, &fail);
-  small_finalize<L1, L2>(a, true, r, *sh_o);
-  if (fail) __hip_atomic_store(a.hand + kHandErr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  stamp_max(a, 11);
 }
 
 template <int L1, int L2>
 __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
+  using C = typename One<L1, L2>::C;
+  using S = SmallTasks<L1, L2>;
+  constexpr int TN1 = L1 / 16, Bp = 32;
   __shared__ __attribute__((aligned(16))) char smem[One<L1, L2>::lds];
-  const int b = blockIdx.x;
-  if (b == 0) head_body<32, L1, L2, false, true>(a, smem);
-  else if (b <= kTiles) one_tile<L1, L2>(a, b - 1, smem);
-  else one_small<L1, L2>(a, b - 1 - kTiles, smem);
+  __shared__ int sh_fail;
+  __bf16* sH2T = (__bf16*)(smem + One<L1, L2>::oImg);
+  __bf16* sDH2T = sH2T + L2 * C::TS;
+  __bf16* sDH1T = sDH2T + L2 * C::TS;
+  __bf16* sX = (__bf16*)(smem + One<L1, L2>::oTile);
+  __bf16* sXn = sX + Bp * kXSS;
+  __bf16* sW = sXn + Bp * kXSS;
+  AdamScal* sh_o = reinterpret_cast<AdamScal*>(sW + L1 * kXSS);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r16 = lane & 15, g = lane >> 4;
+  const int blk = blockIdx.x;
+  const bool tile = blk >= 1 && blk <= kTiles, small = blk > kTiles;
+  const int kt = blk - 1;
+  if (a.stamps && blk == 1 && tid == 0) a.stamps[8] = __builtin_amdgcn_s_memrealtime();
+
+  // the state of this step: nobody overwrites it before every block's ack
+  const int64_t c0 = ld_state(a.counters, 0), cursor = ld_state(a.counters, 1);
+  const int64_t slot = ld_state(a.counters, 3), ob = ld_state(a.counters, 4);
+  const int64_t seq = ld_state(a.counters, kSeq);
+  const int B = a.B;
+
+  // ---- tail-role loads that need nothing from this step, issued before the head
+  // pass and consumed after it (unconditional, clamped addresses: no wait here) ----
+  const int m = w * 16 + r16, pix = kt * 16 + 4 * g;
+  const bool mw = tile && w < TN1;  // tile waves owning a 16-neuron column
+  const int64_t gidx = mw ? (int64_t)m * kD + pix : 0;
+  F4 p4 = *reinterpret_cast<const F4*>(a.params + gidx);
+  F4 m4 = *reinterpret_cast<const F4*>(a.exp_avg + gidx);
+  F4 v4 = *reinterpret_cast<const F4*>(a.exp_avg_sq + gidx);
+  SmallRes r;
+  r.kind = -1;
+  const int task = (blk - 1 - kTiles) * kWaves + w;
+  if (small) small_compute<L1, L2, true>(a, true, task, r);  // setup + Adam state prefetch
+  const float lr_now = a.lr_ptr ? a.lr_ptr[0] : a.lr;
+  // wave 0 of a tile: row (lane & 31) of X[t] (parked by the previous step) and the
+  // sample index of row (lane & 31) of the NEXT batch (its pixels load after the head pass)
+  __bf16* XR = reinterpret_cast<__bf16*>(a.xring);
+  constexpr int64_t tile_elems = (int64_t)Bp * 16;
+  const int xb = lane & 31;
+  bf16x8 xc0 = zero8(), xc1 = zero8();
+  int64_t si = 0;
+  int64_t nc = cursor + 1, nob = ob;
+  if (nc >= a.n_batches) { nc = 0; nob ^= 1; }
+  if (tile && w == 0) {  // wave-uniform
+    const __bf16* cur = XR + (slot * kTiles + kt) * tile_elems + xb * 16;
+    xc0 = ld8(cur);
+    xc1 = ld8(cur + 8);
+    si = a.order[nob * a.order_stride + nc * B + (xb < B ? xb : 0)];
+  }
+  if (tid == 0 && blk > 0)
+    adam_scalars(*sh_o, a.advance_step ? c0 + 1 : c0, lr_now, a.beta1, a.beta2, a.eps, a.weight_decay, a.adamw);
+
+  // ---- the serial chain, on this CU ----
+  head_body<32, L1, L2, false, true>(a, smem);
+
+  // every load of this step's state has been consumed (head_body ends on a barrier)
+  if (tid == 0)
+    __hip_atomic_fetch_add(reinterpret_cast<long long*>(a.hand + kHandAck), 1ll, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  if (a.stamps && blk == 1 && tid == 0) a.stamps[9] = __builtin_amdgcn_s_memrealtime();
+
+  if (tile) {
+    uint4 xn = make_uint4(0u, 0u, 0u, 0u);
+    int yn = -1;
+    if (w == 0) {
+      if (lane < 32) {
+        *reinterpret_cast<bf16x8*>(sX + xb * kXSS) = xc0;
+        *reinterpret_cast<bf16x8*>(sX + xb * kXSS + 8) = xc1;
+      }
+      // the next batch's pixels (+ label, tile 0): in flight during dW1 / Adam
+      xn = *reinterpret_cast<const uint4*>(a.x_u8 + si * kD + kt * 16);
+      if (kt == 0) yn = (int)a.labels[si];
+    }
+    __syncthreads();
+    bf16x4 w4;
+    if (mw) {
+      // dW1 tile: D[pixel pix+i][neuron m] = sum_b X[b][pix+i] dH1[b][m]
+      const int q = r16 >> 2, pp = r16 & 3;
+      const bf16x4 lo = tr_read(sX + (8 * g + q) * kXSS + 4 * pp);
+      const bf16x4 hi = tr_read(sX + (8 * g + 4 + q) * kXSS + 4 * pp);
+      const bf16x8 afrag = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      const f32x4 acc = mfma16(afrag, ld8(sDH1T + m * C::TS + 8 * g), f32x4{0.f, 0.f, 0.f, 0.f});
+      const AdamScal o = *sh_o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        p4.v[i] = adam1(p4.v[i], acc[i], m4.v[i], v4.v[i], o);
+        w4[i] = (__bf16)p4.v[i];
+      }
+      *reinterpret_cast<F4*>(a.params + gidx) = p4;
+      *reinterpret_cast<F4*>(a.exp_avg + gidx) = m4;
+      *reinterpret_cast<F4*>(a.exp_avg_sq + gidx) = v4;
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.shadow) + gidx) = w4;
+      *reinterpret_cast<bf16x4*>(sW + m * kXSS + 4 * g) = w4;
+    }
+    if (w == 0 && lane >= 32) {
+      // X[t+1] row xb -> sXn, parked in xring[slot ^ 1] for the next step (+ its labels, tile 0)
+      bf16x8 lo = zero8(), hi = zero8();
+      if (xb < B) u8x16_to_bf16(xn, lo, hi);
+      *reinterpret_cast<bf16x8*>(sXn + xb * kXSS) = lo;
+      *reinterpret_cast<bf16x8*>(sXn + xb * kXSS + 8) = hi;
+      __bf16* nx = XR + ((slot ^ 1) * kTiles + kt) * tile_elems + xb * 16;
+      *reinterpret_cast<bf16x8*>(nx) = lo;
+      *reinterpret_cast<bf16x8*>(nx + 8) = hi;
+      if (kt == 0) a.yring[(slot ^ 1) * Bp + xb] = xb < B ? yn : -1;
+    }
+    __syncthreads();
+    if (mw) {
+      // next step's layer-1 partial: H1pre[b][m] += sum_{16 px} X'[b][px] W1[m][px]
+      unsigned long long* h1 = reinterpret_cast<unsigned long long*>(a.h1pre + (slot ^ 1) * (int64_t)Bp * L1);
+      const bf16x8 bfrag = (g < 2) ? ld8(sW + (w * 16 + r16) * kXSS + 8 * g) : zero8();
+#pragma unroll
+      for (int mt = 0; mt < Bp / 16; ++mt) {
+        const bf16x8 afrag = (g < 2) ? ld8(sXn + (mt * 16 + r16) * kXSS + 8 * g) : zero8();
+        const f32x4 d = mfma16(afrag, bfrag, f32x4{0.f, 0.f, 0.f, 0.f});
+        unsigned long long* dst = h1 + (int64_t)((mt * TN1 + w) * 4) * 64 + lane;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) atomicAdd(dst + i * 64, f32_to_fixed(d[i]));
+      }
+    }
+    if (a.stamps && blk == 1 && tid == 0) a.stamps[10] = __builtin_amdgcn_s_memrealtime();
+  } else if (small) {
+    const RepLds L{(const __bf16*)(smem + C::oH1T), sH2T, sDH2T, (const __bf16*)(smem + C::odZT), sDH1T, C::TS};
+    small_compute<L1, L2, true>(a, true, task, r, &L);
+    one_wait_acks(a, seq, &sh_fail);  // every block has read the weights / biases this overwrites
+    small_finalize<L1, L2>(a, true, r, *sh_o);
+  } else {
+    // block 0: stats, the consumed H1pre slot zeroed (the invariant), then the advanced state
+    one_wait_acks(a, seq, &sh_fail);
+    uint4* z = reinterpret_cast<uint4*>(a.h1pre + slot * (int64_t)Bp * L1);
+    for (int i = tid; i < Bp * L1 / 2; i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (tid == 0) {
+      const float* misc = (const float*)(smem + C::oMisc);
+      const int64_t t = c0 + 1;
+      int64_t nc = cursor + 1, nob = ob;
+      if (nc >= a.n_batches) { nc = 0; nob ^= 1; }
+      const int64_t st[kCnt] = {a.advance_step ? t : t - 1, nc, cursor, slot ^ 1, nob};
+      for (int k = 0; k < kCnt; ++k) a.counters[k] = a.counters[kCnt + k] = st[k];
+      a.counters[kSeq] = seq + 1;
+      if (a.stats) {
+        float* sr = a.stats + (int)((t - 1) % (a.stats_ring > 0 ? a.stats_ring : 1)) * 4;
+        sr[0] = misc[0] * (1.f / (float)B);
+        sr[1] = misc[1];
+        sr[2] = misc[2];
+        sr[3] = (float)t;
+      }
+      if (a.stamps) a.stamps[4] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+  stamp_max(a, 11);
 }
 
 template <int L1, int L2>
 int dispatch3(const MLP3Args& a, int kind, hipStream_t stream) {
   if (kind == kMLP3Step1) {
-    if (a.B > 32 || !a.hand) return -5;
+    if (a.B > 32 || !a.hand || 1 + kTiles + One<L1, L2>::NSMALL > 256) return -5;
     hipLaunchKernelGGL((mlp3_one_kernel<L1, L2>), dim3(1 + kTiles + One<L1, L2>::NSMALL), dim3(kThreads), 0, stream,
                        a);
     return 0;
@@ -1404,7 +1409,7 @@ static_assert(fits3<kHeadRows, 128, 256>(), "v3 head LDS budget");
 }  // namespace
 
 int mlp3_act_rows(int L1, int L2) { return L1 + 2 * L2 + 16; }
-int64_t mlp3_hand_words(int L1, int L2) { return hand_act_base(L1) + (int64_t)(L1 + 2 * L2 + 16) * 16; }
+int64_t mlp3_hand_words(int, int) { return kHandWords; }
 
 int launch_mlp3(const MLP3Args& a, int kind, hipStream_t stream) {
   if (a.B > kBMax || a.B < 1) return -2;

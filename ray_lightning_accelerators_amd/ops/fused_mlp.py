@@ -172,8 +172,8 @@ ONE_LAUNCH_MAX_B = 32  # MLP3_STEP1: one head workgroup
 
 
 def mlp3_hand_words(L1: int, L2: int) -> int:
-    """int64 words of the one-launch step's in-launch hand-off buffer (csrc/mlp_step3.hip)."""
-    return 48 + (L1 + L1 + 2 * L2 + 16) * 16
+    """int64 words of the one-launch step's acknowledgement / error buffer (csrc/mlp_step3.hip)."""
+    return 32
 W1_TILES = IN_FEATURES // 16
 
 
@@ -190,7 +190,7 @@ def mlp3_buffers(L1: int, L2: int, B: int, device) -> Dict[str, torch.Tensor]:
         # [0, 5) current state, [5, 10) the head's advanced copy (published by the tail),
         # [10] the one-launch step's launch sequence number (its hand-off tag)
         "counters": torch.zeros(16, dtype=torch.int64, device=device),
-        # one-launch step: acknowledgement / error words + tagged granules (head -> tiles)
+        # one-launch step: [0] per-block state acknowledgements (monotonic), [16] wait-timeout flag
         "hand": torch.zeros(mlp3_hand_words(L1, L2), dtype=torch.int64, device=device),
         # per-head-workgroup (sum NLL, #correct, #rows, -) when the batch spans several
         "head_part": torch.zeros(bp // 32 * 4, device=device),
@@ -239,8 +239,8 @@ def mlp3_launch(
     caller zeroes ``h1pre`` first), MLP3_STEP_DP (head + tail whose Adam epilogue
     sums the gradient tiles of all ranks over xGMI itself; ``dp_ctx`` is
     ``NativeCommunicator.dp_context``), MLP3_STEP1 (the whole step in ONE launch,
-    world size 1, B <= 32: the tail's blocks run beside the head and take its
-    activations as tagged granules from ``hand``).  ``order`` is [2, n_batches * B]:
+    world size 1, B <= 32: every block replays the head's serial chain on its own
+    CU and then does its tail share; ``hand`` holds the blocks' acknowledgements).  ``order`` is [2, n_batches * B]:
     the current and the next epoch's sample order (counters[4] selects)."""
     require().mlp3(
         int(kind), x_u8, labels, order, counters, int(n_batches), int(B), int(L1), int(L2), params, grads, exp_avg,
