@@ -551,11 +551,15 @@ def run_rank(args):
     if rank == 0:
         default_cfg = (args.layer_1, args.layer_2, args.batch_size) == (32, 64, 32)
         base_impl, base = None, None
-        if not rn and default_cfg and n_ranks == 1 and dev.type == "cuda":
+        if not rn and default_cfg and dev.type == "cuda":
             known = {k: v for k, v in STOCK_BASELINE.items() if v}
             if known:
                 base_impl = max(known, key=known.get)
                 base = known[base_impl]
+                if n_ranks > 1:
+                    # no stock N-GPU measurement here: the 1-GPU stock number scaled
+                    # linearly (an upper bound for stock DDP, so the ratio is conservative)
+                    base_impl, base = f"{base_impl} x{n_ranks} (ideal linear)", round(base * n_ranks, 1)
         out = {
             "metric": RESNET_METRIC if rn else METRIC,
             "value": round(value, 1),

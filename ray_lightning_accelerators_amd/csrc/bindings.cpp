@@ -175,7 +175,7 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
           double beta1, double beta2, double eps, double weight_decay, double grad_scale, optional<Tensor> lr_t,
           bool adamw, optional<Tensor> stamps, std::vector<int64_t> dp_ctx, optional<Tensor> head_part,
           optional<Tensor> hand) {
-  TORCH_CHECK(kind >= 0 && kind <= 6, "mlp3: bad kind ", kind);
+  TORCH_CHECK(kind >= 0 && kind <= 7, "mlp3: bad kind ", kind);
   TORCH_CHECK(rla::mlp_supported((int)L1, (int)L2), "no fused MLP kernel for layer sizes ", L1, "/", L2);
   TORCH_CHECK(B >= 1 && B <= 256, "fused MLP step supports 1 <= batch <= 256");
   const int64_t np = mlp_param_count(L1, L2);
@@ -230,7 +230,7 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
   a.stats_ring = a.stats ? (int)(stats->numel() / 4) : 0;
   a.head_part = ptr_or_null<float>(head_part, "head_part", at::kFloat, (Bp / 32) * 4);
   TORCH_CHECK(B <= 32 || a.head_part != nullptr, "mlp3: batches above 32 rows need head_part [ceil(B/32), 4]");
-  if (kind == rla::kMLP3Step1) {
+  if (kind == rla::kMLP3Step1 || kind == rla::kMLP3Step1DP) {
     TORCH_CHECK(B <= 32, "the one-launch step handles batches of up to 32 rows");
     TORCH_CHECK(counters.numel() >= 16, "the one-launch step needs counters of >= 16 int64 (launch sequence)");
     a.hand = reinterpret_cast<unsigned long long*>(
@@ -246,7 +246,7 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
   a.lr_ptr = ptr_or_null<const float>(lr_t, "lr", at::kFloat, 1);
   a.adamw = adamw;
   a.stamps = ptr_or_null<int64_t>(stamps, "stamps", at::kLong, 16);
-  if (kind == rla::kMLP3StepDP) {
+  if (kind == rla::kMLP3StepDP || kind == rla::kMLP3Step1DP) {
     // [world, rank, stride, spin, gen_ptr, err_ptr, region_ptr x world] from the comm engine
     TORCH_CHECK(dp_ctx.size() >= 6 && dp_ctx[0] >= 1 && dp_ctx[0] <= 8 && (int64_t)dp_ctx.size() == 6 + dp_ctx[0],
                 "mlp3 StepDP needs the comm engine's aux_context()");
@@ -266,6 +266,9 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
     const std::string pr = proto ? proto : "granule";
     a.dp_lite = pr == "all" ? 0 : (pr == "wave" ? 1 : 2);
     if (a.dp_lite == 2 && a.dp_stride < 2 * np) a.dp_lite = 1;  // area too small for granules
+    TORCH_CHECK(kind != rla::kMLP3Step1DP || a.dp_lite == 2,
+                "the one-launch data-parallel step exchanges tagged granules only (RLA_DP_PROTO=granule, "
+                "a receive area of 2 floats per parameter)");
   }
   TORCH_CHECK(rla::launch_mlp3(a, (int)kind, cur_stream(params)) == 0, "fused MLP v3 launch failed");
 }

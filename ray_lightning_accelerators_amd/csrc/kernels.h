@@ -188,7 +188,7 @@ struct MLP3Args {
   int64_t hand_spin;
 };
 enum MLP3Kind { kMLP3Step = 0, kMLP3Head = 1, kMLP3TailGrad = 2, kMLP3TailAdam = 3, kMLP3Prime = 4,
-                kMLP3StepDP = 5, kMLP3Step1 = 6 };
+                kMLP3StepDP = 5, kMLP3Step1 = 6, kMLP3Step1DP = 7 };
 int64_t mlp3_hand_words(int L1, int L2);  // int64 words of the one-launch step's hand-off buffer
 int launch_mlp3(const MLP3Args& a, int kind, hipStream_t stream);
 int mlp3_act_rows(int L1, int L2);

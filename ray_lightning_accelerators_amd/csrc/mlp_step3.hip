@@ -1212,7 +1212,10 @@ __device__ __forceinline__ void one_wait_acks(const MLP3Args& a, int64_t seq, in
   __syncthreads();
 }
 
-template <int L1, int L2>
+// DP (kind Step1DP, world size > 1): each tile's dW1 and each small wave's values
+// are allreduced over xGMI (tagged granules, as the two-launch StepDP tail) between
+// the block's gradient and its Adam -- the exchange sits inside the one launch.
+template <int L1, int L2, bool DP>
 __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
   using C = typename One<L1, L2>::C;
   using S = SmallTasks<L1, L2>;
@@ -1292,13 +1295,29 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
     }
     __syncthreads();
     bf16x4 w4;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     if (mw) {
       // dW1 tile: D[pixel pix+i][neuron m] = sum_b X[b][pix+i] dH1[b][m]
       const int q = r16 >> 2, pp = r16 & 3;
       const bf16x4 lo = tr_read(sX + (8 * g + q) * kXSS + 4 * pp);
       const bf16x4 hi = tr_read(sX + (8 * g + 4 + q) * kXSS + 4 * pp);
       const bf16x8 afrag = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-      const f32x4 acc = mfma16(afrag, ld8(sDH1T + m * C::TS + 8 * g), f32x4{0.f, 0.f, 0.f, 0.f});
+      acc = mfma16(afrag, ld8(sDH1T + m * C::TS + 8 * g), acc);
+    }
+    if constexpr (DP) {  // the tile's allreduce: push to every rank, fixed rank-order sum
+      __shared__ uint32_t sh_dgen;
+      const int dslot = dp_begin(a, &sh_dgen);
+      const uint32_t gen = sh_dgen;
+      int fail = 0;
+      if (mw) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dp_push_gran(a, dslot, gidx + i, acc[i], gen);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] = dp_sum_gran(a, dslot, gidx + i, gen, &fail) * a.grad_scale;
+      }
+      dp_gran_end(a, gen, fail, &sh_fail);
+    }
+    if (mw) {
       const AdamScal o = *sh_o;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -1340,6 +1359,19 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
   } else if (small) {
     const RepLds L{(const __bf16*)(smem + C::oH1T), sH2T, sDH2T, (const __bf16*)(smem + C::odZT), sDH1T, C::TS};
     small_compute<L1, L2, true>(a, true, task, r, &L);
+    if constexpr (DP) {
+      __shared__ uint32_t sh_sgen;
+      const int dslot = dp_begin(a, &sh_sgen);
+      const uint32_t gen = sh_sgen;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (r.valid[i]) dp_push_gran(a, dslot, r.gi[i], r.v[i], gen);
+      int fail = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (r.valid[i]) r.v[i] = dp_sum_gran(a, dslot, r.gi[i], gen, &fail) * a.grad_scale;
+      dp_gran_end(a, gen, fail, &sh_fail);
+    }
     one_wait_acks(a, seq, &sh_fail);  // every block has read the weights / biases this overwrites
     small_finalize<L1, L2>(a, true, r, *sh_o);
   } else {
@@ -1370,10 +1402,18 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
 
 template <int L1, int L2>
 int dispatch3(const MLP3Args& a, int kind, hipStream_t stream) {
+  constexpr int kOneGrid = 1 + kTiles + One<L1, L2>::NSMALL;
   if (kind == kMLP3Step1) {
-    if (a.B > 32 || !a.hand || 1 + kTiles + One<L1, L2>::NSMALL > 256) return -5;
-    hipLaunchKernelGGL((mlp3_one_kernel<L1, L2>), dim3(1 + kTiles + One<L1, L2>::NSMALL), dim3(kThreads), 0, stream,
-                       a);
+    if (a.B > 32 || !a.hand || kOneGrid > 256) return -5;
+    hipLaunchKernelGGL((mlp3_one_kernel<L1, L2, false>), dim3(kOneGrid), dim3(kThreads), 0, stream, a);
+    return 0;
+  }
+  if (kind == kMLP3Step1DP) {
+    // granule exchange only (the flag protocols stay on the two-launch StepDP)
+    if (a.B > 32 || !a.hand || kOneGrid > kDpMaxBlocks || a.dp_lite != 2 || a.dp_world < 1 ||
+        a.dp_world > kXgmiMaxRanks || !a.dp_gen || !a.dp_err || a.dp_stride < 2 * Off<L1, L2>::NP)
+      return -6;
+    hipLaunchKernelGGL((mlp3_one_kernel<L1, L2, true>), dim3(kOneGrid), dim3(kThreads), 0, stream, a);
     return 0;
   }
   constexpr int NT = 64 * (L1 / 16);

@@ -523,7 +523,9 @@ class Trainer:
         meta = self._results.get("_meta", {})
         out = {}
         for name, vals in store.items():
-            v = torch.stack([x.float().mean().cpu() for x in vals]).mean()
+            # reduced where the values live: one device tensor, no host sync per value
+            dev = vals[0].device
+            v = torch.stack([x.float().mean().to(dev) for x in vals]).mean()
             prog_bar, logger, on_step, on_epoch = meta.get(name, (False, True, False, True))
             key = f"{name}_epoch" if on_step else name
             out[key] = v

@@ -167,8 +167,8 @@ def mlp_refresh_shadow(params: torch.Tensor, shadow: torch.Tensor, L1: int, L2: 
         shadow[lay["w3t"]: lay["total"]].copy_(w3t.reshape(-1))
 
 
-MLP3_STEP, MLP3_HEAD, MLP3_TAIL_GRAD, MLP3_TAIL_ADAM, MLP3_PRIME, MLP3_STEP_DP, MLP3_STEP1 = range(7)
-ONE_LAUNCH_MAX_B = 32  # MLP3_STEP1: one head workgroup
+MLP3_STEP, MLP3_HEAD, MLP3_TAIL_GRAD, MLP3_TAIL_ADAM, MLP3_PRIME, MLP3_STEP_DP, MLP3_STEP1, MLP3_STEP1_DP = range(8)
+ONE_LAUNCH_MAX_B = 32  # MLP3_STEP1 / MLP3_STEP1_DP: one head workgroup
 
 
 def mlp3_hand_words(L1: int, L2: int) -> int:
@@ -240,7 +240,10 @@ def mlp3_launch(
     sums the gradient tiles of all ranks over xGMI itself; ``dp_ctx`` is
     ``NativeCommunicator.dp_context``), MLP3_STEP1 (the whole step in ONE launch,
     world size 1, B <= 32: every block replays the head's serial chain on its own
-    CU and then does its tail share; ``hand`` holds the blocks' acknowledgements).  ``order`` is [2, n_batches * B]:
+    CU and then does its tail share; ``hand`` holds the blocks' acknowledgements), MLP3_STEP1_DP
+    (MLP3_STEP1 for world size > 1: each block allreduces its gradient values over xGMI as
+    tagged granules between its gradient and its Adam; ``dp_ctx`` as for MLP3_STEP_DP,
+    receive area >= 2 floats per parameter).  ``order`` is [2, n_batches * B]:
     the current and the next epoch's sample order (counters[4] selects)."""
     require().mlp3(
         int(kind), x_u8, labels, order, counters, int(n_batches), int(B), int(L1), int(L2), params, grads, exp_avg,

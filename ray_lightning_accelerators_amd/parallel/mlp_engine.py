@@ -12,11 +12,13 @@ re-designed for MI355X instead of translating PL's DDP loop:
 * parameters, gradients and Adam state are flat fp32 arenas; the whole model's
   gradient is ONE allreduce bucket (27,882 floats = 109 KiB at the default
   32/64 config -- far below the ~1 MiB where splitting pays on 7 xGMI links);
-* world size 1: TWO launches per step (csrc/mlp_step3.hip: head + 49-workgroup
-  tail; Adam fused into both, the next step's layer 1 computed by the tail);
-  world size > 1: with a ``dp_context`` the same two launches, the tail
-  exchanging each gradient tile with the peers over xGMI inside its Adam
-  epilogue (kind StepDP); otherwise head -> tail(grad) -> allreduce(SUM) ->
+* world size 1: ONE launch per step for B <= 32 (csrc/mlp_step3.hip kind Step1:
+  every block replays the serial head chain on its own CU, then does its tail
+  share), else TWO (head + 49-workgroup tail; Adam fused into both, the next
+  step's layer 1 computed by the tail);
+  world size > 1: with a ``dp_context`` the same launches, each block exchanging
+  its gradient values with the peers over xGMI inside its Adam epilogue (kinds
+  Step1DP / StepDP); otherwise head -> tail(grad) -> allreduce(SUM) ->
   tail(adam), the 1/world average folded into ``grad_scale``;
 * the step's device work can be captured into a hipGraph (``capture``): batch
   cursor, step counter, ring slot and epoch buffer live on the device, so
@@ -125,6 +127,11 @@ class FusedMLPEngine:
         # world size 1, B <= 32: the whole step as ONE launch (RLA_MLP_ONE_LAUNCH=0: head + tail)
         self.one_launch = (self.B <= fused_mlp.ONE_LAUNCH_MAX_B
                            and os.environ.get("RLA_MLP_ONE_LAUNCH", "1") != "0")
+        # world size > 1 with the xGMI context: the same one launch, exchanging tagged
+        # granules (needs the granule protocol and a receive area of 2 floats / parameter)
+        self.one_launch_dp = (self.one_launch and self.dp_ctx is not None
+                              and os.environ.get("RLA_DP_PROTO", "granule") == "granule"
+                              and self.dp_ctx[2] >= 2 * n)
         self.stats = torch.zeros(stats_ring, 4, device=self.device)
         self.seed = seed
         self.epoch = 0
@@ -284,7 +291,8 @@ class FusedMLPEngine:
                 kind = fused_mlp.MLP3_STEP1 if self.one_launch else fused_mlp.MLP3_STEP
                 fused_mlp.mlp3_launch(kind, stats=self.stats, **kw)
             elif self.dp_ctx is not None:
-                fused_mlp.mlp3_launch(fused_mlp.MLP3_STEP_DP, stats=self.stats, grad_scale=1.0 / self.world_size,
+                kind = fused_mlp.MLP3_STEP1_DP if self.one_launch_dp else fused_mlp.MLP3_STEP_DP
+                fused_mlp.mlp3_launch(kind, stats=self.stats, grad_scale=1.0 / self.world_size,
                                       dp_ctx=self.dp_ctx, **kw)
             else:
                 fused_mlp.mlp3_launch(fused_mlp.MLP3_HEAD, stats=self.stats, **kw)

@@ -348,8 +348,10 @@ def _gpu_worker(rank, world, port, q, mode):
             ctx = comm.dp_context(2 * 27882)  # tagged-granule receive area
             res["dp_ctx"] = ctx is not None
 
+            bsz = int(os.environ.get("RLA_TEST_DP_BATCH", "64"))  # <= 32: the one-launch DP step
+
             def make(dp):
-                e = FusedMLPEngine(32, 64, 64, lr=1e-2, device=dev, world_size=world, rank=rank,
+                e = FusedMLPEngine(32, 64, bsz, lr=1e-2, device=dev, world_size=world, rank=rank,
                                    allreduce=comm.allreduce_, dp_context=ctx if dp else None)
                 e.set_data(xs, ys, shuffle=True)
                 return e
@@ -364,6 +366,7 @@ def _gpu_worker(rank, world, port, q, mode):
             else:
                 e_dp, e_ref = make(True), make(False)
                 res["dp_mode"] = e_dp.dp_ctx is not None
+                res["one_launch_dp"] = e_dp.one_launch_dp
                 e_dp.run(6)
                 e_ref.run(6)
                 torch.cuda.synchronize()
@@ -380,6 +383,7 @@ def _gpu_worker(rank, world, port, q, mode):
                 res["match_graph"] = bool(torch.allclose(e_dp.params, e_ref.params, atol=1e-5, rtol=0))
                 res["params"] = e_dp.params.cpu().numpy().tobytes()  # no shared-memory fds through the queue
                 comm.check()
+                e_dp.check()
         elif mode == "timeout":
             x = torch.ones(1024, device=dev)
             if rank == 0:
@@ -466,13 +470,16 @@ def test_xgmi_dead_peer_times_out_instead_of_hanging():
 
 
 @gpu
-@pytest.mark.parametrize("proto", ["granule", "wave"])
-def test_fused_dp_mlp_step_matches_split_allreduce(proto, monkeypatch):
-    # granule: tagged 8-byte words, no fences (default); wave: flags + one fencing wave
+@pytest.mark.parametrize("proto,batch", [("granule", 64), ("wave", 64), ("granule", 32), ("wave", 32)])
+def test_fused_dp_mlp_step_matches_split_allreduce(proto, batch, monkeypatch):
+    # granule: tagged 8-byte words, no fences (default); wave: flags + one fencing wave.
+    # batch 32 + granule: the one-launch DP step (kind Step1DP); otherwise head + DP tail
     monkeypatch.setenv("RLA_DP_PROTO", proto)
+    monkeypatch.setenv("RLA_TEST_DP_BATCH", str(batch))
     out = _run_gpu("mlp_dp")
     for r, res in out.items():
         assert res["dp_ctx"] and res["dp_mode"], (r, res)
+        assert res["one_launch_dp"] == (batch <= 32 and proto == "granule"), (r, res)
         assert res["match"] and res["match_graph"], (r, {k: v for k, v in res.items() if k != "params"})
         assert res["graph"]
     # replicas stay bitwise identical (every rank sums the tiles in rank order)
@@ -480,7 +487,9 @@ def test_fused_dp_mlp_step_matches_split_allreduce(proto, monkeypatch):
 
 
 @gpu
-def test_fused_dp_mlp_step_dead_peer_times_out():
+@pytest.mark.parametrize("batch", [64, 32])
+def test_fused_dp_mlp_step_dead_peer_times_out(batch, monkeypatch):
+    monkeypatch.setenv("RLA_TEST_DP_BATCH", str(batch))
     out = _run_gpu("mlp_dp_timeout")
     assert out[0]["state"] == 1 and out[1]["state"] == 0, out
 
