@@ -243,7 +243,9 @@ def make_native(args, world, rank, dev, x, y, force_split=False):
     def replica_checksum():
         return float(eng.params.double().sum()) + 1e-3 * float(eng.params.double().abs().sum())
 
-    info = {"route": route, "hip_graph_steps": gsteps if graphed else 0}
+    one = eng.native and (eng.one_launch_dp if world > 1 else eng.one_launch)
+    info = {"route": route, "hip_graph_steps": gsteps if graphed else 0,
+            "step_kernel": ("one-launch" if one else "head+tail") if eng.native else "torch-cpu"}
     return eng.run, (lambda: float(eng.recent_stats(20)[:, 0].mean())), replica_checksum, info
 
 
