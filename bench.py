@@ -607,6 +607,25 @@ def run_rank(args):
 
 
 # -------------------------------------------------------------- trainer
+def _sync_debug() -> None:
+    """Print the call stack of each distinct implicit host<->device synchronisation
+    (torch's sync debug mode; explicit torch.cuda.synchronize() is not reported)."""
+    import traceback
+    import warnings
+
+    seen = set()
+
+    def show(msg, cat, filename, lineno, file=None, line=None):
+        stack = "".join(traceback.format_stack(limit=10)[:-2])
+        if stack not in seen and len(seen) < 30:
+            seen.add(stack)
+            print(f"[sync-debug] {msg}\n{stack}", file=sys.stderr, flush=True)
+
+    warnings.showwarning = show
+    warnings.simplefilter("always")
+    torch.cuda.set_sync_debug_mode("warn")
+
+
 class _EpochClock(Callback):
     """Callback: wall-clock of every epoch from one epoch start to the next (so an
     epoch's time includes its validation pass, checkpoint write and logging),
@@ -712,8 +731,21 @@ def run_trainer(args):
         trainer = pl.Trainer(default_root_dir=root, max_epochs=args.trainer_epochs, gpus=int(gpu),
                              progress_bar_refresh_rate=0, callbacks=[clock], accelerator=acc)
         t0 = time.perf_counter()
+        if os.environ.get("RLA_SYNC_DEBUG") == "1" and gpu:
+            _sync_debug()  # report every implicit host<->device sync of an in-process fit
+        prof_path = os.environ.get("RLA_BENCH_CPROFILE")  # host profile of an in-process fit
+        if prof_path:
+            import cProfile
+            import pstats
+
+            pr = cProfile.Profile()
+            pr.enable()
         assert trainer.fit(model) == 1
         fit_s = time.perf_counter() - t0
+        if prof_path:
+            pr.disable()
+            with open(prof_path, "w") as f:
+                pstats.Stats(pr, stream=f).sort_stats("tottime").print_stats(45)
     finally:
         if started:
             ray.shutdown()

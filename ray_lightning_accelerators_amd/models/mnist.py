@@ -307,11 +307,12 @@ class FusedMNISTStep:
 
     def _graph_steps(self) -> int:
         """Steps per captured graph: the Trainer cuts dispatches at multiples of
-        ``log_every_n_steps``, so the largest divisor of it up to 32 (25 for the
-        default 50) makes a typical chunk whole replays (with 8-step graphs a
-        50-step chunk was 6 replays + 2 eager steps)."""
+        ``log_every_n_steps``, so the largest divisor of it up to the stats ring
+        (64; 50 for the default 50) makes a typical chunk ONE replay (a graph
+        launch costs the host tens of us; the engine's 1/2/4/... remainder
+        graphs cover the chunks cut short by validation or the epoch end)."""
         every = max(1, int(getattr(self.trainer, "log_every_n_steps", 50) or 50))
-        for g in range(min(32, every), 3, -1):
+        for g in range(min(self.max_chunk, every), 3, -1):
             if every % g == 0:
                 return g
         return 8
@@ -320,7 +321,7 @@ class FusedMNISTStep:
         """``n_steps`` consecutive resident-mode steps in one dispatch (hipGraph
         replays of ``graph_steps`` steps each, captured once per epoch); the
         Trainer uses it when nothing observes individual batches.  Returns the
-        per-step ``{"loss"}`` outputs (rows of one device gather, no host sync)."""
+        per-step ``{"loss"}`` outputs (views of one device copy, no host sync)."""
         if graph_steps is None:
             graph_steps = self._graph_steps()
         eng = self.eng
@@ -329,7 +330,7 @@ class FusedMNISTStep:
         eng.lr, eng.betas, eng.eps, eng.wd = self.lr_val, tuple(g["betas"]), g["eps"], g["weight_decay"]
         done = 0
         if graph_steps > 1 and eng._graph is None and not self._capture_failed and get_config().use_hip_graph \
-                and n_steps > graph_steps and eng.steps_to_epoch_end() > graph_steps:
+                and n_steps >= graph_steps and eng.steps_to_epoch_end() >= graph_steps:
             # one real (warm-up) step, then the recording; identical on every rank
             self._capture_failed = not eng.capture(graph_steps)
             done = 1
@@ -342,21 +343,23 @@ class FusedMNISTStep:
                 st["step"].fill_(float(self.gs.step))
         ring = eng.stats.size(0)
         k = min(n_steps, ring)
-        # Snapshot the whole ring in step order (the ring wraps in later chunks) and
-        # keep the last k rows as a view.  The gather is the SAME size every chunk:
-        # a chunk-sized gather picked a different ROCm index kernel for small
-        # chunks, and loading that kernel's code object the first time one
-        # appeared stalled that epoch by ~60 ms (profiles/r2_c05).  The slot list
-        # is built on the device: a host list would be a blocking H2D copy per chunk.
-        if getattr(self, "_ring_ar", None) is None or self._ring_ar.numel() != ring:
-            self._ring_ar = torch.arange(ring, device=self.dev)
-        slots = (self._ring_ar + (first + n_steps)) % ring
-        rows = eng.stats.index_select(0, slots)[ring - k:]
+        # Rows of the chunk's last k steps, in step order: step first + 1 + i sits in
+        # ring slot (first + i) % ring, which the host knows -- so one or two
+        # contiguous device-to-device copies into a fresh tensor (the ring wraps in
+        # later chunks).  No index kernel: a chunk-sized gather picked a different
+        # ROCm index kernel for small chunks, whose code object loaded mid-epoch and
+        # stalled it by ~60 ms (profiles/r2_c05); no host sync either.
+        s0 = (first + n_steps - k) % ring
+        n1 = min(k, ring - s0)
+        rows = torch.empty(k, 4, device=self.dev)
+        rows[:n1].copy_(eng.stats[s0:s0 + n1])
+        if n1 < k:
+            rows[n1:].copy_(eng.stats[: k - n1])
         last = rows[-1]
         self.model.log("ptl/train_loss", last[0])
         self.model.log("ptl/train_accuracy", last[1] / last[2].clamp(min=1))
         self.trainer.callback_metrics["loss"] = last[0]
-        return [{"loss": rows[i, 0]} for i in range(k)]
+        return [{"loss": v} for v in rows[:, 0].unbind(0)]
 
     # ---------------------------------------------------------- validation
     def eval_compatible(self, model) -> bool:

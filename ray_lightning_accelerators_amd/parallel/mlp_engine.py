@@ -139,6 +139,7 @@ class FusedMLPEngine:
         self.global_step = 0
         self._graph = None
         self._graph_steps = 0
+        self._tail_graphs: Dict[int, "torch.cuda.CUDAGraph"] = {}  # remainder sizes (powers of two)
         self._primed = False
         self._host_epochs = False
         self.x_u8 = self.labels = self.order = None
@@ -186,7 +187,7 @@ class FusedMLPEngine:
             # the captured graph bakes the order pointer and n_batches: only a new
             # shape forces a re-capture, a new epoch of the same shape reuses it
             self.order = torch.empty(2, order.numel(), dtype=torch.int64, device=self.device)
-            self._graph = None
+            self._drop_graphs()
         if order.device.type == "cpu" and self.native:
             # staged through a pinned buffer: an async H2D copy instead of a blocking
             # pageable one; the previous epoch's copy must be done before reuse
@@ -227,7 +228,7 @@ class FusedMLPEngine:
         self._publish_counters()
         self.epoch = 0
         self.step_in_epoch = 0
-        self._graph = None
+        self._drop_graphs()
         self._primed = False
 
     def _fill_order(self, epoch: int) -> None:
@@ -339,8 +340,18 @@ class FusedMLPEngine:
     def steps_to_epoch_end(self) -> int:
         return self.n_batches - self.step_in_epoch
 
-    def capture(self, steps_per_graph: int = 1) -> bool:
-        """Capture ``steps_per_graph`` consecutive steps into one hipGraph."""
+    def _drop_graphs(self) -> None:
+        self._graph = None
+        self._tail_graphs = {}
+
+    def capture(self, steps_per_graph: int = 1, remainders: bool = True) -> bool:
+        """Capture ``steps_per_graph`` consecutive steps into one hipGraph.
+
+        ``remainders``: also capture 1, 2, 4, ... step graphs below it, so a
+        dispatch that is not a multiple of ``steps_per_graph`` (the Trainer's
+        chunks end at log / validation / epoch boundaries) runs as a few replays
+        instead of eager launches (~40 us of host work per eager step against
+        ~9 us of GPU time, so eager remainders starved the GPU)."""
         if not self.native:
             return False
         s = torch.cuda.Stream()
@@ -350,22 +361,45 @@ class FusedMLPEngine:
             self._device_step()
         torch.cuda.current_stream().wait_stream(s)
         self._advance_host(1)
-        g = torch.cuda.CUDAGraph()
-        try:
+
+        def record(n: int):
+            g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
-                for _ in range(steps_per_graph):
+                for _ in range(n):
                     self._device_step()
+            return g
+
+        try:
+            g = record(steps_per_graph)
         except Exception:
-            self._graph = None
+            self._drop_graphs()
             return False
         self._graph = g
         self._graph_steps = steps_per_graph
+        self._tail_graphs = {}
+        if remainders:
+            k = 1
+            while k < steps_per_graph:
+                try:
+                    self._tail_graphs[k] = record(k)  # capture only: the device state does not move
+                except Exception:
+                    break
+                k *= 2
         return True
 
-    def _graph_ok(self, remaining: int) -> bool:
-        k = self._graph_steps
+    def _graph_ok(self, remaining: int, k: Optional[int] = None) -> bool:
+        k = self._graph_steps if k is None else k
         return (self._graph is not None and self._primed and remaining >= k
                 and self.step_in_epoch + k <= self.n_batches)
+
+    def _pick_graph(self, remaining: int):
+        """The largest captured graph that fits the remaining steps (and the epoch)."""
+        if self._graph_ok(remaining):
+            return self._graph, self._graph_steps
+        for k in sorted(self._tail_graphs, reverse=True):
+            if self._graph_ok(remaining, k):
+                return self._tail_graphs[k], k
+        return None, 1
 
     def step(self) -> None:
         """Run one (or ``steps_per_graph`` when captured) optimizer step(s)."""
@@ -379,14 +413,13 @@ class FusedMLPEngine:
     def run(self, n_steps: int) -> None:
         done = 0
         while done < n_steps:
-            if self._graph_ok(n_steps - done):
-                self._graph.replay()
-                self._advance_host(self._graph_steps)
-                done += self._graph_steps
+            g, k = self._pick_graph(n_steps - done)
+            if g is not None:
+                g.replay()
             else:
                 self._device_step()
-                self._advance_host(1)
-                done += 1
+            self._advance_host(k)
+            done += k
 
     # --------------------------------------------------------------- export
     def recent_stats(self, n: int = 1) -> torch.Tensor:

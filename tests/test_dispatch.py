@@ -161,7 +161,10 @@ def test_fused_mnist_chunked_dispatch_matches_per_batch(tmpdir):
         assert tr._fused is not None and tr._fused.eng is not None
         assert tr.global_step == 260
         if spd > 1:
-            assert tr._fused.eng._graph is not None or tr._fused._capture_failed is False
+            # the chunks (50, 50, 30 steps) run as replays of the 50-step graph and the
+            # 1/2/4/.../32-step remainder graphs
+            assert tr._fused.eng._graph is not None and not tr._fused._capture_failed
+            assert tr._fused.eng._graph_steps == 50 and sorted(tr._fused.eng._tail_graphs) == [1, 2, 4, 8, 16, 32]
         res[spd] = ({k: v.detach().cpu().clone() for k, v in model.state_dict().items()},
                     float(tr.callback_metrics["ptl/train_loss"]))
     for k, v in res[1][0].items():

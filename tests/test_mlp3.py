@@ -247,19 +247,22 @@ def test_mlp3_one_launch_interleaves_with_two_launch():
 
 
 @gpu
-def test_mlp3_graph_replay_matches_eager():
+@pytest.mark.parametrize("nb,gsteps,remainders", [(5, 3, False), (5, 3, True), (7, 5, True)])
+def test_mlp3_graph_replay_matches_eager(nb, gsteps, remainders):
     dev = _dev()
-    # 5 batches per epoch, 3 steps per graph: replays, eager remainders and
-    # several epoch switches
-    x, y = _data(32 * 5 + 8, seed=5)
+    # nb batches per epoch, gsteps steps per graph: replays, remainders (eager, or
+    # replays of the 1/2/4-step graphs) and several epoch switches
+    x, y = _data(32 * nb + 8, seed=5)
     a = FusedMLPEngine(32, 64, 32, lr=1e-3, device=dev)
     b = FusedMLPEngine(32, 64, 32, lr=1e-3, device=dev)
     a.set_data(x, y)
     b.set_data(x, y)
-    assert b.capture(3)
+    assert b.capture(gsteps, remainders=remainders)
+    assert sorted(b._tail_graphs) == ([k for k in (1, 2, 4) if k < gsteps] if remainders else [])
     a.run(1)  # capture() ran one real step
     a.run(23)
-    b.run(23)
+    for n in (6, 1, 9, 7):  # dispatches that are not multiples of gsteps
+        b.run(n)
     torch.cuda.synchronize()
     assert a.global_step == b.global_step == 24
     assert torch.equal(a.counters.cpu(), b.counters.cpu())
