@@ -746,6 +746,8 @@ def run_trainer(args):
             pr.disable()
             with open(prof_path, "w") as f:
                 pstats.Stats(pr, stream=f).sort_stats("tottime").print_stats(45)
+                # the framework's own functions by cumulative time (per-chunk costs)
+                pstats.Stats(pr, stream=f).sort_stats("cumulative").print_stats("ray_lightning_accelerators_amd", 60)
     finally:
         if started:
             ray.shutdown()

@@ -68,8 +68,8 @@ class CSVLogger(LightningLoggerBase):
     def log_metrics(self, metrics: Dict[str, Any], step: Optional[int] = None) -> None:
         if self.rank != 0:
             return
-        row = {k: (float(v.detach().float().mean()) if isinstance(v, torch.Tensor) else v)
-               for k, v in metrics.items()}
+        row = {k: ((float(v) if v.numel() == 1 else float(v.detach().float().mean()))
+                   if isinstance(v, torch.Tensor) else v) for k, v in metrics.items()}
         row["step"] = step
         for k in row:
             if k not in self._keys:

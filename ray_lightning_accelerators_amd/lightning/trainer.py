@@ -18,6 +18,8 @@ from __future__ import annotations
 import gc
 import math
 import os
+import sys
+import time
 from collections import defaultdict
 from typing import Any, Dict, List, Optional, Sequence, Union
 
@@ -551,36 +553,44 @@ class Trainer:
 
     def _flush_logger(self, defer: bool = False) -> None:
         """Hand ``logged_metrics`` to the logger.  ``defer`` (multi-step dispatch):
-        device values are copied to the host asynchronously and written once their
-        copy has landed -- a log point never waits for the GPU queue to drain
-        (only a backlog of more than a few unfinished snapshots does)."""
+        the device values are only referenced (no copy, no wait) and written, in
+        step order, at the next blocking flush (validation / epoch end, which sync
+        anyway) with ONE batched device->host transfer for all of them.  A
+        per-log-point D2H copy made the host wait for the GPU queue at every
+        50-step dispatch chunk (the host then could not run ahead, and its ~0.5 ms
+        of per-chunk work showed up as GPU idle time)."""
         self._write_pending_log(block=not defer)
         if self.logger is None or not self.logged_metrics or not self.is_global_zero:
             return
         metrics = dict(self.logged_metrics)
         if defer and any(isinstance(v, torch.Tensor) and v.is_cuda for v in metrics.values()):
-            snap = {k: (v.detach().to("cpu", non_blocking=True) if isinstance(v, torch.Tensor) and v.is_cuda else v)
-                    for k, v in metrics.items()}
-            ev = torch.cuda.Event()
-            ev.record()
+            snap = {k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in metrics.items()}
             if self._pending_log is None:
                 self._pending_log = []
-            self._pending_log.append((snap, self.global_step, ev))
+            self._pending_log.append((snap, self.global_step))
             return
         self.logger.log_metrics(metrics, step=self.global_step)
 
     def _write_pending_log(self, block: bool = True) -> None:
-        """Write deferred snapshots in step order: all of them (``block``), else the
-        ones whose copy has completed, plus the oldest while more than 4 wait."""
+        """Write the deferred snapshots in step order (``block``, or once more than
+        1024 are held), their device values fetched by one batched transfer."""
         pending = self._pending_log or []
-        while pending:
-            snap, step, ev = pending[0]
-            if not block and len(pending) <= 4 and not ev.query():
-                break
-            ev.synchronize()
-            pending.pop(0)
+        if not pending or (not block and len(pending) <= 1024):
+            return
+        dev_vals = [(i, k, v) for i, (snap, _) in enumerate(pending) for k, v in snap.items()
+                    if isinstance(v, torch.Tensor) and v.is_cuda]
+        if dev_vals:
+            flat = torch.cat([v.reshape(-1).to(torch.float64) for _, _, v in dev_vals]).cpu()
+            vals = flat.tolist()
+            off = 0
+            for i, k, v in dev_vals:
+                n = v.numel()
+                # scalars as Python floats (what the logger records), tensors re-shaped
+                pending[i][0][k] = vals[off] if n == 1 else flat[off: off + n].reshape(v.shape).to(v.dtype)
+                off += n
+        for snap, step in pending:
             self.logger.log_metrics(snap, step=step)
-        self._pending_log = pending or None
+        self._pending_log = None
 
     # ---------------------------------------------------------- evaluation
     def run_sanity_check(self, model: LightningModule) -> None:
@@ -820,8 +830,13 @@ class Trainer:
         every = max(1, self.log_every_n_steps)
         bsz = int(getattr(self._fused, "_B", 0))
         validated = False
+        # RLA_CHUNK_TIMING=1 (diagnostic): host time per chunk vs the GPU time
+        # between chunk-end events, reported at the epoch end (which syncs anyway)
+        timing = [] if os.environ.get("RLA_CHUNK_TIMING") == "1" and torch.cuda.is_available() else None
         b = 0
         while b < n:
+            if timing is not None:
+                h0 = time.perf_counter()
             e = b
             while True:
                 e += 1
@@ -841,14 +856,36 @@ class Trainer:
                     fn(self, model, outs, k, k * bsz)
             if self.global_step % every == 0:
                 self._flush_logger(defer=True)
+            if timing is not None:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                timing.append((k, time.perf_counter() - h0, ev, getattr(self._fused, "_last_run_us", 0.0)))
             is_last = e >= n or (self.max_steps is not None and self.global_step >= self.max_steps)
             if self._should_validate(e - 1, is_last):
+                if timing is not None:
+                    self._report_chunk_timing(timing)
+                    timing = None
                 self.run_evaluation(test_mode=False)
                 validated = True
             if is_last or self.should_stop:
                 break
             b = e
+        if timing:
+            self._report_chunk_timing(timing)
         return validated
+
+    @staticmethod
+    def _report_chunk_timing(timing) -> None:
+        torch.cuda.synchronize()
+        host = sorted(t[1] * 1e6 for t in timing)
+        run = sorted(t[3] for t in timing)
+        gpu = sorted(a[2].elapsed_time(b[2]) * 1e3 / b[0] for a, b in zip(timing, timing[1:]))
+        if gpu:
+            print(f"[chunk-timing] chunks={len(timing)} host_us_per_chunk_median={host[len(host) // 2]:.1f} "
+                  f"engine_run_us_median={run[len(run) // 2]:.1f} "
+                  f"host_us_max={host[-1]:.1f} gpu_us_per_step_median={gpu[len(gpu) // 2]:.3f} "
+                  f"gpu_us_per_step_max={gpu[-1]:.3f} steps={sum(t[0] for t in timing)}", file=sys.stderr,
+                  flush=True)
 
     def _eval_batch_hooks_overridden(self, model: LightningModule) -> bool:
         names = ("on_validation_batch_start", "on_validation_batch_end")

@@ -20,11 +20,12 @@ kernel; CPU / unsupported shapes use the ordinary autograd path.
 from __future__ import annotations
 
 import os
+import time
 from typing import Any, Dict, Optional
 
 import torch
 import torch.nn.functional as F
-from torch.utils.data import DataLoader, DistributedSampler, SequentialSampler, Subset, random_split
+from torch.utils.data import DataLoader, DistributedSampler, RandomSampler, SequentialSampler, Subset, random_split
 
 from ..config import get_config
 from ..lightning import LightningModule
@@ -147,6 +148,20 @@ def _sampler_order(sampler) -> torch.Tensor:
         return idx[sampler.rank:total:sampler.num_replicas].contiguous()
     if isinstance(sampler, SequentialSampler):
         return torch.arange(len(sampler.data_source))
+    if type(sampler) is RandomSampler and not sampler.replacement:
+        # torch.utils.data.RandomSampler.__iter__ without replacement: the same
+        # global-RNG seed draw (when no generator is set) and the same randperm calls
+        n = len(sampler.data_source)
+        if sampler.generator is None:
+            seed = int(torch.empty((), dtype=torch.int64).random_().item())
+            generator = torch.Generator()
+            generator.manual_seed(seed)
+        else:
+            generator = sampler.generator
+        m = sampler.num_samples
+        parts = [torch.randperm(n, generator=generator) for _ in range(m // n)]
+        parts.append(torch.randperm(n, generator=generator)[: m % n])
+        return torch.cat(parts)
     return torch.as_tensor(list(iter(sampler)), dtype=torch.int64)
 
 
@@ -219,9 +234,19 @@ class FusedMNISTStep:
         return eng
 
     # ---------------------------------------------------------- data plane
+    def _source(self, dataset):
+        """``_u8_source`` resolved once per dataset object: rebuilding random_split's
+        55K-int index list as a tensor every epoch cost ~2 ms of host time while
+        the GPU sat idle at the epoch start."""
+        cache = self.__dict__.setdefault("_src_cache", {})
+        ent = cache.get(id(dataset))
+        if ent is None or ent[0] is not dataset:
+            ent = cache[id(dataset)] = (dataset, _u8_source(dataset))
+        return ent[1]
+
     def make_epoch_batches(self, dl, n_batches: int):
         """Resident-data mode: upload this epoch's sampler order once; yield batch indices."""
-        src = _u8_source(dl.dataset)
+        src = self._source(dl.dataset)
         if src is None or dl.batch_size is None:
             return None
         images, targets, idx_map = src
@@ -334,7 +359,9 @@ class FusedMNISTStep:
             # one real (warm-up) step, then the recording; identical on every rank
             self._capture_failed = not eng.capture(graph_steps)
             done = 1
+        t_run = time.perf_counter()
         eng.run(n_steps - done)
+        self._last_run_us = (time.perf_counter() - t_run) * 1e6  # diagnostic (RLA_CHUNK_TIMING)
         first = self.gs.step
         self.gs.step += n_steps
         for q in g["params"]:
@@ -388,7 +415,7 @@ class FusedMNISTStep:
         validation_step + validation_epoch_end produce -- or None when the loader
         cannot be served from the resident data (the Trainer then runs the
         per-batch loop)."""
-        src = _u8_source(dl.dataset)
+        src = self._source(dl.dataset)
         if src is None or dl.batch_size is None or n_batches <= 0:
             return None
         images, targets, idx_map = src

@@ -188,3 +188,30 @@ def test_sampler_order_matches_iteration(shuffle, drop_last, world, rank):
         assert torch.equal(_sampler_order(s), torch.tensor(list(iter(s)))), epoch
     q = SequentialSampler(ds)
     assert torch.equal(_sampler_order(q), torch.tensor(list(iter(q))))
+
+
+@pytest.mark.parametrize("num_samples", [None, 500, 2500])
+@pytest.mark.parametrize("with_generator", [False, True])
+def test_random_sampler_order_matches_iteration(num_samples, with_generator):
+    """RandomSampler (world size 1's shuffled loader): the tensor rebuild draws the
+    same seed / permutations as iterating, and leaves the global RNG in the same state."""
+    from torch.utils.data import RandomSampler
+
+    from ray_lightning_accelerators_amd.models.mnist import _sampler_order
+
+    ds = RandomDataset(4, 1003)
+
+    def make():
+        g = torch.Generator().manual_seed(11) if with_generator else None
+        return RandomSampler(ds, num_samples=num_samples, generator=g)
+
+    torch.manual_seed(5)
+    a, b = make(), make()
+    ref = [torch.tensor(list(iter(a))) for _ in range(2)]
+    after_ref = torch.rand(3)
+    torch.manual_seed(5)
+    got = [_sampler_order(b) for _ in range(2)]
+    after_got = torch.rand(3)
+    for r, o in zip(ref, got):
+        assert torch.equal(r, o)
+    assert torch.equal(after_ref, after_got)
