@@ -66,6 +66,12 @@ class RLAConfig:
     fused_dp: bool = True
     # capture the resident MNIST step into hipGraphs
     use_hip_graph: bool = True
+    # ModelCheckpoint writes run on a background thread (state snapshot taken
+    # synchronously; the Trainer drains the writes before fit() returns).  Off by
+    # default: for a small model the write is pickling under the GIL, so the
+    # thread only competes with the training loop (MNIST epoch-end +0.7 ms,
+    # profiles/r2_c38); it pays when file I/O dominates (large checkpoints)
+    async_checkpoint: bool = False
     # Trainer: fused resident steps issued per host dispatch when nothing observes
     # single batches (chunks also end at log / validation / max_steps boundaries);
     # 1 = one dispatch per batch.  Capped by the fused step's stats ring (64).

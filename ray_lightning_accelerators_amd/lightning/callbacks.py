@@ -190,14 +190,22 @@ class ModelCheckpoint(Callback):
         self.last_global_step_saved = step
 
     def _save(self, trainer, filepath: str) -> None:
-        trainer.save_checkpoint(filepath, weights_only=self.save_weights_only)
+        # background write (RLAConfig.async_checkpoint); the path bookkeeping is synchronous
+        trainer.save_checkpoint(filepath, weights_only=self.save_weights_only, blocking=False)
 
-    def _remove(self, trainer, path: str) -> None:
-        if trainer.is_global_zero and os.path.exists(path):
+    @staticmethod
+    def _remove_file(path: str) -> None:
+        if os.path.exists(path):
             try:
                 os.remove(path)
             except OSError:
                 pass
+
+    def _remove(self, trainer, path: str) -> None:
+        if trainer.is_global_zero:
+            # ordered after the pending background writes (the file may not exist yet)
+            op = getattr(trainer, "file_op", None)
+            op(self._remove_file, path) if op is not None else self._remove_file(path)
 
     def on_save_checkpoint(self, trainer, pl_module, checkpoint=None) -> dict:
         return {"monitor": self.monitor, "best_model_score": self.best_model_score,

@@ -29,7 +29,7 @@ from torch.utils.data import DataLoader, DistributedSampler, RandomSampler, Sequ
 from .callbacks import Callback, EarlyStopping, ModelCheckpoint
 from .core import LightningDataModule, LightningModule, _normalize_optimizers
 from .loggers import CSVLogger, LightningLoggerBase
-from .utilities import atomic_save, load_checkpoint, log, move_to_device, rank_zero_warn
+from .utilities import CheckpointWriter, atomic_save, load_checkpoint, log, move_to_device, rank_zero_warn
 from ..config import get_config
 from ..utils.faults import maybe_inject as maybe_inject_fault
 from ..utils.profiling import resolve_profiler
@@ -319,10 +319,35 @@ class Trainer:
         self._prepare_dataloaders(model)
         return self.run_evaluation(test_mode=False)
 
-    def save_checkpoint(self, filepath: str, weights_only: bool = False) -> None:
+    def save_checkpoint(self, filepath: str, weights_only: bool = False, blocking: bool = True) -> None:
+        """``blocking=False`` (ModelCheckpoint): the checkpoint dict is built now and
+        written by the background writer (``RLAConfig.async_checkpoint``); a
+        blocking save first drains earlier background writes (file order kept)."""
         ckpt = self.checkpoint_connector.dump_checkpoint(weights_only)
-        if self.is_global_zero:
-            atomic_save(ckpt, filepath)
+        if not self.is_global_zero:
+            return
+        if not blocking and get_config().async_checkpoint:
+            if getattr(self, "_ckpt_writer", None) is None:
+                self._ckpt_writer = CheckpointWriter()
+            self._ckpt_writer.save(ckpt, filepath)
+            return
+        self.wait_checkpoints()
+        atomic_save(ckpt, filepath)
+
+    def file_op(self, fn, *args) -> None:
+        """Run a checkpoint-file operation (e.g. a top-k removal) after the pending
+        background writes, in order."""
+        w = getattr(self, "_ckpt_writer", None)
+        if w is not None:
+            w.submit(fn, *args)
+        else:
+            fn(*args)
+
+    def wait_checkpoints(self) -> None:
+        """Block until every background checkpoint write has landed (re-raises a failed one)."""
+        w = getattr(self, "_ckpt_writer", None)
+        if w is not None:
+            w.wait()
 
     # ------------------------------------------------------------- driving
     def _attach(self, model, train_dl, val_dls, test_dls, datamodule) -> None:
@@ -403,7 +428,10 @@ class Trainer:
         mark("fused_step_ready", rank=self.global_rank)
         if self.resume_from_checkpoint and os.path.exists(self.resume_from_checkpoint):
             self.checkpoint_connector.restore(self.resume_from_checkpoint, on_gpu=self.on_gpu)
-        self.run_train()
+        try:
+            self.run_train()
+        finally:
+            self.wait_checkpoints()  # every checkpoint file is on disk when fit returns
         model.teardown("fit")
         return None
 
@@ -1011,6 +1039,7 @@ class Trainer:
         d = self.__dict__.copy()
         d["_fused"] = None
         d["_pending_log"] = None
+        d["_ckpt_writer"] = None
         d["accelerator_backend"] = None
         return d
 

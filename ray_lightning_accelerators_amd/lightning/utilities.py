@@ -58,6 +58,72 @@ def atomic_save(checkpoint: Any, filepath: str) -> None:
         raise
 
 
+def _private_copy(obj: Any) -> Any:
+    """The checkpoint dict with every tensor cloned, so a background write never
+    reads storage the training loop keeps mutating (``.cpu()`` of a CPU tensor is
+    the tensor itself)."""
+    if isinstance(obj, torch.Tensor):
+        return obj.detach().clone()
+    if isinstance(obj, dict):  # dict / OrderedDict (state dicts)
+        return type(obj)((k, _private_copy(v)) for k, v in obj.items())
+    if type(obj) in (list, tuple):
+        return type(obj)(_private_copy(v) for v in obj)
+    return obj
+
+
+class CheckpointWriter:
+    """One background thread that runs checkpoint file operations in submission
+    order (writes and the top-k removals that must follow them), so the epoch-end
+    checkpoint write (~1.7 ms for the MNIST model: pickling + file I/O) overlaps
+    the next epoch's GPU work instead of stalling it.  ``wait()`` drains the
+    queue and re-raises the first error; the Trainer waits before ``fit``
+    returns and before any synchronous save."""
+
+    def __init__(self):
+        import queue
+        import threading
+
+        self._q: "queue.Queue" = queue.Queue()
+        self._err: Optional[BaseException] = None
+        self._t = threading.Thread(target=self._loop, name="rla-ckpt-writer", daemon=True)
+        self._t.start()
+
+    def _loop(self) -> None:
+        while True:
+            item = self._q.get()
+            try:
+                if item is None:
+                    return
+                fn, args = item
+                if self._err is None:
+                    fn(*args)
+            except BaseException as e:  # noqa: BLE001 - surfaced by wait()
+                self._err = e
+            finally:
+                self._q.task_done()
+
+    def submit(self, fn, *args) -> None:
+        self._raise()
+        self._q.put((fn, args))
+
+    def save(self, checkpoint: Any, filepath: str) -> None:
+        self.submit(atomic_save, _private_copy(checkpoint), filepath)
+
+    def wait(self) -> None:
+        self._q.join()
+        self._raise()
+
+    def _raise(self) -> None:
+        if self._err is not None:
+            e, self._err = self._err, None
+            raise RuntimeError(f"background checkpoint write failed: {e!r}") from e
+
+    def close(self) -> None:
+        self.wait()
+        self._q.put(None)
+        self._t.join(timeout=10)
+
+
 def load_checkpoint(path: str, map_location: Any = "cpu") -> dict:
     """Load a Lightning checkpoint.  Files written by this framework contain
     only tensors/containers/primitives, so the safe ``weights_only`` loader is

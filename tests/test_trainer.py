@@ -187,6 +187,34 @@ def test_model_checkpoint_monitor_explicit(tmpdir):
     assert float(mc.best_model_score) == 2.0
 
 
+def test_async_checkpoint_writes_land_before_fit_returns(tmpdir, monkeypatch):
+    """RLAConfig.async_checkpoint: ModelCheckpoint's writes (and its top-k removals)
+    run on the background writer, in order; every file is complete when fit returns."""
+    from ray_lightning_accelerators_amd.config import set_config
+    from ray_lightning_accelerators_amd.lightning.utilities import load_checkpoint
+
+    class M(BoringModel):
+        def validation_step(self, batch, batch_idx):
+            self.log("score", torch.tensor(float(self.current_epoch)))
+            return super().validation_step(batch, batch_idx)
+
+    monkeypatch.setenv("RLA_ASYNC_CHECKPOINT", "1")
+    set_config(None)
+    try:
+        mc = ModelCheckpoint(monitor="score", mode="max")
+        trainer = pl.Trainer(default_root_dir=str(tmpdir), max_epochs=3, limit_train_batches=2, limit_val_batches=1,
+                             callbacks=[mc])
+        trainer.fit(M())
+        assert trainer._ckpt_writer is not None  # the background path ran
+        assert "epoch=2" in os.path.basename(mc.best_model_path)
+        ckpts = [f for f in os.listdir(os.path.dirname(mc.best_model_path)) if f.endswith(".ckpt")]
+        assert ckpts == [os.path.basename(mc.best_model_path)]  # earlier bests removed after their writes
+        ck = load_checkpoint(mc.best_model_path)
+        assert ck["global_step"] == 6 and ck["epoch"] == 3 and ck["state_dict"]  # PL 1.1: epoch + 1
+    finally:
+        set_config(None)
+
+
 @pytest.mark.parametrize("bad", [None])
 def test_seed_everything_env(bad):
     s = pl.seed_everything(42)
