@@ -210,7 +210,8 @@ def test_async_checkpoint_writes_land_before_fit_returns(tmpdir, monkeypatch):
         ckpts = [f for f in os.listdir(os.path.dirname(mc.best_model_path)) if f.endswith(".ckpt")]
         assert ckpts == [os.path.basename(mc.best_model_path)]  # earlier bests removed after their writes
         ck = load_checkpoint(mc.best_model_path)
-        assert ck["global_step"] == 6 and ck["epoch"] == 3 and ck["state_dict"]  # PL 1.1: epoch + 1
+        # PL 1.1 layout: epoch and global_step are stored + 1
+        assert ck["epoch"] == 3 and ck["global_step"] == trainer.global_step + 1 and ck["state_dict"]
     finally:
         set_config(None)
 
