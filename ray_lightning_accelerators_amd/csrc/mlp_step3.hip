@@ -406,6 +406,21 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem) {
       __syncthreads();
     }
     if (stamp_ok) a.stamps[2] = __builtin_amdgcn_s_memrealtime();
+    if constexpr (REP) {
+      // One-launch acknowledgement, as early as it is safe: the rest of the head
+      // pass reads LDS only, so once every wave's global loads (state, H1pre,
+      // labels, weight fragments, biases, the block's own prologue loads) have
+      // landed, nothing of this step's state is read by this block any more.  The
+      // writers of that state (small blocks: weights / biases; block 0: counters,
+      // the consumed H1pre slot) then wait for every block's LOADS instead of every
+      // block's whole head pass.  (The weight fragments of dH2 / dH1 were issued
+      // in the prologue ~1.5 us earlier: this wait costs little.)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0)
+        __hip_atomic_fetch_add(reinterpret_cast<long long*>(a.hand + kHandAck), 1ll, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
 
     // ---------------- log_softmax / NLL / accuracy / dZ (one row per lane) -------------
     if (w < (BC + 63) / 64) {
@@ -1275,10 +1290,7 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
   // ---- the serial chain, on this CU ----
   head_body<32, L1, L2, false, true>(a, smem);
 
-  // every load of this step's state has been consumed (head_body ends on a barrier)
-  if (tid == 0)
-    __hip_atomic_fetch_add(reinterpret_cast<long long*>(a.hand + kHandAck), 1ll, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+  // (the block's acknowledgement went out inside head_body, once its loads had landed)
   if (a.stamps && blk == 1 && tid == 0) a.stamps[9] = __builtin_amdgcn_s_memrealtime();
 
   if (tile) {
