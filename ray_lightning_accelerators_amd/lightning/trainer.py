@@ -1028,7 +1028,7 @@ class Trainer:
     def _model_state_dict(self, model: LightningModule) -> Dict[str, torch.Tensor]:
         if self._fused is not None:
             self._fused.sync_params_to_module()
-        return {k: v.detach().cpu() for k, v in model.state_dict().items()}
+        return _to_cpu(dict(model.state_dict()))
 
     def _optimizer_state_dict(self, opt) -> dict:
         if self._fused is not None and hasattr(self._fused, "optimizer_state_dict"):
@@ -1045,10 +1045,46 @@ class Trainer:
 
 
 def _to_cpu(obj):
-    if isinstance(obj, torch.Tensor):
-        return obj.detach().cpu()
-    if isinstance(obj, dict):
-        return {k: _to_cpu(v) for k, v in obj.items()}
-    if isinstance(obj, (list, tuple)):
-        return type(obj)(_to_cpu(v) for v in obj)
-    return obj
+    """Host copy of a (nested) state dict.  Device tensors move in ONE transfer per
+    dtype (flattened into a device buffer, copied, split into host views) instead of
+    one blocking copy each: a checkpoint of the MNIST model was ~24 synchronous
+    small copies, ResNet-50's ~800."""
+    leaves: List[torch.Tensor] = []
+
+    def collect(o):
+        if isinstance(o, torch.Tensor):
+            if o.device.type != "cpu" and o.numel() > 0:
+                leaves.append(o)
+        elif isinstance(o, dict):
+            for v in o.values():
+                collect(v)
+        elif isinstance(o, (list, tuple)):
+            for v in o:
+                collect(v)
+
+    collect(obj)
+    host: Dict[int, torch.Tensor] = {}
+    groups: Dict[tuple, List[torch.Tensor]] = {}
+    for t in leaves:
+        if id(t) not in host:
+            host[id(t)] = None  # placeholder: de-duplicates a tensor referenced twice
+            groups.setdefault((t.device, t.dtype), []).append(t)
+    for (_, dtype), ts in groups.items():
+        flat = torch.cat([t.detach().reshape(-1) for t in ts]).cpu() if len(ts) > 1 else \
+            ts[0].detach().reshape(-1).cpu()
+        off = 0
+        for t in ts:
+            n = t.numel()
+            host[id(t)] = flat[off: off + n].view(t.shape)
+            off += n
+
+    def rebuild(o):
+        if isinstance(o, torch.Tensor):
+            return host[id(o)] if id(o) in host else o.detach().cpu()
+        if isinstance(o, dict):
+            return {k: rebuild(v) for k, v in o.items()}
+        if isinstance(o, (list, tuple)):
+            return type(o)(rebuild(v) for v in o)
+        return o
+
+    return rebuild(obj)

@@ -10,7 +10,7 @@ if [ "${RLA_CHUNK_PROBE:-0}" = 1 ]; then
   timeout -k 10 300 python scripts/chunk_probe.py > "$O/chunk_probe.log" 2>&1 || { tail -20 "$O/chunk_probe.log"; exit 1; }
   grep -v amdgpu.ids "$O/chunk_probe.log"
 fi
-timeout -k 10 300 python -u -m pytest tests/test_dispatch.py tests/test_trainer.py tests/test_fused_validation.py -x -q -m gpu \
+timeout -k 10 300 python -u -m pytest tests/test_dispatch.py tests/test_trainer.py tests/test_fused_validation.py tests/test_checkpoint_writer.py tests/test_ddp_gpu.py -x -q -m gpu \
   --timeout 180 --timeout-method thread > "$O/pytest.log" 2>&1 || { tail -20 "$O/pytest.log"; exit 1; }
 tail -1 "$O/pytest.log"
 timeout -k 10 300 python bench.py --steps 2000 --warmup 200 > "$O/bench_one.log" 2>&1 || { tail -20 "$O/bench_one.log"; exit 1; }

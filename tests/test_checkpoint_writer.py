@@ -46,3 +46,35 @@ def test_error_surfaces_at_wait(tmp_path):
     with pytest.raises(RuntimeError, match="disk full"):
         w.wait()
     w.close()
+
+
+@pytest.mark.gpu
+def test_batched_state_dict_transfer_matches_per_tensor():
+    """trainer._to_cpu: one transfer per dtype, same values / shapes / dtypes / structure."""
+    from ray_lightning_accelerators_amd.lightning.trainer import _to_cpu
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(0)
+    w = torch.randn(3, 5, generator=g).to(dev)
+    sd = {"state": {0: {"step": torch.tensor(7.0), "exp_avg": w * 2, "exp_avg_sq": torch.randn(4, generator=g).to(dev)},
+                    1: {"idx": torch.arange(5, device=dev), "half": torch.randn(6, generator=g).to(dev).bfloat16()}},
+          "param_groups": [{"lr": 0.1, "params": [0, 1]}], "w": w, "w_again": w, "empty": torch.zeros(0, device=dev),
+          "scalar": torch.tensor(2.5, device=dev), "t": (w[:, 1],)}
+    out = _to_cpu(sd)
+
+    def check(a, b):
+        if isinstance(a, torch.Tensor):
+            assert b.device.type == "cpu" and b.dtype == a.dtype and b.shape == a.shape
+            assert torch.equal(a.cpu(), b)
+        elif isinstance(a, dict):
+            assert a.keys() == b.keys()
+            for k in a:
+                check(a[k], b[k])
+        elif isinstance(a, (list, tuple)):
+            assert type(a) is type(b) and len(a) == len(b)
+            for x, y in zip(a, b):
+                check(x, y)
+        else:
+            assert a == b
+
+    check(sd, out)
