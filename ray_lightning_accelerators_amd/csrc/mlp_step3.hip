@@ -169,8 +169,20 @@ constexpr int kHandAck = 0, kHandErr = 16, kHandWords = 32;
 // H2^T / dH2^T / dH1^T images at OneLds offsets) for the block's own tail role;
 // no H1pre zeroing (invariant: the slot the tiles accumulate into is zero at a
 // step's start), no state advance (block 0 does it after every block's ack).
+// REP: the one-launch tile's loads of the NEXT batch (pixels of sample `si`, tile
+// `kt`, and its label), issued by head_body right after its acknowledgement (its
+// vmcnt(0) has resolved the sample index; the rest of the head pass reads LDS
+// only) by the one wave that uses them, so the round trip hides under the head pass.
+struct RepPre {
+  bool active;  // wave-uniform: wave 0 of a W1 tile block
+  int64_t si;
+  int kt;
+  uint4 xn;
+  int64_t yn;
+};
+
 template <int BC, int L1, int L2, bool MULTI, bool REP>
-__device__ __forceinline__ void head_body(const MLP3Args& a, char* smem) {
+__device__ __forceinline__ void head_body(const MLP3Args& a, char* smem, RepPre* pre = nullptr) {
   using C = Cfg3<BC, L1, L2>;
   using O = Off<L1, L2>;
   using A = Act<L1, L2>;
@@ -420,6 +432,10 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem) {
       if (tid == 0)
         __hip_atomic_fetch_add(reinterpret_cast<long long*>(a.hand + kHandAck), 1ll, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+      if (pre->active) {
+        pre->xn = *reinterpret_cast<const uint4*>(a.x_u8 + pre->si * kD + pre->kt * 16);
+        pre->yn = a.labels[pre->si];
+      }
     }
 
     // ---------------- log_softmax / NLL / accuracy / dZ (one row per lane) -------------
@@ -1287,23 +1303,25 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
   if (tid == 0 && blk > 0)
     adam_scalars(*sh_o, a.advance_step ? c0 + 1 : c0, lr_now, a.beta1, a.beta2, a.eps, a.weight_decay, a.adamw);
 
-  // ---- the serial chain, on this CU ----
-  head_body<32, L1, L2, false, true>(a, smem);
+  // ---- the serial chain, on this CU (tile wave 0 also issues the next batch's loads) ----
+  RepPre pre;
+  pre.active = tile && w == 0;
+  pre.si = si;
+  pre.kt = tile ? kt : 0;
+  pre.xn = make_uint4(0u, 0u, 0u, 0u);
+  pre.yn = -1;
+  head_body<32, L1, L2, false, true>(a, smem, &pre);
 
   // (the block's acknowledgement went out inside head_body, once its loads had landed)
   if (a.stamps && blk == 1 && tid == 0) a.stamps[9] = __builtin_amdgcn_s_memrealtime();
 
   if (tile) {
-    uint4 xn = make_uint4(0u, 0u, 0u, 0u);
-    int yn = -1;
-    if (w == 0) {
-      if (lane < 32) {
-        *reinterpret_cast<bf16x8*>(sX + xb * kXSS) = xc0;
-        *reinterpret_cast<bf16x8*>(sX + xb * kXSS + 8) = xc1;
-      }
-      // the next batch's pixels (+ label, tile 0): in flight during dW1 / Adam
-      xn = *reinterpret_cast<const uint4*>(a.x_u8 + si * kD + kt * 16);
-      if (kt == 0) yn = (int)a.labels[si];
+    // the next batch's pixels (+ label, tile 0) were issued inside the head pass
+    const uint4 xn = pre.xn;
+    const int yn = (int)pre.yn;
+    if (w == 0 && lane < 32) {
+      *reinterpret_cast<bf16x8*>(sX + xb * kXSS) = xc0;
+      *reinterpret_cast<bf16x8*>(sX + xb * kXSS + 8) = xc1;
     }
     __syncthreads();
     bf16x4 w4;
