@@ -68,6 +68,12 @@ STOCK_BASELINE = {
     "torch": 53015.0,        # eager nn.Linear + torch.optim.Adam (profiles/r1_first/bench_torch.jsonl)
     "torch-graph": 165417.2,  # the same step under torch.cuda.graph, 8 steps/graph (profiles/r2_c03)
 }
+# where each hard-coded number was measured (printed in the JSON next to it;
+# ``--compare-stock`` re-measures the eager stock step inside the same job)
+STOCK_BASELINE_SOURCE = {
+    "torch": "profiles/r1_first/bench_torch.jsonl (round 1, one MI355X, 2000 steps)",
+    "torch-graph": "profiles/r2_c03/bench_torch_graph.log (round 2, one MI355X, 2000 steps)",
+}
 
 
 def parse(argv=None):
@@ -100,9 +106,12 @@ def parse(argv=None):
                     help="resnet50: torch.backends.cudnn.benchmark (MIOpen find per shape), both impls")
     ap.add_argument("--grad-dtype", choices=["fp32", "bf16"], default="fp32",
                     help="resnet50 gradient wire dtype (bf16: converted inside the xGMI two-shot kernel)")
-    ap.add_argument("--dp", choices=["fused", "split"], default=None,
-                    help="mnist N>1: 'fused' exchanges gradients inside the tail kernel over xGMI; 'split' = "
-                         "head/tail/allreduce/tail (default: fused for ddp, split for horovod)")
+    ap.add_argument("--dp", choices=["fused", "split"], default="fused",
+                    help="mnist N>1: 'fused' exchanges gradients inside the step kernel over xGMI (both "
+                         "accelerators); 'split' = head/tail/allreduce/tail")
+    ap.add_argument("--compare-stock", action="store_true",
+                    help="mnist: after the native timing, time the stock step (nn.Linear + torch.optim.Adam, "
+                         "torch DDP over RCCL for N > 1) in the same job and report it as stock_*")
     ap.add_argument("--comm", choices=["auto", "xgmi", "rccl", "torch"], default="auto",
                     help="N>1 gradient allreduce: native xGMI (auto/xgmi), native RCCL, or c10d")
     args = ap.parse_args(argv)
@@ -113,8 +122,6 @@ def parse(argv=None):
         args.warmup = 5 if rn else 200
     if args.batch_size is None:
         args.batch_size = 128 if rn else 32
-    if args.dp is None:
-        args.dp = "split" if args.accelerator == "horovod" else "fused"
     if args.device == "auto":
         # device_count() does not initialise HIP on this image (the launcher stays GPU-free)
         args.device = "cuda" if torch.cuda.device_count() > 0 else "cpu"
@@ -480,11 +487,11 @@ def make_resnet(args, world, rank, dev, x, y, bucket_mb=None):
 
 
 # ------------------------------------------------------------ measurement
-def timed(run, steps, world, dev) -> float:
+def timed(run, steps, world, dev, per_rank=None) -> float:
     """EXACTLY ``steps`` steps, bracketed by barrier + device sync on both sides;
     each rank's clock stops at its own sync (before the closing barrier, whose
     ~50-100 us collective would otherwise be billed to a 20-step window), and the
-    slowest rank's time is reported."""
+    slowest rank's time is reported (``per_rank``: list to receive every rank's)."""
     barrier(world)
     sync(dev)
     t0 = time.perf_counter()
@@ -493,11 +500,34 @@ def timed(run, steps, world, dev) -> float:
     elapsed = time.perf_counter() - t0
     barrier(world)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device=dev if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        t = torch.zeros(world, dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+        t[dist.get_rank()] = elapsed
+        dist.all_reduce(t)  # SUM of one-hot rows = every rank's time
+        times = t.cpu().tolist()
+        elapsed = max(times)
+    else:
+        times = [elapsed]
+    if per_rank is not None:
+        per_rank[:] = times
     return elapsed
+
+
+def dp_diagnostics(world, per_rank, steps) -> dict:
+    """N > 1: what the driver's multi-GPU run should tell a reader:
+    per-rank step time, the communicator's bring-up verdict, its RCCL world."""
+    us = [t / steps * 1e6 for t in per_rank]
+    out = {"per_rank_us_per_step": {"min": round(min(us), 3), "max": round(max(us), 3)}}
+    if world > 1:
+        from ray_lightning_accelerators_amd.parallel.comm import get_native_comm
+
+        comm = get_native_comm(create=False)
+        if comm is not None:
+            out["comm"] = comm.describe()
+            out["comm_failed_validation"] = list(comm.fallbacks)
+            out["rccl_world"] = int(comm._c.rccl_count)
+            out["comm_error_state"] = int(comm._c.error_state())
+        out["process_group"] = {"backend": dist.get_backend(), "world": dist.get_world_size()}
+    return out
 
 
 def run_rank(args):
@@ -529,7 +559,9 @@ def run_rank(args):
             run, last_loss, checksum, info = degrade_to_split(args, world, rank, dev, x, y)
     run(args.warmup)
     log(rank, f"world={world} route={info.get('route')} device={dev}")
-    elapsed = timed(run, args.steps, world, dev)
+    per_rank = []
+    elapsed = timed(run, args.steps, world, dev, per_rank)
+    diag = dp_diagnostics(world, per_rank, args.steps)
     curve = None
     if sweep:
         curve = {}
@@ -549,6 +581,17 @@ def run_rank(args):
     n_ranks = dist.get_world_size() if world > 1 else 1
     value = args.steps * args.batch_size * n_ranks / elapsed
     loss = last_loss()
+    stock = None
+    if args.compare_stock and not rn and args.impl == "native" and dev.type == "cuda":
+        # the stock stack in the same job, same ranks / data / batch / step count
+        # (torch DDP over RCCL for N > 1): both scaling curves from one command
+        srun, *_ = make_torch(args, world, rank, dev, x, y)
+        srun(min(args.warmup, 50))
+        ssteps = min(args.steps, 1000)
+        st = timed(srun, ssteps, world, dev)
+        stock = {"impl": "torch" + (f"+ddp({dist.get_backend()})" if world > 1 else ""), "steps": ssteps,
+                 "value": round(ssteps * args.batch_size * n_ranks / st, 1),
+                 "ms_per_step": round(st / ssteps * 1e3, 5)}
     out = None
     if rank == 0:
         default_cfg = (args.layer_1, args.layer_2, args.batch_size) == (32, 64, 32)
@@ -575,6 +618,7 @@ def run_rank(args):
             "vs_baseline": (round(value / base, 3) if base else None),
             "baseline_impl": base_impl,
             "baseline_value": base,
+            "baseline_source": STOCK_BASELINE_SOURCE.get((base_impl or "").split(" ")[0]),
             "dtype": "bf16" if dev.type == "cuda" else "fp32",
             "data": "synthetic",
             "config": {
@@ -591,6 +635,10 @@ def run_rank(args):
                 **info,
             },
         }
+        if world > 1 or args.compare_stock:
+            out["dp"] = diag
+        if stock:
+            out["stock"] = stock
         if curve:
             out["bucket_curve_images_per_s"] = curve
     if world > 1:

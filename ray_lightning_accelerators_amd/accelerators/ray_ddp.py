@@ -75,10 +75,7 @@ def find_free_port() -> int:
 
 def setup_address() -> str:
     """``tcp://<node ip>:<free port>`` chosen on the calling worker's node."""
-    ip = ray.get_node_ip_address()
-    if os.environ.get("RLA_NODE_IP"):  # simulated multi-node: every "node" is this host
-        ip = "127.0.0.1"
-    return f"tcp://{ip}:{find_free_port()}"
+    return f"tcp://{ray.get_node_address()}:{find_free_port()}"
 
 
 def _tune_session_enabled() -> bool:

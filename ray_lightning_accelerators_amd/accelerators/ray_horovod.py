@@ -80,8 +80,10 @@ class HorovodRayExecutor:
         for ip, g in zip(ips, gpu_ids):
             local_sizes[ip] += 1
             host_gpus[ip].extend(str(x) for x in g)
+        # the Gloo rendezvous server runs on worker 0's node (port chosen there):
+        # every slot, on every host, dials that node's reachable address
         port = ray.get(self.workers[0].execute.remote(find_free_port))
-        master = "127.0.0.1"
+        master = ray.get(self.workers[0].execute.remote(ray.get_node_address))
         envs = []
         for rank, ip in enumerate(ips):
             lr = local_counter[ip]

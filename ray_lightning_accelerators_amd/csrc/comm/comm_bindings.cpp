@@ -54,6 +54,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("rank", &Communicator::rank)
       .def_property_readonly("world", &Communicator::world)
       .def_property_readonly("has_rccl", &Communicator::has_rccl)
+      .def_property_readonly("rccl_count", &Communicator::rccl_count)
       .def_property_readonly("has_xgmi", &Communicator::has_xgmi)
       .def_property_readonly("xgmi_capacity", &Communicator::xgmi_capacity)
       .def("allreduce",

@@ -38,6 +38,13 @@ ncclRedOp_t to_nccl(RedOp o) {
 
 }  // namespace
 
+int Communicator::rccl_count() const {
+  if (!comm_ || aborted_.load()) return -1;
+  int n = -1;
+  if (ncclCommCount(comm_, &n) != ncclSuccess) return -1;
+  return n;
+}
+
 Communicator::Communicator(int rank, int world, int device) : rank_(rank), world_(world), device_(device) {
   if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("bad rank / world size");
 }

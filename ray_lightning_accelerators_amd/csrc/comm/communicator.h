@@ -43,6 +43,8 @@ class Communicator {
   // ---- RCCL ----
   void init_rccl(const std::string& uid);
   bool has_rccl() const { return comm_ != nullptr; }
+  // ranks the RCCL communicator itself reports (ncclCommCount; -1 without one)
+  int rccl_count() const;
   void allreduce(void* buf, int64_t count, DType dt, RedOp op, hipStream_t s);
   void broadcast(void* buf, int64_t count, DType dt, int root, hipStream_t s);
   void allgather(const void* in, void* out, int64_t count, DType dt, hipStream_t s);

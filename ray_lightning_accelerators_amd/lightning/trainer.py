@@ -592,7 +592,9 @@ class Trainer:
             return
         metrics = dict(self.logged_metrics)
         if defer and any(isinstance(v, torch.Tensor) and v.is_cuda for v in metrics.values()):
-            snap = {k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in metrics.items()}
+            # a device-side copy (no host sync): a logged tensor the module later
+            # changes in place must still be written with its value at log time
+            snap = {k: (v.detach().clone() if isinstance(v, torch.Tensor) else v) for k, v in metrics.items()}
             if self._pending_log is None:
                 self._pending_log = []
             self._pending_log.append((snap, self.global_step))
@@ -826,6 +828,11 @@ class Trainer:
         comm = get_native_comm(create=False)
         if comm is not None:
             comm.check()
+        # the fused one-launch step's in-launch hand-off (a bounded wait that expired
+        # means a block overwrote state another block was still reading)
+        f = getattr(self, "_fused", None)
+        if f is not None and hasattr(f, "check"):
+            f.check()
 
     def _dispatch_chunk(self, model: LightningModule) -> int:
         """Steps per host dispatch of the fused resident step (1 = one per batch).
@@ -1075,7 +1082,12 @@ def _to_cpu(obj):
         off = 0
         for t in ts:
             n = t.numel()
-            host[id(t)] = flat[off: off + n].view(t.shape)
+            # each leaf gets its OWN storage (a host memcpy): a view would pickle the
+            # whole flat buffer once per leaf (cloudpickle writes a view's storage,
+            # torch.save dedups it) -- the worker -> driver state-dict return would
+            # grow by a factor of the leaf count
+            v = flat[off: off + n].view(t.shape)
+            host[id(t)] = v.clone() if len(ts) > 1 else v
             off += n
 
     def rebuild(o):

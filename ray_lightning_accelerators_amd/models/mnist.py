@@ -124,6 +124,13 @@ def _u8_source(dataset):
     return None
 
 
+def _deterministic_sampler(sampler) -> bool:
+    """True when every epoch iterates the sampler in the same order."""
+    if isinstance(sampler, DistributedSampler):
+        return not sampler.shuffle
+    return isinstance(sampler, SequentialSampler)
+
+
 def _sampler_order(sampler) -> torch.Tensor:
     """The sampler's epoch order as an int64 tensor.  DistributedSampler /
     RandomSampler(no replacement) / SequentialSampler orders are rebuilt with
@@ -422,6 +429,10 @@ class FusedMNISTStep:
         B = int(dl.batch_size)
         key = (id(dl), id(images), int(n_batches))
         cached = self.__dict__.setdefault("_eval_orders", {}).get(key)
+        # the entry holds `dl` and `images` themselves: an id reused after garbage
+        # collection must not return another loader's order
+        if cached is not None and (cached[2] is not dl or cached[3] is not images):
+            cached = None
         if cached is None:
             order = _sampler_order(dl.sampler)
             if idx_map is not None:
@@ -434,9 +445,13 @@ class FusedMNISTStep:
                 return None
             order = order[: nb * B]
             assert int(order.max()) < images.size(0) and int(order.min()) >= 0  # the kernel trusts indices
-            cached = (order.to(self.dev), nb)
-            self._eval_orders[key] = cached
-        order_dev, nb = cached
+            cached = (order.to(self.dev), nb, dl, images)
+            # reuse only an order that cannot change between epochs (a deterministic
+            # sampler): a shuffled sampler is re-drawn every call, as eager iteration
+            # does (same subset under limit_val_batches, same global-RNG draws)
+            if _deterministic_sampler(dl.sampler):
+                self._eval_orders[key] = cached
+        order_dev, nb = cached[0], cached[1]
         u8, labels = self._resident(images, targets)
         n = nb * B
         part = torch.empty((n + 31) // 32, 2, device=self.dev)
@@ -444,6 +459,11 @@ class FusedMNISTStep:
                            x_u8=u8, index=order_dev)
         tot = part.sum(0) / n
         return {"val_loss": tot[0], "val_accuracy": tot[1]}
+
+    def check(self) -> None:
+        """Raise if the engine's in-launch hand-off ever timed out (epoch end)."""
+        if self.eng is not None:
+            self.eng.check()
 
     # --------------------------------------------------------------- state
     def sync_params_to_module(self) -> None:

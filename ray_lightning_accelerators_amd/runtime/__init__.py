@@ -15,6 +15,7 @@ from .client import (  # noqa: F401
     get,
     get_actor_id,
     get_gpu_ids,
+    get_node_address,
     get_node_ip_address,
     init,
     is_initialized,

@@ -612,5 +612,11 @@ def get_node_ip_address() -> str:
     return P.node_ip_address()
 
 
+def get_node_address() -> str:
+    """Where this node's sockets are reachable (rendezvous servers): the node IP
+    of a real node, a loopback alias of a simulated one."""
+    return P.node_address()
+
+
 def get_actor_id() -> Optional[str]:
     return os.environ.get(P.ENV_ACTOR_ID)

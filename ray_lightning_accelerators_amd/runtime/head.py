@@ -34,8 +34,13 @@ from . import protocol as P
 
 
 class Node:
-    def __init__(self, ip: str, num_cpus: float, num_gpus: int, gpu_ids: List[str], resources: Dict[str, float]):
+    def __init__(self, ip: str, num_cpus: float, num_gpus: int, gpu_ids: List[str], resources: Dict[str, float],
+                 address: str = ""):
         self.ip = ip
+        # where a socket on this node is reachable from the other nodes (rendezvous
+        # servers bind on the node's worker 0): the IP itself for a real node, a
+        # loopback alias for a simulated one (every simulated node is this host)
+        self.address = address or ip
         self.total = {"CPU": float(num_cpus), "GPU": float(num_gpus), **{k: float(v) for k, v in resources.items()}}
         self.avail = dict(self.total)
         self.free_gpus = list(gpu_ids)  # visible-device tokens in allocation order
@@ -181,6 +186,7 @@ class Head:
         env[P.ENV_AUTH] = self.authkey.hex()
         env[P.ENV_SESSION_DIR] = self.session_dir
         env[P.ENV_NODE_IP] = node.ip
+        env[P.ENV_NODE_ADDR] = node.address
         env[P.ENV_ACTOR_ID] = actor_id
         env[P.ENV_SYS_PATH] = msg.get("sys_path") or self.sys_path
         if "GPU" in req:
@@ -383,13 +389,14 @@ class Head:
 
 
 def parse_nodes(spec: str) -> List[Node]:
-    """spec: JSON list of {ip, num_cpus, num_gpus, gpu_ids, resources}."""
+    """spec: JSON list of {ip, num_cpus, num_gpus, gpu_ids, resources[, address]}."""
     import json
 
     nodes = []
-    for d in json.loads(spec):
+    for i, d in enumerate(json.loads(spec)):
         nodes.append(Node(d["ip"], d.get("num_cpus", 1), int(d.get("num_gpus", 0)),
-                          [str(x) for x in d.get("gpu_ids", [])], d.get("resources", {})))
+                          [str(x) for x in d.get("gpu_ids", [])], d.get("resources", {}),
+                          d.get("address") or P.reachable_address(d["ip"], i)))
     return nodes
 
 

@@ -21,6 +21,7 @@ ENV_HEAD = "RLA_HEAD_ADDRESS"
 ENV_AUTH = "RLA_AUTHKEY"
 ENV_SESSION_DIR = "RLA_SESSION_DIR"
 ENV_NODE_IP = "RLA_NODE_IP"
+ENV_NODE_ADDR = "RLA_NODE_ADDR"
 ENV_ACTOR_ID = "RLA_ACTOR_ID"
 ENV_SYS_PATH = "RLA_SYS_PATH"
 
@@ -74,11 +75,8 @@ def new_session_dir() -> str:
     return tempfile.mkdtemp(prefix="rla-session-", dir=base)
 
 
-def node_ip_address() -> str:
-    """This process's node IP (overridable per worker for multi-node simulation)."""
-    ip = os.environ.get(ENV_NODE_IP)
-    if ip:
-        return ip
+def host_ip_address() -> str:
+    """This host's outbound IP (no per-worker override)."""
     try:
         s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
         try:
@@ -88,6 +86,27 @@ def node_ip_address() -> str:
             s.close()
     except OSError:
         return "127.0.0.1"
+
+
+def reachable_address(ip: str, index: int) -> str:
+    """Address at which sockets of node ``ip`` (the ``index``-th node of the session)
+    are reachable: the IP of a real node (this host's, or a loopback address), a
+    distinct loopback alias (127.0.0.<index + 1>) for a simulated node -- every
+    simulated node is a process group on this host, and Linux routes all of
+    127/8 to loopback, so per-node rendezvous addresses stay distinguishable."""
+    if ip.startswith("127.") or ip in ("localhost", host_ip_address()):
+        return ip
+    return f"127.0.0.{index % 254 + 1}"
+
+
+def node_address() -> str:
+    """Reachable address of this process's node (see :func:`reachable_address`)."""
+    return os.environ.get(ENV_NODE_ADDR) or node_ip_address()
+
+
+def node_ip_address() -> str:
+    """This process's node IP (overridable per worker for multi-node simulation)."""
+    return os.environ.get(ENV_NODE_IP) or host_ip_address()
 
 
 class RemoteError(Exception):

@@ -78,3 +78,20 @@ def test_batched_state_dict_transfer_matches_per_tensor():
             assert a == b
 
     check(sd, out)
+
+
+@pytest.mark.gpu
+def test_batched_state_dict_pickles_at_raw_size():
+    """the host leaves must not be views of one shared buffer, or
+    cloudpickle (the worker -> driver return path) writes that buffer once per leaf."""
+    import cloudpickle
+
+    from ray_lightning_accelerators_amd.lightning.trainer import _to_cpu
+
+    dev = torch.device("cuda", 0)
+    sd = {f"w{i}": torch.full((1024,), float(i), device=dev) for i in range(100)}  # 100 x 4 KiB
+    out = _to_cpu(sd)
+    raw = 100 * 1024 * 4
+    size = len(cloudpickle.dumps(out))
+    assert size < 1.5 * raw, (size, raw)
+    assert all(torch.equal(out[k], sd[k].cpu()) for k in sd)
