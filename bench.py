@@ -112,6 +112,9 @@ def parse(argv=None):
     ap.add_argument("--compare-stock", action="store_true",
                     help="mnist: after the native timing, time the stock step (nn.Linear + torch.optim.Adam, "
                          "torch DDP over RCCL for N > 1) in the same job and report it as stock_*")
+    ap.add_argument("--dp-proto", choices=["auto", "packed", "owner", "granule"], default="auto",
+                    help="mnist N>1 fused exchange: 'auto' times packed (one-shot) and owner (reduce-scatter / "
+                         "owner Adam / all-gather) on this node's links during warm-up and keeps the faster")
     ap.add_argument("--comm", choices=["auto", "xgmi", "rccl", "torch"], default="auto",
                     help="N>1 gradient allreduce: native xGMI (auto/xgmi), native RCCL, or c10d")
     args = ap.parse_args(argv)
@@ -192,6 +195,7 @@ def make_native(args, world, rank, dev, x, y, force_split=False):
 
     allreduce = None
     dp_ctx = None
+    rearm = None
     route = "single"
     if world > 1:
         from ray_lightning_accelerators_amd.parallel.comm import get_native_comm
@@ -215,9 +219,10 @@ def make_native(args, world, rank, dev, x, y, force_split=False):
             else:
                 allreduce = comm.allreduce_
             if args.dp == "fused" and not force_split:
-                from ray_lightning_accelerators_amd.ops.fused_mlp import mlp_param_count
+                from ray_lightning_accelerators_amd.ops.fused_mlp import mlp3_dp_capacity
 
-                dp_ctx = comm.dp_context(2 * mlp_param_count(args.layer_1, args.layer_2))  # granule area
+                dp_ctx = comm.dp_context(mlp3_dp_capacity(args.layer_1, args.layer_2))
+                rearm = comm.dp_rearm
             route = "xgmi-fused" if dp_ctx else "split-native"
         else:
             def allreduce(t):
@@ -229,7 +234,8 @@ def make_native(args, world, rank, dev, x, y, force_split=False):
                     dist.all_reduce(t)
             route = f"split-c10d-{dist.get_backend()}"
     eng = FusedMLPEngine(args.layer_1, args.layer_2, args.batch_size, lr=args.lr, device=dev,
-                         world_size=world, rank=rank, allreduce=allreduce, seed=0, dp_context=dp_ctx)
+                         world_size=world, rank=rank, allreduce=allreduce, seed=0, dp_context=dp_ctx,
+                         dp_rearm=rearm, dp_proto=None if args.dp_proto == "auto" else args.dp_proto)
     eng.set_data(x, y, shuffle=True)
     eng.broadcast_from(0)
     if route == "split-native":
@@ -238,6 +244,9 @@ def make_native(args, world, rank, dev, x, y, force_split=False):
         route = f"split-{get_native_comm(create=False).route(eng.comm_buffer)}"  # oneshot / rccl / torch
     graphed = False
     gsteps = graph_steps_for(args.graph_steps, args.steps)
+    tuned = None
+    if eng.one_launch_dp and args.dp_proto == "auto" and gsteps > 0:
+        tuned = tune_dp_proto(eng, world, rank, dev, gsteps)
     if gsteps > 0 and dev.type == "cuda" and route not in ("split-c10d-gloo", "split-torch"):
         graphed = eng.capture(gsteps)
         if graphed:
@@ -253,7 +262,42 @@ def make_native(args, world, rank, dev, x, y, force_split=False):
     one = eng.native and (eng.one_launch_dp if world > 1 else eng.one_launch)
     info = {"route": route, "hip_graph_steps": gsteps if graphed else 0,
             "step_kernel": ("one-launch" if one else "head+tail") if eng.native else "torch-cpu"}
+    if eng.dp_ctx is not None:
+        info["dp_proto"] = eng.dp_proto
+        if tuned is not None:
+            info["dp_proto_tuning_us_per_step"] = tuned
     return eng.run, (lambda: float(eng.recent_stats(20)[:, 0].mean())), replica_checksum, info
+
+
+def tune_dp_proto(eng, world, rank, dev, gsteps, candidates=("packed", "owner"), windows=8):
+    """Time each one-launch exchange protocol on THIS node's links (graph replays,
+    slowest rank, after a warm replay) and keep the fastest -- the link's small-write
+    bandwidth against its hop latency decides between one hop of all the bytes
+    (packed) and two hops of 1/N of them (owner); see csrc/mlp_step3.hip.  Every
+    rank switches together (collective re-arm of the exchange region).  A protocol
+    whose polls time out is discarded.  Returns {proto: us/step}."""
+    from ray_lightning_accelerators_amd.parallel.comm import _agree, get_native_comm
+
+    comm = get_native_comm(create=False)
+    res = {}
+    for name in candidates:
+        eng.set_dp_proto(name)
+        if not eng.one_launch_dp or not eng.capture(gsteps):
+            continue
+        eng.run(gsteps)
+        t = timed(eng.run, windows * gsteps, world, dev)
+        healthy = _agree(comm is None or comm._c.error_state() == 0)
+        if not healthy:
+            sync(dev)
+            barrier(world)
+            comm._c.reset_error()
+            barrier(world)
+            continue
+        res[name] = round(t / (windows * gsteps) * 1e6, 3)
+    best = min(res, key=res.get) if res else "packed"
+    eng.set_dp_proto(best)
+    log(rank, f"dp protocol tuning (us/step, slowest rank): {res} -> {best}")
+    return res
 
 
 def degrade_to_split(args, world, rank, dev, x, y):

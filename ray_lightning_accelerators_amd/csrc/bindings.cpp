@@ -9,6 +9,7 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
 #include "kernels.h"
+#include "comm/xgmi.h"
 
 namespace {
 
@@ -174,7 +175,7 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
           bool advance_step, double lr,
           double beta1, double beta2, double eps, double weight_decay, double grad_scale, optional<Tensor> lr_t,
           bool adamw, optional<Tensor> stamps, std::vector<int64_t> dp_ctx, optional<Tensor> head_part,
-          optional<Tensor> hand) {
+          optional<Tensor> hand, int64_t dp_proto, bool dp_loop) {
   TORCH_CHECK(kind >= 0 && kind <= 7, "mlp3: bad kind ", kind);
   TORCH_CHECK(rla::mlp_supported((int)L1, (int)L2), "no fused MLP kernel for layer sizes ", L1, "/", L2);
   TORCH_CHECK(B >= 1 && B <= 256, "fused MLP step supports 1 <= batch <= 256");
@@ -262,13 +263,24 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
     // exchange protocol: "granule" (default: tagged 8-byte words, no fences; needs a
     // receive area of 2 floats per parameter), "wave" (flags, one wave fences),
     // "all" (flags, every wave fences)
+    // one-launch step (dp_proto): 0 "granule" (round 2, arena-indexed), 1 "packed"
+    // one-shot, 2 "owner" (reduce-scatter / owner Adam / all-gather); -1: RLA_DP_PROTO
     const char* proto = std::getenv("RLA_DP_PROTO");
-    const std::string pr = proto ? proto : "granule";
+    const std::string pr = proto ? proto : "";
     a.dp_lite = pr == "all" ? 0 : (pr == "wave" ? 1 : 2);
     if (a.dp_lite == 2 && a.dp_stride < 2 * np) a.dp_lite = 1;  // area too small for granules
-    TORCH_CHECK(kind != rla::kMLP3Step1DP || a.dp_lite == 2,
-                "the one-launch data-parallel step exchanges tagged granules only (RLA_DP_PROTO=granule, "
-                "a receive area of 2 floats per parameter)");
+    if (dp_proto < 0) dp_proto = pr == "granule" ? 0 : (pr == "owner" ? 2 : 1);
+    TORCH_CHECK(dp_proto >= 0 && dp_proto <= 2, "dp_proto: 0 granule, 1 packed, 2 owner");
+    a.dp_proto = (int)dp_proto;
+    a.dp_loop = dp_loop ? 1 : 0;
+    if (kind == rla::kMLP3Step1DP) {
+      TORCH_CHECK(a.dp_proto != 0 || (a.dp_lite == 2 && a.dp_stride >= 2 * np),
+                  "the one-launch step's granule protocol needs a receive area of 2 floats per parameter");
+      TORCH_CHECK(a.dp_proto == 0 || a.dp_stride >= rla::comm::kDpUnitAreaFloats,
+                  "the packed / owner protocols need a receive area of ", rla::comm::kDpUnitAreaFloats,
+                  " floats (mlp3_dp_area_floats())");
+    }
+    TORCH_CHECK(!dp_loop || kind == rla::kMLP3Step1DP, "loopback is a one-launch-step diagnostic");
   }
   TORCH_CHECK(rla::launch_mlp3(a, (int)kind, cur_stream(params)) == 0, "fused MLP v3 launch failed");
 }
@@ -484,6 +496,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp3", &mlp3, "fused MNIST-MLP step v3 (pipelined layer 1): kind 0 step, 1 head, 2 tail-grad, "
         "3 tail-adam, 4 prime, 5 step with the in-kernel xGMI exchange, 6 one-launch step (B <= 32)");
   m.def("mlp3_hand_words", [](int64_t l1, int64_t l2) { return rla::mlp3_hand_words((int)l1, (int)l2); });
+  m.def("mlp3_dp_area_floats", []() { return rla::comm::kDpUnitAreaFloats; },
+        "aux receive-area stride (floats) of the one-launch step's packed / owner protocols");
   m.def("mlp_adam", &mlp_adam, "MLP arena Adam + bf16 shadow refresh (update=False: refresh only)");
   m.def("mlp_shadow_size", [](int64_t l1, int64_t l2) { return rla::mlp_shadow_layout((int)l1, (int)l2).total; });
   m.def("mlp_supported", [](int64_t a, int64_t b) { return rla::mlp_supported((int)a, (int)b); });

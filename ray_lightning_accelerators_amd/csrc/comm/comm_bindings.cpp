@@ -143,6 +143,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            })
       .def_property_readonly("has_aux", &Communicator::has_aux)
       .def("aux_context", &Communicator::aux_context)
+      .def("aux_rearm", &Communicator::aux_rearm)
       .def("set_spin_limit", &Communicator::set_spin_limit)
       .def("error_state", &Communicator::error_state)
       .def("error_message", &Communicator::error_message)

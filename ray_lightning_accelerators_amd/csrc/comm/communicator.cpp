@@ -295,14 +295,27 @@ std::string Communicator::aux_handle(int64_t capacity_floats) {
     const int64_t bytes = xgmi_region_bytes(aux_stride_);
     hip_check(hipExtMallocWithFlags(reinterpret_cast<void**>(&aux_region_), (size_t)bytes, hipDeviceMallocUncached),
               "hipExtMallocWithFlags(uncached aux)");
-    hip_check(hipMemset(aux_region_, 0, (size_t)bytes), "hipMemset(aux)");
     hip_check(hipMalloc(reinterpret_cast<void**>(&aux_gen_), kDpMaxBlocks * sizeof(uint32_t)), "hipMalloc(aux gen)");
-    hip_check(hipMemset(aux_gen_, 0, kDpMaxBlocks * sizeof(uint32_t)), "hipMemset(aux gen)");
-    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    aux_rearm();
   }
   hipIpcMemHandle_t h;
   hip_check(hipIpcGetMemHandle(&h, aux_region_), "hipIpcGetMemHandle(aux)");
   return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void Communicator::aux_rearm() {
+  // Flags 0, every receive-area byte 0xFF (a packed granule's tag 3, a {gen, fp32}
+  // granule's generation 0xFFFFFFFF: neither matches the first steps' tags), block
+  // generations 0.  Collective in effect: the caller guarantees no peer kernel is
+  // writing into this region (parallel/comm.py dp_rearm: device sync + barriers).
+  if (!aux_region_) throw std::runtime_error("aux_handle() first");
+  hip_check(hipSetDevice(device_), "hipSetDevice");
+  const int64_t bytes = xgmi_region_bytes(aux_stride_);
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  hip_check(hipMemset(aux_region_, 0, (size_t)kXgmiFlagBytes), "hipMemset(aux flags)");
+  hip_check(hipMemset(aux_region_ + kXgmiFlagBytes, 0xFF, (size_t)(bytes - kXgmiFlagBytes)), "hipMemset(aux data)");
+  hip_check(hipMemset(aux_gen_, 0, kDpMaxBlocks * sizeof(uint32_t)), "hipMemset(aux gen)");
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
 }
 
 void Communicator::aux_open(const std::vector<std::string>& handles) {

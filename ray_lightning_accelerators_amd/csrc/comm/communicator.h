@@ -93,6 +93,8 @@ class Communicator {
   // allreduce's areas or generations)
   std::string aux_handle(int64_t capacity_floats);
   void aux_open(const std::vector<std::string>& handles);
+  // reset the region for a new exchange protocol / job (see communicator.cpp)
+  void aux_rearm();
   bool has_aux() const { return aux_ready_; }
   // [world, rank, slot_stride, spin_limit, gen_ptr, err_ptr, region_ptr x world]
   std::vector<int64_t> aux_context() const;

@@ -15,6 +15,19 @@ constexpr int64_t kXgmiFlagBytes = 64 * 1024;
 // uint32 in the same 64 KiB header, then the same receive-area layout.
 constexpr int kDpMaxBlocks = 128;
 
+// Wave-positioned areas of the one-launch step's exchange protocols (mlp_step3.hip,
+// "packed" and "owner"): one exchange UNIT per (block, wave) = 64 lanes x 4 values.
+//   packed / reduce-scatter area: [2 slots][kXgmiMaxRanks srcs][kDpMaxUnits][2][64] 8-B granules
+//     (two values per granule, the tag in the low mantissa bits of the first)
+//   all-gather area:              [2 slots][kDpMaxUnits][4][64] 8-B {generation, fp32} granules
+// Every store instruction of a wave covers 512 contiguous bytes (whole 64-B lines
+// over the link), not 64 scattered arena positions.
+constexpr int kDpMaxUnits = kDpMaxBlocks * 8;
+constexpr int64_t kDpPackedGranules = 2LL * kXgmiMaxRanks * kDpMaxUnits * 128;
+constexpr int64_t kDpGatherGranules = 2LL * kDpMaxUnits * 256;
+// receive-area stride (floats per (slot, rank)) that holds both areas behind the flag header
+constexpr int64_t kDpUnitAreaFloats = (kDpPackedGranules + kDpGatherGranules) * 8 / (2 * kXgmiMaxRanks * 4);
+
 // Region of one rank: flags, then receive areas [2 slots][kXgmiMaxRanks][slot_stride] fp32.
 inline int64_t xgmi_region_bytes(int64_t slot_stride_floats) {
   return kXgmiFlagBytes + 2 * (int64_t)kXgmiMaxRanks * slot_stride_floats * 4;

@@ -183,6 +183,13 @@ struct MLP3Args {
   int64_t dp_spin;          // poll bound
   int dp_rank, dp_world;
   int dp_lite;              // exchange protocol: 2 tagged granules (default), 1 flags + one fencing wave, 0 flags + all waves
+  // one-launch step (kMLP3Step1DP) exchange: 0 arena-indexed {gen, fp32} granules (round 2),
+  // 1 "packed" one-shot (wave-positioned, two values per granule), 2 "owner" (reduce-scatter to
+  // the task's owner rank, Adam there, all-gather of the fp32 weights)
+  int dp_proto;
+  // loopback (diagnostic): one process plays all dp_world ranks through its own region
+  // (every region pointer is this rank's; the block writes every source slot itself)
+  int dp_loop;
   // one-launch step (kMLP3Step1): in-launch hand-off words (mlp_step3.hip) and their poll bound
   unsigned long long* hand;
   int64_t hand_spin;

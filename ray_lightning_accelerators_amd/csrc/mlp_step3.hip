@@ -781,6 +781,31 @@ __device__ __forceinline__ void small_finalize(const MLP3Args& a, bool adam, con
   if (adam && r.kind == 1) *reinterpret_cast<bf16x4*>(SHW + O::W3T + (int64_t)r.colv * 16 + r.rowv) = sh4;
 }
 
+// Owner protocol: r.v[] already holds the new fp32 weights (from the owner's Adam or
+// its all-gather); store them and the bf16 shadows, and m / v where this rank owns
+// the task (r.mv / r.vv advanced by the owner's Adam).
+template <int L1, int L2>
+__device__ __forceinline__ void small_store(const MLP3Args& a, const SmallRes& r, bool store_mv) {
+  using O = Off<L1, L2>;
+  if (r.kind < 0) return;
+  __bf16* SHW = reinterpret_cast<__bf16*>(a.shadow);
+  bf16x4 sh4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    sh4[i] = (__bf16)0.f;
+    if (!r.valid[i]) continue;
+    a.params[r.gi[i]] = r.v[i];
+    if (store_mv) {
+      a.exp_avg[r.gi[i]] = r.mv[i];
+      a.exp_avg_sq[r.gi[i]] = r.vv[i];
+    }
+    SHW[r.gi[i]] = (__bf16)r.v[i];
+    sh4[i] = (__bf16)r.v[i];
+  }
+  if (r.kind == 0) *reinterpret_cast<bf16x4*>(SHW + O::W2T + (int64_t)r.colv * L2 + r.rowv) = sh4;
+  if (r.kind == 1) *reinterpret_cast<bf16x4*>(SHW + O::W3T + (int64_t)r.colv * 16 + r.rowv) = sh4;
+}
+
 // ---------------------------------------------------------------------------
 // In-kernel xGMI exchange of the fused data-parallel tail (kind StepDP): every
 // block pushes its gradient values into the peers' receive areas (at their arena
@@ -929,6 +954,184 @@ __device__ __forceinline__ float dp_sum1(const MLP3Args& a, int slot, int64_t id
     s += __builtin_nontemporal_load(dp_data(a.dp_regions[a.dp_rank], slot, r, a.dp_stride) + idx);
   return s;
 }
+
+// ---------------------------------------------------------------------------
+// Wave-positioned exchange protocols of the one-launch data-parallel step
+// (a.dp_proto 1 "packed", 2 "owner"; layout in comm/xgmi.h).  The unit of
+// exchange is one wave: 64 lanes x 4 values (a 16x16 gradient tile, 64 biases, or
+// a W1 tile's 16-neuron slice), at unit = block * 8 + wave.
+//
+// Cost model per step, world N, P parameters (4P bytes of fp32 gradient), per link:
+//   round-2 granules  (N-1 peers) x 8P bytes out, 8P per link     one hop
+//   packed one-shot   4P per link (two values per 8-B granule)    one hop
+//   owner             4P/N (reduce-scatter) + 8P/N (all-gather)   two hops
+// At the default 32-64 model (P = 27,882) and N = 8: 223 / 112 / 42 KB per link.
+// Which wins depends on the link's small-write bandwidth against its one-way
+// latency (break-even ~ (70 KB / bandwidth) = one extra hop) -- measured per job:
+// bench.py times both at start-up and keeps the faster (scripts/dp_overhead_probe.py
+// prices the in-kernel part with loopback ranks).
+//
+// Packed granule: {bits(v0) rounded to a multiple of 4 ulp | tag, bits(v1)}; the
+// 2-bit tag ((gen >> 1) & 3) is this step's: a slot (gen & 1) is rewritten every
+// second step, so its stale granules carry the previous tag (gen - 2).  Regions are
+// re-armed (all bits set: tag 3; generations 0) whenever a job starts using them,
+// so the first tag-3 step (gen 6) finds slot 0 already rewritten at gen 4.  An
+// aligned 8-byte store is not torn, so no flag and no fence: a reader accepts a
+// granule exactly when its tag matches.  Gradient values lose at most 2 ulp of
+// fp32 (2^-22 relative) on the wire; every rank sums the SAME granules in fixed
+// rank order (its own from registers, rounded identically), so replicas stay
+// bitwise equal.
+// ---------------------------------------------------------------------------
+typedef unsigned long long u64;
+
+__device__ __forceinline__ u64 pk2(float v0, float v1, uint32_t tag) {
+  const uint32_t b0 = ((__float_as_uint(v0) + 2u) & ~3u) | tag;
+  return ((u64)__float_as_uint(v1) << 32) | (u64)b0;
+}
+__device__ __forceinline__ float pk_lo(u64 w) { return __uint_as_float((uint32_t)w & ~3u); }
+__device__ __forceinline__ float pk_hi(u64 w) { return __uint_as_float((uint32_t)(w >> 32)); }
+
+__device__ __forceinline__ u64* dp_pk_area(char* region, int slot, int src, int unit) {
+  return reinterpret_cast<u64*>(region + kXgmiFlagBytes) +
+         (((int64_t)slot * kXgmiMaxRanks + src) * comm::kDpMaxUnits + unit) * 128;
+}
+__device__ __forceinline__ u64* dp_ag_area(char* region, int slot, int unit) {
+  return reinterpret_cast<u64*>(region + kXgmiFlagBytes) + comm::kDpPackedGranules +
+         ((int64_t)slot * comm::kDpMaxUnits + unit) * 256;
+}
+__device__ __forceinline__ void st_sys(u64* p, u64 w) {
+  __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ u64 ld_sys(const u64* p) {
+  return __hip_atomic_load(const_cast<u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Poll granules 0..n-1 (address addr(i), n <= NMAX): every load is issued before
+// any check, then only the mismatched ones are re-read, so the common case is ONE
+// round trip for all of them.  Returns when every tag matches or the bound expires
+// (*fail set).  Unrolled over NMAX: w[] stays in registers.
+template <int NMAX, typename Addr, typename TagOk>
+__device__ __forceinline__ void dp_poll(const MLP3Args& a, u64 (&w)[NMAX], int n, Addr addr, TagOk ok, int* fail) {
+#pragma unroll
+  for (int i = 0; i < NMAX; ++i)
+    if (i < n) w[i] = ld_sys(addr(i));
+  int64_t spins = 0;
+  while (true) {
+    bool all = true;
+#pragma unroll
+    for (int i = 0; i < NMAX; ++i)
+      if (i < n && !ok(w[i])) all = false;
+    if (all) return;
+    if (++spins > a.dp_spin) {
+      *fail = 1;
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int i = 0; i < NMAX; ++i)
+      if (i < n && !ok(w[i])) w[i] = ld_sys(addr(i));
+  }
+}
+
+// Fixed-rank-order sum of every rank's packed contribution to this lane's 4 values
+// (our own from registers): polls the W - 1 peers' granules of slot / unit.
+__device__ __forceinline__ void dp_packed_sum(const MLP3Args& a, int unit, int slot, uint32_t tag, u64 g0, u64 g1,
+                                              float (&v)[4], float scale, int* fail) {
+  const int lane = threadIdx.x & 63, me = a.dp_rank, W = a.dp_world;
+  char* mine = a.dp_regions[me];
+  // granule i: peer s = i / 2 (skipping me), half i & 1
+  auto addr = [&](int i) {
+    const int k = i >> 1, s = k < me ? k : k + 1;
+    return dp_pk_area(mine, slot, s, unit) + (i & 1) * 64 + lane;
+  };
+  u64 w[2 * (kXgmiMaxRanks - 1)];
+  dp_poll(a, w, 2 * (W - 1), addr, [tag](u64 x) { return ((uint32_t)x & 3u) == tag; }, fail);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+  for (int s = 0; s < kXgmiMaxRanks; ++s) {
+    if (s >= W) break;
+    const int k = s < me ? s : s - 1;
+    u64 a0 = g0, a1 = g1;
+    if (s != me) {
+#pragma unroll
+      for (int q = 0; q < kXgmiMaxRanks - 1; ++q)  // register-resident select (no indexed access)
+        if (q == k) { a0 = w[2 * q]; a1 = w[2 * q + 1]; }
+    }
+    s0 += pk_lo(a0); s1 += pk_hi(a0); s2 += pk_lo(a1); s3 += pk_hi(a1);
+  }
+  v[0] = s0 * scale; v[1] = s1 * scale; v[2] = s2 * scale; v[3] = s3 * scale;
+}
+
+__device__ __forceinline__ void dp_push_packed(char* region, int slot, int src, int unit, u64 g0, u64 g1) {
+  const int lane = threadIdx.x & 63;
+  u64* d = dp_pk_area(region, slot, src, unit);
+  st_sys(d + lane, g0);
+  st_sys(d + 64 + lane, g1);
+}
+
+// "packed" one-shot: push this wave's 4 values to every peer, sum all ranks' in
+// fixed order; v[] becomes the sum times `scale`.  Whole-wave call.
+__device__ __forceinline__ void dp_packed_exchange(const MLP3Args& a, int unit, uint32_t gen, float (&v)[4],
+                                                   float scale, int* fail) {
+  const int slot = (int)(gen & 1u), me = a.dp_rank, W = a.dp_world;
+  const uint32_t tag = (gen >> 1) & 3u;
+  const u64 g0 = pk2(v[0], v[1], tag), g1 = pk2(v[2], v[3], tag);
+  // 2 x 512 contiguous bytes per peer (loopback: every peer's source slot of our own region)
+  for (int r = 0; r < W; ++r)
+    if (r != me) dp_push_packed(a.dp_regions[r], slot, a.dp_loop ? r : me, unit, g0, g1);
+  dp_packed_sum(a, unit, slot, tag, g0, g1, v, scale, fail);
+}
+
+// "owner": the task's gradient goes to its owner rank only (reduce-scatter, one
+// hop: 1 / N of the one-shot bytes), the owner sums every rank's contribution,
+// runs `adam(v)` (v: summed gradient in, new fp32 weights out; it also advances
+// the caller's m / v registers) and publishes the weights to every other rank as
+// {gen, fp32} granules (all-gather, the second hop); the others wait for them.
+// On return v[] holds the new weights on every rank; true on the owner (whose
+// m / v registers are then the ones to store).  Loopback: a wave whose task
+// another (absent) rank owns plays that owner itself.
+template <typename AdamFn>
+__device__ __forceinline__ bool dp_owner_step(const MLP3Args& a, int unit, int owner, uint32_t gen, float (&v)[4],
+                                              float scale, int* fail, AdamFn adam) {
+  const int lane = threadIdx.x & 63, slot = (int)(gen & 1u), me = a.dp_rank, W = a.dp_world;
+  const uint32_t tag = (gen >> 1) & 3u;
+  const bool own = owner == me;
+  const u64 g0 = pk2(v[0], v[1], tag), g1 = pk2(v[2], v[3], tag);
+  if (!own) dp_push_packed(a.dp_regions[owner], slot, me, unit, g0, g1);
+  if (own || a.dp_loop) {
+    if (own) {
+      if (a.dp_loop)
+        for (int s = 0; s < W; ++s)
+          if (s != me) dp_push_packed(a.dp_regions[me], slot, s, unit, g0, g1);
+      dp_packed_sum(a, unit, slot, tag, g0, g1, v, scale, fail);
+    } else {  // loopback stand-in of the owner: W identical contributions
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+      for (int s = 0; s < W; ++s) { s0 += pk_lo(g0); s1 += pk_hi(g0); s2 += pk_lo(g1); s3 += pk_hi(g1); }
+      v[0] = s0 * scale; v[1] = s1 * scale; v[2] = s2 * scale; v[3] = s3 * scale;
+    }
+    adam(v);
+    const u64 tg = (u64)gen << 32;
+    for (int r = 0; r < W; ++r) {
+      if (own ? r == me : r != owner) continue;  // loopback stand-in: publish once, to ourselves
+      u64* d = dp_ag_area(a.dp_regions[r], slot, unit);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) st_sys(d + i * 64 + lane, tg | (u64)__float_as_uint(v[i]));
+    }
+    if (own) return true;
+  }
+  const u64* src = dp_ag_area(a.dp_regions[me], slot, unit) + lane;
+  u64 w[4];
+  dp_poll(a, w, 4, [src](int i) { return src + i * 64; }, [gen](u64 x) { return (uint32_t)(x >> 32) == gen; },
+          fail);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = __uint_as_float((uint32_t)w[i]);
+  return false;
+}
+
+// Owner of a task of the one-launch step: W1 tile kt -> task kt; small-parameter
+// task t -> kTiles + t; round robin over the ranks (mirrored by
+// parallel/mlp_engine.py dp_owner_mask for optimizer-state consolidation).
+__device__ __forceinline__ int dp_task_owner(const MLP3Args& a, int task) { return task % a.dp_world; }
 
 // ADAM mode: flat Adam over every non-W1 parameter (after the allreduce).
 template <int L1, int L2>
@@ -1235,11 +1438,24 @@ __device__ __forceinline__ void one_wait_acks(const MLP3Args& a, int64_t seq, in
       if (++n > a.hand_spin) {
         *sh_fail = 1;
         __hip_atomic_store(a.hand + kHandErr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // data-parallel step: also the comm engine's host-mapped error word, which the
+        // Trainer / bench check at every epoch end without a device sync
+        if (a.dp_err) __hip_atomic_store(a.dp_err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
   }
+  // Why relaxed atomics suffice for this hand-off: it orders READS
+  // before WRITES (write-after-read), not data.  The acknowledging wave's loads have
+  // RETURNED (s_waitcnt vmcnt(0) in head_body) before its ack is issued, so no later
+  // store can change what they read; the waiter issues its stores only after the
+  // poll observed every ack (in-order issue; the stores depend on the loop's exit).
+  // What remains is the compiler: the "memory" clobbers (the waitcnt asm on the ack
+  // side, this one on the waiter's) stop it from moving memory operations across
+  // either point.  No cache maintenance is needed -- nothing the waiter stores is
+  // read back by the acknowledged blocks in this launch.
+  asm volatile("" ::: "memory");
   __syncthreads();
 }
 
@@ -1334,29 +1550,54 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
       const bf16x8 afrag = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       acc = mfma16(afrag, ld8(sDH1T + m * C::TS + 8 * g), acc);
     }
-    if constexpr (DP) {  // the tile's allreduce: push to every rank, fixed rank-order sum
+    bool adam_done = false, store_mv = true;
+    if constexpr (DP) {  // the tile's allreduce, inside the epilogue (protocol: a.dp_proto)
       __shared__ uint32_t sh_dgen;
       const int dslot = dp_begin(a, &sh_dgen);
       const uint32_t gen = sh_dgen;
       int fail = 0;
       if (mw) {
+        if (a.dp_proto == 0) {  // round 2: arena-indexed {gen, fp32} granules
 #pragma unroll
-        for (int i = 0; i < 4; ++i) dp_push_gran(a, dslot, gidx + i, acc[i], gen);
+          for (int i = 0; i < 4; ++i) dp_push_gran(a, dslot, gidx + i, acc[i], gen);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i] = dp_sum_gran(a, dslot, gidx + i, gen, &fail) * a.grad_scale;
+          for (int i = 0; i < 4; ++i) acc[i] = dp_sum_gran(a, dslot, gidx + i, gen, &fail) * a.grad_scale;
+        } else {
+          float v[4] = {acc[0], acc[1], acc[2], acc[3]};
+          const int unit = blk * kWaves + w;
+          if (a.dp_proto == 1) {
+            dp_packed_exchange(a, unit, gen, v, a.grad_scale, &fail);
+          } else {
+            const AdamScal o = *sh_o;
+            store_mv = dp_owner_step(a, unit, dp_task_owner(a, kt), gen, v, a.grad_scale, &fail,
+                                     [&](float (&x)[4]) {
+#pragma unroll
+                                       for (int i = 0; i < 4; ++i) x[i] = adam1(p4.v[i], x[i], m4.v[i], v4.v[i], o);
+                                     });
+            store_mv = store_mv || a.dp_loop;  // loopback: this process holds every rank's state
+            adam_done = true;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) p4.v[i] = v[i];
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i] = v[i];
+        }
       }
       dp_gran_end(a, gen, fail, &sh_fail);
     }
     if (mw) {
-      const AdamScal o = *sh_o;
+      if (!adam_done) {
+        const AdamScal o = *sh_o;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        p4.v[i] = adam1(p4.v[i], acc[i], m4.v[i], v4.v[i], o);
-        w4[i] = (__bf16)p4.v[i];
+        for (int i = 0; i < 4; ++i) p4.v[i] = adam1(p4.v[i], acc[i], m4.v[i], v4.v[i], o);
       }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w4[i] = (__bf16)p4.v[i];
       *reinterpret_cast<F4*>(a.params + gidx) = p4;
-      *reinterpret_cast<F4*>(a.exp_avg + gidx) = m4;
-      *reinterpret_cast<F4*>(a.exp_avg_sq + gidx) = v4;
+      if (store_mv) {  // owner protocol: only the task's owner holds its current Adam state
+        *reinterpret_cast<F4*>(a.exp_avg + gidx) = m4;
+        *reinterpret_cast<F4*>(a.exp_avg_sq + gidx) = v4;
+      }
       *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.shadow) + gidx) = w4;
       *reinterpret_cast<bf16x4*>(sW + m * kXSS + 4 * g) = w4;
     }
@@ -1389,21 +1630,44 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
   } else if (small) {
     const RepLds L{(const __bf16*)(smem + C::oH1T), sH2T, sDH2T, (const __bf16*)(smem + C::odZT), sDH1T, C::TS};
     small_compute<L1, L2, true>(a, true, task, r, &L);
+    bool adam_done = false, store_mv = true;
     if constexpr (DP) {
       __shared__ uint32_t sh_sgen;
       const int dslot = dp_begin(a, &sh_sgen);
       const uint32_t gen = sh_sgen;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (r.valid[i]) dp_push_gran(a, dslot, r.gi[i], r.v[i], gen);
       int fail = 0;
+      if (a.dp_proto == 0) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (r.valid[i]) r.v[i] = dp_sum_gran(a, dslot, r.gi[i], gen, &fail) * a.grad_scale;
+        for (int i = 0; i < 4; ++i)
+          if (r.valid[i]) dp_push_gran(a, dslot, r.gi[i], r.v[i], gen);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (r.valid[i]) r.v[i] = dp_sum_gran(a, dslot, r.gi[i], gen, &fail) * a.grad_scale;
+      } else if (task < S::NTASK) {  // whole waves (idle lanes exchange zeros)
+        float v[4] = {r.v[0], r.v[1], r.v[2], r.v[3]};
+        const int unit = blk * kWaves + w;
+        if (a.dp_proto == 1) {
+          dp_packed_exchange(a, unit, gen, v, a.grad_scale, &fail);
+        } else {
+          // Adam in registers before the acknowledgement wait below: the owner
+          // publishes the weights as early as possible, stores after the wait
+          const AdamScal o = *sh_o;
+          store_mv = dp_owner_step(a, unit, dp_task_owner(a, kTiles + task), gen, v, a.grad_scale, &fail,
+                                   [&](float (&x)[4]) {
+#pragma unroll
+                                     for (int i = 0; i < 4; ++i) x[i] = adam1(r.pv[i], x[i], r.mv[i], r.vv[i], o);
+                                   });
+          store_mv = store_mv || a.dp_loop;
+          adam_done = true;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r.v[i] = v[i];
+      }
       dp_gran_end(a, gen, fail, &sh_fail);
     }
     one_wait_acks(a, seq, &sh_fail);  // every block has read the weights / biases this overwrites
-    small_finalize<L1, L2>(a, true, r, *sh_o);
+    if (adam_done) small_store<L1, L2>(a, r, store_mv);  // r.v: the new weights
+    else small_finalize<L1, L2>(a, true, r, *sh_o);
   } else {
     // block 0: stats, the consumed H1pre slot zeroed (the invariant), then the advanced state
     one_wait_acks(a, seq, &sh_fail);
@@ -1440,9 +1704,12 @@ int dispatch3(const MLP3Args& a, int kind, hipStream_t stream) {
   }
   if (kind == kMLP3Step1DP) {
     // granule exchange only (the flag protocols stay on the two-launch StepDP)
-    if (a.B > 32 || !a.hand || kOneGrid > kDpMaxBlocks || a.dp_lite != 2 || a.dp_world < 1 ||
-        a.dp_world > kXgmiMaxRanks || !a.dp_gen || !a.dp_err || a.dp_stride < 2 * Off<L1, L2>::NP)
+    if (a.B > 32 || !a.hand || kOneGrid > kDpMaxBlocks || a.dp_world < 1 || a.dp_world > kXgmiMaxRanks ||
+        !a.dp_gen || !a.dp_err || a.dp_proto < 0 || a.dp_proto > 2)
       return -6;
+    // round-2 granules need 2 floats per parameter, the wave-positioned areas their fixed size
+    if (a.dp_proto == 0 ? (a.dp_lite != 2 || a.dp_stride < 2 * Off<L1, L2>::NP) : a.dp_stride < comm::kDpUnitAreaFloats)
+      return -7;
     hipLaunchKernelGGL((mlp3_one_kernel<L1, L2, true>), dim3(kOneGrid), dim3(kThreads), 0, stream, a);
     return 0;
   }

@@ -224,16 +224,18 @@ class FusedMNISTStep:
         bufs = dict(params=self.arena.data[: self.np], grads=self.arena.grad[: self.np],
                     exp_avg=self.gs.m[: self.np], exp_avg_sq=self.gs.v[: self.np])
         dp_ctx = None
+        rearm = None
         if self.world > 1 and get_config().fused_dp:
             from ..parallel.comm import get_native_comm
 
             comm = get_native_comm()  # every rank reaches here together (first epoch)
             if comm is not None:
-                dp_ctx = comm.dp_context(2 * self.np)  # tagged-granule receive area
+                dp_ctx = comm.dp_context(fused_mlp.mlp3_dp_capacity(self.L1, self.L2))
+                rearm = comm.dp_rearm
         eng = FusedMLPEngine(self.L1, self.L2, B, lr=float(g["lr"]), betas=tuple(g["betas"]), eps=g["eps"],
                              weight_decay=g["weight_decay"], device=self.dev, world_size=self.world,
                              rank=self.trainer.global_rank, allreduce=self._allreduce, buffers=bufs,
-                             stats_ring=self.stats.size(0), dp_context=dp_ctx)
+                             stats_ring=self.stats.size(0), dp_context=dp_ctx, dp_rearm=rearm)
         eng.set_step(self.gs.step)
         eng.lr_tensor = self.lr_tensor  # LR schedulers update one device scalar
         eng.attach_dataset(self._u8, self._labels)

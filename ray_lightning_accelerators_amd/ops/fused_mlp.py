@@ -169,6 +169,18 @@ def mlp_refresh_shadow(params: torch.Tensor, shadow: torch.Tensor, L1: int, L2: 
 
 MLP3_STEP, MLP3_HEAD, MLP3_TAIL_GRAD, MLP3_TAIL_ADAM, MLP3_PRIME, MLP3_STEP_DP, MLP3_STEP1, MLP3_STEP1_DP = range(8)
 ONE_LAUNCH_MAX_B = 32  # MLP3_STEP1 / MLP3_STEP1_DP: one head workgroup
+# exchange protocols of MLP3_STEP1_DP (csrc/mlp_step3.hip, "Wave-positioned exchange protocols")
+DP_GRANULE, DP_PACKED, DP_OWNER = 0, 1, 2
+DP_PROTOS = {"granule": DP_GRANULE, "packed": DP_PACKED, "owner": DP_OWNER}
+# floats per (slot, rank) receive area of the packed / owner protocols (comm/xgmi.h kDpUnitAreaFloats)
+DP_AREA_FLOATS = 327680
+
+
+def mlp3_dp_capacity(L1: int, L2: int) -> int:
+    """Receive-area capacity (floats) for NativeCommunicator.dp_context that every
+    one-launch protocol fits: 2 floats per parameter (granule) or the wave-positioned
+    areas (packed / owner)."""
+    return max(2 * mlp_param_count(L1, L2), DP_AREA_FLOATS)
 
 
 def mlp3_hand_words(L1: int, L2: int) -> int:
@@ -231,6 +243,8 @@ def mlp3_launch(
     dp_ctx: Optional[Sequence[int]] = None,
     head_part: Optional[torch.Tensor] = None,
     hand: Optional[torch.Tensor] = None,
+    dp_proto: int = -1,
+    dp_loop: bool = False,
 ) -> None:
     """One v3 launch (GPU only).  ``kind``: MLP3_STEP (head + fused tail, world size 1),
     MLP3_HEAD / MLP3_TAIL_GRAD (gradients, before the allreduce), MLP3_TAIL_ADAM
@@ -243,13 +257,17 @@ def mlp3_launch(
     CU and then does its tail share; ``hand`` holds the blocks' acknowledgements), MLP3_STEP1_DP
     (MLP3_STEP1 for world size > 1: each block allreduces its gradient values over xGMI as
     tagged granules between its gradient and its Adam; ``dp_ctx`` as for MLP3_STEP_DP,
-    receive area >= 2 floats per parameter).  ``order`` is [2, n_batches * B]:
+    receive area >= 2 floats per parameter for ``dp_proto`` 0).  ``dp_proto``: the
+    one-launch exchange -- DP_GRANULE (0, round 2), DP_PACKED (1, one-shot, two values
+    per granule), DP_OWNER (2, reduce-scatter / owner Adam / all-gather); -1 reads
+    ``RLA_DP_PROTO``.  ``dp_loop``: loopback diagnostic (one process plays every rank of
+    ``dp_ctx`` through its own region).  ``order`` is [2, n_batches * B]:
     the current and the next epoch's sample order (counters[4] selects)."""
     require().mlp3(
         int(kind), x_u8, labels, order, counters, int(n_batches), int(B), int(L1), int(L2), params, grads, exp_avg,
         exp_avg_sq, shadow, dh1t, xring, h1pre, act, yring, stats, bool(advance_step), float(lr), float(betas[0]),
         float(betas[1]), float(eps), float(weight_decay), float(grad_scale), lr_tensor, bool(adamw), stamps,
-        [int(v) for v in (dp_ctx or ())], head_part, hand,
+        [int(v) for v in (dp_ctx or ())], head_part, hand, int(dp_proto), bool(dp_loop),
     )
 
 

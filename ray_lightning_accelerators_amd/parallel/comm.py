@@ -293,6 +293,17 @@ class NativeCommunicator:
             return None
         return list(self._c.aux_context())
 
+    def dp_rearm(self) -> None:
+        """Re-arm the auxiliary region for a new exchange protocol (collective): every
+        rank drains its device, no kernel of any peer can still be writing, each rank
+        resets its own region (tags that match no coming step, generations 0)."""
+        if not self._c.has_aux:
+            return
+        torch.cuda.synchronize(self.device)
+        dist.barrier(group=self.group)
+        self._c.aux_rearm()
+        dist.barrier(group=self.group)
+
     # ------------------------------------------------------- collectives
     def allreduce_(self, t: torch.Tensor, average: bool = False, bf16_wire: bool = False) -> torch.Tensor:
         """In-place SUM (``average``: mean).  fp32 GPU buckets go through the C++

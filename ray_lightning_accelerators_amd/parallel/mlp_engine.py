@@ -74,6 +74,9 @@ class FusedMLPEngine:
         seed: int = 0,
         buffers: Optional[Dict[str, torch.Tensor]] = None,
         dp_context: Optional[Sequence[int]] = None,
+        dp_proto: Optional[str] = None,
+        dp_rearm: Optional[Callable[[], None]] = None,
+        dp_loop: bool = False,
     ):
         """``buffers``: optional external fp32 tensors ``params`` / ``grads`` /
         ``exp_avg`` / ``exp_avg_sq`` (e.g. views of a Trainer's parameter arena,
@@ -81,7 +84,13 @@ class FusedMLPEngine:
         ``dp_context``: ``NativeCommunicator.dp_context(...)`` -- world size > 1
         then runs the fused data-parallel step (the tail kernel exchanges its
         gradient tiles with the peers over xGMI inside the Adam epilogue: two
-        launches per step, no separate allreduce)."""
+        launches per step, no separate allreduce).  ``dp_proto``: the one-launch
+        step's exchange -- "packed" (one-shot, default), "owner" (reduce-scatter to
+        the task's owner, Adam there, all-gather of the weights) or "granule" (round
+        2); unset: ``RLA_DP_PROTO``.  ``dp_rearm``: collective reset of the exchange
+        region (``NativeCommunicator.dp_rearm``), run before a protocol is first used.
+        ``dp_loop``: loopback diagnostic (``dp_context`` of one process whose regions
+        all point at its own; see scripts/dp_overhead_probe.py)."""
         if not fused_mlp.mlp_supported(layer_1, layer_2):
             raise ValueError(f"no fused kernel for layer sizes {layer_1}/{layer_2}")
         if not 1 <= batch_size <= 256:
@@ -93,11 +102,14 @@ class FusedMLPEngine:
         self.world_size, self.rank = int(world_size), int(rank)
         self.allreduce = allreduce
         self.dp_ctx = None
-        if dp_context is not None and self.world_size > 1 and self.device.type == "cuda":
+        self.dp_loop = bool(dp_loop)
+        if dp_context is not None and (self.world_size > 1 or self.dp_loop) and self.device.type == "cuda":
             ctx = [int(v) for v in dp_context]
-            if ctx[0] != self.world_size or ctx[1] != self.rank:
+            if not self.dp_loop and (ctx[0] != self.world_size or ctx[1] != self.rank):
                 raise ValueError("dp_context belongs to a different (world, rank)")
             self.dp_ctx = ctx
+        self._dp_rearm = dp_rearm
+        self._owner_masks = None
         n = fused_mlp.mlp_param_count(self.L1, self.L2)
         if buffers is not None:
             for k in ("params", "grads", "exp_avg", "exp_avg_sq"):
@@ -127,11 +139,12 @@ class FusedMLPEngine:
         # world size 1, B <= 32: the whole step as ONE launch (RLA_MLP_ONE_LAUNCH=0: head + tail)
         self.one_launch = (self.B <= fused_mlp.ONE_LAUNCH_MAX_B
                            and os.environ.get("RLA_MLP_ONE_LAUNCH", "1") != "0")
-        # world size > 1 with the xGMI context: the same one launch, exchanging tagged
-        # granules (needs the granule protocol and a receive area of 2 floats / parameter)
-        self.one_launch_dp = (self.one_launch and self.dp_ctx is not None
-                              and os.environ.get("RLA_DP_PROTO", "granule") == "granule"
-                              and self.dp_ctx[2] >= 2 * n)
+        # world size > 1 with the xGMI context: the same one launch, each block
+        # exchanging its values with the peers (protocol: self.dp_proto)
+        self.dp_proto = "packed"
+        self.one_launch_dp = False
+        # (collective with a rearm callable: every rank builds its engine together)
+        self.set_dp_proto(dp_proto or os.environ.get("RLA_DP_PROTO") or "packed", rearm=True)
         self.stats = torch.zeros(stats_ring, 4, device=self.device)
         self.seed = seed
         self.epoch = 0
@@ -145,6 +158,65 @@ class FusedMLPEngine:
         self.x_u8 = self.labels = self.order = None
         self.n_batches = 0
         self.refresh_shadow()
+
+    # ------------------------------------------------- exchange protocol
+    def set_dp_proto(self, name: str, rearm: bool = True) -> None:
+        """Select the one-launch step's exchange protocol ("packed" / "owner" /
+        "granule"; "wave" / "all" are two-launch flag protocols).  Collective when
+        ``rearm`` (every rank switches together): the region is reset first, because
+        a granule left by another protocol could carry a current-looking tag."""
+        n = fused_mlp.mlp_param_count(self.L1, self.L2)
+        if name not in fused_mlp.DP_PROTOS and name not in ("wave", "all"):
+            raise ValueError(f"unknown data-parallel exchange protocol {name!r}")
+        if self.dp_proto == "owner" and name != "owner" and getattr(self, "_stepped_owner", False):
+            # leaving owner: non-owners' Adam state is stale -- consolidate first
+            self.sync_optimizer_state()
+        self._stepped_owner = False
+        self.dp_proto = name
+        ctx = self.dp_ctx
+        need = 2 * n if name == "granule" else fused_mlp.DP_AREA_FLOATS
+        self.one_launch_dp = (self.one_launch and ctx is not None and name in fused_mlp.DP_PROTOS
+                              and ctx[2] >= need)
+        if rearm and self.dp_ctx is not None and self._dp_rearm is not None:
+            self._dp_rearm()
+        self._drop_graphs()
+
+    def dp_owner_mask(self, rank: Optional[int] = None) -> torch.Tensor:
+        """Bool mask over the parameter arena: the elements whose Adam state this rank
+        keeps under the "owner" protocol (mirror of the kernel's dp_task_owner: W1
+        tile kt -> task kt; dW2 tile (ct, nt) -> 49 + ct * (L2/16) + nt; dW3 tile nt ->
+        49 + (L1/16)(L2/16) + nt; bias chunk of 64 -> after those; owner = task % N)."""
+        rank = self.rank if rank is None else int(rank)
+        world = self.dp_ctx[0] if self.dp_ctx is not None else self.world_size
+        L1, L2 = self.L1, self.L2
+        tn1, tn2 = L1 // 16, L2 // 16
+        tiles = 784 // 16
+        w1 = (torch.arange(784) // 16).repeat(L1)  # [L1 rows][784 pixels], row-major
+        nb = L1 + L2 + 10
+        w2 = tiles + (torch.arange(L1) // 16).repeat(L2) * tn2 + (torch.arange(L2) // 16).repeat_interleave(L1)
+        w3 = tiles + tn1 * tn2 + (torch.arange(L2) // 16).repeat(10)
+        bias = tiles + tn1 * tn2 + tn2 + torch.arange(nb) // 64
+        b1, b2, b3 = bias[:L1], bias[L1:L1 + L2], bias[L1 + L2:]
+        task = torch.cat([w1, b1, w2, b2, w3, b3])  # arena order: W1 B1 W2 B2 W3 B3
+        assert task.numel() == fused_mlp.mlp_param_count(L1, L2)
+        return (task % world) == rank
+
+    def sync_optimizer_state(self) -> None:
+        """Owner protocol: every rank's Adam state becomes the owners' (each element's
+        current m / v live only on its task's owner) -- a masked SUM allreduce, exact
+        (one nonzero term).  Collective; run before anything reads exp_avg /
+        exp_avg_sq (checkpoints, optimizer_state_dict, a protocol switch)."""
+        if not (self.native and self.one_launch_dp and self.dp_proto == "owner" and self.world_size > 1):
+            return
+        if self.dp_loop:
+            return  # loopback: one process holds every "rank's" state
+        if self.allreduce is None:
+            raise RuntimeError("owner protocol: sync_optimizer_state needs the engine's allreduce")
+        if self._owner_masks is None:
+            self._owner_masks = self.dp_owner_mask().to(self.device, torch.float32)
+        for t in (self.exp_avg, self.exp_avg_sq):
+            t.mul_(self._owner_masks)
+            self.allreduce(t)
 
     def _publish_counters(self) -> None:
         """Host edits of the device state go to both copies (current / advanced)."""
@@ -288,13 +360,15 @@ class FusedMLPEngine:
             self._reference_step()
         else:
             kw = self._kw3()
-            if self.world_size == 1:
+            if self.world_size == 1 and not self.dp_loop:
                 kind = fused_mlp.MLP3_STEP1 if self.one_launch else fused_mlp.MLP3_STEP
                 fused_mlp.mlp3_launch(kind, stats=self.stats, **kw)
             elif self.dp_ctx is not None:
                 kind = fused_mlp.MLP3_STEP1_DP if self.one_launch_dp else fused_mlp.MLP3_STEP_DP
-                fused_mlp.mlp3_launch(kind, stats=self.stats, grad_scale=1.0 / self.world_size,
-                                      dp_ctx=self.dp_ctx, **kw)
+                fused_mlp.mlp3_launch(kind, stats=self.stats, grad_scale=1.0 / self.dp_ctx[0],
+                                      dp_ctx=self.dp_ctx, dp_proto=fused_mlp.DP_PROTOS.get(self.dp_proto, -1),
+                                      dp_loop=self.dp_loop, **kw)
+                self._stepped_owner = self._stepped_owner or (self.one_launch_dp and self.dp_proto == "owner")
             else:
                 fused_mlp.mlp3_launch(fused_mlp.MLP3_HEAD, stats=self.stats, **kw)
                 fused_mlp.mlp3_launch(fused_mlp.MLP3_TAIL_GRAD, stats=self.stats, **kw)  # multi-block head stats
@@ -433,7 +507,9 @@ class FusedMLPEngine:
         return {k: v.detach().cpu().clone() for k, v in fused_mlp.mlp_unpack(self.params, self.L1, self.L2).items()}
 
     def optimizer_state_dict(self) -> Dict:
-        """torch.optim.Adam.state_dict() layout (Lightning checkpoint `optimizer_states`)."""
+        """torch.optim.Adam.state_dict() layout (Lightning checkpoint `optimizer_states`).
+        Collective under the owner protocol (state consolidation)."""
+        self.sync_optimizer_state()
         step = float(self.counters[0].item())
         m = fused_mlp.mlp_unpack(self.exp_avg, self.L1, self.L2)
         v = fused_mlp.mlp_unpack(self.exp_avg_sq, self.L1, self.L2)

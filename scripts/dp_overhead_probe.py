@@ -1,9 +1,19 @@
-"""Diagnostic: intrinsic cost of the fused data-parallel tail's in-kernel exchange
-protocol on ONE GPU.  A world-1 aux region (push to self, then tagged-granule polls
--- or, with RLA_DP_PROTO=wave|all, system fences + flags --
-and a fixed-order sum) is driven by the StepDP kernel and timed against the
-plain fused step, both replayed from hipGraphs -- a lower bound of what the
-exchange adds per step at N > 1 (where the pushes also cross xGMI)."""
+"""Diagnostic: in-kernel cost of the one-launch data-parallel step's exchange
+protocols on ONE GPU, per world size.
+
+Loopback world N: one process plays all N ranks through its own aux region (the
+block writes every source slot itself, polls N granules per value pair, sums;
+"owner" also plays every owner: Adam + all-gather publish).  What this prices is
+the issue / poll / sum work inside the kernel -- a LOWER bound of what the
+exchange adds per step at N ranks, where the pushes also cross xGMI (one hop for
+packed, two for owner; see the cost model in csrc/mlp_step3.hip).  Every variant
+is replayed from hipGraphs (25 steps per graph) and timed against the plain
+one-launch step.  Prints one JSON line per variant.
+
+  python scripts/dp_overhead_probe.py [--steps 4000] [--worlds 1,2,4,8]
+"""
+import argparse
+import json
 import sys
 import time
 
@@ -15,45 +25,48 @@ from ray_lightning_accelerators_amd.ops import fused_mlp  # noqa: E402
 from ray_lightning_accelerators_amd.parallel.comm import native_comm_module  # noqa: E402
 from ray_lightning_accelerators_amd.parallel.mlp_engine import FusedMLPEngine  # noqa: E402
 
+ap = argparse.ArgumentParser()
+ap.add_argument("--steps", type=int, default=4000)
+ap.add_argument("--worlds", default="1,2,4,8")
+ap.add_argument("--layers", default="32,64")
+args = ap.parse_args()
+L1, L2 = (int(v) for v in args.layers.split(","))
+
 dev = torch.device("cuda", 0)
 x, y = synthetic_mnist(55000, seed=0)
 mod = native_comm_module()
 c = mod.Communicator(0, 1, 0)
-c.aux_open([c.aux_handle(2 * fused_mlp.mlp_param_count(32, 64))])  # granule area
-ctx = [int(v) for v in c.aux_context()]
+c.aux_open([c.aux_handle(fused_mlp.mlp3_dp_capacity(L1, L2))])
+base_ctx = [int(v) for v in c.aux_context()]
 
 
-def run(kind, n=4000, G=25):
-    eng = FusedMLPEngine(32, 64, 32, lr=0.1, device=dev, seed=0)
+def run(proto=None, world=1, G=25):
+    kw = {}
+    if proto is not None:
+        ctx = base_ctx[:6] + [base_ctx[6]] * world
+        kw = dict(dp_context=ctx, dp_proto=proto, dp_loop=True, dp_rearm=c.aux_rearm)
+    eng = FusedMLPEngine(L1, L2, 32, lr=1e-3, device=dev, seed=0, **kw)
     eng.set_data(x, y)
-    eng.prime()
-    kw = eng._kw3()
-
-    def step():
-        if kind == "dp":
-            fused_mlp.mlp3_launch(fused_mlp.MLP3_STEP_DP, stats=eng.stats, grad_scale=1.0, dp_ctx=ctx, **kw)
-        else:
-            fused_mlp.mlp3_launch(fused_mlp.MLP3_STEP, stats=eng.stats, **kw)
-    for _ in range(50):
-        step()
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=s):
-        for _ in range(G):
-            step()
-    g.replay()
+    assert eng.capture(G)
+    eng.run(4 * G)
     torch.cuda.synchronize()
+    n = args.steps // G * G
     t0 = time.perf_counter()
-    for _ in range(n // G):
-        g.replay()
+    eng.run(n)
     torch.cuda.synchronize()
-    us = (time.perf_counter() - t0) / (n // G * G) * 1e6
+    us = (time.perf_counter() - t0) / n * 1e6
     assert c.error_state() == 0, c.error_message()
-    return us, float(eng.stats[:, 0].mean())
+    return us, float(eng.recent_stats(50)[:, 0].mean())
 
 
+rows = []
 for rep in range(2):
-    for kind in ("plain", "dp"):
-        us, loss = run(kind)
-        print(f"{kind} us_per_step {us:.2f} loss {loss:.4f}", flush=True)
+    plain, loss = run()
+    rows.append({"variant": "plain", "world": 1, "us_per_step": round(plain, 3), "loss": round(loss, 4), "rep": rep})
+    print(json.dumps(rows[-1]), flush=True)
+    for proto in ("packed", "owner"):
+        for w in (int(v) for v in args.worlds.split(",")):
+            us, loss = run(proto, w)
+            rows.append({"variant": proto, "world": w, "us_per_step": round(us, 3),
+                         "overhead_us": round(us - plain, 3), "loss": round(loss, 4), "rep": rep})
+            print(json.dumps(rows[-1]), flush=True)

@@ -73,3 +73,38 @@ def test_steal_grads_matches_torch_gpu(accumulate):
     for p, q in zip(model.parameters(), ref.parameters()):
         assert torch.allclose(p, q, atol=1e-5), (p - q).abs().max()
     assert len(arena._tables) >= 1  # the gather ran through the cached multi-copy table
+
+
+@pytest.mark.parametrize("L1,L2,world", [(32, 64, 8), (128, 256, 8), (64, 128, 3), (32, 32, 2)])
+def test_dp_owner_masks_partition_the_arena(L1, L2, world):
+    """Owner protocol: every parameter's Adam state lives on exactly one rank, and
+    the tasks spread evenly (kernel dp_task_owner: tiles then small tasks, round robin)."""
+    from ray_lightning_accelerators_amd.ops import fused_mlp
+    from ray_lightning_accelerators_amd.parallel.mlp_engine import FusedMLPEngine
+
+    eng = FusedMLPEngine(L1, L2, 32, world_size=world)
+    masks = torch.stack([eng.dp_owner_mask(r) for r in range(world)])
+    assert masks.shape[1] == fused_mlp.mlp_param_count(L1, L2)
+    assert torch.equal(masks.sum(0), torch.ones(masks.shape[1], dtype=torch.long))
+    # W1: tile kt (pixels 16kt..16kt+15 of every neuron row) belongs to rank kt % world
+    w1 = masks[:, : L1 * 784].view(world, L1, 784)
+    for kt in (0, 7, 48):
+        assert bool(w1[kt % world, :, 16 * kt: 16 * kt + 16].all())
+    # W2 element (n, m) -> task 49 + (m // 16) * (L2 // 16) + n // 16
+    off = L1 * 784 + L1
+    n, m = L2 - 1, L1 - 1
+    task = 49 + (m // 16) * (L2 // 16) + n // 16
+    assert bool(masks[task % world, off + n * L1 + m])
+    # balanced: ranks hold equal task counts up to one
+    tn1, tn2 = L1 // 16, L2 // 16
+    ntask = 49 + tn1 * tn2 + tn2 + (L1 + L2 + 10 + 63) // 64
+    counts = [len([t for t in range(ntask) if t % world == r]) for r in range(world)]
+    assert max(counts) - min(counts) <= 1
+
+
+def test_dp_area_constant_matches_kernel():
+    from ray_lightning_accelerators_amd.ops import fused_mlp
+
+    C = pytest.importorskip("ray_lightning_accelerators_amd._C")
+    assert fused_mlp.DP_AREA_FLOATS == C.mlp3_dp_area_floats()
+    assert fused_mlp.mlp3_dp_capacity(128, 256) >= 2 * fused_mlp.mlp_param_count(128, 256)

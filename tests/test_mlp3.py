@@ -305,3 +305,70 @@ def test_mlp3_reload_params_reprimes():
     idx = shard_indices(256, 2, 0, epoch, 0, True)[cur * 32:(cur + 1) * 32]
     emu = _emulate_bf16_grads(newp, x[idx].float() / 255.0, y[idx], 32, 64, 32)
     assert _rel(captured[-1][: emu.numel()], emu) < 2e-2
+
+
+def _loopback_ctx(world, L1=32, L2=64):
+    """A world-1 communicator's aux region presented as `world` ranks that all live
+    in this process (loopback: every region pointer is our own)."""
+    from ray_lightning_accelerators_amd.parallel.comm import native_comm_module
+
+    mod = native_comm_module()
+    c = mod.Communicator(0, 1, 0)
+    c.aux_open([c.aux_handle(fused_mlp.mlp3_dp_capacity(L1, L2))])
+    ctx = [int(v) for v in c.aux_context()]
+    return c, ctx[:6] + [ctx[6]] * world
+
+
+@gpu
+@pytest.mark.parametrize("proto", ["packed", "owner"])
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_mlp3_dp_loopback_tracks_single_rank(proto, world):
+    """Loopback world-N (one process writes every rank's source slots, polls N
+    granules per value, sums, and -- owner -- plays every owner): the exchange of N
+    identical contributions averages back to this rank's own gradient, so the run
+    follows the plain one-launch step up to the protocol's wire rounding (4 ulp of
+    fp32 per value).  Exercises every in-kernel path of the N-rank exchange on one GPU."""
+    from ray_lightning_accelerators_amd.models.data import synthetic_mnist
+
+    dev = _dev()
+    x, y = synthetic_mnist(2048, seed=0)
+    c, ctx = _loopback_ctx(world)
+    lb = FusedMLPEngine(32, 64, 32, lr=1e-3, device=dev, dp_context=ctx, dp_proto=proto, dp_loop=True)
+    ref = FusedMLPEngine(32, 64, 32, lr=1e-3, device=dev)
+    assert lb.one_launch_dp and lb.dp_ctx[0] == world
+    lb.set_data(x, y)
+    ref.set_data(x, y)
+    lb.run(3)  # eager, then graph replays
+    ref.run(3)
+    assert lb.capture(8)
+    ref.run(1)
+    lb.run(96)
+    ref.run(96)
+    torch.cuda.synchronize()
+    assert c.error_state() == 0, c.error_message()
+    lb.check()
+    d = (lb.params - ref.params).abs().max().item()
+    assert d < 2e-4, d  # 100 Adam steps at lr 1e-3 of 2^-22-relative gradient rounding
+    ll, lr_ = lb.recent_stats(20)[:, 0], ref.recent_stats(20)[:, 0]
+    assert torch.allclose(ll, lr_, rtol=1e-2, atol=1e-3), (ll, lr_)
+    assert torch.allclose(lb.exp_avg, ref.exp_avg, rtol=1e-2, atol=1e-6)
+
+
+@gpu
+def test_mlp3_dp_loopback_timeout_is_reported():
+    """Rank 1 of a 2-rank packed exchange whose peer never runs: its polls give up
+    after the bound and set the error word instead of hanging the GPU."""
+    from ray_lightning_accelerators_amd.models.data import synthetic_mnist
+
+    dev = _dev()
+    x, y = synthetic_mnist(512, seed=0)
+    c, ctx = _loopback_ctx(2)
+    ctx[1] = 1  # rank 1 of 2, not loopback: it waits for rank 0, which never runs
+    c.set_spin_limit(1 << 12)
+    ctx[3] = 1 << 12
+    e = FusedMLPEngine(32, 64, 32, lr=1e-3, device=dev, world_size=2, rank=1, dp_context=ctx, dp_proto="packed")
+    e.set_data(x, y)
+    e.run(1)
+    torch.cuda.synchronize()
+    assert c.error_state() != 0
+    c.reset_error()
