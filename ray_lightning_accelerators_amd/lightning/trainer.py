@@ -646,6 +646,7 @@ class Trainer:
             return []
         was_training = model.training
         model.eval()
+        mark("eval_start", stage=stage)
         self.call_hook(f"on_{stage}_start")
         self.call_hook(f"on_{stage}_epoch_start")
         fused_eval = (self._fused is not None and not test_mode and hasattr(self._fused, "eval_epoch")
@@ -678,6 +679,7 @@ class Trainer:
                     if out is not None:
                         outputs.append(out)
                 all_outputs.append(outputs)
+        mark("eval_launched", stage=stage)
         self._current_fx = f"{stage}_epoch_end"
         epoch_out = getattr(model, f"{stage}_epoch_end")(all_outputs[0] if len(dls) == 1 else all_outputs)
         self._absorb_legacy(epoch_out)
@@ -687,7 +689,9 @@ class Trainer:
         metrics.update(self._reduce_epoch_metrics(f"{stage}_step_end"))
         metrics.update(self._reduce_epoch_metrics(f"{stage}_epoch_end"))
         self.call_hook(f"on_{stage}_epoch_end")
+        mark("eval_epoch_end_hooks", stage=stage)
         self.call_hook(f"on_{stage}_end")
+        mark("eval_end_hooks", stage=stage)
         if stage == "validation" and getattr(self, "world_size", 1) > 1:
             # ModelCheckpoint (on_validation_end) may have rank 0 writing a file: the
             # other ranks wait for it here, not inside the next step's gradient
@@ -699,7 +703,9 @@ class Trainer:
             model.train()
         if not self.running_sanity_check:
             self._flush_logger()
-        return [{k: float(v) for k, v in metrics.items()}]
+        out = [{k: float(v) for k, v in metrics.items()}]
+        mark("eval_done", stage=stage)
+        return out
 
     def run_test(self):
         model = self.get_model()
@@ -780,6 +786,7 @@ class Trainer:
         if self._fused is not None and hasattr(self._fused, "make_epoch_batches") and \
                 (chunk > 1 or not self._batch_hooks_overridden(model)) and dl is not None and n > 0:
             batches = self._fused.make_epoch_batches(dl, n)  # data stays resident on the device
+            mark("epoch_order_ready", epoch=self.current_epoch)
             if batches is not None:
                 n = min(n, len(batches))
         if dl is not None and n > 0 and chunk > 1 and batches is not None:
@@ -801,6 +808,7 @@ class Trainer:
                     break
                 if self.should_stop:
                     break
+        mark("epoch_train_done", epoch=self.current_epoch)
         self._current_fx = "training_epoch_end"
         res = model.training_epoch_end(epoch_outputs)
         self._absorb_legacy(res)
@@ -817,6 +825,7 @@ class Trainer:
         if not validated:
             self._flush_logger()
         self._check_collectives()
+        mark("epoch_end", epoch=self.current_epoch)
 
     def _check_collectives(self) -> None:
         """Fail fast on a collective that went wrong this epoch: the xGMI kernels'
@@ -883,6 +892,8 @@ class Trainer:
             self.profiler.start("run_training_batch")
             outs = self._fused.train_chunk(k)
             self.profiler.stop("run_training_batch")
+            if b == 0:
+                mark("first_chunk_dispatched", epoch=self.current_epoch)
             self.global_step += k
             epoch_outputs.extend(outs)
             for cb in self.callbacks:

@@ -396,6 +396,52 @@ def _gpu_worker(rank, world, port, q, mode):
                 res["mv"] = torch.cat([e_dp.exp_avg, e_dp.exp_avg_sq]).cpu().numpy().tobytes()
                 comm.check()
                 e_dp.check()
+        elif mode == "mlp_fidelity":
+            # Step1DP at world 2 against fp32 autograd of BOTH ranks' batches (the DDP
+            # average), every step over 2+ epochs
+            import torch.nn.functional as F
+
+            from ray_lightning_accelerators_amd.models.data import synthetic_mnist
+            from ray_lightning_accelerators_amd.ops import fused_mlp
+            from ray_lightning_accelerators_amd.parallel.mlp_engine import FusedMLPEngine, shard_indices
+
+            L1, L2, B = 32, 64, 32
+            x, y = synthetic_mnist(2 * B * 16 + 5, seed=14)
+            ctx = comm.dp_context(fused_mlp.mlp3_dp_capacity(L1, L2))
+            e = FusedMLPEngine(L1, L2, B, lr=1e-3, device=dev, world_size=world, rank=rank,
+                               allreduce=comm.allreduce_, dp_context=ctx, dp_rearm=comm.dp_rearm,
+                               dp_proto=os.environ.get("RLA_DP_PROTO", "packed"))
+            e.set_data(x, y, shuffle=True)
+            e.broadcast_from(0)
+            res["one_launch_dp"] = e.one_launch_dp
+            names = ("W1", "b1", "W2", "b2", "W3", "b3")
+
+            def ref_grad(flat, idx):
+                p = {k: v.clone().requires_grad_(True) for k, v in
+                     zip(names, fused_mlp.mlp_unpack(flat.cpu(), L1, L2).values())}
+                h = torch.relu(F.linear(x[idx].float() / 255.0, p["W1"], p["b1"]))
+                h = torch.relu(F.linear(h, p["W2"], p["b2"]))
+                F.nll_loss(torch.log_softmax(F.linear(h, p["W3"], p["b3"]), 1), y[idx]).backward()
+                return torch.cat([p[k].grad.reshape(-1) for k in names])
+
+            worst = {k: 0.0 for k in names}
+            b1 = e.betas[0]
+            nb = e.n_batches
+            for _ in range(2 * nb + 3):
+                epoch, cur = e.epoch, e.step_in_epoch
+                p0, m0 = e.params.clone(), e.exp_avg.clone()
+                e.step()
+                g = (e.exp_avg - b1 * m0) / (1 - b1)
+                ref = sum(ref_grad(p0, shard_indices(x.size(0), world, r, epoch, 0, True)[cur * B:(cur + 1) * B])
+                          for r in range(world)) / world
+                for k, a, b in zip(names, fused_mlp.mlp_unpack(g.cpu(), L1, L2).values(),
+                                   fused_mlp.mlp_unpack(ref, L1, L2).values()):
+                    worst[k] = max(worst[k], (a - b).norm().item() / max(b.norm().item(), 1e-12))
+            torch.cuda.synchronize()
+            comm.check()
+            e.check()
+            res["worst"] = worst
+            res["params"] = e.params.cpu().numpy().tobytes()
         elif mode == "timeout":
             x = torch.ones(1024, device=dev)
             if rank == 0:
@@ -502,6 +548,22 @@ def test_fused_dp_mlp_step_matches_split_allreduce(proto, batch, monkeypatch):
     # owner's weights are everyone's), Adam state too once consolidated
     assert out[0]["params"] == out[1]["params"]
     assert out[0]["mv"] == out[1]["mv"]
+
+
+@gpu
+def test_fused_dp_one_launch_grads_vs_fp32_autograd_two_ranks(monkeypatch):
+    """Step1DP (packed, 2 ranks) applies the DDP-averaged gradient of both ranks'
+    batches: per tensor within the bf16 bounds of the one-rank kernel test."""
+    from test_mlp3 import GRAD_BOUND, _fidelity_log
+
+    monkeypatch.setenv("RLA_DP_PROTO", "packed")
+    out = _run_gpu("mlp_fidelity")
+    for r, res in out.items():
+        assert res["one_launch_dp"], (r, res)
+        for k, v in res["worst"].items():
+            assert v < GRAD_BOUND[k], (r, k, res["worst"])
+    _fidelity_log("dp_two_ranks_packed_grads", {"max_rel_err": out[0]["worst"]})
+    assert out[0]["params"] == out[1]["params"]
 
 
 @gpu
