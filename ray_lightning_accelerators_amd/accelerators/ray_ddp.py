@@ -33,6 +33,7 @@ import torch
 import torch.distributed as dist
 
 from .. import runtime as ray
+from ..config import GPU_WORKER_REUSE_KEY, get_config
 from ..lightning.accelerators import DataParallelAccelerator
 from ..lightning.utilities import log
 from ..session import init_session, shutdown_session
@@ -64,6 +65,25 @@ class RayExecutor:
 
     def execute(self, fn: Callable, *args, **kwargs):
         return fn(*args, **kwargs)
+
+    def __rla_park__(self) -> None:
+        """Reset before the runtime recycles this process for the next actor (same
+        GPU): process group, native communicator, worker session and the
+        process-wide config go; the HIP context, loaded kernels, imports and the
+        caching allocator's memory stay (what a fresh worker would pay again)."""
+        from ..config import set_config
+        from ..parallel.comm import reset_native_comm
+
+        reset_native_comm()
+        if dist.is_available() and dist.is_initialized():
+            dist.destroy_process_group()
+        shutdown_session()
+        set_config(None)
+        if "torch" in sys.modules and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+
+
+RECYCLE_KEY = GPU_WORKER_REUSE_KEY
 
 
 def find_free_port() -> int:
@@ -116,7 +136,12 @@ class RayAccelerator(DataParallelAccelerator):
 
     # ----------------------------------------------------------- driver side
     def _create_worker(self):
-        return RayExecutor.options(num_cpus=self.num_cpus_per_worker, num_gpus=int(self.use_gpu)).remote()
+        opts = dict(num_cpus=self.num_cpus_per_worker, num_gpus=int(self.use_gpu))
+        if self.use_gpu and get_config().reuse_workers:
+            # a recycled GPU worker (HIP context + kernels already loaded) when one is
+            # parked for this GPU: Tune trials stop paying worker start-up each
+            opts["_reuse"] = RECYCLE_KEY
+        return RayExecutor.options(**opts).remote()
 
     def setup(self, model) -> None:
         assert self.trainer is not None, "trainer must be attached before setup()"

@@ -72,6 +72,10 @@ class RLAConfig:
     # thread only competes with the training loop (MNIST epoch-end +0.7 ms,
     # profiles/r2_c38); it pays when file I/O dominates (large checkpoints)
     async_checkpoint: bool = False
+    # RayAccelerator GPU workers are recycled across fits (Tune trials): a finished
+    # fit parks its worker processes with their HIP context and loaded kernels, and
+    # the next fit on the same GPUs takes them over (runtime actor reuse)
+    reuse_workers: bool = True
     # Trainer: fused resident steps issued per host dispatch when nothing observes
     # single batches (chunks also end at log / validation / max_steps boundaries);
     # 1 = one dispatch per batch.  Capped by the fused step's stats ring (64).
@@ -163,6 +167,9 @@ def _parse(typ, raw: str, key: str):
     except ValueError as e:
         raise ValueError(f"env {key}={raw!r} is not a valid {t}") from e
 
+
+# runtime reuse key of RayAccelerator's GPU workers (recycled / pre-warmed processes)
+GPU_WORKER_REUSE_KEY = "rla-ddp-gpu-worker"
 
 _current: Optional[RLAConfig] = None
 

@@ -1010,11 +1010,20 @@ __device__ __forceinline__ u64 ld_sys(const u64* p) {
 // any check, then only the mismatched ones are re-read, so the common case is ONE
 // round trip for all of them.  Returns when every tag matches or the bound expires
 // (*fail set).  Unrolled over NMAX: w[] stays in registers.
-template <int NMAX, typename Addr, typename TagOk>
-__device__ __forceinline__ void dp_poll(const MLP3Args& a, u64 (&w)[NMAX], int n, Addr addr, TagOk ok, int* fail) {
+template <int NMAX, typename Addr>
+__device__ __forceinline__ void dp_poll_issue(u64 (&w)[NMAX], int n, Addr addr) {
 #pragma unroll
   for (int i = 0; i < NMAX; ++i)
     if (i < n) w[i] = ld_sys(addr(i));
+}
+
+// Check / re-poll granules issued by dp_poll_issue.  gfx950 counts loads AND stores
+// in one in-order vmcnt, so a wave's own pushes issued BEFORE its polls would make
+// the first wait cover their completion acks too (a full remote round trip); the
+// protocols below issue the first polls before their pushes.
+template <int NMAX, typename Addr, typename TagOk>
+__device__ __forceinline__ void dp_poll_finish(const MLP3Args& a, u64 (&w)[NMAX], int n, Addr addr, TagOk ok,
+                                               int* fail) {
   int64_t spins = 0;
   while (true) {
     bool all = true;
@@ -1035,17 +1044,25 @@ __device__ __forceinline__ void dp_poll(const MLP3Args& a, u64 (&w)[NMAX], int n
 
 // Fixed-rank-order sum of every rank's packed contribution to this lane's 4 values
 // (our own from registers): polls the W - 1 peers' granules of slot / unit.
-__device__ __forceinline__ void dp_packed_sum(const MLP3Args& a, int unit, int slot, uint32_t tag, u64 g0, u64 g1,
-                                              float (&v)[4], float scale, int* fail) {
-  const int lane = threadIdx.x & 63, me = a.dp_rank, W = a.dp_world;
-  char* mine = a.dp_regions[me];
-  // granule i: peer s = i / 2 (skipping me), half i & 1
-  auto addr = [&](int i) {
+// granule i of the W - 1 peers' packed contributions to unit / slot: peer i / 2
+// (ranks in order, skipping ours), half i & 1
+struct DpPeerAddr {
+  char* mine;
+  int slot, unit, me, lane;
+  __device__ __forceinline__ const u64* operator()(int i) const {
     const int k = i >> 1, s = k < me ? k : k + 1;
     return dp_pk_area(mine, slot, s, unit) + (i & 1) * 64 + lane;
-  };
-  u64 w[2 * (kXgmiMaxRanks - 1)];
-  dp_poll(a, w, 2 * (W - 1), addr, [tag](u64 x) { return ((uint32_t)x & 3u) == tag; }, fail);
+  }
+};
+constexpr int kDpPeerGran = 2 * (kXgmiMaxRanks - 1);
+
+__device__ __forceinline__ void dp_packed_sum(const MLP3Args& a, int unit, int slot, uint32_t tag, u64 g0, u64 g1,
+                                              float (&v)[4], float scale, int* fail, u64 (&w)[kDpPeerGran],
+                                              bool issued) {
+  const int me = a.dp_rank, W = a.dp_world;
+  const DpPeerAddr addr{a.dp_regions[me], slot, unit, me, (int)(threadIdx.x & 63)};
+  if (!issued) dp_poll_issue(w, 2 * (W - 1), addr);
+  dp_poll_finish(a, w, 2 * (W - 1), addr, [tag](u64 x) { return ((uint32_t)x & 3u) == tag; }, fail);
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll
   for (int s = 0; s < kXgmiMaxRanks; ++s) {
@@ -1076,10 +1093,13 @@ __device__ __forceinline__ void dp_packed_exchange(const MLP3Args& a, int unit, 
   const int slot = (int)(gen & 1u), me = a.dp_rank, W = a.dp_world;
   const uint32_t tag = (gen >> 1) & 3u;
   const u64 g0 = pk2(v[0], v[1], tag), g1 = pk2(v[2], v[3], tag);
+  u64 w[kDpPeerGran];
+  // first polls before the pushes (see dp_poll_finish); loopback reads its own pushes
+  if (!a.dp_loop) dp_poll_issue(w, 2 * (W - 1), DpPeerAddr{a.dp_regions[me], slot, unit, me, (int)(threadIdx.x & 63)});
   // 2 x 512 contiguous bytes per peer (loopback: every peer's source slot of our own region)
   for (int r = 0; r < W; ++r)
     if (r != me) dp_push_packed(a.dp_regions[r], slot, a.dp_loop ? r : me, unit, g0, g1);
-  dp_packed_sum(a, unit, slot, tag, g0, g1, v, scale, fail);
+  dp_packed_sum(a, unit, slot, tag, g0, g1, v, scale, fail, w, !a.dp_loop);
 }
 
 // "owner": the task's gradient goes to its owner rank only (reduce-scatter, one
@@ -1097,13 +1117,18 @@ __device__ __forceinline__ bool dp_owner_step(const MLP3Args& a, int unit, int o
   const uint32_t tag = (gen >> 1) & 3u;
   const bool own = owner == me;
   const u64 g0 = pk2(v[0], v[1], tag), g1 = pk2(v[2], v[3], tag);
+  const u64* agsrc = dp_ag_area(a.dp_regions[me], slot, unit) + lane;
+  auto agaddr = [agsrc](int i) { return agsrc + i * 64; };
+  u64 wa[4];
+  if (!own && !a.dp_loop) dp_poll_issue(wa, 4, agaddr);  // first polls before the push
   if (!own) dp_push_packed(a.dp_regions[owner], slot, me, unit, g0, g1);
   if (own || a.dp_loop) {
     if (own) {
+      u64 w[kDpPeerGran];
       if (a.dp_loop)
         for (int s = 0; s < W; ++s)
           if (s != me) dp_push_packed(a.dp_regions[me], slot, s, unit, g0, g1);
-      dp_packed_sum(a, unit, slot, tag, g0, g1, v, scale, fail);
+      dp_packed_sum(a, unit, slot, tag, g0, g1, v, scale, fail, w, false);
     } else {  // loopback stand-in of the owner: W identical contributions
       float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
       for (int s = 0; s < W; ++s) { s0 += pk_lo(g0); s1 += pk_hi(g0); s2 += pk_lo(g1); s3 += pk_hi(g1); }
@@ -1119,13 +1144,24 @@ __device__ __forceinline__ bool dp_owner_step(const MLP3Args& a, int unit, int o
     }
     if (own) return true;
   }
-  const u64* src = dp_ag_area(a.dp_regions[me], slot, unit) + lane;
-  u64 w[4];
-  dp_poll(a, w, 4, [src](int i) { return src + i * 64; }, [gen](u64 x) { return (uint32_t)(x >> 32) == gen; },
-          fail);
+  if (a.dp_loop) dp_poll_issue(wa, 4, agaddr);
+  dp_poll_finish(a, wa, 4, agaddr, [gen](u64 x) { return (uint32_t)(x >> 32) == gen; }, fail);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = __uint_as_float((uint32_t)w[i]);
+  for (int i = 0; i < 4; ++i) v[i] = __uint_as_float((uint32_t)wa[i]);
   return false;
+}
+
+// One-launch DP: this launch's generation, read with the step state at kernel start
+// (a scalar load -- the kernel boundary's cache invalidation covers it), so no block
+// waits on a dependent global load and a barrier before its exchange; the end
+// needs no barrier either (every thread holds the same value; timeouts go straight
+// to the host-mapped error word).
+__device__ __forceinline__ uint32_t dp_gen_now(const MLP3Args& a) {
+  return ((const __attribute__((address_space(4))) uint32_t*)(a.dp_gen))[blockIdx.x] + 1u;
+}
+__device__ __forceinline__ void dp_end_nosync(const MLP3Args& a, uint32_t gen, int fail) {
+  if (threadIdx.x == 0) a.dp_gen[blockIdx.x] = gen;
+  if (fail) __hip_atomic_store(a.dp_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Owner of a task of the one-launch step: W1 tile kt -> task kt; small-parameter
@@ -1486,6 +1522,7 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
   const int64_t c0 = ld_state(a.counters, 0), cursor = ld_state(a.counters, 1);
   const int64_t slot = ld_state(a.counters, 3), ob = ld_state(a.counters, 4);
   const int64_t seq = ld_state(a.counters, kSeq);
+  const uint32_t dgen = DP ? dp_gen_now(a) : 0u;
   const int B = a.B;
 
   // ---- tail-role loads that need nothing from this step, issued before the head
@@ -1552,9 +1589,8 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
     }
     bool adam_done = false, store_mv = true;
     if constexpr (DP) {  // the tile's allreduce, inside the epilogue (protocol: a.dp_proto)
-      __shared__ uint32_t sh_dgen;
-      const int dslot = dp_begin(a, &sh_dgen);
-      const uint32_t gen = sh_dgen;
+      const uint32_t gen = dgen;
+      const int dslot = (int)(gen & 1u);
       int fail = 0;
       if (mw) {
         if (a.dp_proto == 0) {  // round 2: arena-indexed {gen, fp32} granules
@@ -1583,7 +1619,7 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
           for (int i = 0; i < 4; ++i) acc[i] = v[i];
         }
       }
-      dp_gran_end(a, gen, fail, &sh_fail);
+      dp_end_nosync(a, gen, fail);
     }
     if (mw) {
       if (!adam_done) {
@@ -1632,9 +1668,8 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
     small_compute<L1, L2, true>(a, true, task, r, &L);
     bool adam_done = false, store_mv = true;
     if constexpr (DP) {
-      __shared__ uint32_t sh_sgen;
-      const int dslot = dp_begin(a, &sh_sgen);
-      const uint32_t gen = sh_sgen;
+      const uint32_t gen = dgen;
+      const int dslot = (int)(gen & 1u);
       int fail = 0;
       if (a.dp_proto == 0) {
 #pragma unroll
@@ -1663,7 +1698,7 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) r.v[i] = v[i];
       }
-      dp_gran_end(a, gen, fail, &sh_fail);
+      dp_end_nosync(a, gen, fail);
     }
     one_wait_acks(a, seq, &sh_fail);  // every block has read the weights / biases this overwrites
     if (adam_done) small_store<L1, L2>(a, r, store_mv);  // r.v: the new weights

@@ -21,6 +21,7 @@ from .client import (  # noqa: F401
     is_initialized,
     kill,
     nodes,
+    prewarm_gpu_workers,
     put,
     remote,
     shutdown,

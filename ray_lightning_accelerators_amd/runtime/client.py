@@ -363,6 +363,9 @@ class ActorClass:
             "sys_path": os.pathsep.join(p for p in sys.path if p),
             "cwd": os.getcwd(), "timeout": float(opts.get("_creation_timeout", 3600)),
             "owner": os.environ.get(P.ENV_ACTOR_ID),
+            # recyclable worker: a kill parks the process (HIP context, loaded kernels,
+            # imports kept) for the next actor with the same key, node and GPUs
+            "reuse": opts.get("_reuse"),
         }
         cls_payload = P.dumps(self._cls)
         init_payload = P.dumps(_deref_args(args, kwargs))
@@ -574,6 +577,14 @@ def kill(actor: ActorHandle, no_restart: bool = True) -> None:
         c = rt._conns.pop(info["address"], None)
     if c is not None:
         c.close()
+
+
+def prewarm_gpu_workers(key: str) -> dict:
+    """Ask the head to start one recyclable worker per free GPU (key ``key``) that
+    initialises HIP and loads the native kernels in the background, so the first
+    actor created with ``.options(_reuse=key, num_gpus=1)`` skips that start-up
+    (Tune sweeps of short trials; idempotent)."""
+    return _runtime().head_call({"op": "prewarm", "key": key})
 
 
 def actors(actor_id: Optional[str] = None) -> Dict[str, dict]:

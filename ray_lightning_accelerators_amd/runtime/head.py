@@ -79,6 +79,7 @@ class ActorRecord:
         self.death_cause: Optional[str] = None
         self.class_name = ""
         self.owner: Optional[str] = None
+        self.reuse: Optional[str] = None  # recyclable worker key (see Head._park)
 
 
 class Head:
@@ -101,6 +102,14 @@ class Head:
         self.pool_starting: Dict[int, subprocess.Popen] = {}
         self.pool_ready: List = []
         self.pool_lock = threading.Lock()
+        # recycled workers (actors created with a reuse key): a kill parks the process
+        # instead of ending it -- HIP context, loaded kernel objects and imports stay
+        # -- and the next actor with the same key, node and GPU tokens takes it over.
+        # parking: pid -> (Popen, key, node, gpu_ids) until the worker reports back;
+        # parked: [(Popen, conn, key, node, gpu_ids)] waiting for an assignment
+        self.parking: Dict[int, tuple] = {}
+        self.parked: List[tuple] = []
+        self.prewarmed: set = set()  # (key, node ip, gpu token) already started
 
     # ------------------------------------------------------------ worker pool
     def _pool_env(self) -> Dict[str, str]:
@@ -179,6 +188,7 @@ class Head:
             rec = ActorRecord(actor_id, msg.get("name"), req, node, gpu_ids)
             rec.class_name = msg.get("class_name", "")
             rec.owner = msg.get("owner")
+            rec.reuse = msg.get("reuse") or None
             self.actors[actor_id] = rec
         env = dict(os.environ)
         env.update(msg.get("env") or {})
@@ -206,8 +216,17 @@ class Head:
         if "OMP_NUM_THREADS" not in (msg.get("env") or {}):
             env["OMP_NUM_THREADS"] = str(max(1, int(req.get("CPU", 1) or 1)))
         log_path = os.path.join(self.log_dir, f"worker-{actor_id[:8]}.log")
-        pooled = self._take_pooled() if self._poolable(msg) else None
         proc = None
+        recycled = self._take_parked(rec.reuse, node, gpu_ids) if rec.reuse and self._poolable(msg) else None
+        if recycled is not None:
+            proc, conn = recycled
+            try:  # the whole environment is replaced (a recycled process carries its last actor's)
+                conn.send({"op": "assign", "env": env, "replace": True, "cwd": msg.get("cwd") or os.getcwd(),
+                           "log": log_path})
+                conn.close()
+            except (OSError, EOFError):
+                proc = None
+        pooled = self._take_pooled() if self._poolable(msg) and proc is None else None
         if pooled is not None:
             proc, conn = pooled
             # the actor-specific part of the environment (a pooled process already
@@ -261,7 +280,68 @@ class Head:
         for o in orphans:
             threading.Thread(target=self._kill, args=(o, f"owner {rec.actor_id[:8]} died"), daemon=True).start()
 
+    # -------------------------------------------------------- recycling
+    def _take_parked(self, key: str, node: Node, gpu_ids: List[str]):
+        with self.pool_lock:
+            for i, (proc, conn, k, nd, ids) in enumerate(self.parked):
+                if k == key and nd is node and sorted(ids) == sorted(gpu_ids) and proc.poll() is None:
+                    del self.parked[i]
+                    return proc, conn
+        return None
+
+    def _park(self, rec: ActorRecord) -> bool:
+        """Ask a recyclable actor's worker to reset and wait for a new assignment
+        (instead of ending it).  True when the worker acknowledged; the caller then
+        marks the actor DEAD (its resources return to the ledger)."""
+        proc = rec.proc
+        if self.stopping or rec.address is None or proc is None or proc.poll() is not None:
+            return False
+        with self.pool_lock:
+            self.parking[proc.pid] = (proc, rec.reuse, rec.node, list(rec.gpu_ids))
+        try:
+            c = P.connect(rec.address, self.authkey)
+            try:
+                c.send({"kind": "park", "call_id": "park", "payload": P.dumps(((), {}))})
+                # a worker still busy in a call (failure teardown) is ended instead
+                ok = c.conn.poll(float(os.environ.get("RLA_PARK_TIMEOUT", "10"))) and bool(c.recv().get("ok"))
+            finally:
+                c.close()
+        except Exception:  # noqa: BLE001 - any failure: end the process instead
+            ok = False
+        if not ok:
+            with self.pool_lock:
+                self.parking.pop(proc.pid, None)
+        return ok
+
+    def prewarm(self, key: str) -> dict:
+        """Start one recyclable worker per free GPU token that initialises HIP and
+        loads the native kernels, then parks under ``key`` (idempotent per token)."""
+        started = 0
+        for node in self.nodes:
+            with self.lock:
+                tokens = list(node.free_gpus)
+            for tok in tokens:
+                tag = (key, node.ip, tok)
+                if tag in self.prewarmed or self.stopping:
+                    continue
+                self.prewarmed.add(tag)
+                env = self._pool_env()
+                env.update({"HIP_VISIBLE_DEVICES": tok, "CUDA_VISIBLE_DEVICES": tok, "RLA_GPU_IDS": tok,
+                            P.ENV_NODE_IP: node.ip, P.ENV_NODE_ADDR: node.address})
+                log = open(os.path.join(self.log_dir, "prewarm.log"), "ab")
+                proc = subprocess.Popen([sys.executable, "-m", "ray_lightning_accelerators_amd.runtime.worker",
+                                         "--prewarm", key], env=env, stdout=log, stderr=subprocess.STDOUT,
+                                        start_new_session=True)
+                log.close()
+                with self.pool_lock:
+                    self.parking[proc.pid] = (proc, key, node, [tok])
+                started += 1
+        return {"ok": True, "started": started}
+
     def _kill(self, rec: ActorRecord, cause: str) -> None:
+        if rec.reuse and rec.state == "ALIVE" and self._park(rec):
+            self._mark_dead(rec, cause + " (worker recycled)")
+            return
         proc = rec.proc
         if proc is not None and proc.poll() is None:
             try:
@@ -298,6 +378,23 @@ class Head:
                             return
                     conn.close()
                     return
+                elif op == "parked":
+                    # a recycled / pre-warmed worker, reset and ready for a new actor
+                    with self.pool_lock:
+                        ent = self.parking.pop(int(msg["pid"]), None)
+                        if ent is not None and not self.stopping and msg.get("ok", True):
+                            proc, key, node, ids = ent
+                            rec = (proc, conn, key, node, ids)
+                            # workers that hold a HIP context are handed out first
+                            if msg.get("gpu_ready"):
+                                self.parked.insert(0, rec)
+                            else:
+                                self.parked.append(rec)
+                            return
+                    conn.close()
+                    return
+                elif op == "prewarm":
+                    reply = self.prewarm(str(msg["key"]))
                 elif op == "register":
                     rec = self.actors.get(msg["actor_id"])
                     if rec is not None:
@@ -360,7 +457,8 @@ class Head:
                 self._kill(rec, "runtime shutdown")
         with self.pool_lock:
             idle = [p for p, _ in self.pool_ready] + list(self.pool_starting.values())
-            self.pool_ready, self.pool_starting = [], {}
+            idle += [e[0] for e in self.parked] + [e[0] for e in self.parking.values()]
+            self.pool_ready, self.pool_starting, self.parked, self.parking = [], {}, [], {}
         for proc in idle:
             try:
                 os.killpg(proc.pid, signal.SIGKILL)

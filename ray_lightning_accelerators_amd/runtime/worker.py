@@ -28,6 +28,45 @@ class WorkerServer:
         self.instance = None
         self.executor = ThreadPoolExecutor(max_workers=1)
         self.exiting = False
+        self.parked = False  # set by a "park" request: serve() returns, the process is recycled
+        self.conns = set()
+        self.conns_lock = threading.Lock()
+
+    def _park(self, conn: P.SafeConn, call_id) -> None:
+        """Recycle this process (head's kill of a reusable actor): run the instance's
+        ``__rla_park__`` reset (process groups, communicators, sessions), drop it,
+        acknowledge, then stop serving -- every client connection is closed, so a
+        stale handle sees the actor as dead, never the next tenant."""
+        ok = True
+        try:
+            fn = getattr(self.instance, "__rla_park__", None)
+            if fn is not None:
+                fn()
+        except BaseException:  # noqa: BLE001 - an unclean reset ends the process instead
+            traceback.print_exc()
+            ok = False
+        self.instance = None
+        import gc
+
+        gc.collect()
+        try:
+            conn.send({"call_id": call_id, "ok": ok})
+        except Exception:
+            pass
+        if not ok:
+            os._exit(1)
+        self.parked = True
+        with self.conns_lock:
+            conns, self.conns = list(self.conns), set()
+        for c in conns:
+            try:
+                c.close()
+            except Exception:
+                pass
+        try:  # wake serve()'s accept (closing a listener does not interrupt a blocked accept)
+            P.connect(self.address, self.authkey).close()
+        except Exception:
+            pass
 
     def _run_call(self, conn: P.SafeConn, msg: dict) -> None:
         kind = msg["kind"]
@@ -78,6 +117,10 @@ class WorkerServer:
                 return
             if msg.get("kind") == "exit":
                 os._exit(0)
+            if msg.get("kind") == "park":
+                # after every call already submitted (same executor, in order)
+                self.executor.submit(self._park, conn, msg.get("call_id"))
+                return
             if msg.get("kind") == "init":
                 # construction must finish before any method runs
                 self._run_call(conn, msg)
@@ -89,18 +132,26 @@ class WorkerServer:
         head.send({"op": "register", "actor_id": self.actor_id, "address": self.address, "pid": os.getpid()})
         head.recv()
         head.close()
-        while True:
+        while not self.parked:
             try:
                 c = self.listener.accept()
             except (OSError, EOFError):
                 continue
-            threading.Thread(target=self._serve_conn, args=(P.SafeConn(c),), daemon=True).start()
+            if self.parked:
+                c.close()
+                break
+            sc = P.SafeConn(c)
+            with self.conns_lock:
+                self.conns.add(sc)
+            threading.Thread(target=self._serve_conn, args=(sc,), daemon=True).start()
+        try:
+            self.listener.close()
+        except Exception:
+            pass
+        self.executor.shutdown(wait=False)
 
 
-def _wait_for_assignment() -> None:
-    """Pre-started pool worker: import the heavy modules now (never touching a
-    GPU), then block until the head assigns an actor; apply its environment
-    (HIP_VISIBLE_DEVICES, actor id, ...), working directory and log file."""
+def _warm_imports() -> None:
     import torch  # noqa: F401 - the import is the point: it is what a pooled worker saves
     import torch.distributed  # noqa: F401
 
@@ -112,13 +163,49 @@ def _wait_for_assignment() -> None:
     import ray_lightning_accelerators_amd.models.datamodules  # noqa: F401
     import ray_lightning_accelerators_amd.tune  # noqa: F401
 
+
+def _warm_gpu() -> bool:
+    """Pre-warmed recyclable worker: initialise HIP on this process's GPU and load
+    the native kernel libraries (what the first step of a fresh worker pays)."""
+    try:
+        import torch
+
+        if not torch.cuda.is_available():
+            return False
+        torch.cuda.init()
+        torch.zeros(1, device="cuda").add_(1)
+        from ray_lightning_accelerators_amd import ops
+        from ray_lightning_accelerators_amd.parallel.comm import native_comm_module
+
+        ops.require()
+        native_comm_module()
+        torch.cuda.synchronize()
+        return True
+    except Exception:  # noqa: BLE001 - no usable GPU here: just do not park
+        traceback.print_exc()
+        return False
+
+
+def _wait_for_assignment(op: str = "pool_ready") -> None:
+    """Block until the head assigns an actor; apply its environment
+    (HIP_VISIBLE_DEVICES, actor id, ...), working directory and log file.
+    ``op``: "pool_ready" (pre-started pool worker: imports done, GPU untouched) or
+    "parked" (recycled / pre-warmed worker: HIP initialised on its GPU; the head
+    only hands it to an actor of the same key and GPU tokens)."""
     head = P.connect(os.environ[P.ENV_HEAD], bytes.fromhex(os.environ[P.ENV_AUTH]))
-    head.send({"op": "pool_ready", "pid": os.getpid()})
+    torch = sys.modules.get("torch")
+    warm = bool(torch is not None and torch.cuda.is_initialized())
+    head.send({"op": op, "pid": os.getpid(), "gpu_ready": warm})
     try:
         msg = head.recv()
     except (EOFError, OSError):
         os._exit(0)  # head gone: nobody will ever assign this worker
     head.close()
+    if msg.get("replace"):
+        # a recycled process: its environment is exactly the new actor's
+        for k in list(os.environ):
+            if k not in msg["env"]:
+                os.environ.pop(k, None)
     for k in msg.get("unset", []):
         os.environ.pop(k, None)
     os.environ.update(msg.get("env") or {})
@@ -130,22 +217,31 @@ def _wait_for_assignment() -> None:
     os.dup2(fd, 2)
     os.close(fd)
     n = os.environ.get("OMP_NUM_THREADS")
-    if n and n.isdigit():
-        torch.set_num_threads(int(n))  # libgomp read the head's value at import
+    if n and n.isdigit() and "torch" in sys.modules:
+        sys.modules["torch"].set_num_threads(int(n))  # libgomp read the head's value at import
 
 
 def main() -> None:
-    pooled = "--pool" in sys.argv[1:]
+    argv = sys.argv[1:]
     extra = os.environ.get(P.ENV_SYS_PATH, "")
     for p in reversed([x for x in extra.split(os.pathsep) if x]):
         if p not in sys.path:
             sys.path.insert(0, p)
-    if pooled:
-        _wait_for_assignment()
+    if "--pool" in argv:
+        _warm_imports()
+        _wait_for_assignment("pool_ready")
+    elif "--prewarm" in argv:
+        _warm_imports()
+        if not _warm_gpu():
+            os._exit(0)
+        _wait_for_assignment("parked")
     from . import client
 
-    client._mark_worker()
-    WorkerServer().serve()
+    while True:
+        client._mark_worker()
+        srv = WorkerServer()
+        srv.serve()  # returns only when the head recycled this process
+        _wait_for_assignment("parked")
 
 
 if __name__ == "__main__":

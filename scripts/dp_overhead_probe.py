@@ -43,7 +43,7 @@ base_ctx = [int(v) for v in c.aux_context()]
 def run(proto=None, world=1, G=25):
     kw = {}
     if proto is not None:
-        ctx = base_ctx[:6] + [base_ctx[6]] * world
+        ctx = [world] + base_ctx[1:6] + [base_ctx[6]] * world
         kw = dict(dp_context=ctx, dp_proto=proto, dp_loop=True, dp_rearm=c.aux_rearm)
     eng = FusedMLPEngine(L1, L2, 32, lr=1e-3, device=dev, seed=0, **kw)
     eng.set_data(x, y)

@@ -1,0 +1,47 @@
+#!/bin/bash
+# Parameterised GPU stages (one gpurun call runs several, chained; each GPU step under
+# its own limit; the first failing step ends the call).
+#   bash scripts/gpu_stage.sh OUT STAGE [STAGE ...]
+# stages: suite (full GPU pytest + smoke + default bench), dp (exchange protocols:
+# loopback / 2-rank tests + per-N cost probe), tune (sweep trials/hour cold + warm),
+# trainer (Trainer.fit bench + epoch-boundary timeline), recycle (worker reuse tests),
+# prof (rocprofv3 kernel stats of the default bench), bench20 (driver-shaped bench)
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"; export TMPDIR=/tmp
+O=${1:-gpurun_out/stage}; shift; mkdir -p "$O"
+run() {  # name limit cmd...
+  local n=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "$O/$n.log" 2>&1
+  local rc=$?
+  if [ $rc -ne 0 ]; then echo "[$n] FAILED rc=$rc"; tail -40 "$O/$n.log"; exit $rc; fi
+  echo "[$n] ok"; grep -h '^{' "$O/$n.log" | cut -c1-600 || true
+}
+PYT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
+for st in "$@"; do
+  case $st in
+    suite)
+      run pytest_gpu 1200 $PYT tests -m gpu
+      tail -3 "$O/pytest_gpu.log"
+      run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+      run bench_default 300 python bench.py ;;
+    dp)
+      RLA_FIDELITY_LOG="$R/$O/fidelity.jsonl" run pytest_dp 600 $PYT tests/test_mlp3.py tests/test_comm.py -k "loopback or fused_dp or fp32"
+      run dp_probe 300 python -u scripts/dp_overhead_probe.py ;;
+    recycle)
+      run pytest_recycle 300 $PYT tests/test_ddp_gpu.py tests/test_runtime.py -k "recycl" ;;
+    tune)
+      run tune_cold 300 python scripts/bench_tune.py --trials 4
+      run tune_cold16 300 python scripts/bench_tune.py --trials 16
+      run tune_warm 300 python scripts/bench_tune.py --trials 8 --warm 8 ;;
+    trainer)
+      RLA_TIMELINE="$R/$O/trainer_timeline.jsonl" run trainer 300 python bench.py --via trainer --trainer-epochs 6
+      python scripts/timeline_report.py "$O/trainer_timeline.jsonl" > "$O/trainer_timeline.txt" 2>&1 || true ;;
+    prof)
+      run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/prof" -o run -- python3 "$R/bench.py"
+      find "$O/prof" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats_default.csv" \; ;;
+    bench20)
+      run bench_k20 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    *) echo "unknown stage $st"; exit 2 ;;
+  esac
+done

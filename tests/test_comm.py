@@ -432,7 +432,7 @@ def _gpu_worker(rank, world, port, q, mode):
                 p0, m0 = e.params.clone(), e.exp_avg.clone()
                 e.step()
                 g = (e.exp_avg - b1 * m0) / (1 - b1)
-                ref = sum(ref_grad(p0, shard_indices(x.size(0), world, r, epoch, 0, True)[cur * B:(cur + 1) * B])
+                ref = sum(ref_grad(p0, shard_indices(x.size(0), world, r, epoch, e.seed, True)[cur * B:(cur + 1) * B])
                           for r in range(world)) / world
                 for k, a, b in zip(names, fused_mlp.mlp_unpack(g.cpu(), L1, L2).values(),
                                    fused_mlp.mlp_unpack(ref, L1, L2).values()):

