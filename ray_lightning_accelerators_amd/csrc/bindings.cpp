@@ -433,6 +433,40 @@ Tensor bn_bwd_finalize(Tensor part, double count, optional<Tensor> weight, Tenso
   return coef;
 }
 
+// x: [N, H, W, C] bf16 (NHWC view of a channels_last tensor); returns (y, argmax bytes)
+std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t s, int64_t pad) {
+  check_dev(x, "x", at::kBFloat16);
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(), "maxpool: x must be a contiguous NHWC [N, H, W, C] view");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(C % 8 == 0 && k >= 1 && s >= 1 && pad >= 0 && 2 * pad <= k, "maxpool: unsupported geometry");
+  const int64_t OH = (H + 2 * pad - k) / s + 1, OW = (W + 2 * pad - k) / s + 1;
+  TORCH_CHECK(OH > 0 && OW > 0, "maxpool: empty output");
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor y = at::empty({N, OH, OW, C}, x.options());
+  Tensor arg = at::empty({N, OH, OW, C}, x.options().dtype(at::kByte));
+  TORCH_CHECK(rla::launch_maxpool_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                      reinterpret_cast<uint16_t*>(y.data_ptr()), arg.data_ptr<uint8_t>(), (int)N, (int)H,
+                                      (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)pad, cur_stream(x)) == 0,
+              "maxpool forward launch failed");
+  return {y, arg};
+}
+
+Tensor maxpool_bwd(Tensor dy, Tensor arg, int64_t H, int64_t W, int64_t k, int64_t s, int64_t pad) {
+  check_dev(dy, "dy", at::kBFloat16);
+  check_dev(arg, "arg", at::kByte);
+  TORCH_CHECK(dy.dim() == 4 && dy.is_contiguous() && arg.sizes() == dy.sizes(), "maxpool backward: bad shapes");
+  const int64_t N = dy.size(0), OH = dy.size(1), OW = dy.size(2), C = dy.size(3);
+  TORCH_CHECK(C % 8 == 0 && OH == (H + 2 * pad - k) / s + 1 && OW == (W + 2 * pad - k) / s + 1,
+              "maxpool backward: geometry does not match the forward");
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  Tensor dx = at::empty({N, H, W, C}, dy.options());
+  TORCH_CHECK(rla::launch_maxpool_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), arg.data_ptr<uint8_t>(),
+                                      reinterpret_cast<uint16_t*>(dx.data_ptr()), (int)N, (int)H, (int)W, (int)C,
+                                      (int)OH, (int)OW, (int)k, (int)s, (int)pad, cur_stream(dy)) == 0,
+              "maxpool backward launch failed");
+  return dx;
+}
+
 void bn_apply(Tensor x, Tensor scale, Tensor shift, optional<Tensor> res, bool relu, Tensor y) {
   const int64_t C = scale.numel();
   const int64_t M = bn_rows(x, "x", C);
@@ -507,6 +541,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_finalize", &bn_finalize, "fused BN: mean/invstd/scale/shift + running stats from partials");
   m.def("bn_bwd_finalize", &bn_bwd_finalize, "fused BN backward: dgamma/dbeta + dx coefficients");
   m.def("bn_apply", &bn_apply, "fused BN apply: y = act(x*scale + shift (+res))");
+  m.def("maxpool_fwd", &maxpool_fwd, "NHWC bf16 max pool -> (y, one-byte window argmax)");
+  m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max pool backward (gather through the argmax bytes)");
   m.def("bn_bwd_apply", &bn_bwd_apply, "fused BN backward apply: dx (+ dres = relu-masked dy)");
   m.attr("ARCH") = "gfx950";
 }

@@ -46,6 +46,12 @@ void launch_sumsq(const float* x, int64_t n, float* out, hipStream_t stream);
 // [M, C] rows (csrc/bn_act.hip).  C % 8 == 0 and C <= kBnMaxC.
 // ---------------------------------------------------------------------------
 constexpr int kBnThreads = 256;
+
+// NHWC bf16 max pooling with a one-byte window argmax (csrc/pool.hip)
+int launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int OH, int OW,
+                       int k, int s, int pad, hipStream_t stream);
+int launch_maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int H, int W, int C, int OH,
+                       int OW, int k, int s, int pad, hipStream_t stream);
 constexpr int kBnMaxC = 2048;  // 8 channels per thread x 256 threads per row
 
 struct BnPlan {

@@ -24,6 +24,7 @@ from torch.utils.data import Dataset
 
 from ..lightning import LightningModule
 from ..ops.bn import BatchNormAct2d
+from ..ops.pool import MaxPool2dNHWC
 
 
 def _conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -75,7 +76,8 @@ class ResNet(nn.Module):
         self.fused_bn = fused_bn
         self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
         self.bn1 = _bn(64, fused_bn)
-        self.maxpool = nn.MaxPool2d(3, 2, 1)
+        # fused path: NHWC bf16 kernels with a one-byte argmax (ops/pool.py)
+        self.maxpool = MaxPool2dNHWC(3, 2, 1) if fused_bn else nn.MaxPool2d(3, 2, 1)
         self.layer1 = self._make(64, layers[0])
         self.layer2 = self._make(128, layers[1], 2)
         self.layer3 = self._make(256, layers[2], 2)

@@ -27,7 +27,10 @@ for st in "$@"; do
       run bench_default 300 python bench.py ;;
     dp)
       RLA_FIDELITY_LOG="$R/$O/fidelity.jsonl" run pytest_dp 600 $PYT tests/test_mlp3.py tests/test_comm.py -k "loopback or fused_dp or fp32"
-      run dp_probe 300 python -u scripts/dp_overhead_probe.py ;;
+      run dp_probe 300 python -u scripts/dp_overhead_probe.py
+      run dp_phases 300 python -u scripts/dp_phase_probe.py ;;
+    dpphase)
+      run dp_phases 300 python -u scripts/dp_phase_probe.py ;;
     recycle)
       run pytest_recycle 300 $PYT tests/test_ddp_gpu.py tests/test_runtime.py -k "recycl" ;;
     tune)
@@ -42,6 +45,17 @@ for st in "$@"; do
       find "$O/prof" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats_default.csv" \; ;;
     bench20)
       run bench_k20 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    rn50)
+      run pytest_bn 300 $PYT tests/test_bn.py
+      RB="python bench.py --model resnet50 --steps 30 --warmup 10"
+      run rn50_base 600 $RB
+      MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC=0 run rn50_no_wrw_gtc 600 $RB
+      MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC=0 MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_FWD_GTC_XDLOPS_NHWC=0 \
+        MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_BWD_GTC_XDLOPS_NHWC=0 run rn50_no_gtc 600 $RB ;;
+    rn50prof)
+      run rn50_prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/rn50prof" -o run -- \
+        python3 "$R/bench.py" --model resnet50 --steps 20 --warmup 10
+      find "$O/rn50prof" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats_rn50.csv" \; ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac
 done

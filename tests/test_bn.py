@@ -247,3 +247,27 @@ def test_lightning_resnet50_trainer_gpu_fused_bn(tmpdir):
     assert trainer.fit(model) == 1
     assert bnmod.stats["fused"] - before >= 2 * 53
     assert torch.isfinite(torch.as_tensor(float(trainer.callback_metrics["train_loss"])))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,k,s,p", [((4, 64, 112, 112), 3, 2, 1), ((2, 16, 9, 7), 3, 2, 1), ((3, 8, 8, 8), 2, 2, 0),
+                                        ((2, 24, 13, 13), 3, 1, 1)])
+def test_maxpool_nhwc_matches_torch(shape, k, s, p):
+    """Fused NHWC max pool (one-byte argmax, gather backward) == F.max_pool2d: same
+    outputs, same gradient (ties broken like PyTorch: first maximum wins)."""
+    from ray_lightning_accelerators_amd.ops.pool import max_pool2d_nhwc
+
+    torch.manual_seed(0)
+    x = torch.randn(*shape, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x[0, 0, :4, :4] = 1.0  # ties inside windows
+    xa = x.detach().clone().requires_grad_(True)
+    xb = x.detach().clone().requires_grad_(True)
+    ya = max_pool2d_nhwc(xa, k, s, p)
+    yb = F.max_pool2d(xb, k, s, p)
+    assert ya.shape == yb.shape and torch.equal(ya, yb)
+    g = torch.randn_like(yb, dtype=torch.float32).to(torch.bfloat16)
+    ya.backward(g)
+    yb.backward(g)
+    # windows sharing an argmax pixel add in fp32 and round once: <= 1 bf16 ulp apart
+    assert torch.allclose(xa.grad.float(), xb.grad.float(), rtol=1e-2, atol=1e-2)
+    assert (xa.grad != 0).sum() == (xb.grad != 0).sum()
