@@ -66,12 +66,11 @@ class RLAConfig:
     fused_dp: bool = True
     # capture the resident MNIST step into hipGraphs
     use_hip_graph: bool = True
-    # ModelCheckpoint writes run on a background thread (state snapshot taken
-    # synchronously; the Trainer drains the writes before fit() returns).  Off by
-    # default: for a small model the write is pickling under the GIL, so the
-    # thread only competes with the training loop (MNIST epoch-end +0.7 ms,
-    # profiles/r2_c38); it pays when file I/O dominates (large checkpoints)
-    async_checkpoint: bool = False
+    # ModelCheckpoint writes run in a writer PROCESS (state snapshot taken
+    # synchronously into shared memory; pickling, file write and rename off this
+    # process; the Trainer drains the writes before fit() returns).  Round 2's
+    # writer thread was slower (GIL: MNIST epoch-end +0.7 ms, profiles/r2_c38).
+    async_checkpoint: bool = True
     # RayAccelerator GPU workers are recycled across fits (Tune trials): a finished
     # fit parks its worker processes with their HIP context and loaded kernels, and
     # the next fit on the same GPUs takes them over (runtime actor reuse)

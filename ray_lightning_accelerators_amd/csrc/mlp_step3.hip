@@ -1498,8 +1498,13 @@ __device__ __forceinline__ void one_wait_acks(const MLP3Args& a, int64_t seq, in
 // DP (kind Step1DP, world size > 1): each tile's dW1 and each small wave's values
 // are allreduced over xGMI (tagged granules, as the two-launch StepDP tail) between
 // the block's gradient and its Adam -- the exchange sits inside the one launch.
-template <int L1, int L2, bool DP>
+// DPP: -1 world size 1 (Step1); else the exchange protocol of Step1DP (0 granule,
+// 1 packed, 2 owner) as a template parameter -- each instance carries only its own
+// protocol's code (a run-time switch over all three cost the head pass ~0.5 us and
+// the tile epilogue ~1.4 us of register pressure, profiles/r3_dp/dp_phases.log)
+template <int L1, int L2, int DPP>
 __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
+  constexpr bool DP = DPP >= 0;
   using C = typename One<L1, L2>::C;
   using S = SmallTasks<L1, L2>;
   constexpr int TN1 = L1 / 16, Bp = 32;
@@ -1593,7 +1598,7 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
       const int dslot = (int)(gen & 1u);
       int fail = 0;
       if (mw) {
-        if (a.dp_proto == 0) {  // round 2: arena-indexed {gen, fp32} granules
+        if constexpr (DPP == 0) {  // round 2: arena-indexed {gen, fp32} granules
 #pragma unroll
           for (int i = 0; i < 4; ++i) dp_push_gran(a, dslot, gidx + i, acc[i], gen);
 #pragma unroll
@@ -1601,7 +1606,7 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
         } else {
           float v[4] = {acc[0], acc[1], acc[2], acc[3]};
           const int unit = blk * kWaves + w;
-          if (a.dp_proto == 1) {
+          if constexpr (DPP == 1) {
             dp_packed_exchange(a, unit, gen, v, a.grad_scale, &fail);
           } else {
             const AdamScal o = *sh_o;
@@ -1671,7 +1676,7 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
       const uint32_t gen = dgen;
       const int dslot = (int)(gen & 1u);
       int fail = 0;
-      if (a.dp_proto == 0) {
+      if constexpr (DPP == 0) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           if (r.valid[i]) dp_push_gran(a, dslot, r.gi[i], r.v[i], gen);
@@ -1681,7 +1686,7 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
       } else if (task < S::NTASK) {  // whole waves (idle lanes exchange zeros)
         float v[4] = {r.v[0], r.v[1], r.v[2], r.v[3]};
         const int unit = blk * kWaves + w;
-        if (a.dp_proto == 1) {
+        if constexpr (DPP == 1) {
           dp_packed_exchange(a, unit, gen, v, a.grad_scale, &fail);
         } else {
           // Adam in registers before the acknowledgement wait below: the owner
@@ -1734,7 +1739,7 @@ int dispatch3(const MLP3Args& a, int kind, hipStream_t stream) {
   constexpr int kOneGrid = 1 + kTiles + One<L1, L2>::NSMALL;
   if (kind == kMLP3Step1) {
     if (a.B > 32 || !a.hand || kOneGrid > 256) return -5;
-    hipLaunchKernelGGL((mlp3_one_kernel<L1, L2, false>), dim3(kOneGrid), dim3(kThreads), 0, stream, a);
+    hipLaunchKernelGGL((mlp3_one_kernel<L1, L2, -1>), dim3(kOneGrid), dim3(kThreads), 0, stream, a);
     return 0;
   }
   if (kind == kMLP3Step1DP) {
@@ -1745,7 +1750,12 @@ int dispatch3(const MLP3Args& a, int kind, hipStream_t stream) {
     // round-2 granules need 2 floats per parameter, the wave-positioned areas their fixed size
     if (a.dp_proto == 0 ? (a.dp_lite != 2 || a.dp_stride < 2 * Off<L1, L2>::NP) : a.dp_stride < comm::kDpUnitAreaFloats)
       return -7;
-    hipLaunchKernelGGL((mlp3_one_kernel<L1, L2, true>), dim3(kOneGrid), dim3(kThreads), 0, stream, a);
+    if (a.dp_proto == 0)
+      hipLaunchKernelGGL((mlp3_one_kernel<L1, L2, 0>), dim3(kOneGrid), dim3(kThreads), 0, stream, a);
+    else if (a.dp_proto == 1)
+      hipLaunchKernelGGL((mlp3_one_kernel<L1, L2, 1>), dim3(kOneGrid), dim3(kThreads), 0, stream, a);
+    else
+      hipLaunchKernelGGL((mlp3_one_kernel<L1, L2, 2>), dim3(kOneGrid), dim3(kThreads), 0, stream, a);
     return 0;
   }
   constexpr int NT = 64 * (L1 / 16);

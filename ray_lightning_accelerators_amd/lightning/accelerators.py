@@ -274,6 +274,12 @@ class DataParallelAccelerator(Accelerator):
             seed_everything(int(os.environ["PL_GLOBAL_SEED"]))
         self.set_world_ranks(process_idx)
         rank_zero_only_state.rank = t.global_rank
+        if t.global_rank == 0 and get_config().async_checkpoint:
+            # the checkpoint writer process, forked now -- before this process
+            # touches a GPU, so it starts in milliseconds (torch already imported)
+            from .utilities import process_checkpoint_writer
+
+            process_checkpoint_writer()
         mark("pg_init_begin", rank=t.global_rank)
         self.init_ddp_connection(t.global_rank, t.world_size)
         mark("pg_init_end", rank=t.global_rank)

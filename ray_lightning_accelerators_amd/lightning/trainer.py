@@ -29,7 +29,8 @@ from torch.utils.data import DataLoader, DistributedSampler, RandomSampler, Sequ
 from .callbacks import Callback, EarlyStopping, ModelCheckpoint
 from .core import LightningDataModule, LightningModule, _normalize_optimizers
 from .loggers import CSVLogger, LightningLoggerBase
-from .utilities import CheckpointWriter, atomic_save, load_checkpoint, log, move_to_device, rank_zero_warn
+from .utilities import (CheckpointWriter, atomic_save, load_checkpoint, log, move_to_device,  # noqa: F401
+                        process_checkpoint_writer, rank_zero_warn)
 from ..config import get_config
 from ..utils.faults import maybe_inject as maybe_inject_fault
 from ..utils.profiling import resolve_profiler
@@ -327,10 +328,14 @@ class Trainer:
         if not self.is_global_zero:
             return
         if not blocking and get_config().async_checkpoint:
-            if getattr(self, "_ckpt_writer", None) is None:
-                self._ckpt_writer = CheckpointWriter()
-            self._ckpt_writer.save(ckpt, filepath)
-            return
+            # the writer PROCESS (pickling + file I/O off this process and its GIL);
+            # until it has started, saves stay synchronous (short fits never wait
+            # for its start-up)
+            w = process_checkpoint_writer()
+            if w.ready() or getattr(self, "_ckpt_writer", None) is w:
+                self._ckpt_writer = w
+                w.save(ckpt, filepath)
+                return
         self.wait_checkpoints()
         atomic_save(ckpt, filepath)
 
@@ -610,14 +615,20 @@ class Trainer:
         dev_vals = [(i, k, v) for i, (snap, _) in enumerate(pending) for k, v in snap.items()
                     if isinstance(v, torch.Tensor) and v.is_cuda]
         if dev_vals:
-            flat = torch.cat([v.reshape(-1).to(torch.float64) for _, _, v in dev_vals]).cpu()
-            vals = flat.tolist()
-            off = 0
-            for i, k, v in dev_vals:
-                n = v.numel()
-                # scalars as Python floats (what the logger records), tensors re-shaped
-                pending[i][0][k] = vals[off] if n == 1 else flat[off: off + n].reshape(v.shape).to(v.dtype)
-                off += n
+            # ONE concatenation kernel and ONE device->host copy per dtype (a per-value
+            # cast launched ~70 kernels per epoch: ~1 ms of host time while the GPU idled)
+            groups: Dict[torch.dtype, list] = {}
+            for e in dev_vals:
+                groups.setdefault(e[2].dtype, []).append(e)
+            for dtype, ents in groups.items():
+                flat = torch.cat([v.reshape(-1) for _, _, v in ents]).cpu()
+                vals = flat.double().tolist()
+                off = 0
+                for i, k, v in ents:
+                    n = v.numel()
+                    # scalars as Python floats (what the logger records), tensors re-shaped
+                    pending[i][0][k] = vals[off] if n == 1 else flat[off: off + n].reshape(v.shape)
+                    off += n
         for snap, step in pending:
             self.logger.log_metrics(snap, step=step)
         self._pending_log = None
@@ -907,6 +918,10 @@ class Trainer:
                 ev.record()
                 timing.append((k, time.perf_counter() - h0, ev, getattr(self._fused, "_last_run_us", 0.0)))
             is_last = e >= n or (self.max_steps is not None and self.global_step >= self.max_steps)
+            if is_last and hasattr(self._fused, "prefetch_next_epoch") and self.train_dataloader is not None \
+                    and self.current_epoch + 1 < self.max_epochs:
+                # host work of the next epoch's start, done while the GPU runs this one's tail
+                self._fused.prefetch_next_epoch(self.train_dataloader, self.current_epoch + 1)
             if self._should_validate(e - 1, is_last):
                 if timing is not None:
                     self._report_chunk_timing(timing)
@@ -1051,6 +1066,11 @@ class Trainer:
     def _optimizer_state_dict(self, opt) -> dict:
         if self._fused is not None and hasattr(self._fused, "optimizer_state_dict"):
             return self._fused.optimizer_state_dict()
+        if self._fused is not None and hasattr(self._fused, "sync_optimizer_state"):
+            # fused data-parallel step with the owner protocol: every element's Adam
+            # state lives on its owner rank until consolidated (collective; every
+            # rank dumps the checkpoint)
+            self._fused.sync_optimizer_state()
         return _to_cpu(opt.state_dict())
 
     def __getstate__(self):

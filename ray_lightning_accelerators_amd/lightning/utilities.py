@@ -6,6 +6,7 @@ from __future__ import annotations
 import logging
 import os
 import random
+import sys
 import tempfile
 from functools import wraps
 from typing import Any, Optional
@@ -122,6 +123,209 @@ class CheckpointWriter:
         self.wait()
         self._q.put(None)
         self._t.join(timeout=10)
+
+
+def _flatten_tensors(obj: Any, out: list) -> Any:
+    """Replace every tensor of a (nested) checkpoint dict by a placeholder; collect them."""
+    if isinstance(obj, torch.Tensor):
+        out.append(obj)
+        return _TensorSlot(len(out) - 1)
+    if isinstance(obj, dict):
+        return type(obj)((k, _flatten_tensors(v, out)) for k, v in obj.items())
+    if type(obj) in (list, tuple):
+        return type(obj)(_flatten_tensors(v, out) for v in obj)
+    return obj
+
+
+class _TensorSlot:
+    __slots__ = ("i",)
+
+    def __init__(self, i: int):
+        self.i = i
+
+
+def _rebuild_tensors(obj: Any, tensors: list) -> Any:
+    if isinstance(obj, _TensorSlot):
+        return tensors[obj.i]
+    if isinstance(obj, dict):
+        return type(obj)((k, _rebuild_tensors(v, tensors)) for k, v in obj.items())
+    if type(obj) in (list, tuple):
+        return type(obj)(_rebuild_tensors(v, tensors) for v in obj)
+    return obj
+
+
+def _writer_main(conn) -> None:  # pragma: no cover - runs in the writer process
+    """Checkpoint writer process: rebuild each checkpoint from the shared-memory
+    block it names, ``atomic_save`` it, run file removals, in submission order."""
+    import pickle
+    from multiprocessing import shared_memory
+
+    conn.send(("ready", None))
+    while True:
+        try:
+            msg = conn.recv()
+        except EOFError:
+            return
+        op = msg[0]
+        err = None
+        try:
+            if op == "save":
+                _, skel, metas, shm_name, filepath = msg
+                shm = shared_memory.SharedMemory(name=shm_name)
+                try:  # attaching registered it with the tracker (py3.10); the trainer owns it
+                    from multiprocessing import resource_tracker
+
+                    resource_tracker.unregister(shm._name, "shared_memory")
+                except Exception:  # noqa: BLE001
+                    pass
+                try:
+                    buf = torch.frombuffer(shm.buf, dtype=torch.uint8)
+                    tensors = [buf[off: off + nb].view(dt).reshape(shape).clone() for dt, shape, off, nb in metas]
+                    del buf
+                finally:
+                    shm.close()
+                atomic_save(_rebuild_tensors(pickle.loads(skel), tensors), filepath)
+            elif op == "remove":
+                if os.path.exists(msg[1]):
+                    try:
+                        os.remove(msg[1])
+                    except OSError:
+                        pass
+            elif op == "exit":
+                conn.send(("done", None))
+                return
+        except BaseException as e:  # noqa: BLE001 - reported to the trainer
+            err = repr(e)
+        conn.send(("done", err))
+
+
+class ProcessCheckpointWriter:
+    """Checkpoint files written by a separate process, in submission order.
+
+    The training process only copies the checkpoint's (host) tensors into one
+    shared-memory block and sends a small pickled skeleton; pickling the tensors,
+    the file write and the atomic rename happen in the writer process -- on
+    another core, off the GIL -- while the training process dispatches the next
+    epoch.  (A writer THREAD competed with the dispatching thread for the GIL and
+    made the MNIST epoch 0.7 ms longer, profiles/r2_c38.)  The writer starts with
+    the first save (``spawn``: a fresh interpreter, never a fork of a process that
+    holds a GPU context); files are identical to ``atomic_save``'s."""
+
+    def __init__(self):
+        import multiprocessing as mp
+
+        # fork (instant: torch is already imported) only while this process holds no
+        # GPU context; otherwise spawn a fresh interpreter (~1-2 s until ready())
+        torch_mod = sys.modules.get("torch")
+        gpu_ctx = torch_mod is not None and torch_mod.cuda.is_initialized()
+        ctx = mp.get_context("spawn" if gpu_ctx else "fork")
+        self._conn, child = ctx.Pipe()
+        self._proc = ctx.Process(target=_writer_main, args=(child,), daemon=True, name="rla-ckpt-writer")
+        self._proc.start()
+        child.close()
+        self._pending = []  # shared-memory blocks (or None) of unacknowledged requests
+        self._err: Optional[str] = None
+        self._ready = False
+
+    def ready(self) -> bool:
+        """The writer finished starting (interpreter + torch import, ~1-2 s)."""
+        if not self._ready and self._proc.is_alive() and self._conn.poll():
+            try:
+                self._ready = self._conn.recv()[0] == "ready"
+            except EOFError:
+                pass
+        return self._ready
+
+    def alive(self) -> bool:
+        return self._proc.is_alive()
+
+    def _reap(self, block: bool) -> None:
+        if self._pending and not self._ready:
+            if not block:
+                return
+            self._ready = self._conn.recv()[0] == "ready"
+        while self._pending and (block or self._conn.poll()):
+            try:
+                _, err = self._conn.recv()
+            except EOFError:
+                err = "checkpoint writer process died"
+                self._pending = [None]
+            shm = self._pending.pop(0)
+            if shm is not None:
+                shm.close()
+                shm.unlink()
+            if err and self._err is None:
+                self._err = err
+
+    def save(self, checkpoint: Any, filepath: str) -> None:
+        import pickle
+        from multiprocessing import shared_memory
+
+        self._reap(block=False)
+        self._raise()
+        tensors: list = []
+        skel = pickle.dumps(_flatten_tensors(checkpoint, tensors), protocol=pickle.HIGHEST_PROTOCOL)
+        metas, off = [], 0
+        flat = [t.detach().cpu().contiguous() for t in tensors]
+        for t in flat:
+            nb = t.numel() * t.element_size()
+            metas.append((t.dtype, tuple(t.shape), off, nb))
+            off += (nb + 63) // 64 * 64
+        shm = shared_memory.SharedMemory(create=True, size=max(off, 64))
+        try:
+            buf = torch.frombuffer(shm.buf, dtype=torch.uint8)
+            for t, (_, _, o, nb) in zip(flat, metas):
+                if nb:
+                    buf[o: o + nb].copy_(t.reshape(-1).view(torch.uint8))
+            del buf
+        except BaseException:
+            shm.close()
+            shm.unlink()
+            raise
+        self._pending.append(shm)
+        self._conn.send(("save", skel, metas, shm.name, filepath))
+
+    def submit(self, fn, *args) -> None:
+        """File operations after the pending writes (only removals are shipped)."""
+        if getattr(fn, "__name__", "") == "_remove_file" and len(args) == 1:
+            self._pending.append(None)
+            self._conn.send(("remove", args[0]))
+        else:
+            self.wait()
+            fn(*args)
+
+    def wait(self) -> None:
+        self._reap(block=True)
+        self._raise()
+
+    def _raise(self) -> None:
+        if self._err is not None:
+            e, self._err = self._err, None
+            raise RuntimeError(f"background checkpoint write failed: {e}")
+
+    def close(self) -> None:
+        try:
+            self.wait()
+        finally:
+            try:
+                self._pending.append(None)
+                self._conn.send(("exit",))
+                self._reap(block=True)
+            except (OSError, EOFError):
+                pass
+            self._proc.join(timeout=10)
+
+
+_process_writer: Optional[ProcessCheckpointWriter] = None
+
+
+def process_checkpoint_writer() -> ProcessCheckpointWriter:
+    """The process-wide checkpoint writer (started on first use; a recycled training
+    worker keeps it across fits, so short Tune trials do not each pay its start-up)."""
+    global _process_writer
+    if _process_writer is None or not _process_writer.alive():
+        _process_writer = ProcessCheckpointWriter()
+    return _process_writer
 
 
 def load_checkpoint(path: str, map_location: Any = "cpu") -> dict:

@@ -263,19 +263,49 @@ class FusedMNISTStep:
             self._u8_host = images
             self._u8 = images.to(self.dev).contiguous()
             self._labels = targets.to(self.dev, torch.int64).contiguous()
-        order = _sampler_order(dl.sampler)
-        if idx_map is not None:
-            order = idx_map[order]
+        pre = getattr(self, "_prefetched", None)
+        self._prefetched = None
+        ep = getattr(dl.sampler, "epoch", None)
+        if pre is not None and pre[0] is dl.sampler and pre[1] == ep:
+            order = pre[2]  # computed (and bounds-checked) while the previous epoch ran
+        else:
+            order = self._epoch_order(dl.sampler, idx_map)
         B = dl.batch_size
         nb = min(n_batches, order.numel() // B if dl.drop_last else -(-order.numel() // B))
         nb = min(nb, order.numel() // B)
         if nb <= 0:
             return None
-        assert int(order.max()) < self._u8.size(0)
         self._B = B
         self._nb = nb
-        self._engine(B).begin_epoch(order[: nb * B], nb)
+        self._engine(B).begin_epoch(order[: nb * B], nb, checked=True)
         return [("__rla_resident__", i) for i in range(nb)]
+
+    def _epoch_order(self, sampler, idx_map):
+        order = _sampler_order(sampler)
+        if idx_map is not None:
+            order = idx_map[order]
+        assert int(order.max()) < self._u8.size(0) and int(order.min()) >= 0  # the kernels trust indices
+        return order
+
+    def prefetch_next_epoch(self, dl, epoch: int) -> None:
+        """Compute epoch ``epoch``'s sample order now -- the Trainer calls this right
+        after dispatching an epoch's last steps, while the host would otherwise just
+        wait for the GPU -- so the next epoch's first launch is not delayed by it
+        (~1 ms of host work for 55K indices).  Only for samplers whose order is a
+        function of the epoch number (DistributedSampler, SequentialSampler)."""
+        import copy
+
+        sampler = dl.sampler
+        if not (isinstance(sampler, DistributedSampler) or isinstance(sampler, SequentialSampler)):
+            return
+        src = self._source(dl.dataset)
+        if src is None or self._u8 is None:
+            return
+        s2 = copy.copy(sampler)
+        if isinstance(s2, DistributedSampler):
+            s2.epoch = epoch
+        self._prefetched = (sampler, epoch if isinstance(sampler, DistributedSampler) else
+                            getattr(sampler, "epoch", None), self._epoch_order(s2, src[2]))
 
     def _sync_lr(self) -> None:
         lr = float(self.opt.param_groups[0]["lr"])
@@ -466,6 +496,11 @@ class FusedMNISTStep:
         """Raise if the engine's in-launch hand-off ever timed out (epoch end)."""
         if self.eng is not None:
             self.eng.check()
+
+    def sync_optimizer_state(self) -> None:
+        """Owner protocol: consolidate the Adam state before it is read (collective)."""
+        if self.eng is not None:
+            self.eng.sync_optimizer_state()
 
     # --------------------------------------------------------------- state
     def sync_params_to_module(self) -> None:

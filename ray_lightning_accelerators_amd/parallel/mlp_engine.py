@@ -246,15 +246,17 @@ class FusedMLPEngine:
         self.n_data = self.x_u8.size(0)
         self._host_epochs = True
 
-    def begin_epoch(self, order: torch.Tensor, n_batches: int) -> None:
+    def begin_epoch(self, order: torch.Tensor, n_batches: int, checked: bool = False) -> None:
         """Load one epoch's sample order ([n_batches * B] indices) and re-prime.
 
         Both order buffers get the same list, so the last step's look-ahead
         gather wraps into valid indices; the next ``begin_epoch`` re-primes."""
         order = order.reshape(-1)[: n_batches * self.B]
         assert n_batches >= 1 and order.numel() == n_batches * self.B
-        # the kernels trust indices (a host order is checked without a device sync)
-        assert int(order.max()) < self.n_data and int(order.min()) >= 0
+        # the kernels trust indices (a host order is checked without a device sync;
+        # ``checked``: the caller already did)
+        if not checked or order.device.type != "cpu":
+            assert int(order.max()) < self.n_data and int(order.min()) >= 0
         if self.order is None or self.order.size(1) != order.numel() or self.n_batches != int(n_batches):
             # the captured graph bakes the order pointer and n_batches: only a new
             # shape forces a re-capture, a new epoch of the same shape reuses it

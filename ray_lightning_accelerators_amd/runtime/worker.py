@@ -170,6 +170,12 @@ def _warm_gpu() -> bool:
     try:
         import torch
 
+        try:  # the checkpoint writer, forked before anything touches the GPU (utilities.py)
+            from ray_lightning_accelerators_amd.lightning.utilities import process_checkpoint_writer
+
+            process_checkpoint_writer()
+        except Exception:  # noqa: BLE001 - optional
+            traceback.print_exc()
         if not torch.cuda.is_available():
             return False
         torch.cuda.init()

@@ -3,9 +3,13 @@
 # its own limit; the first failing step ends the call).
 #   bash scripts/gpu_stage.sh OUT STAGE [STAGE ...]
 # stages: suite (full GPU pytest + smoke + default bench), dp (exchange protocols:
-# loopback / 2-rank tests + per-N cost probe), tune (sweep trials/hour cold + warm),
-# trainer (Trainer.fit bench + epoch-boundary timeline), recycle (worker reuse tests),
-# prof (rocprofv3 kernel stats of the default bench), bench20 (driver-shaped bench)
+# loopback / 2-rank tests + per-N cost probe + phase stamps), dpphase, tune (sweep
+# trials/hour cold + warm), trainer (Trainer.fit bench + epoch-boundary timeline),
+# recycle (worker reuse tests), prof (rocprofv3 kernel stats of the default bench),
+# pmc (counter passes of the default step, one pass per run), bench20 (driver-shaped
+# bench), share2 (N = 2 rehearsals with both ranks on the one GPU), corners (Tune
+# search-space corners), selftest (native comm self-test, plain + host ASan/UBSan),
+# rn50 (ResNet-50 bench + MIOpen solver variants), rn50prof (its kernel stats)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; export TMPDIR=/tmp
@@ -56,6 +60,31 @@ for st in "$@"; do
       run rn50_prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/rn50prof" -o run -- \
         python3 "$R/bench.py" --model resnet50 --steps 20 --warmup 10
       find "$O/rn50prof" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats_rn50.csv" \; ;;
+    pmc)
+      B="python bench.py --steps 300 --warmup 30 --graph-steps 0"
+      for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS" \
+                  "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_WAIT_INST_LDS" "FETCH_SIZE" "WRITE_SIZE"; do
+        n=$(echo $pass | cut -d' ' -f1)
+        timeout -s KILL 60 rocprofv3 --pmc $pass --output-format csv -d "$O/pmc_$n" -o run -- $B > "$O/pmc_$n.log" 2>&1 \
+          || { echo "pmc pass $n failed"; tail -20 "$O/pmc_$n.log"; exit 1; }
+      done
+      find "$O" -name "*counter_collection.csv" ;;
+    share2)
+      RLA_BENCH_SHARE_GPU=1 run share2_ray 300 python bench.py --gpus 2 --steps 500 --warmup 50
+      RLA_BENCH_SHARE_GPU=1 run share2_hvd 300 python bench.py --gpus 2 --steps 500 --warmup 50 --accelerator horovod
+      RLA_BENCH_SHARE_GPU=1 run share2_torchrun 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29541 bench.py --gpus 2 --steps 500 --warmup 50 ;;
+    corners)
+      for c in "128 256 128" "128 256 32" "64 128 64" "32 256 32"; do
+        set -- $c
+        run corner_$1_$2_b$3 300 python bench.py --layer-1 $1 --layer-2 $2 --batch-size $3
+      done ;;
+    selftest)
+      run selftest_w2 120 ./build/comm_selftest 2
+      run selftest_w4 180 ./build/comm_selftest 4
+      ASAN_OPTIONS=detect_leaks=1:abort_on_error=0:halt_on_error=1:protect_shadow_gap=0 \
+      LSAN_OPTIONS=suppressions=$R/scripts/sanitizers/lsan.supp:print_suppressions=0 \
+      UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 run selftest_asan_w2 300 ./build/comm_selftest_asan 2 ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac
 done

@@ -95,3 +95,37 @@ def test_batched_state_dict_pickles_at_raw_size():
     size = len(cloudpickle.dumps(out))
     assert size < 1.5 * raw, (size, raw)
     assert all(torch.equal(out[k], sd[k].cpu()) for k in sd)
+
+
+def test_process_checkpoint_writer_matches_atomic_save(tmp_path):
+    """The writer PROCESS (shared-memory hand-off, pickling + I/O off the training
+    process) writes files identical in content to atomic_save, in submission order,
+    with removals ordered after the writes they follow."""
+    import os
+
+    from ray_lightning_accelerators_amd.lightning.utilities import ProcessCheckpointWriter, atomic_save
+
+    w = ProcessCheckpointWriter()
+    ck = {"epoch": 3, "state_dict": {"w": torch.randn(10, 5), "b": torch.arange(5), "e": torch.zeros(0)},
+          "optimizer_states": [{"state": {0: {"step": torch.tensor(2.0), "m": torch.ones(3, dtype=torch.bfloat16)}},
+                                "param_groups": [{"lr": 0.1, "params": [0]}]}], "hp": (1, "a")}
+    for i in range(3):
+        w.save(ck, str(tmp_path / f"c{i}.ckpt"))
+
+    def _remove_file(p):
+        os.remove(p)
+
+    w.submit(_remove_file, str(tmp_path / "c0.ckpt"))
+    w.wait()
+    assert sorted(os.listdir(tmp_path)) == ["c1.ckpt", "c2.ckpt"]
+    atomic_save(ck, str(tmp_path / "ref.ckpt"))
+    a = torch.load(tmp_path / "c2.ckpt", weights_only=True)
+    b = torch.load(tmp_path / "ref.ckpt", weights_only=True)
+    assert a.keys() == b.keys() and a["hp"] == b["hp"] and a["epoch"] == 3
+    for k in ck["state_dict"]:
+        assert torch.equal(a["state_dict"][k], b["state_dict"][k])
+    assert a["optimizer_states"][0]["state"][0]["m"].dtype == torch.bfloat16
+    with pytest.raises(RuntimeError):
+        w.save(ck, "/proc/definitely/not/writable.ckpt")
+        w.wait()
+    w.close()
