@@ -104,6 +104,9 @@ def parse(argv=None):
                     help="resnet50: comma list of bucket caps (MiB) measured in one run, e.g. 1,2,4,8,16,25")
     ap.add_argument("--benchmark-algos", type=int, default=1,
                     help="resnet50: torch.backends.cudnn.benchmark (MIOpen find per shape), both impls")
+    ap.add_argument("--deterministic-conv", type=int, default=0,
+                    help="resnet50: torch.backends.cudnn.deterministic (MIOpen solvers without atomics: no "
+                         "zero-fill / cast passes around split-K weight-gradient kernels)")
     ap.add_argument("--grad-dtype", choices=["fp32", "bf16"], default="fp32",
                     help="resnet50 gradient wire dtype (bf16: converted inside the xGMI two-shot kernel)")
     ap.add_argument("--dp", choices=["fused", "split"], default="fused",
@@ -468,6 +471,7 @@ def make_resnet(args, world, rank, dev, x, y, bucket_mb=None):
         raise SystemExit("--model resnet50 needs a GPU")
     torch.manual_seed(0)
     torch.backends.cudnn.benchmark = bool(args.benchmark_algos)
+    torch.backends.cudnn.deterministic = bool(args.deterministic_conv)
     # native: BatchNorm+ReLU(+residual add) in the fused gfx950 kernels (ops/bn.py)
     model = resnet50(fused_bn=args.impl == "native").to(dev).to(memory_format=torch.channels_last)
     B = args.batch_size

@@ -36,7 +36,7 @@ from .. import runtime as ray
 from ..config import GPU_WORKER_REUSE_KEY, get_config
 from ..lightning.accelerators import DataParallelAccelerator
 from ..lightning.utilities import log
-from ..session import init_session, shutdown_session
+from ..session import finish_session, init_session, shutdown_session
 from ..utils.timeline import mark
 from ..util import Queue, process_results
 
@@ -160,13 +160,16 @@ class RayAccelerator(DataParallelAccelerator):
             self._failed = False
             return
 
+        recycled = self.use_gpu and get_config().reuse_workers
+
         def shutdown_remote():
             from ..parallel.comm import reset_native_comm
 
             reset_native_comm()  # RCCL comm destroy + IPC unmap before the group goes
             if dist.is_available() and dist.is_initialized():
                 dist.destroy_process_group()
-            if torch.cuda.is_available():
+            # a recycled worker keeps its cached blocks for the next tenant (same GPU)
+            if torch.cuda.is_available() and not recycled:
                 torch.cuda.empty_cache()
             shutdown_session()
 
@@ -249,7 +252,7 @@ class RayAccelerator(DataParallelAccelerator):
         try:
             self.ddp_train(process_idx=global_rank, model=model)
         finally:
-            shutdown_session()
+            finish_session()
         return self.results, self.best_model_path, self.model_state_dict
 
     def set_world_ranks(self, process_idx: int) -> None:

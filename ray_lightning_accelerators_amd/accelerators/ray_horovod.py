@@ -28,7 +28,7 @@ from .. import horovod as hvd
 from .. import runtime as ray
 from ..lightning.accelerators import Accelerator
 from ..lightning.utilities import rank_zero_only_state, seed_everything
-from ..session import init_session, shutdown_session
+from ..session import finish_session, init_session, shutdown_session
 from ..util import Queue, process_results
 from .ray_ddp import RayExecutor, _tune_session_enabled, find_free_port
 
@@ -232,7 +232,7 @@ class HorovodRayAccelerator(Accelerator):
             results = trainer._run(model)
             hvd.join()
         finally:
-            shutdown_session()
+            finish_session()
         if hvd.rank() != 0:
             return None
         cb = trainer.checkpoint_callback

@@ -372,8 +372,15 @@ const float* f32_vec(const optional<Tensor>& t, const char* name, int64_t C) {
   return ptr_or_null<const float>(t, name, at::kFloat, C);
 }
 
+// optional dy2 (backward only): a second incoming gradient summed with dy in-kernel
+const uint16_t* bn_dy2(const Tensor& x, const optional<Tensor>& dy2, int64_t C) {
+  if (!dy2.has_value() || !dy2->defined()) return nullptr;
+  bn_same(x, *dy2, "dy2", C);
+  return reinterpret_cast<const uint16_t*>(dy2->data_ptr());
+}
+
 Tensor bn_partial(Tensor x, optional<Tensor> y, optional<Tensor> dy, int64_t C, int64_t mode, bool relu,
-                  optional<Tensor> nbt) {
+                  optional<Tensor> nbt, optional<Tensor> dy2) {
   const int64_t M = bn_rows(x, "x", C);
   TORCH_CHECK(M > 0, "fused BN: empty input");
   TORCH_CHECK(mode == 0 || mode == 1, "fused BN: mode 0 (forward) or 1 (backward)");
@@ -394,7 +401,7 @@ Tensor bn_partial(Tensor x, optional<Tensor> y, optional<Tensor> dy, int64_t C, 
   Tensor part = at::empty({plan.blocks, 2, C}, x.options().dtype(at::kFloat));
   int64_t* nbtp = mode == 0 ? ptr_or_null<int64_t>(nbt, "num_batches_tracked", at::kLong, 1) : nullptr;
   rla::launch_bn_partial(reinterpret_cast<const uint16_t*>(x.data_ptr()), yp, dyp, M, (int)C, (int)mode, relu,
-                         plan, part.data_ptr<float>(), nbtp, cur_stream(x));
+                         plan, part.data_ptr<float>(), nbtp, cur_stream(x), mode == 1 ? bn_dy2(x, dy2, C) : nullptr);
   return part;
 }
 
@@ -486,7 +493,7 @@ void bn_apply(Tensor x, Tensor scale, Tensor shift, optional<Tensor> res, bool r
 }
 
 void bn_bwd_apply(Tensor x, optional<Tensor> y, Tensor dy, Tensor coef, bool relu, Tensor dx,
-                  optional<Tensor> dres) {
+                  optional<Tensor> dres, optional<Tensor> dy2) {
   check_dev(coef, "coef", at::kFloat);
   TORCH_CHECK(coef.dim() == 2 && coef.size(0) == 5, "coef must be [5, C]");
   const int64_t C = coef.size(1);
@@ -507,7 +514,7 @@ void bn_bwd_apply(Tensor x, optional<Tensor> y, Tensor dy, Tensor coef, bool rel
   const at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   rla::launch_bn_bwd_apply(reinterpret_cast<const uint16_t*>(x.data_ptr()), yp,
                            reinterpret_cast<const uint16_t*>(dy.data_ptr()), coef.data_ptr<float>(), M, (int)C,
-                           relu, reinterpret_cast<uint16_t*>(dx.data_ptr()), drp, cur_stream(x));
+                           relu, reinterpret_cast<uint16_t*>(dx.data_ptr()), drp, cur_stream(x), bn_dy2(x, dy2, C));
 }
 
 }  // namespace
@@ -537,12 +544,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp_supported", [](int64_t a, int64_t b) { return rla::mlp_supported((int)a, (int)b); });
   m.def("mlp_param_count", &mlp_param_count);
   m.def("bn_partial", &bn_partial, "fused BN: per-block partial sums (mode 0 fwd stats, 1 bwd dz/dz*x)",
-        py::arg("x"), py::arg("y"), py::arg("dy"), py::arg("C"), py::arg("mode"), py::arg("relu"), py::arg("nbt"));
+        py::arg("x"), py::arg("y"), py::arg("dy"), py::arg("C"), py::arg("mode"), py::arg("relu"), py::arg("nbt"),
+        py::arg("dy2") = py::none());
   m.def("bn_finalize", &bn_finalize, "fused BN: mean/invstd/scale/shift + running stats from partials");
   m.def("bn_bwd_finalize", &bn_bwd_finalize, "fused BN backward: dgamma/dbeta + dx coefficients");
   m.def("bn_apply", &bn_apply, "fused BN apply: y = act(x*scale + shift (+res))");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC bf16 max pool -> (y, one-byte window argmax)");
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max pool backward (gather through the argmax bytes)");
-  m.def("bn_bwd_apply", &bn_bwd_apply, "fused BN backward apply: dx (+ dres = relu-masked dy)");
+  m.def("bn_bwd_apply", &bn_bwd_apply, "fused BN backward apply: dx (+ dres = relu-masked dy)", py::arg("x"),
+        py::arg("y"), py::arg("dy"), py::arg("coef"), py::arg("relu"), py::arg("dx"), py::arg("dres"),
+        py::arg("dy2") = py::none());
   m.attr("ARCH") = "gfx950";
 }

@@ -60,12 +60,15 @@ __device__ __forceinline__ f8 relu_mask(f8 d, f8 y) {
 }
 
 // ---------------------------------------------------------------- partial sums
-template <int MODE, bool RELU>
+// DY2 (backward): the incoming gradient is dy + dy2 -- the residual-branch gradient
+// of the NEXT bottleneck (its bn3's dres), folded here instead of autograd adding
+// the two into a new tensor first (ops/bn.py, fold_residual_grad)
+template <int MODE, bool RELU, bool DY2 = false>
 __global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(const uint16_t* __restrict__ x,
                                                                 const uint16_t* __restrict__ y,
                                                                 const uint16_t* __restrict__ dy, int64_t M, int C,
                                                                 int64_t rows_per_blk, float* __restrict__ part,
-                                                                int64_t* nbt) {
+                                                                int64_t* nbt, const uint16_t* __restrict__ dy2 = nullptr) {
   __shared__ float sh[2][kBnThreads * 8];
   const int G = C >> 3, rpi = kBnThreads / G, tid = threadIdx.x;
   const int g = tid % G, r0 = tid / G;
@@ -86,6 +89,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(const uint16_t* 
         if (MODE == 1) {
           const int64_t off = (px - x) + u * step;
           dv[u] = ld8(dy + off);
+          if (DY2) dv[u] += ld8(dy2 + off);
           if (RELU) dv[u] = relu_mask(dv[u], ld8(y + off));
         }
       }
@@ -108,6 +112,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(const uint16_t* 
       } else {
         const int64_t off = px - x;
         f8 d = ld8(dy + off);
+        if (DY2) d += ld8(dy2 + off);
         if (RELU) d = relu_mask(d, ld8(y + off));
         s += d;
         q += d * xv;
@@ -257,13 +262,14 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_kernel(const uint16_t* __
   }
 }
 
-template <bool RELU, bool DRES>
+template <bool RELU, bool DRES, bool DY2 = false>
 __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_kernel(const uint16_t* __restrict__ x,
                                                                   const uint16_t* __restrict__ y,
                                                                   const uint16_t* __restrict__ dy,
                                                                   const float* __restrict__ coef, int64_t M, int C,
                                                                   uint16_t* __restrict__ dx,
-                                                                  uint16_t* __restrict__ dres) {
+                                                                  uint16_t* __restrict__ dres,
+                                                                  const uint16_t* __restrict__ dy2 = nullptr) {
   const int G = C >> 3, rpi = kBnThreads / G, tid = threadIdx.x;
   const int g = tid % G, r0 = tid / G;
   if (r0 >= rpi) return;
@@ -272,6 +278,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_kernel(const uint16_t
   for (int64_t r = (int64_t)blockIdx.x * rpi + r0; r < M; r += rstride) {
     const int64_t o = r * C + col;
     f8 d = ld8(dy + o);
+    if (DY2) d += ld8(dy2 + o);
     if (RELU) d = relu_mask(d, ld8(y + o));
     const f8 xv = ld8(x + o);
     st8(dx + o, A * d + B * xv + Cc);
@@ -305,8 +312,17 @@ BnPlan bn_plan(int64_t M, int C) {
 }
 
 void launch_bn_partial(const uint16_t* x, const uint16_t* y, const uint16_t* dy, int64_t M, int C, int mode,
-                       bool relu, const BnPlan& plan, float* part, int64_t* nbt, hipStream_t s) {
+                       bool relu, const BnPlan& plan, float* part, int64_t* nbt, hipStream_t s, const uint16_t* dy2) {
   const dim3 grid(plan.blocks), block(kBnThreads);
+  if (mode == 1 && dy2) {
+    if (relu)
+      hipLaunchKernelGGL((bn_partial_kernel<1, true, true>), grid, block, 0, s, x, y, dy, M, C, plan.rows_per_blk,
+                         part, nullptr, dy2);
+    else
+      hipLaunchKernelGGL((bn_partial_kernel<1, false, true>), grid, block, 0, s, x, y, dy, M, C, plan.rows_per_blk,
+                         part, nullptr, dy2);
+    return;
+  }
   if (mode == 0)
     hipLaunchKernelGGL((bn_partial_kernel<0, false>), grid, block, 0, s, x, y, dy, M, C, plan.rows_per_blk, part,
                        nbt);
@@ -345,8 +361,23 @@ void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* scale,
 }
 
 void launch_bn_bwd_apply(const uint16_t* x, const uint16_t* y, const uint16_t* dy, const float* coef, int64_t M,
-                         int C, bool relu, uint16_t* dx, uint16_t* dres, hipStream_t s) {
+                         int C, bool relu, uint16_t* dx, uint16_t* dres, hipStream_t s, const uint16_t* dy2) {
   const dim3 grid(apply_grid(M, C)), block(kBnThreads);
+  if (dy2) {  // the folded residual gradient; ResNet's bn3 (relu, its own dres) is the user
+    if (relu && dres)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<true, true, true>), grid, block, 0, s, x, y, dy, coef, M, C, dx, dres,
+                         dy2);
+    else if (relu)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false, true>), grid, block, 0, s, x, y, dy, coef, M, C, dx,
+                         dres, dy2);
+    else if (dres)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true, true>), grid, block, 0, s, x, y, dy, coef, M, C, dx,
+                         dres, dy2);
+    else
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<false, false, true>), grid, block, 0, s, x, y, dy, coef, M, C, dx,
+                         dres, dy2);
+    return;
+  }
   if (relu && dres)
     hipLaunchKernelGGL((bn_bwd_apply_kernel<true, true>), grid, block, 0, s, x, y, dy, coef, M, C, dx, dres);
   else if (relu)

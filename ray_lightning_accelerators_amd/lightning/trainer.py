@@ -755,7 +755,8 @@ class Trainer:
         # out of the cyclic GC's generations, so a full collection during the
         # epochs scans only the loop's own garbage instead of pausing the
         # dispatching host for ~100 ms (measured on the fused MNIST epochs).
-        gc.collect()
+        # No collection first: it cost 80-240 ms per Tune trial (profiles/r3_tune);
+        # garbage frozen here is collected after the fit (gc.unfreeze below).
         gc.freeze()
         try:
             while self.current_epoch < self.max_epochs:

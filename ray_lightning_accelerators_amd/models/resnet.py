@@ -61,7 +61,9 @@ class Bottleneck(nn.Module):
         idt = x if self.downsample is None else self.downsample(x)
         if self.fused_bn:
             out = self.bn2(self.conv2(self.bn1(self.conv1(x))))
-            return self.bn3(self.conv3(out), idt)
+            # identity shortcut: x is an ancestor of conv3's output, so bn3 may fold
+            # its residual gradient into the previous block's bn3 backward (ops/bn.py)
+            return self.bn3(self.conv3(out), idt, residual_is_ancestor=self.downsample is None)
         out = F.relu(self.bn1(self.conv1(x)), inplace=True)
         out = F.relu(self.bn2(self.conv2(out)), inplace=True)
         out = self.bn3(self.conv3(out))

@@ -12,6 +12,16 @@ activations (ResNet-50 under bf16 autocast) it runs the gfx950 kernels of
 
 which replaces MIOpen's six batch-norm kernels per layer plus the separate
 ReLU, residual-add and ReLU-backward passes (profiles/r1_resnet50_v2).
+
+Residual-gradient fold: when the residual of one fused layer is the OUTPUT of
+another fused layer (ResNet's identity shortcut: block k adds block k-1's
+output), autograd would sum the two gradients of that tensor (the next conv's
+dgrad and this layer's dres) in a separate add kernel (read 2, write 1 over the
+activation).  Instead the residual enters the autograd graph detached, this
+layer's backward parks dres in the producer's ``_FoldSlot``, and the producer's
+backward kernels read it as a second incoming gradient (``dy2``).  The chain
+conv1 -> bn1 -> ... -> bn3 of the consumer guarantees its backward runs first.
+
 ``Trainer(sync_batchnorm=True)`` goes through :func:`convert_sync_batchnorm`,
 which keeps the fusion and all-reduces the per-channel sums (SyncBatchNorm
 semantics: global statistics, local weight/bias gradients).
@@ -52,9 +62,25 @@ def fused_ok(x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> bool:
     return use_native(x)
 
 
+class _FoldSlot:
+    """Hand-off of a consumer layer's residual gradient to the producer of that residual."""
+
+    __slots__ = ("dres", "claimed")
+
+    def __init__(self):
+        self.dres = None
+        self.claimed = False
+
+
+fold_stats = {"folded": 0}
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu, group):
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu, group,
+                slot=None, sink=None):
+        # slot: this layer's own _FoldSlot (a consumer may park dres for our backward);
+        # sink: the producer slot of `residual` (residual is then passed detached)
         mod = require()
         C = x.size(1)
         xv = _nhwc(x)
@@ -70,6 +96,7 @@ class _BNActFn(torch.autograd.Function):
         y = torch.empty_like(x, memory_format=torch.channels_last)
         mod.bn_apply(xv, st[2], st[3], _nhwc(residual) if residual is not None else None, relu, _nhwc(y))
         ctx.relu, ctx.has_res, ctx.group, ctx.count = relu, residual is not None, group, count
+        ctx.slot, ctx.sink = slot, sink
         ctx.save_for_backward(x, y if relu else None, weight, st[0], st[1])
         return y
 
@@ -81,7 +108,11 @@ class _BNActFn(torch.autograd.Function):
         C = x.size(1)
         xv, dyv = _nhwc(x), _nhwc(dy)
         yv = _nhwc(y) if ctx.relu else None
-        part = mod.bn_partial(xv, yv, dyv, C, 1, ctx.relu, None)
+        dy2 = None
+        if ctx.slot is not None and ctx.slot.dres is not None:
+            dy2, ctx.slot.dres = _nhwc(ctx.slot.dres), None
+            fold_stats["folded"] += 1
+        part = mod.bn_partial(xv, yv, dyv, C, 1, ctx.relu, None, dy2)
         local = None
         if ctx.group is not None:
             local = mod.bn_bwd_finalize(part, ctx.count, weight, mean, invstd)  # local dgamma / dbeta
@@ -90,12 +121,14 @@ class _BNActFn(torch.autograd.Function):
         coef = mod.bn_bwd_finalize(part, ctx.count, weight, mean, invstd)
         dx = torch.empty_like(x, memory_format=torch.channels_last)
         dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
-        mod.bn_bwd_apply(xv, yv, dyv, coef, ctx.relu, _nhwc(dx), _nhwc(dres) if dres is not None else None)
+        mod.bn_bwd_apply(xv, yv, dyv, coef, ctx.relu, _nhwc(dx), _nhwc(dres) if dres is not None else None, dy2)
+        if ctx.sink is not None:
+            ctx.sink.dres, dres = dres, None  # the producer's backward consumes it
         wsrc = local if local is not None else coef
         # views of the coefficient tensor (no copy kernels): autograd hands them to .grad
         dgamma = wsrc[0] if weight is not None and ctx.needs_input_grad[1] else None
         dbeta = wsrc[1] if ctx.needs_input_grad[2] else None
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None
 
 
 class BatchNormAct2d(nn.BatchNorm2d):
@@ -111,6 +144,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
         self.sync = False
         self.process_group = None
         self._warned = False
+        self.fold_residual_grad = True  # see the module docstring
 
     def extra_repr(self) -> str:
         return super().extra_repr() + f", act={self.act}, sync={self.sync}"
@@ -121,7 +155,11 @@ class BatchNormAct2d(nn.BatchNorm2d):
             return self.process_group if self.process_group is not None else dist.group.WORLD
         return None
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                residual_is_ancestor: bool = False) -> torch.Tensor:
+        """``residual_is_ancestor``: the caller guarantees ``x`` is computed from
+        ``residual`` (ResNet identity shortcut), so this layer's backward runs before
+        the residual producer's and the residual gradient can be folded into it."""
         relu = self.act == "relu"
         use_batch_stats = self.training or not self.track_running_stats
         if fused_ok(x, residual):
@@ -129,10 +167,21 @@ class BatchNormAct2d(nn.BatchNorm2d):
                 stats["fused"] += 1
                 track = self.training and self.track_running_stats
                 momentum = -1.0 if self.momentum is None else float(self.momentum)
-                return _BNActFn.apply(
+                slot = sink = None
+                if self.fold_residual_grad and torch.is_grad_enabled():
+                    slot = _FoldSlot()
+                    src = getattr(residual, "_rla_fold", None) if residual is not None else None
+                    if residual_is_ancestor and src is not None and not src.claimed and residual.requires_grad:
+                        src.claimed, sink = True, src
+                        residual = residual.detach()
+                y = _BNActFn.apply(
                     x, self.weight, self.bias, residual,
                     self.running_mean if track else None, self.running_var if track else None,
-                    self.num_batches_tracked if track else None, momentum, float(self.eps), relu, self._group())
+                    self.num_batches_tracked if track else None, momentum, float(self.eps), relu, self._group(),
+                    slot, sink)
+                if slot is not None:
+                    y._rla_fold = slot
+                return y
             if not torch.is_grad_enabled() or not (x.requires_grad or (self.weight is not None
                                                                           and self.weight.requires_grad)):
                 stats["fused"] += 1

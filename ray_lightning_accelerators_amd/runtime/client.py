@@ -173,6 +173,13 @@ class _ActorConn:
 
 # ------------------------------------------------------------- object refs
 _MISSING = object()
+_MARK_BYTES = 1 << 16  # timeline marks for payloads at least this large
+
+
+def _mark(event: str, **fields) -> None:
+    from ..utils.timeline import mark
+
+    mark(event, **fields)
 
 
 class ObjectRef:
@@ -280,6 +287,8 @@ class ActorHandle:
     def _submit(self, msg: dict, args, kwargs) -> ObjectRef:
         args, kwargs = _deref_args(args, kwargs)
         payload = P.dumps((args, kwargs))
+        if len(payload) > _MARK_BYTES:
+            _mark("submit_pickled", bytes=len(payload), method=msg.get("method"))
         out: Future = Future()
 
         def go(f_addr: Future):

@@ -102,6 +102,7 @@ class Head:
         self.pool_starting: Dict[int, subprocess.Popen] = {}
         self.pool_ready: List = []
         self.pool_lock = threading.Lock()
+        self.pool_cond = threading.Condition(self.pool_lock)  # notified when a worker parks
         # recycled workers (actors created with a reuse key): a kill parks the process
         # instead of ending it -- HIP context, loaded kernel objects and imports stay
         # -- and the next actor with the same key, node and GPU tokens takes it over.
@@ -109,6 +110,7 @@ class Head:
         # parked: [(Popen, conn, key, node, gpu_ids)] waiting for an assignment
         self.parking: Dict[int, tuple] = {}
         self.parked: List[tuple] = []
+        self.prewarming: set = set()  # pids of pre-warming workers (in `parking` until warm)
         self.prewarmed: set = set()  # (key, node ip, gpu token) already started
 
     # ------------------------------------------------------------ worker pool
@@ -282,12 +284,25 @@ class Head:
 
     # -------------------------------------------------------- recycling
     def _take_parked(self, key: str, node: Node, gpu_ids: List[str]):
-        with self.pool_lock:
-            for i, (proc, conn, k, nd, ids) in enumerate(self.parked):
-                if k == key and nd is node and sorted(ids) == sorted(gpu_ids) and proc.poll() is None:
-                    del self.parked[i]
-                    return proc, conn
-        return None
+        """A parked worker of this key / node / GPU set.  When none is parked yet but
+        one is on its way (acknowledged a park moments ago: a sequential sweep's next
+        trial asks right after the previous one released it), wait for it briefly
+        instead of starting another process (``RLA_PARK_WAIT`` seconds, default 1)."""
+        want = sorted(gpu_ids)
+        deadline = time.time() + float(os.environ.get("RLA_PARK_WAIT", "1.0"))
+        with self.pool_cond:
+            while True:
+                for i, (proc, conn, k, nd, ids) in enumerate(self.parked):
+                    if k == key and nd is node and sorted(ids) == want and proc.poll() is None:
+                        del self.parked[i]
+                        return proc, conn
+                coming = any(k == key and nd is node and sorted(ids) == want and p.poll() is None
+                             and pid not in self.prewarming
+                             for pid, (p, k, nd, ids) in self.parking.items())
+                left = deadline - time.time()
+                if not coming or left <= 0 or self.stopping:
+                    return None
+                self.pool_cond.wait(min(left, 0.05))
 
     def _park(self, rec: ActorRecord) -> bool:
         """Ask a recyclable actor's worker to reset and wait for a new assignment
@@ -335,6 +350,7 @@ class Head:
                 log.close()
                 with self.pool_lock:
                     self.parking[proc.pid] = (proc, key, node, [tok])
+                    self.prewarming.add(proc.pid)  # seconds away: never waited for
                 started += 1
         return {"ok": True, "started": started}
 
@@ -390,6 +406,8 @@ class Head:
                                 self.parked.insert(0, rec)
                             else:
                                 self.parked.append(rec)
+                            self.prewarming.discard(proc.pid)
+                            self.pool_cond.notify_all()
                             return
                     conn.close()
                     return

@@ -87,11 +87,18 @@ class _QueueActor:
         return [first] + self.drain()
 
 
+QUEUE_REUSE_KEY = "rla-queue"
+
+
 class Queue:
     def __init__(self, maxsize: int = 0, actor_options: Optional[Dict] = None) -> None:
         actor_options = dict(actor_options or {})
         actor_options.setdefault("num_cpus", 0)
         actor_options.setdefault("max_concurrency", 8)
+        from ..config import get_config
+
+        if get_config().reuse_workers:
+            actor_options.setdefault("_reuse", QUEUE_REUSE_KEY)  # recycled, not restarted
         self.maxsize = maxsize
         self.actor = client.ActorClass(_QueueActor).options(**actor_options).remote(maxsize)
 

@@ -46,9 +46,6 @@ class WorkerServer:
             traceback.print_exc()
             ok = False
         self.instance = None
-        import gc
-
-        gc.collect()
         try:
             conn.send({"call_id": call_id, "ok": ok})
         except Exception:
@@ -67,12 +64,19 @@ class WorkerServer:
             P.connect(self.address, self.authkey).close()
         except Exception:
             pass
+        import gc
+
+        gc.collect()  # after the ack: the killer (a trial's teardown) does not wait for it
 
     def _run_call(self, conn: P.SafeConn, msg: dict) -> None:
         kind = msg["kind"]
         call_id = msg["call_id"]
         try:
             args, kwargs = P.loads(msg["payload"])
+            if len(msg["payload"]) > (1 << 16):
+                from ..utils.timeline import mark
+
+                mark("call_unpickled", bytes=len(msg["payload"]), method=msg.get("method"))
             if kind == "init":
                 cls = P.loads(msg["cls"])
                 conc = int(msg.get("max_concurrency", 1) or 1)
@@ -185,6 +189,16 @@ def _warm_gpu() -> bool:
 
         ops.require()
         native_comm_module()
+        # first-use costs a training worker would otherwise pay inside its first fit:
+        # the optimizer's device paths and a GEMM library (measured: ~1.6 s in the
+        # first Tune trial's configure_optimizers / first steps, profiles/r3_tune)
+        p = torch.nn.Parameter(torch.zeros(64, device="cuda"))
+        opt = torch.optim.Adam([p], lr=1e-3)
+        lin = torch.nn.Linear(64, 64).cuda()
+        (lin(p.view(1, 64)).sum()).backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        del opt, lin, p
         torch.cuda.synchronize()
         return True
     except Exception:  # noqa: BLE001 - no usable GPU here: just do not park
@@ -237,9 +251,14 @@ def main() -> None:
         _warm_imports()
         _wait_for_assignment("pool_ready")
     elif "--prewarm" in argv:
+        from ..utils.timeline import mark
+
+        mark("prewarm_start")
         _warm_imports()
+        mark("prewarm_imports_done")
         if not _warm_gpu():
             os._exit(0)
+        mark("prewarm_gpu_done")
         _wait_for_assignment("parked")
     from . import client
 

@@ -45,6 +45,22 @@ def shutdown_session() -> None:
     _session = None
 
 
+# a worker's last queue item: the driver's result pump (util.process_results) stops
+# polling the queue once every rank sent it and waits on the results directly
+WORKER_DONE = "__rla_worker_done__"
+
+
+def finish_session() -> None:
+    """End of a worker's run: tell the driver no queue item follows, then shut down."""
+    s = _session
+    if s is not None and s._queue is not None:
+        try:
+            s._queue.put((s._rank, WORKER_DONE))
+        except Exception:  # noqa: BLE001 - the pump falls back to polling
+            pass
+    shutdown_session()
+
+
 def get_session() -> RayLightningSession:
     if _session is None or not isinstance(_session, RayLightningSession):
         raise ValueError("Trying to access RayLightningSession from outside a training run.\n"

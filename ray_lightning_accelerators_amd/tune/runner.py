@@ -25,10 +25,30 @@ from . import session as tsession
 from .analysis import ExperimentAnalysis, Trial
 from .sample import generate_variants
 from .schedulers import FIFOScheduler, TrialScheduler
+from ..utils.timeline import mark
+
+
+TRIAL_REUSE_KEY = "rla-tune-trial"
 
 
 class _TrialActor:
-    """Runs one trial's trainable inside its own process."""
+    """Runs one trial's trainable inside its own process.  With
+    ``config.reuse_workers`` the process is recycled for the next trial (the
+    runtime parks it instead of ending it), so trials after the first skip the
+    interpreter + torch start-up."""
+
+    def __rla_park__(self) -> None:
+        # undo what run() changed in the process (the head's assignment resets the
+        # environment, working directory and log descriptors)
+        for name in ("stdout", "stderr"):
+            cur, orig = getattr(sys, name), getattr(sys, f"__{name}__")
+            if cur is not orig:
+                try:
+                    cur.close()
+                except Exception:  # noqa: BLE001
+                    pass
+                setattr(sys, name, orig)
+        tsession.shutdown_trial_session()
 
     def run(self, fn: Callable, config: Dict[str, Any], trial_id: str, trial_dir: str, report_queue,
             experiment_id: str, log_to_file: bool) -> Dict[str, Any]:
@@ -127,6 +147,9 @@ def run(
                 pass
     reports = Queue(actor_options={"num_cpus": 0})
     trial_cls = runtime.ActorClass(_TrialActor)
+    from ..config import get_config
+
+    trial_opts = {"_reuse": TRIAL_REUSE_KEY} if get_config().reuse_workers else {}
     pending = list(trials)
     running: Dict[str, Trial] = {}
     used_cpu = used_gpu = 0.0
@@ -151,7 +174,7 @@ def run(
                     break
                 t = pending.pop(0)
                 actor = trial_cls.options(num_cpus=res["cpu"], num_gpus=res["gpu"],
-                                          resources=res["custom"] or None).remote()
+                                          resources=res["custom"] or None, **trial_opts).remote()
                 t.actor = actor
                 t.future = actor.run.remote(fn, t.config, t.trial_id, t.logdir, reports, experiment_id, log_to_file)
                 t.status = "RUNNING"
@@ -186,7 +209,9 @@ def run(
                             print(f"Trial {tid} errored: {t.error[:2000]}", file=sys.stderr)
                 else:
                     t.status = "TERMINATED"
+                mark("trial_reaped", trial=tid)
                 runtime.kill(t.actor)
+                mark("trial_actor_released", trial=tid)
                 t.end_time = time.time()
                 del running[tid]
                 used_cpu -= need_cpu

@@ -20,10 +20,17 @@ class Unavailable:
         raise RuntimeError("This class should never be instantiated.")
 
 
-def _run_items(items) -> None:
+from .session import WORKER_DONE  # every worker's last queue item (session.finish_session)
+
+
+def _run_items(items) -> int:
+    done = 0
     for actor_rank, item in items:
         if isinstance(item, Callable):
             item()
+        elif isinstance(item, str) and item == WORKER_DONE:
+            done += 1
+    return done
 
 
 def _handle_queue(queue) -> None:
@@ -34,13 +41,14 @@ def _handle_queue(queue) -> None:
 def process_results(training_result_futures: List[runtime.ObjectRef], queue: Optional[Queue] = None,
                     poll_s: float = 0.2):
     not_ready = list(training_result_futures)
+    done = 0
     while not_ready:
-        if queue is not None:
-            _run_items(queue.get_blocking_batch(timeout=poll_s))
+        if queue is not None and done < len(training_result_futures):
+            done += _run_items(queue.get_blocking_batch(timeout=poll_s))
             ready, not_ready = runtime.wait(not_ready, num_returns=len(not_ready), timeout=0)
         else:
             ready, not_ready = runtime.wait(not_ready, num_returns=1, timeout=None)
         runtime.get(ready)  # re-raises the first worker failure right away
-    if queue is not None:
+    if queue is not None and done < len(training_result_futures):
         _handle_queue(queue)
     return runtime.get(training_result_futures)

@@ -9,7 +9,8 @@
 # pmc (counter passes of the default step, one pass per run), bench20 (driver-shaped
 # bench), share2 (N = 2 rehearsals with both ranks on the one GPU), corners (Tune
 # search-space corners), selftest (native comm self-test, plain + host ASan/UBSan),
-# rn50 (ResNet-50 bench + MIOpen solver variants), rn50prof (its kernel stats)
+# rn50 (ResNet-50 bench, native + stock torch; --deterministic-conv
+# is not run: MIOpen's atomic-free solvers compile for > 3 min without output), rn50prof (its kernel stats)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; export TMPDIR=/tmp
@@ -41,25 +42,32 @@ for st in "$@"; do
       run tune_cold 300 python scripts/bench_tune.py --trials 4
       run tune_cold16 300 python scripts/bench_tune.py --trials 16
       run tune_warm 300 python scripts/bench_tune.py --trials 8 --warm 8 ;;
+    tunetl)  # cold sweep with the cross-process start-up timeline
+      RLA_TIMELINE="$R/$O/tune_timeline.jsonl" run tune_tl 300 python scripts/bench_tune.py --trials 6
+      python scripts/timeline_report.py "$O/tune_timeline.jsonl" --merged > "$O/tune_timeline.txt" 2>&1 || true ;;
     trainer)
       RLA_TIMELINE="$R/$O/trainer_timeline.jsonl" run trainer 300 python bench.py --via trainer --trainer-epochs 6
       python scripts/timeline_report.py "$O/trainer_timeline.jsonl" > "$O/trainer_timeline.txt" 2>&1 || true ;;
     prof)
       run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/prof" -o run -- python3 "$R/bench.py"
-      find "$O/prof" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats_default.csv" \; ;;
+      find "$O/prof" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats_default.csv" \;
+      rm -rf "$O/prof" ;;  # raw traces exceed gpurun's 64 MiB copy-back
     bench20)
       run bench_k20 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     rn50)
       run pytest_bn 300 $PYT tests/test_bn.py
       RB="python bench.py --model resnet50 --steps 30 --warmup 10"
       run rn50_base 600 $RB
-      MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC=0 run rn50_no_wrw_gtc 600 $RB
-      MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_WRW_GTC_XDLOPS_NHWC=0 MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_FWD_GTC_XDLOPS_NHWC=0 \
-        MIOPEN_DEBUG_CONV_IMPLICIT_GEMM_ASM_BWD_GTC_XDLOPS_NHWC=0 run rn50_no_gtc 600 $RB ;;
+      run rn50_torch 600 $RB --impl torch ;;
     rn50prof)
       run rn50_prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/rn50prof" -o run -- \
         python3 "$R/bench.py" --model resnet50 --steps 20 --warmup 10
-      find "$O/rn50prof" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats_rn50.csv" \; ;;
+      find "$O/rn50prof" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats_rn50_all.csv" \;
+      # steady state: the last 20 steps (MIOpen's find runs during warm-up on a fresh box)
+      MS=$(python -c "import json,sys; print([json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]['ms_per_step'])" "$O/rn50_prof.log")
+      python scripts/kernel_window.py "$(find "$O/rn50prof" -name '*kernel_trace.csv' | head -1)" \
+        --window-ms "$(python -c "print($MS * 20)")" --steps 20 > "$O/kernel_stats_rn50.csv" 2> "$O/kernel_window.txt"
+      rm -rf "$O/rn50prof" ;;
     pmc)
       B="python bench.py --steps 300 --warmup 30 --graph-steps 0"
       for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS" \

@@ -24,3 +24,11 @@ for pid, rs in by_pid.items():
 print("largest in-process gaps:")
 for g in sorted(gaps, reverse=True)[:15]:
     print(f"  {g[0]:9.1f} ms  pid {g[1]}  {g[2]} -> {g[3]}")
+if "--merged" in sys.argv:
+    print("all processes, in time order:")
+    prev = t0
+    for r in rows:
+        extra = {k: v for k, v in r.items() if k not in ("t", "pid", "event")}
+        print(f"  {(r['t'] - t0):8.3f}s (+{(r['t'] - prev) * 1e3:7.1f} ms) pid {r['pid']:>7} {r['event']} "
+              f"{extra if extra else ''}")
+        prev = r["t"]

@@ -110,6 +110,49 @@ def test_fused_bn_matches_fp32_reference(shape, relu, with_res):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("relu_b", [True, False])
+def test_residual_grad_fold_matches_autograd_sum(relu_b):
+    """y1 = bn_a(x); y2 = bn_b(conv(y1), residual=y1): with the fold, bn_b's dres reaches
+    bn_a's backward kernels as dy2 instead of through autograd's add -- gradients must
+    match the unfolded run and the fp32 reference."""
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(3)
+    C = 64
+    x0 = (torch.randn(4, C, 12, 12, device=dev) * 1.5 + 0.2).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    conv = nn.Conv2d(C, C, 3, 1, 1, bias=False).to(dev).to(memory_format=torch.channels_last)
+    dy = torch.randn(4, C, 12, 12, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    grads = []
+    for fold in (True, False, None):  # None: fp32 reference composition
+        a = BatchNormAct2d(C).to(dev)
+        b = BatchNormAct2d(C, act="relu" if relu_b else None).to(dev)
+        a.fold_residual_grad = b.fold_residual_grad = bool(fold)
+        x = (x0.float() if fold is None else x0).detach().requires_grad_()
+        before = bnmod.fold_stats["folded"]
+        if fold is None:
+            y1 = F.relu(F.batch_norm(x, None, None, a.weight, a.bias, True))
+            z = F.batch_norm(F.conv2d(y1, conv.weight.float(), padding=1), None, None, b.weight, b.bias, True) + y1
+            y2 = F.relu(z) if relu_b else z
+        else:
+            y1 = a(x)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                h = conv(y1)
+            y2 = b(h, y1, residual_is_ancestor=True)
+        y2.backward(dy.to(y2.dtype))
+        if fold:
+            assert bnmod.fold_stats["folded"] == before + 1, "fold path not taken"
+        elif fold is False:
+            assert bnmod.fold_stats["folded"] == before
+        grads.append([x.grad.float(), a.weight.grad, a.bias.grad, b.weight.grad])
+    for g_fold, g_plain, g_ref in zip(*grads):
+        scale = g_ref.abs().max().clamp(min=1e-3)
+        e_fold = float((g_fold - g_ref).abs().max() / scale)
+        e_plain = float((g_plain - g_ref).abs().max() / scale)
+        assert e_fold <= 1.25 * e_plain + 1e-2, (e_fold, e_plain)
+        assert float((g_fold - g_plain).abs().max() / scale) < 4e-2
+
+
+@pytest.mark.gpu
 def test_fused_bn_eval_and_cumulative_momentum():
     dev = torch.device("cuda", 0)
     m = BatchNormAct2d(64, momentum=None).to(dev)
@@ -144,13 +187,14 @@ def test_resnet50_fused_bn_matches_unfused_step():
     x = torch.randn(16, 3, 64, 64, device=dev).contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 10, (16,), device=dev)
     logits = []
-    before = bnmod.stats["fused"]
+    before, folded0 = bnmod.stats["fused"], bnmod.fold_stats["folded"]
     for m, bf16 in ((a, True), (b, True), (ref, False)):
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16):
             out = m(x).float()
         F.cross_entropy(out, y).backward()
         logits.append(out.detach())
     assert bnmod.stats["fused"] - before == 53, "every BN layer of the fused model must take the kernel path"
+    assert bnmod.fold_stats["folded"] - folded0 == 12, "the 12 identity shortcuts fold their residual grads"
 
     def rel(g, r):
         return float((g.float() - r).norm() / r.norm())

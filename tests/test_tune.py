@@ -141,3 +141,27 @@ def test_last_report_of_a_finishing_trial_is_kept(tmpdir, ray_start_4_cpus):
     df = analysis.results_df
     assert len(df) == 8
     assert sorted(df["score"]) == list(range(8))
+
+
+def _report_pid(config):
+    import sys
+
+    print("trial output", config["i"])  # goes to the trial's own stdout file (log_to_file)
+    tune.report(pid=os.getpid(), cwd=os.getcwd(), redirected=sys.stdout is not sys.__stdout__)
+
+
+def test_sequential_trials_recycle_the_trial_process(tmpdir, ray_start_4_cpus):
+    """config.reuse_workers: a finished trial's process is parked and the next trial
+    runs in it (no interpreter + torch start-up), with its own working directory and
+    the previous trial's stdout redirection undone."""
+    analysis = tune.run(_report_pid, config={"i": tune.grid_search(list(range(4)))},
+                        resources_per_trial={"cpu": 1}, local_dir=str(tmpdir), max_concurrent_trials=1,
+                        log_to_file=True)
+    df = analysis.results_df
+    assert len(df) == 4
+    assert df["pid"].nunique() <= 2, list(df["pid"])  # trials after the first reuse its process
+    for t in analysis.trials:
+        assert t.last_result["cwd"] == t.logdir
+        assert t.last_result["redirected"]
+        with open(os.path.join(t.logdir, "stdout")) as f:
+            assert f.read().count("trial output") == 1  # no other trial's output leaked in
