@@ -218,6 +218,10 @@ class ProcessCheckpointWriter:
         # GPU context; otherwise spawn a fresh interpreter (~1-2 s until ready())
         torch_mod = sys.modules.get("torch")
         gpu_ctx = torch_mod is not None and torch_mod.cuda.is_initialized()
+        if not gpu_ctx:
+            from ..utils import warmup
+
+            warmup.join()  # never fork while a warm-up thread may hold an import lock
         ctx = mp.get_context("spawn" if gpu_ctx else "fork")
         self._conn, child = ctx.Pipe()
         self._proc = ctx.Process(target=_writer_main, args=(child,), daemon=True, name="rla-ckpt-writer")

@@ -130,11 +130,31 @@ def _generate(n: int, seed: int, noise: float, jitter: int, blob_sd: float = 0.8
     return (res.clamp(0, 1) * 255).round().to(torch.uint8).reshape(n, IMG * IMG), labels
 
 
+def _synthetic_mnist_from_spec(n: int, seed: int, train: bool) -> "SyntheticMNIST":
+    return SyntheticMNIST(n, seed, train)
+
+
 class SyntheticMNIST(Dataset):
-    """Map-style dataset yielding (float [1,28,28] in [0,1], label) like torchvision MNIST+ToTensor."""
+    """Map-style dataset yielding (float [1,28,28] in [0,1], label) like torchvision MNIST+ToTensor.
+
+    Pickles as its generation spec while the arrays are untouched: a model or
+    data module that carries it to a worker ships ~100 bytes instead of 47 MB
+    (measured: 70 ms per Tune trial, profiles/r3_tune), and the worker loads the
+    arrays from its process memo / the disk cache.  Modified arrays (replaced or
+    changed in place) pickle by value."""
 
     def __init__(self, n: int = 60000, seed: int = 0, train: bool = True):
+        self._spec = (n, seed, train)
         self.images, self.targets = synthetic_mnist(n, seed=seed if train else seed + 1)
+        self._stamp = self._fingerprint()
+
+    def _fingerprint(self):
+        return tuple((id(t), t.data_ptr(), t._version) for t in (self.images, self.targets))
+
+    def __reduce__(self):
+        if getattr(self, "_stamp", None) is not None and self._fingerprint() == self._stamp:
+            return _synthetic_mnist_from_spec, self._spec
+        return super().__reduce__()
 
     def __len__(self) -> int:
         return self.targets.numel()

@@ -155,17 +155,32 @@ class WorkerServer:
         self.executor.shutdown(wait=False)
 
 
-def _warm_imports() -> None:
+def _warm_optimizer() -> None:
+    import torch
+
+    # the first optimizer construction imports torch._dynamo (~1 s)
+    torch.optim.Adam([torch.nn.Parameter(torch.zeros(1))])
+
+
+def _warm_imports(background: bool = False) -> None:
+    """``background``: report ready after the module imports and finish the
+    optimizer warm-up on a thread (utils/warmup.py) -- a pooled worker becomes
+    usable ~1 s sooner, which a cold Tune sweep's first trial driver waits for."""
     import torch  # noqa: F401 - the import is the point: it is what a pooled worker saves
     import torch.distributed  # noqa: F401
 
-    # the first optimizer construction imports torch._dynamo (~1 s); the framework's
-    # pure-Python layers are what every training worker unpickles next (no GPU call)
-    torch.optim.Adam([torch.nn.Parameter(torch.zeros(1))])
+    # the framework's pure-Python layers are what every training worker unpickles next
     import ray_lightning_accelerators_amd.accelerators.ray_ddp  # noqa: F401
     import ray_lightning_accelerators_amd.lightning  # noqa: F401
     import ray_lightning_accelerators_amd.models.datamodules  # noqa: F401
     import ray_lightning_accelerators_amd.tune  # noqa: F401
+
+    if background:
+        from ..utils import warmup
+
+        warmup.start(_warm_optimizer)
+    else:
+        _warm_optimizer()
 
 
 def _warm_gpu() -> bool:
@@ -248,7 +263,7 @@ def main() -> None:
         if p not in sys.path:
             sys.path.insert(0, p)
     if "--pool" in argv:
-        _warm_imports()
+        _warm_imports(background=True)
         _wait_for_assignment("pool_ready")
     elif "--prewarm" in argv:
         from ..utils.timeline import mark

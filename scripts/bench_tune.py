@@ -57,16 +57,18 @@ def main():
     try:
         analysis = ray_ddp_tune.tune_mnist(os.path.join(tempfile.gettempdir(), "mnist_data_"), args.trials,
                                            args.epochs, args.workers, gpu)
+        wall = time.perf_counter() - t0  # the sweep: first trial launched .. last result in
     finally:
+        t1 = time.perf_counter()
         ray.shutdown()
-    wall = time.perf_counter() - t0
+        shutdown_s = time.perf_counter() - t1
     df = analysis.results_df
     iters = [int(v) for v in df["training_iteration"]] if "training_iteration" in df else []
     print(json.dumps({
         "metric": "Tune sweep trials/hour (tune_mnist, RayAccelerator workers)",
         "value": round(args.trials / wall * 3600.0, 1), "unit": "trials/hour", "trials": args.trials,
         "workers_per_trial": args.workers, "gpus": n_gpus, "epochs_per_trial": args.epochs,
-        "wall_s": round(wall, 2), "pool_warm_s": args.warm, "virtual_gpus_on_one": args.share_gpu, "s_per_trial": round(wall / args.trials, 2), "reports_per_trial": iters,
+        "wall_s": round(wall, 2), "runtime_shutdown_s": round(shutdown_s, 2), "pool_warm_s": args.warm, "virtual_gpus_on_one": args.share_gpu, "s_per_trial": round(wall / args.trials, 2), "reports_per_trial": iters,
         "best_config": analysis.best_config, "data": "synthetic"}), flush=True)
 
 

@@ -165,3 +165,23 @@ def test_sequential_trials_recycle_the_trial_process(tmpdir, ray_start_4_cpus):
         assert t.last_result["redirected"]
         with open(os.path.join(t.logdir, "stdout")) as f:
             assert f.read().count("trial output") == 1  # no other trial's output leaked in
+
+
+def test_synthetic_mnist_pickles_by_spec_until_modified():
+    """The dataset a model carries to its workers ships as its spec (not 47 MB of
+    pixels) while untouched, and by value once changed."""
+    import pickle
+
+    from ray_lightning_accelerators_amd.models.data import SyntheticMNIST
+
+    d = SyntheticMNIST(1000, seed=5)
+    blob = pickle.dumps(d)
+    assert len(blob) < 1024
+    e = pickle.loads(blob)
+    assert bool((e.images == d.images).all()) and bool((e.targets == d.targets).all())
+    d.images[0, 0] = 3  # in place
+    f = pickle.loads(pickle.dumps(d))
+    assert int(f.images[0, 0]) == 3
+    d2 = SyntheticMNIST(1000, seed=5)
+    d2.targets = d2.targets.clone()  # replaced
+    assert len(pickle.dumps(d2)) > 1024
