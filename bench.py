@@ -725,19 +725,35 @@ def _sync_debug() -> None:
 class _EpochClock(Callback):
     """Callback: wall-clock of every epoch from one epoch start to the next (so an
     epoch's time includes its validation pass, checkpoint write and logging),
-    max over ranks, plus the per-epoch split train / validation / rest (device
-    synced at each mark); ``trace`` also marks every dispatch chunk.  Rank 0
-    writes the rows to ``path``."""
+    max over ranks, plus the per-epoch split train / validation / rest; ``trace``
+    also marks every dispatch chunk.  Rank 0 writes the rows to ``path``.
+
+    On the GPU the marks are HIP events recorded on the stream (no host sync: a
+    ``synchronize`` per mark stalled the dispatching host at every validation
+    start / end and made the measured epoch longer than an unobserved one); the
+    interval between two epoch-start events is the epoch's period on the device
+    timeline, host stalls included (the device idles while it waits for work)."""
 
     def __init__(self, path, trace=False):
         self.path = path
         self.trace = trace
-        self.marks = []  # (epoch, name, t)
+        self.marks = []  # (epoch, name, t or event)
 
     def _mark(self, trainer, name):
         if trainer.on_gpu:
-            torch.cuda.synchronize()
-        self.marks.append((trainer.current_epoch, name, time.perf_counter()))
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self.marks.append((trainer.current_epoch, name, ev))
+        else:
+            self.marks.append((trainer.current_epoch, name, time.perf_counter()))
+
+    def _resolve(self):
+        """Event marks -> seconds on one clock (relative to the first mark)."""
+        if not self.marks or not isinstance(self.marks[0][2], torch.cuda.Event):
+            return
+        torch.cuda.synchronize()
+        first = self.marks[0][2]
+        self.marks = [(e, n, 0.0 if ev is first else first.elapsed_time(ev) / 1e3) for e, n, ev in self.marks]
 
     def on_train_epoch_start(self, trainer, pl_module):
         self._mark(trainer, "epoch_start")
@@ -756,6 +772,7 @@ class _EpochClock(Callback):
 
     def on_train_end(self, trainer, pl_module):
         self._mark(trainer, "train_end")
+        self._resolve()
         starts = [t for _, n, t in self.marks if n in ("epoch_start", "train_end")]
         secs = torch.tensor([b - a for a, b in zip(starts, starts[1:])], dtype=torch.float64)
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
@@ -779,6 +796,7 @@ class _EpochClock(Callback):
         if trainer.global_rank == 0:
             with open(self.path, "w") as f:
                 json.dump({"epoch_s": secs.tolist(), "split": split, "world": trainer.world_size,
+                           "clock": "hip-events" if trainer.on_gpu else "host",
                            "batches": int(trainer.num_training_batches),
                            "val_batches": [int(v) for v in trainer.num_val_batches],
                            "fused": trainer._fused is not None,
@@ -887,6 +905,7 @@ def run_trainer(args):
             "fused_step": rows["fused"],
         },
         "epoch_wall_s": [round(v, 5) for v in epochs],
+        "epoch_clock": rows.get("clock", "host"),
         "epoch_split": rows["split"],
         "median_steady_epoch_samples_per_s": round(per_epoch / med, 1),
         "steady_epoch_spread": round(max(steady) / min(steady), 3),

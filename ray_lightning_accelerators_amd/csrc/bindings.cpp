@@ -379,8 +379,18 @@ const uint16_t* bn_dy2(const Tensor& x, const optional<Tensor>& dy2, int64_t C) 
   return reinterpret_cast<const uint16_t*>(dy2->data_ptr());
 }
 
+// optional forward statistics [4, C] (mean, invstd, scale, shift): the backward's
+// ReLU mask is recomputed from x instead of read from the saved output y
+const float* bn_ss(const optional<Tensor>& ss, int64_t C) {
+  if (!ss.has_value() || !ss->defined()) return nullptr;
+  check_dev(*ss, "stats", at::kFloat);
+  TORCH_CHECK(ss->dim() == 2 && ss->size(0) == 4 && ss->size(1) == C && ss->is_contiguous(),
+              "stats must be a contiguous [4, C] fp32 tensor");
+  return ss->data_ptr<float>();
+}
+
 Tensor bn_partial(Tensor x, optional<Tensor> y, optional<Tensor> dy, int64_t C, int64_t mode, bool relu,
-                  optional<Tensor> nbt, optional<Tensor> dy2) {
+                  optional<Tensor> nbt, optional<Tensor> dy2, optional<Tensor> ss) {
   const int64_t M = bn_rows(x, "x", C);
   TORCH_CHECK(M > 0, "fused BN: empty input");
   TORCH_CHECK(mode == 0 || mode == 1, "fused BN: mode 0 (forward) or 1 (backward)");
@@ -390,8 +400,8 @@ Tensor bn_partial(Tensor x, optional<Tensor> y, optional<Tensor> dy, int64_t C, 
     TORCH_CHECK(dy.has_value(), "backward partial needs dy");
     bn_same(x, *dy, "dy", C);
     dyp = reinterpret_cast<const uint16_t*>(dy->data_ptr());
-    if (relu) {
-      TORCH_CHECK(y.has_value(), "ReLU backward needs the saved output y");
+    if (relu && !(ss.has_value() && ss->defined())) {
+      TORCH_CHECK(y.has_value(), "ReLU backward needs the saved output y (or the forward stats)");
       bn_same(x, *y, "y", C);
       yp = reinterpret_cast<const uint16_t*>(y->data_ptr());
     }
@@ -401,7 +411,8 @@ Tensor bn_partial(Tensor x, optional<Tensor> y, optional<Tensor> dy, int64_t C, 
   Tensor part = at::empty({plan.blocks, 2, C}, x.options().dtype(at::kFloat));
   int64_t* nbtp = mode == 0 ? ptr_or_null<int64_t>(nbt, "num_batches_tracked", at::kLong, 1) : nullptr;
   rla::launch_bn_partial(reinterpret_cast<const uint16_t*>(x.data_ptr()), yp, dyp, M, (int)C, (int)mode, relu,
-                         plan, part.data_ptr<float>(), nbtp, cur_stream(x), mode == 1 ? bn_dy2(x, dy2, C) : nullptr);
+                         plan, part.data_ptr<float>(), nbtp, cur_stream(x), mode == 1 ? bn_dy2(x, dy2, C) : nullptr,
+                         mode == 1 && relu ? bn_ss(ss, C) : nullptr);
   return part;
 }
 
@@ -493,7 +504,7 @@ void bn_apply(Tensor x, Tensor scale, Tensor shift, optional<Tensor> res, bool r
 }
 
 void bn_bwd_apply(Tensor x, optional<Tensor> y, Tensor dy, Tensor coef, bool relu, Tensor dx,
-                  optional<Tensor> dres, optional<Tensor> dy2) {
+                  optional<Tensor> dres, optional<Tensor> dy2, optional<Tensor> ss) {
   check_dev(coef, "coef", at::kFloat);
   TORCH_CHECK(coef.dim() == 2 && coef.size(0) == 5, "coef must be [5, C]");
   const int64_t C = coef.size(1);
@@ -501,8 +512,9 @@ void bn_bwd_apply(Tensor x, optional<Tensor> y, Tensor dy, Tensor coef, bool rel
   bn_same(x, dy, "dy", C);
   bn_same(x, dx, "dx", C);
   const uint16_t* yp = nullptr;
-  if (relu) {
-    TORCH_CHECK(y.has_value(), "ReLU backward needs the saved output y");
+  const float* ssp = relu ? bn_ss(ss, C) : nullptr;
+  if (relu && !ssp) {
+    TORCH_CHECK(y.has_value(), "ReLU backward needs the saved output y (or the forward stats)");
     bn_same(x, *y, "y", C);
     yp = reinterpret_cast<const uint16_t*>(y->data_ptr());
   }
@@ -514,7 +526,8 @@ void bn_bwd_apply(Tensor x, optional<Tensor> y, Tensor dy, Tensor coef, bool rel
   const at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   rla::launch_bn_bwd_apply(reinterpret_cast<const uint16_t*>(x.data_ptr()), yp,
                            reinterpret_cast<const uint16_t*>(dy.data_ptr()), coef.data_ptr<float>(), M, (int)C,
-                           relu, reinterpret_cast<uint16_t*>(dx.data_ptr()), drp, cur_stream(x), bn_dy2(x, dy2, C));
+                           relu, reinterpret_cast<uint16_t*>(dx.data_ptr()), drp, cur_stream(x), bn_dy2(x, dy2, C),
+                           ssp);
 }
 
 }  // namespace
@@ -545,7 +558,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp_param_count", &mlp_param_count);
   m.def("bn_partial", &bn_partial, "fused BN: per-block partial sums (mode 0 fwd stats, 1 bwd dz/dz*x)",
         py::arg("x"), py::arg("y"), py::arg("dy"), py::arg("C"), py::arg("mode"), py::arg("relu"), py::arg("nbt"),
-        py::arg("dy2") = py::none());
+        py::arg("dy2") = py::none(), py::arg("ss") = py::none());
   m.def("bn_finalize", &bn_finalize, "fused BN: mean/invstd/scale/shift + running stats from partials");
   m.def("bn_bwd_finalize", &bn_bwd_finalize, "fused BN backward: dgamma/dbeta + dx coefficients");
   m.def("bn_apply", &bn_apply, "fused BN apply: y = act(x*scale + shift (+res))");
@@ -553,6 +566,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max pool backward (gather through the argmax bytes)");
   m.def("bn_bwd_apply", &bn_bwd_apply, "fused BN backward apply: dx (+ dres = relu-masked dy)", py::arg("x"),
         py::arg("y"), py::arg("dy"), py::arg("coef"), py::arg("relu"), py::arg("dx"), py::arg("dres"),
-        py::arg("dy2") = py::none());
+        py::arg("dy2") = py::none(), py::arg("ss") = py::none());
   m.attr("ARCH") = "gfx950";
 }

@@ -53,6 +53,10 @@ __device__ __forceinline__ f8 ld8f(const float* p) {  // 8 fp32 per-channel coef
   return r;
 }
 
+// the forward's affine map; the backward recomputes the ReLU mask with this exact
+// expression (one fused multiply-add per element) instead of re-reading y
+__device__ __forceinline__ f8 bn_affine(f8 x, f8 sc, f8 sf) { return __builtin_elementwise_fma(x, sc, sf); }
+
 __device__ __forceinline__ f8 relu_mask(f8 d, f8 y) {
 #pragma unroll
   for (int k = 0; k < 8; ++k) d[k] = y[k] > 0.f ? d[k] : 0.f;
@@ -63,12 +67,17 @@ __device__ __forceinline__ f8 relu_mask(f8 d, f8 y) {
 // DY2 (backward): the incoming gradient is dy + dy2 -- the residual-branch gradient
 // of the NEXT bottleneck (its bn3's dres), folded here instead of autograd adding
 // the two into a new tensor first (ops/bn.py, fold_residual_grad)
-template <int MODE, bool RELU, bool DY2 = false>
+// RECOMP (backward, ReLU without residual): the mask is x*scale+shift > 0 recomputed
+// from the forward statistics `ss` ([4, C]: mean, invstd, scale, shift) -- y is not read
+template <int MODE, bool RELU, bool DY2 = false, bool RECOMP = false>
 __global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(const uint16_t* __restrict__ x,
                                                                 const uint16_t* __restrict__ y,
                                                                 const uint16_t* __restrict__ dy, int64_t M, int C,
                                                                 int64_t rows_per_blk, float* __restrict__ part,
-                                                                int64_t* nbt, const uint16_t* __restrict__ dy2 = nullptr) {
+                                                                int64_t* nbt, const uint16_t* __restrict__ dy2 = nullptr,
+                                                                const float* __restrict__ ss = nullptr) {
+  // forward: one input stream, so twice the rows in flight per thread
+  constexpr int U = MODE == 0 ? 8 : 4;
   __shared__ float sh[2][kBnThreads * 8];
   const int G = C >> 3, rpi = kBnThreads / G, tid = threadIdx.x;
   const int g = tid % G, r0 = tid / G;
@@ -78,23 +87,29 @@ __global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(const uint16_t* 
   const int64_t re = rb + rows_per_blk < M ? rb + rows_per_blk : M;
   if (r0 < rpi) {
     const int64_t col = (int64_t)g * 8, step = (int64_t)rpi * C;
+    f8 sc, sf;
+    if (RECOMP) {
+      sc = ld8f(ss + 2 * C + col);
+      sf = ld8f(ss + 3 * C + col);
+    }
     int64_t r = rb + r0;
     const uint16_t* px = x + r * C + col;
-    // 4 rows in flight per thread (x, and dy / y in the backward)
-    for (; r + 3 * rpi < re; r += 4 * rpi, px += 4 * step) {
-      f8 xv[4], dv[4];
+    // U rows in flight per thread (x, and dy [/ y] in the backward)
+    for (; r + (U - 1) * rpi < re; r += U * rpi, px += U * step) {
+      f8 xv[U], dv[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         xv[u] = ld8(px + u * step);
         if (MODE == 1) {
           const int64_t off = (px - x) + u * step;
           dv[u] = ld8(dy + off);
           if (DY2) dv[u] += ld8(dy2 + off);
-          if (RELU) dv[u] = relu_mask(dv[u], ld8(y + off));
+          if (RELU && !RECOMP) dv[u] = relu_mask(dv[u], ld8(y + off));
         }
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
+        if (MODE == 1 && RECOMP) dv[u] = relu_mask(dv[u], bn_affine(xv[u], sc, sf));
         if (MODE == 0) {
           s += xv[u];
           q += xv[u] * xv[u];
@@ -113,7 +128,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(const uint16_t* 
         const int64_t off = px - x;
         f8 d = ld8(dy + off);
         if (DY2) d += ld8(dy2 + off);
-        if (RELU) d = relu_mask(d, ld8(y + off));
+        if (RELU) d = relu_mask(d, RECOMP ? bn_affine(xv, sc, sf) : ld8(y + off));
         s += d;
         q += d * xv;
       }
@@ -240,8 +255,8 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_kernel(const uint16_t* __
       a0 = ld8(res + o0);
       a1 = ld8(res + o1);
     }
-    v0 = v0 * sc + sf;
-    v1 = v1 * sc + sf;
+    v0 = bn_affine(v0, sc, sf);
+    v1 = bn_affine(v1, sc, sf);
     if (RES) {
       v0 += a0;
       v1 += a1;
@@ -255,32 +270,38 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_kernel(const uint16_t* __
   }
   if (r < M) {
     const int64_t o = r * C + col;
-    f8 v = ld8(x + o) * sc + sf;
+    f8 v = bn_affine(ld8(x + o), sc, sf);
     if (RES) v += ld8(res + o);
     if (RELU) v = relu_mask(v, v);
     st8(y + o, v);
   }
 }
 
-template <bool RELU, bool DRES, bool DY2 = false>
+template <bool RELU, bool DRES, bool DY2 = false, bool RECOMP = false>
 __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_kernel(const uint16_t* __restrict__ x,
                                                                   const uint16_t* __restrict__ y,
                                                                   const uint16_t* __restrict__ dy,
                                                                   const float* __restrict__ coef, int64_t M, int C,
                                                                   uint16_t* __restrict__ dx,
                                                                   uint16_t* __restrict__ dres,
-                                                                  const uint16_t* __restrict__ dy2 = nullptr) {
+                                                                  const uint16_t* __restrict__ dy2 = nullptr,
+                                                                  const float* __restrict__ ss = nullptr) {
   const int G = C >> 3, rpi = kBnThreads / G, tid = threadIdx.x;
   const int g = tid % G, r0 = tid / G;
   if (r0 >= rpi) return;
   const f8 A = ld8f(coef + 2 * C + g * 8), B = ld8f(coef + 3 * C + g * 8), Cc = ld8f(coef + 4 * C + g * 8);
+  f8 sc, sf;
+  if (RECOMP) {
+    sc = ld8f(ss + 2 * C + g * 8);
+    sf = ld8f(ss + 3 * C + g * 8);
+  }
   const int64_t col = (int64_t)g * 8, rstride = (int64_t)gridDim.x * rpi;
   for (int64_t r = (int64_t)blockIdx.x * rpi + r0; r < M; r += rstride) {
     const int64_t o = r * C + col;
     f8 d = ld8(dy + o);
     if (DY2) d += ld8(dy2 + o);
-    if (RELU) d = relu_mask(d, ld8(y + o));
     const f8 xv = ld8(x + o);
+    if (RELU) d = relu_mask(d, RECOMP ? bn_affine(xv, sc, sf) : ld8(y + o));
     st8(dx + o, A * d + B * xv + Cc);
     if (DRES) st8(dres + o, d);
   }
@@ -297,11 +318,12 @@ int apply_grid(int64_t M, int C) {
 
 BnPlan bn_plan(int64_t M, int C) {
   const int rpi = kBnThreads / (C >> 3);
-  // >= 16 row iterations per thread, at most 512 blocks (2 per CU) and 128K partial
-  // floats, so the finalize kernel's 16 slices each sum <= 32 partial rows
+  // >= 16 row iterations per thread, at most 1024 blocks (4 per CU) and 256K partial
+  // floats (1 MB; the wide layers of the last stages got only 64-128 blocks under
+  // the earlier 128K cap -- a quarter of the chip)
   int64_t blocks = (M + (int64_t)rpi * 16 - 1) / ((int64_t)rpi * 16);
-  int64_t cap = (int64_t(1) << 17) / C;
-  if (cap > 512) cap = 512;
+  int64_t cap = (int64_t(1) << 18) / C;
+  if (cap > 1024) cap = 1024;
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   BnPlan p;
@@ -312,8 +334,18 @@ BnPlan bn_plan(int64_t M, int C) {
 }
 
 void launch_bn_partial(const uint16_t* x, const uint16_t* y, const uint16_t* dy, int64_t M, int C, int mode,
-                       bool relu, const BnPlan& plan, float* part, int64_t* nbt, hipStream_t s, const uint16_t* dy2) {
+                       bool relu, const BnPlan& plan, float* part, int64_t* nbt, hipStream_t s, const uint16_t* dy2,
+                       const float* ss) {
   const dim3 grid(plan.blocks), block(kBnThreads);
+  if (mode == 1 && relu && ss) {
+    if (dy2)
+      hipLaunchKernelGGL((bn_partial_kernel<1, true, true, true>), grid, block, 0, s, x, y, dy, M, C,
+                         plan.rows_per_blk, part, nullptr, dy2, ss);
+    else
+      hipLaunchKernelGGL((bn_partial_kernel<1, true, false, true>), grid, block, 0, s, x, y, dy, M, C,
+                         plan.rows_per_blk, part, nullptr, nullptr, ss);
+    return;
+  }
   if (mode == 1 && dy2) {
     if (relu)
       hipLaunchKernelGGL((bn_partial_kernel<1, true, true>), grid, block, 0, s, x, y, dy, M, C, plan.rows_per_blk,
@@ -361,8 +393,18 @@ void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* scale,
 }
 
 void launch_bn_bwd_apply(const uint16_t* x, const uint16_t* y, const uint16_t* dy, const float* coef, int64_t M,
-                         int C, bool relu, uint16_t* dx, uint16_t* dres, hipStream_t s, const uint16_t* dy2) {
+                         int C, bool relu, uint16_t* dx, uint16_t* dres, hipStream_t s, const uint16_t* dy2,
+                         const float* ss) {
   const dim3 grid(apply_grid(M, C)), block(kBnThreads);
+  if (relu && ss && !dres) {  // no residual: the mask is recomputed from x and the forward stats
+    if (dy2)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false, true, true>), grid, block, 0, s, x, y, dy, coef, M, C, dx,
+                         dres, dy2, ss);
+    else
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false, false, true>), grid, block, 0, s, x, y, dy, coef, M, C,
+                         dx, dres, nullptr, ss);
+    return;
+  }
   if (dy2) {  // the folded residual gradient; ResNet's bn3 (relu, its own dres) is the user
     if (relu && dres)
       hipLaunchKernelGGL((bn_bwd_apply_kernel<true, true, true>), grid, block, 0, s, x, y, dy, coef, M, C, dx, dres,

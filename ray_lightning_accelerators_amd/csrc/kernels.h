@@ -65,7 +65,8 @@ BnPlan bn_plan(int64_t M, int C);
 //   mode 1 (backward): sum dz, sum dz*x with dz = dy * (y > 0 if relu)
 void launch_bn_partial(const uint16_t* x, const uint16_t* y, const uint16_t* dy, int64_t M, int C, int mode,
                        bool relu, const BnPlan& plan, float* part, int64_t* nbt, hipStream_t s,
-                       const uint16_t* dy2 = nullptr);  // backward: gradient = dy + dy2
+                       const uint16_t* dy2 = nullptr,   // backward: gradient = dy + dy2
+                       const float* ss = nullptr);      // backward ReLU mask from the fwd stats, not y
 
 // forward finalize of `nparts` partial rows: stats[0]=mean [1]=invstd [2]=scale [3]=shift ([4, C]);
 // running stats update (momentum < 0: cumulative average over num_batches_tracked)
@@ -84,7 +85,8 @@ void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* scale,
 // dz = dy * (y > 0 if relu); dx = A*dz + B*x + Cc; dres = dz (if dres)
 void launch_bn_bwd_apply(const uint16_t* x, const uint16_t* y, const uint16_t* dy, const float* coef, int64_t M,
                          int C, bool relu, uint16_t* dx, uint16_t* dres, hipStream_t s,
-                         const uint16_t* dy2 = nullptr);  // gradient = dy + dy2
+                         const uint16_t* dy2 = nullptr,  // gradient = dy + dy2
+                         const float* ss = nullptr);     // ReLU mask from the fwd stats [4, C], not y
 
 // ---------------------------------------------------------------------------
 // Fused MNIST-MLP training step (784 -> L1 -> L2 -> 10, ReLU, log_softmax+NLL).

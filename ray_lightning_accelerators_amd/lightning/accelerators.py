@@ -294,22 +294,7 @@ class DataParallelAccelerator(Accelerator):
             convert_sync_batchnorm(model)
         self.model_to_device(model)
         mark("model_on_device", rank=t.global_rank)
-        prof_path = os.environ.get("RLA_PROFILE_FIT")
-        if prof_path:  # host-side profile of the fit (diagnostics: where the epoch boundary's time goes)
-            import cProfile
-            import io
-            import pstats
-
-            prof = cProfile.Profile()
-            results = prof.runcall(t._run, model)
-            buf = io.StringIO()
-            st = pstats.Stats(prof, stream=buf)
-            st.sort_stats("tottime").print_stats(45)
-            st.sort_stats("cumulative").print_stats(70)
-            with open(f"{prof_path}.rank{t.global_rank}.txt", "w") as f:
-                f.write(buf.getvalue())
-        else:
-            results = t._run(model)
+        results = t._run(model)
         mark("run_end", rank=t.global_rank)
         self.transfer_distrib_spawn_state_on_fit_end(model, results)
         mark("state_handed_back", rank=t.global_rank)

@@ -758,8 +758,18 @@ class Trainer:
         # No collection first: it cost 80-240 ms per Tune trial (profiles/r3_tune);
         # garbage frozen here is collected after the fit (gc.unfreeze below).
         gc.freeze()
+        # RLA_PROFILE_EPOCHS=<path>: host profile (cProfile) of the steady epochs (the
+        # first is skipped: imports / graph capture), written per rank on fit end
+        prof_path = os.environ.get("RLA_PROFILE_EPOCHS")
+        prof = None
+        if prof_path:
+            import cProfile
+
+            prof = cProfile.Profile()
         try:
             while self.current_epoch < self.max_epochs:
+                if prof is not None and self.current_epoch == 1:
+                    prof.enable()
                 self._run_epoch(model)
                 if self.max_steps is not None and self.global_step >= self.max_steps:
                     break
@@ -772,6 +782,9 @@ class Trainer:
             self.call_hook("on_keyboard_interrupt")
         finally:
             gc.unfreeze()
+            if prof is not None:
+                prof.disable()
+                self._dump_profile(prof, prof_path)
         self.call_hook("on_train_end")
         self.call_hook("on_fit_end")
         if self.logger is not None:
@@ -781,6 +794,17 @@ class Trainer:
         self.profiler_summary = self.profiler.summary()
         if self.profiler_summary and self.is_global_zero:
             print(self.profiler_summary, flush=True)
+
+    def _dump_profile(self, prof, path: str) -> None:
+        import io
+        import pstats
+
+        buf = io.StringIO()
+        st = pstats.Stats(prof, stream=buf)
+        st.sort_stats("tottime").print_stats(40)
+        st.sort_stats("cumulative").print_stats(80)
+        with open(f"{path}.rank{self.global_rank}.txt", "w") as f:
+            f.write(buf.getvalue())
 
     def _run_epoch(self, model: LightningModule) -> None:
         dl = self.train_dataloader

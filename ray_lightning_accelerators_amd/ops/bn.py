@@ -8,7 +8,9 @@ activations (ResNet-50 under bf16 autocast) it runs the gfx950 kernels of
 
   forward   partial sums (1 read of x) -> finalize ([C]; running stats and
             num_batches_tracked updated in-kernel) -> apply (read x [+res], write y)
-  backward  partial sums (read x, y, dy) -> finalize -> apply (write dx [+dres])
+  backward  partial sums (read x, dy [, y]) -> finalize -> apply (write dx [+dres])
+            (without a residual the ReLU mask is recomputed from x and the
+            forward's scale/shift, so y is not re-read)
 
 which replaces MIOpen's six batch-norm kernels per layer plus the separate
 ReLU, residual-add and ReLU-backward passes (profiles/r1_resnet50_v2).
@@ -97,22 +99,28 @@ class _BNActFn(torch.autograd.Function):
         mod.bn_apply(xv, st[2], st[3], _nhwc(residual) if residual is not None else None, relu, _nhwc(y))
         ctx.relu, ctx.has_res, ctx.group, ctx.count = relu, residual is not None, group, count
         ctx.slot, ctx.sink = slot, sink
-        ctx.save_for_backward(x, y if relu else None, weight, st[0], st[1])
+        # ReLU without a residual: the backward recomputes the mask x*scale+shift > 0
+        # from the stats (one stream less to read in both backward passes); with a
+        # residual the mask needs the sum, so y is kept
+        ctx.recomp = relu and residual is None
+        ctx.save_for_backward(x, y if relu and not ctx.recomp else None, weight, st)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         mod = require()
-        x, y, weight, mean, invstd = ctx.saved_tensors
+        x, y, weight, st = ctx.saved_tensors
+        mean, invstd = st[0], st[1]
+        ss = st if ctx.recomp else None
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         C = x.size(1)
         xv, dyv = _nhwc(x), _nhwc(dy)
-        yv = _nhwc(y) if ctx.relu else None
+        yv = _nhwc(y) if y is not None else None
         dy2 = None
         if ctx.slot is not None and ctx.slot.dres is not None:
             dy2, ctx.slot.dres = _nhwc(ctx.slot.dres), None
             fold_stats["folded"] += 1
-        part = mod.bn_partial(xv, yv, dyv, C, 1, ctx.relu, None, dy2)
+        part = mod.bn_partial(xv, yv, dyv, C, 1, ctx.relu, None, dy2, ss)
         local = None
         if ctx.group is not None:
             local = mod.bn_bwd_finalize(part, ctx.count, weight, mean, invstd)  # local dgamma / dbeta
@@ -121,7 +129,8 @@ class _BNActFn(torch.autograd.Function):
         coef = mod.bn_bwd_finalize(part, ctx.count, weight, mean, invstd)
         dx = torch.empty_like(x, memory_format=torch.channels_last)
         dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
-        mod.bn_bwd_apply(xv, yv, dyv, coef, ctx.relu, _nhwc(dx), _nhwc(dres) if dres is not None else None, dy2)
+        mod.bn_bwd_apply(xv, yv, dyv, coef, ctx.relu, _nhwc(dx), _nhwc(dres) if dres is not None else None, dy2,
+                         ss)
         if ctx.sink is not None:
             ctx.sink.dres, dres = dres, None  # the producer's backward consumes it
         wsrc = local if local is not None else coef

@@ -43,7 +43,9 @@ for st in "$@"; do
       run tune_cold16 300 python scripts/bench_tune.py --trials 16
       run tune_warm 300 python scripts/bench_tune.py --trials 8 --warm 8 ;;
     trainerprof)  # host profile of the worker's fit (cProfile, rank 0)
-      RLA_PROFILE_FIT="$R/$O/trainer_fit_prof" run trainer_prof 300 python bench.py --via trainer --trainer-epochs 6 ;;
+      RLA_PROFILE_EPOCHS="$R/$O/trainer_epochs_prof" run trainer_prof 300 python bench.py --via trainer --trainer-epochs 6 ;;
+    conv1x1)
+      run conv1x1 300 python -u scripts/conv1x1_probe.py ;;
     tunetl)  # cold sweep with the cross-process start-up timeline
       RLA_TIMELINE="$R/$O/tune_timeline.jsonl" run tune_tl 300 python scripts/bench_tune.py --trials 6
       python scripts/timeline_report.py "$O/tune_timeline.jsonl" --merged > "$O/tune_timeline.txt" 2>&1 || true ;;
