@@ -538,7 +538,10 @@ class Trainer:
             on_epoch = not training
         if not isinstance(value, torch.Tensor):
             value = torch.tensor(float(value))
+        fresh = getattr(value, "_rla_fresh", False)
         value = value.detach()
+        if fresh:  # framework-made value that nothing writes before the log flush
+            value._rla_fresh = True
         if sync_dist and self.accelerator_backend is not None:
             value = self.accelerator_backend.sync_tensor(value.float(), reduce_op=sync_dist_op)
         store = self._results.setdefault(fx, defaultdict(list))
@@ -599,7 +602,8 @@ class Trainer:
         if defer and any(isinstance(v, torch.Tensor) and v.is_cuda for v in metrics.values()):
             # a device-side copy (no host sync): a logged tensor the module later
             # changes in place must still be written with its value at log time
-            snap = {k: (v.detach().clone() if isinstance(v, torch.Tensor) else v) for k, v in metrics.items()}
+            snap = {k: (v.detach().clone() if isinstance(v, torch.Tensor) and not getattr(v, "_rla_fresh", False)
+                        else v) for k, v in metrics.items()}
             if self._pending_log is None:
                 self._pending_log = []
             self._pending_log.append((snap, self.global_step))

@@ -172,6 +172,11 @@ def _sampler_order(sampler) -> torch.Tensor:
     return torch.as_tensor(list(iter(sampler)), dtype=torch.int64)
 
 
+# rows of the engine's per-step (loss, correct, count, step) ring: two MNIST epochs at
+# batch 32, so chunk outputs can be views of it (train_chunk)
+ENGINE_STATS_RING = 4096
+
+
 class FusedMNISTStep:
     """Drives the fused HIP step from the Trainer's loop (replaces autograd + optimizer)."""
 
@@ -235,7 +240,7 @@ class FusedMNISTStep:
         eng = FusedMLPEngine(self.L1, self.L2, B, lr=float(g["lr"]), betas=tuple(g["betas"]), eps=g["eps"],
                              weight_decay=g["weight_decay"], device=self.dev, world_size=self.world,
                              rank=self.trainer.global_rank, allreduce=self._allreduce, buffers=bufs,
-                             stats_ring=self.stats.size(0), dp_context=dp_ctx, dp_rearm=rearm)
+                             stats_ring=ENGINE_STATS_RING, dp_context=dp_ctx, dp_rearm=rearm)
         eng.set_step(self.gs.step)
         eng.lr_tensor = self.lr_tensor  # LR schedulers update one device scalar
         eng.attach_dataset(self._u8, self._labels)
@@ -410,21 +415,32 @@ class FusedMNISTStep:
         ring = eng.stats.size(0)
         k = min(n_steps, ring)
         # Rows of the chunk's last k steps, in step order: step first + 1 + i sits in
-        # ring slot (first + i) % ring, which the host knows -- so one or two
-        # contiguous device-to-device copies into a fresh tensor (the ring wraps in
-        # later chunks).  No index kernel: a chunk-sized gather picked a different
+        # ring slot (first + i) % ring, which the host knows.  When the ring holds two
+        # epochs (MNIST: 1,718 steps in 4,096 rows) the rows are handed out as VIEWS of
+        # it: an epoch's outputs stay intact until the end of the next epoch, past its
+        # training_epoch_end and the blocking log flush -- no copy kernel per chunk
+        # (each small kernel between two graph replays left the GPU idle for a few us,
+        # ~1 ms per epoch in all).  Otherwise: one or two device-to-device copies into a
+        # fresh tensor.  Never an index kernel: a chunk-sized gather picked a different
         # ROCm index kernel for small chunks, whose code object loaded mid-epoch and
         # stalled it by ~60 ms (profiles/r2_c05); no host sync either.
         s0 = (first + n_steps - k) % ring
         n1 = min(k, ring - s0)
-        rows = torch.empty(k, 4, device=self.dev)
-        rows[:n1].copy_(eng.stats[s0:s0 + n1])
-        if n1 < k:
-            rows[n1:].copy_(eng.stats[: k - n1])
+        if n1 == k and 2 * max(int(getattr(self.trainer, "num_training_batches", ring)), 1) <= ring:
+            rows = eng.stats[s0:s0 + k]
+        else:
+            rows = torch.empty(k, 4, device=self.dev)
+            rows[:n1].copy_(eng.stats[s0:s0 + n1])
+            if n1 < k:
+                rows[n1:].copy_(eng.stats[: k - n1])
         last = rows[-1]
-        self.model.log("ptl/train_loss", last[0])
-        self.model.log("ptl/train_accuracy", last[1] / last[2].clamp(min=1))
-        self.trainer.callback_metrics["loss"] = last[0]
+        loss = last[0]
+        acc = last[1] / last[2]  # every step counts B > 0 rows
+        # neither tensor is written again before the deferred log flush: no snapshot copy
+        loss._rla_fresh = acc._rla_fresh = True
+        self.model.log("ptl/train_loss", loss)
+        self.model.log("ptl/train_accuracy", acc)
+        self.trainer.callback_metrics["loss"] = loss
         return [{"loss": v} for v in rows[:, 0].unbind(0)]
 
     # ---------------------------------------------------------- validation
