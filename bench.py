@@ -683,6 +683,10 @@ def run_rank(args):
                 **info,
             },
         }
+        if rn and args.impl == "native":
+            from ray_lightning_accelerators_amd.ops import conv as _conv1x1
+
+            out["conv1x1_backends"] = _conv1x1.choices()
         if world > 1 or args.compare_stock:
             out["dp"] = diag
         if stock:

@@ -24,6 +24,7 @@ from torch.utils.data import Dataset
 
 from ..lightning import LightningModule
 from ..ops.bn import BatchNormAct2d
+from ..ops.conv import Conv1x1NHWC
 from ..ops.pool import MaxPool2dNHWC
 
 
@@ -31,7 +32,11 @@ def _conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
     return nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
 
 
-def _conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
+def _conv1x1(cin: int, cout: int, stride: int = 1, fused: bool = False) -> nn.Conv2d:
+    # fused: stride-1 1x1 convs pick MIOpen or a GEMM per operation (ops/conv.py);
+    # same parameter / state-dict key as nn.Conv2d either way
+    if fused and stride == 1:
+        return Conv1x1NHWC(cin, cout)
     return nn.Conv2d(cin, cout, 1, stride, bias=False)
 
 
@@ -49,11 +54,11 @@ class Bottleneck(nn.Module):
         super().__init__()
         cout = width * self.expansion
         self.fused_bn = fused_bn
-        self.conv1 = _conv1x1(cin, width)
+        self.conv1 = _conv1x1(cin, width, fused=fused_bn)
         self.bn1 = _bn(width, fused_bn)
         self.conv2 = _conv3x3(width, width, stride)
         self.bn2 = _bn(width, fused_bn)
-        self.conv3 = _conv1x1(width, cout)
+        self.conv3 = _conv1x1(width, cout, fused=fused_bn)
         self.bn3 = _bn(cout, fused_bn)  # fused: relu(bn3(x) + identity) in one pass
         self.downsample = downsample
 
@@ -100,7 +105,8 @@ class ResNet(nn.Module):
         down = None
         cout = width * Bottleneck.expansion
         if stride != 1 or self.inplanes != cout:
-            down = nn.Sequential(_conv1x1(self.inplanes, cout, stride), _bn(cout, self.fused_bn, act=None))
+            down = nn.Sequential(_conv1x1(self.inplanes, cout, stride, fused=self.fused_bn),
+                                 _bn(cout, self.fused_bn, act=None))
         layers = [Bottleneck(self.inplanes, width, stride, down, self.fused_bn)]
         self.inplanes = cout
         layers += [Bottleneck(cout, width, fused_bn=self.fused_bn) for _ in range(1, blocks)]

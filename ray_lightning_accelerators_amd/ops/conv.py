@@ -1,0 +1,163 @@
+"""Stride-1 1x1 convolution on NHWC bf16 activations, backend chosen per operation.
+
+A 1x1 convolution over a channels_last tensor IS a GEMM on the [N*H*W, C] view:
+
+  forward  y[M, Cout]  = x[M, Cin]  . W^T
+  dgrad    dx[M, Cin]  = dy[M, Cout] . W
+  wgrad    dW[Cout, Cin] = dy^T . x      (fp32 output: the fp32 master gradient)
+
+MIOpen runs these as convolutions; for ResNet-50's shapes it is the faster choice
+for some (e.g. the wgrad of the large 56x56 layers) and far slower for others: its
+wgrad costs ~80 us whatever the size (zero-fill + split-K atomics + a bf16->fp32
+cast, profiles/r3_rn50/kernel_stats_rn50_steady.csv) and its forward of the
+14x14 / 7x7 layers runs 2-5x a hipBLASLt GEMM (profiles/r3_rn50/conv1x1_probe_perop.log).
+So every (operation, shape) picks its backend once, timed on the device at first
+use (like cudnn.benchmark), and the GEMM wgrad writes fp32 directly -- no zero
+fill, no atomics, no cast kernel.
+
+``Conv1x1NHWC`` is a drop-in ``nn.Conv2d(cin, cout, 1, bias=False)`` (same
+parameter and state-dict key); anything outside the fast path (CPU, fp32, NCHW,
+odd alignment) runs the stock convolution.  ``RLA_CONV1X1=miopen|gemm|auto``.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Tuple
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+_choice: Dict[Tuple[str, int, int, int], str] = {}
+_timings: Dict[Tuple[str, int, int, int], Dict[str, float]] = {}
+stats = {"fast": 0, "fallback": 0}
+
+_conv = torch.ops.aten.convolution
+_conv_bwd = torch.ops.aten.convolution_backward
+
+
+def _mode() -> str:
+    return os.environ.get("RLA_CONV1X1", "auto")
+
+
+def _time(fn, reps: int = 3) -> float:
+    """Device time of ``reps`` calls.  The device is held by a spin kernel while the
+    host enqueues them, so the calls run back to back: a backend's host-side cost
+    (MIOpen's is tens of us per call) is hidden, as it is inside a GPU-bound step --
+    timing an idle device would charge it to the kernels."""
+    fn()  # warm: library kernel load / solver search
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda._sleep(2_000_000)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e)
+
+
+def _pick(op: str, key: Tuple[int, int, int], cands) -> str:
+    mode = _mode()
+    if mode in ("miopen", "gemm"):
+        return mode
+    k = (op,) + key
+    c = _choice.get(k)
+    if c is None and torch.cuda.is_current_stream_capturing():
+        return "miopen"  # no timing inside a graph capture (it synchronises)
+    if c is None:
+        t = {name: _time(fn) for name, fn in cands.items()}
+        c = min(t, key=t.get)
+        _choice[k] = c
+        _timings[k] = {name: round(v * 1e3 / 3, 1) for name, v in t.items()}  # device us per call
+    return c
+
+
+def choices() -> Dict[str, Dict[str, float]]:
+    """The autotuned backends so far: ``"op M Cin Cout" -> {backend: us, ..., "pick": name}``."""
+    return {" ".join(map(str, k)): dict(_timings.get(k, {}), pick=c) for k, c in _choice.items()}
+
+
+def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
+    n, c, h, w = t.shape
+    return t.permute(0, 2, 3, 1).reshape(n * h * w, c)
+
+
+def _from2d(t2: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
+    return t2.view(n, h, w, t2.size(1)).permute(0, 3, 1, 2)
+
+
+class _Conv1x1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight):
+        n, cin, h, w = x.shape
+        cout = weight.size(0)
+        wb = weight.detach().to(torch.bfloat16).reshape(cout, cin)
+        x2 = _nhwc2d(x)
+        key = (x2.size(0), cin, cout)
+        be = _pick("fwd", key, {
+            "gemm": lambda: torch.mm(x2, wb.t()),
+            "miopen": lambda: _conv(x, wb.view(cout, cin, 1, 1), None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1),
+        })
+        if be == "gemm":
+            y = _from2d(torch.mm(x2, wb.t()), n, h, w)
+        else:
+            y = _conv(x, wb.view(cout, cin, 1, 1), None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
+        ctx.save_for_backward(x, wb)
+        ctx.key = key
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wb = ctx.saved_tensors
+        n, cin, h, w = x.shape
+        cout = wb.size(0)
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dy2, x2 = _nhwc2d(dy), _nhwc2d(x)
+        w4 = wb.view(cout, cin, 1, 1)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            be = _pick("dgrad", ctx.key, {
+                "gemm": lambda: torch.mm(dy2, wb),
+                "miopen": lambda: _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                            [True, False, False]),
+            })
+            if be == "gemm":
+                dx = _from2d(torch.mm(dy2, wb), n, h, w)
+            else:
+                dx = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            be = _pick("wgrad", ctx.key, {
+                "gemm": lambda: torch.ops.aten.mm.dtype(dy2.t(), x2, torch.float32),
+                "miopen": lambda: _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                            [False, True, False])[1].float(),
+            })
+            if be == "gemm":
+                dw = torch.ops.aten.mm.dtype(dy2.t(), x2, torch.float32).view(cout, cin, 1, 1)
+            else:
+                dw = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                               [False, True, False])[1].float()
+        return dx, dw
+
+
+def fast_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    return (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and x.numel() > 0
+            and x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0
+            and conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.padding == (0, 0)
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
+            and x.size(1) % 8 == 0 and conv.out_channels % 8 == 0)
+
+
+class Conv1x1NHWC(nn.Conv2d):
+    """``nn.Conv2d(cin, cout, 1, bias=False)`` with per-operation MIOpen / GEMM backends."""
+
+    def __init__(self, in_channels: int, out_channels: int, device=None, dtype=None):
+        super().__init__(in_channels, out_channels, 1, 1, 0, bias=False, device=device, dtype=dtype)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if torch.is_autocast_enabled("cuda") and x.is_cuda and x.dtype == torch.float32:
+            x = x.to(torch.bfloat16)
+        if fast_ok(x, self) and _mode() != "off":
+            stats["fast"] += 1
+            return _Conv1x1Fn.apply(x, self.weight)
+        stats["fallback"] += 1
+        return F.conv2d(x, self.weight)

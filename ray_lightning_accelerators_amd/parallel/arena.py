@@ -50,23 +50,52 @@ class ParamArena:
         self.numel = off
         self.data = torch.zeros(off, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(off, dtype=torch.float32, device=dev)
+        # each view keeps its parameter's memory format: a channels_last conv weight
+        # stays channels_last (NHWC convolutions would otherwise re-layout -- clone --
+        # every bf16 weight on every use, and its channels_last gradient would need a
+        # strided copy into a contiguous arena view; profiles/r3_rn50)
+        self.strides: List[Optional[Tuple[int, ...]]] = [
+            tuple(p.stride()) if (not p.is_contiguous() and p.dim() == 4
+                                  and p.is_contiguous(memory_format=torch.channels_last)) else None
+            for p in params]
         with torch.no_grad():
-            for p, (o, n) in zip(params, self.offsets):
-                view = self.data[o:o + n].view_as(p)
+            for i, (p, (o, n)) in enumerate(zip(params, self.offsets)):
+                view = self._shaped(self.data, i, p)
                 view.copy_(p.data)
                 p.data = view
-                p.grad = self.grad[o:o + n].view_as(p)
+                p.grad = self._shaped(self.grad, i, p)
         self._index: Dict[int, int] = {id(p): i for i, p in enumerate(params)}
         self.steal_grads = (dev.type == "cuda") if steal_grads is None else bool(steal_grads)
         self._tables: "OrderedDict[tuple, torch.Tensor]" = OrderedDict()
 
-    def param_view(self, i: int) -> torch.Tensor:
+    def _shaped(self, flat: torch.Tensor, i: int, like: torch.Tensor, base: int = 0) -> torch.Tensor:
         o, n = self.offsets[i]
-        return self.data[o:o + n].view_as(self.params[i])
+        st = self.strides[i]
+        seg = flat[o - base:o - base + n]
+        if st is None:
+            return seg.view_as(like)
+        return seg.as_strided(like.shape, st)
+
+    def shaped_slice(self, flat: torch.Tensor, i: int, base: int = 0) -> torch.Tensor:
+        """Parameter ``i``'s segment of a buffer laid out like the arena (optimizer
+        state; ``flat`` starts at arena element ``base``), in the parameter's layout."""
+        return self._shaped(flat, i, self.params[i], base)
+
+    def param_view(self, i: int) -> torch.Tensor:
+        return self._shaped(self.data, i, self.params[i])
 
     def grad_view(self, i: int) -> torch.Tensor:
-        o, n = self.offsets[i]
-        return self.grad[o:o + n].view_as(self.params[i])
+        return self._shaped(self.grad, i, self.params[i])
+
+    def _flat_like_view(self, i: int, g: torch.Tensor) -> Optional[torch.Tensor]:
+        """``g`` as a flat tensor in the arena's element order, when its layout matches
+        the arena view's (contiguous, or the same dense channels_last strides)."""
+        st = self.strides[i]
+        if st is None:
+            return g.reshape(-1) if g.is_contiguous() else None
+        if tuple(g.stride()) == st:
+            return g.as_strided((g.numel(),), (1,))
+        return None
 
     def index_of(self, p: torch.Tensor) -> Optional[int]:
         return self._index.get(id(p))
@@ -92,8 +121,8 @@ class ParamArena:
             o, n = self.offsets[i]
             if p.data.data_ptr() != self.data.data_ptr() + o * 4:
                 with torch.no_grad():
-                    self.data[o:o + n].view_as(p).copy_(p.data)
-                p.data = self.data[o:o + n].view_as(p)
+                    self._shaped(self.data, i, p).copy_(p.data)
+                p.data = self._shaped(self.data, i, p)
         self.gather_grads()
 
     def gather_grads(self, indices: Optional[Sequence[int]] = None) -> None:
@@ -109,11 +138,12 @@ class ParamArena:
                 if g is None:
                     self.rebind_grad(i)
                 continue
-            if g.dtype != torch.float32 or not g.is_contiguous() or g.device != self.device:
+            flat = self._flat_like_view(i, g) if g.dtype == torch.float32 and g.device == self.device else None
+            if flat is None:
                 self.rebind_grad(i)
                 continue
             o, n = self.offsets[i]
-            pairs.append((g.reshape(-1), self.grad[o:o + n]))
+            pairs.append((flat, self.grad[o:o + n]))
             moved.append(i)
         if not pairs:
             return

@@ -64,13 +64,12 @@ def fuse_optimizer(opt: torch.optim.Optimizer, arena: ParamArena,
         # expose per-param views in torch's state layout
         for p in g["params"]:
             i = arena.index_of(p)
-            o, n = arena.offsets[i]
             if kind == "adam":
                 opt.state[p] = {"step": torch.tensor(0.0),
-                                "exp_avg": gs.m[o - s:o - s + n].view_as(p),
-                                "exp_avg_sq": gs.v[o - s:o - s + n].view_as(p)}
+                                "exp_avg": arena.shaped_slice(gs.m, i, s),
+                                "exp_avg_sq": arena.shaped_slice(gs.v, i, s)}
             elif g.get("momentum", 0) != 0:
-                opt.state[p] = {"momentum_buffer": gs.buf[o - s:o - s + n].view_as(p)}
+                opt.state[p] = {"momentum_buffer": arena.shaped_slice(gs.buf, i, s)}
 
     def step(self, closure=None):
         loss = None
@@ -111,18 +110,18 @@ def fuse_optimizer(opt: torch.optim.Optimizer, arena: ParamArena,
             for p in g["params"]:
                 st = self.state.get(p, {})
                 i = arena.index_of(p)
-                o, n = arena.offsets[i]
-                sl = slice(o - gs.start, o - gs.start + n)
                 if gs.kind == "adam" and "exp_avg" in st:
-                    gs.m[sl].copy_(st["exp_avg"].reshape(-1))
-                    gs.v[sl].copy_(st["exp_avg_sq"].reshape(-1))
+                    m_v = arena.shaped_slice(gs.m, i, gs.start)
+                    v_v = arena.shaped_slice(gs.v, i, gs.start)
+                    m_v.copy_(st["exp_avg"].reshape(p.shape))
+                    v_v.copy_(st["exp_avg_sq"].reshape(p.shape))
                     gs.step = int(float(st.get("step", 0)))
-                    self.state[p] = {"step": torch.tensor(float(gs.step)),
-                                     "exp_avg": gs.m[sl].view_as(p), "exp_avg_sq": gs.v[sl].view_as(p)}
+                    self.state[p] = {"step": torch.tensor(float(gs.step)), "exp_avg": m_v, "exp_avg_sq": v_v}
                 elif gs.kind == "sgd" and "momentum_buffer" in st and st["momentum_buffer"] is not None:
-                    gs.buf[sl].copy_(st["momentum_buffer"].reshape(-1))
+                    b_v = arena.shaped_slice(gs.buf, i, gs.start)
+                    b_v.copy_(st["momentum_buffer"].reshape(p.shape))
                     gs.step = max(gs.step, 1)
-                    self.state[p] = {"momentum_buffer": gs.buf[sl].view_as(p)}
+                    self.state[p] = {"momentum_buffer": b_v}
 
     # keep torch's LR-scheduler bookkeeping happy (it wraps optimizer.step)
     step._wrapped_by_lr_sched = True

@@ -108,3 +108,39 @@ def test_dp_area_constant_matches_kernel():
     C = pytest.importorskip("ray_lightning_accelerators_amd._C")
     assert fused_mlp.DP_AREA_FLOATS == C.mlp3_dp_area_floats()
     assert fused_mlp.mlp3_dp_capacity(128, 256) >= 2 * fused_mlp.mlp_param_count(128, 256)
+
+
+def test_arena_keeps_channels_last_layout_and_state():
+    """Channels_last conv weights stay channels_last as arena views (NHWC convs must
+    not re-layout them every use); SGD-momentum through the arena matches torch's,
+    and the momentum buffers round-trip through state_dict in the parameter layout."""
+    from torch import nn
+
+    from ray_lightning_accelerators_amd.parallel.arena import ParamArena
+    from ray_lightning_accelerators_amd.parallel.fused_optim import fuse_optimizer
+
+    torch.manual_seed(0)
+    m = nn.Sequential(nn.Conv2d(8, 16, 3, padding=1), nn.Conv2d(16, 8, 1)).to(memory_format=torch.channels_last)
+    ref = nn.Sequential(nn.Conv2d(8, 16, 3, padding=1), nn.Conv2d(16, 8, 1))
+    ref.load_state_dict(m.state_dict())
+    arena = ParamArena(m)
+    assert m[0].weight.is_contiguous(memory_format=torch.channels_last)
+    assert m[0].weight.grad.stride() == m[0].weight.stride()
+    opt = fuse_optimizer(torch.optim.SGD(m.parameters(), lr=0.01, momentum=0.9), arena)
+    ro = torch.optim.SGD(ref.parameters(), lr=0.01, momentum=0.9)
+    x = torch.randn(2, 8, 5, 5)
+    for _ in range(3):
+        m(x.contiguous(memory_format=torch.channels_last)).square().mean().backward()
+        opt.step()
+        opt.zero_grad()
+        ref(x).square().mean().backward()
+        ro.step()
+        ro.zero_grad()
+    for p, q in zip(m.parameters(), ref.parameters()):
+        assert torch.allclose(p, q, atol=1e-5)
+    sd, rsd = opt.state_dict(), ro.state_dict()
+    for k in sd["state"]:
+        assert torch.allclose(sd["state"][k]["momentum_buffer"], rsd["state"][k]["momentum_buffer"], atol=1e-5)
+    opt.load_state_dict(rsd)
+    for k, p in enumerate(m.parameters()):
+        assert torch.allclose(opt.state[p]["momentum_buffer"], rsd["state"][k]["momentum_buffer"], atol=1e-6)

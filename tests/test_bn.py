@@ -315,3 +315,32 @@ def test_maxpool_nhwc_matches_torch(shape, k, s, p):
     # windows sharing an argmax pixel add in fp32 and round once: <= 1 bf16 ulp apart
     assert torch.allclose(xa.grad.float(), xb.grad.float(), rtol=1e-2, atol=1e-2)
     assert (xa.grad != 0).sum() == (xb.grad != 0).sum()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["gemm", "miopen", "auto"])
+def test_conv1x1_backends_match_fp32(mode, monkeypatch):
+    """Conv1x1NHWC's GEMM and MIOpen backends: forward, dgrad and the fp32 wgrad
+    against an fp32 reference convolution of the same bf16 inputs."""
+    from ray_lightning_accelerators_amd.ops import conv as convmod
+
+    monkeypatch.setenv("RLA_CONV1X1", mode)
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(4)
+    m = convmod.Conv1x1NHWC(64, 128).to(dev)
+    x = torch.randn(8, 64, 14, 14, device=dev).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_()
+    before = convmod.stats["fast"]
+    y = m(x)
+    assert convmod.stats["fast"] == before + 1
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_()
+    wr = m.weight.detach().to(torch.bfloat16).float().requires_grad_()
+    yr = F.conv2d(xr, wr)
+    yr.backward(dy.float())
+    rel = lambda a, b: float((a.float() - b).abs().max() / b.abs().max())  # noqa: E731
+    assert rel(y, yr) < 1e-2
+    assert rel(x.grad, xr.grad) < 1e-2
+    assert m.weight.grad.dtype == torch.float32 and rel(m.weight.grad, wr.grad) < 1e-2
