@@ -486,6 +486,10 @@ def make_resnet(args, world, rank, dev, x, y, bucket_mb=None):
         from ray_lightning_accelerators_amd.parallel.fused_optim import fuse_optimizer
 
         arena = ParamArena(model)
+        from ray_lightning_accelerators_amd.ops.shadow import wants_shadow
+
+        if wants_shadow(model):
+            arena.enable_bf16_shadow(model)  # bf16 weights written by the fused SGD step
         sync_ = None
         if world > 1:
             from ray_lightning_accelerators_amd.parallel.comm import get_native_comm

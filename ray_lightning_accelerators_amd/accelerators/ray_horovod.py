@@ -259,6 +259,8 @@ class HorovodRayAccelerator(Accelerator):
             if hasattr(sch, "base_lrs"):
                 sch.base_lrs = [lr * hvd.size() for lr in sch.base_lrs]
         hvd.broadcast_parameters(model.state_dict(), root_rank=0)
+        if getattr(self, "arena", None) is not None:
+            self.arena.invalidate_bf16()  # written by a collective, behind the version counters
         for opt in optimizers:
             hvd.broadcast_optimizer_state(opt, root_rank=0)
         named = list(model.named_parameters())

@@ -109,9 +109,15 @@ class Accelerator:
             except ValueError:
                 self.arena = None
         if self.arena is not None and self.fused_optimizer and get_config().fused_optimizer:
+            fused = False
             for opt in optimizers:
                 if can_fuse(opt, self.arena):
                     fuse_optimizer(opt, self.arena, grad_scale_fn=lambda: self.grad_scale)
+                    fused = True
+            from ..ops.shadow import wants_shadow
+
+            if fused and self.arena.device.type == "cuda" and wants_shadow(model):
+                self.arena.enable_bf16_shadow(model)  # the fused step writes bf16 weights too
         return optimizers, schedulers
 
     @property

@@ -26,10 +26,12 @@ from ..lightning import LightningModule
 from ..ops.bn import BatchNormAct2d
 from ..ops.conv import Conv1x1NHWC
 from ..ops.pool import MaxPool2dNHWC
+from ..ops.shadow import ConvBF16
 
 
-def _conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
-    return nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+def _conv3x3(cin: int, cout: int, stride: int = 1, fused: bool = False) -> nn.Conv2d:
+    # fused: reads the arena's bf16 weight shadow under autocast (ops/shadow.py)
+    return (ConvBF16 if fused else nn.Conv2d)(cin, cout, 3, stride, 1, bias=False)
 
 
 def _conv1x1(cin: int, cout: int, stride: int = 1, fused: bool = False) -> nn.Conv2d:
@@ -37,7 +39,7 @@ def _conv1x1(cin: int, cout: int, stride: int = 1, fused: bool = False) -> nn.Co
     # same parameter / state-dict key as nn.Conv2d either way
     if fused and stride == 1:
         return Conv1x1NHWC(cin, cout)
-    return nn.Conv2d(cin, cout, 1, stride, bias=False)
+    return (ConvBF16 if fused else nn.Conv2d)(cin, cout, 1, stride, bias=False)
 
 
 def _bn(c: int, fused: bool, act: Optional[str] = "relu") -> nn.BatchNorm2d:
@@ -56,7 +58,7 @@ class Bottleneck(nn.Module):
         self.fused_bn = fused_bn
         self.conv1 = _conv1x1(cin, width, fused=fused_bn)
         self.bn1 = _bn(width, fused_bn)
-        self.conv2 = _conv3x3(width, width, stride)
+        self.conv2 = _conv3x3(width, width, stride, fused=fused_bn)
         self.bn2 = _bn(width, fused_bn)
         self.conv3 = _conv1x1(width, cout, fused=fused_bn)
         self.bn3 = _bn(cout, fused_bn)  # fused: relu(bn3(x) + identity) in one pass
@@ -81,7 +83,7 @@ class ResNet(nn.Module):
         super().__init__()
         self.inplanes = 64
         self.fused_bn = fused_bn
-        self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.conv1 = (ConvBF16 if fused_bn else nn.Conv2d)(3, 64, 7, 2, 3, bias=False)
         self.bn1 = _bn(64, fused_bn)
         # fused path: NHWC bf16 kernels with a one-byte argmax (ops/pool.py)
         self.maxpool = MaxPool2dNHWC(3, 2, 1) if fused_bn else nn.MaxPool2d(3, 2, 1)

@@ -114,6 +114,7 @@ class GradSynchronizer:
     def broadcast_parameters(self, src: int = 0) -> None:
         if self.world > 1:
             dist.broadcast(self.arena.data, src, group=self.pg)
+            self.arena.invalidate_bf16()
             for b in self.module.buffers():
                 dist.broadcast(b, src, group=self.pg)
 

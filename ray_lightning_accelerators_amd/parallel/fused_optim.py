@@ -95,7 +95,10 @@ def fuse_optimizer(opt: torch.optim.Optimizer, arena: ParamArena,
                 fused_sgd_(p, gr, gs.buf if g.get("momentum", 0) != 0 else None, lr=float(g["lr"]),
                            momentum=g.get("momentum", 0.0), dampening=g.get("dampening", 0.0),
                            weight_decay=g.get("weight_decay", 0.0), nesterov=g.get("nesterov", False),
-                           maximize=g.get("maximize", False), grad_scale=scale, step=gs.step)
+                           maximize=g.get("maximize", False), grad_scale=scale, step=gs.step,
+                           p_bf16=arena.bf16[gs.start:gs.end] if arena.bf16 is not None else None)
+            if gs.kind == "adam" and arena.bf16 is not None:
+                arena.bf16[gs.start:gs.end].copy_(p)  # Adam path: shadow refreshed by one cast
         return loss
 
     def zero_grad(self, set_to_none: bool = True):

@@ -344,3 +344,48 @@ def test_conv1x1_backends_match_fp32(mode, monkeypatch):
     assert rel(y, yr) < 1e-2
     assert rel(x.grad, xr.grad) < 1e-2
     assert m.weight.grad.dtype == torch.float32 and rel(m.weight.grad, wr.grad) < 1e-2
+
+
+@pytest.mark.gpu
+def test_bf16_shadow_weights_track_fp32_master():
+    """Shadow-reading convs (ConvBF16 / Conv1x1NHWC) under autocast: the same loss and
+    gradients as autocast's own casts, the shadow follows every fused SGD step, and an
+    outside write to the fp32 weights (load_state_dict) refreshes it."""
+    from ray_lightning_accelerators_amd.ops import shadow as shmod
+    from ray_lightning_accelerators_amd.ops.conv import Conv1x1NHWC
+    from ray_lightning_accelerators_amd.parallel.arena import ParamArena
+    from ray_lightning_accelerators_amd.parallel.fused_optim import fuse_optimizer
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(2)
+
+    def build(shadowed):
+        c3 = shmod.ConvBF16(16, 32, 3, 1, 1, bias=False) if shadowed else nn.Conv2d(16, 32, 3, 1, 1, bias=False)
+        c1 = Conv1x1NHWC(32, 16) if shadowed else nn.Conv2d(32, 16, 1, bias=False)
+        return nn.Sequential(c3, c1).to(dev).to(memory_format=torch.channels_last)
+
+    a, b = build(True), build(False)
+    b.load_state_dict(a.state_dict())
+    arena = ParamArena(a)
+    opt = fuse_optimizer(torch.optim.SGD(a.parameters(), lr=0.05, momentum=0.9), arena)
+    arena.enable_bf16_shadow(a)
+    ref_opt = torch.optim.SGD(b.parameters(), lr=0.05, momentum=0.9)
+    x = torch.randn(4, 16, 10, 10, device=dev).contiguous(memory_format=torch.channels_last)
+    for it in range(3):
+        before = shmod.stats["shadow"]
+        for m, o in ((a, opt), (b, ref_opt)):
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = m(x).float().square().mean()
+            loss.backward()
+            o.step()
+            o.zero_grad()
+        assert shmod.stats["shadow"] >= before + 1, "shadow path not taken"
+        for p, q in zip(a.parameters(), b.parameters()):
+            assert torch.allclose(p, q, atol=2e-3, rtol=2e-2), (it, (p - q).abs().max())
+            assert torch.equal(arena.bf16_weight(p).float(), p.detach().to(torch.bfloat16).float())
+    # an outside write: the next forward must see the new weights
+    sd = {k: torch.zeros_like(v) for k, v in a.state_dict().items()}
+    a.load_state_dict(sd)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = a(x)
+    assert float(out.float().abs().max()) == 0.0
