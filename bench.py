@@ -104,6 +104,8 @@ def parse(argv=None):
                     help="resnet50: comma list of bucket caps (MiB) measured in one run, e.g. 1,2,4,8,16,25")
     ap.add_argument("--benchmark-algos", type=int, default=1,
                     help="resnet50: torch.backends.cudnn.benchmark (MIOpen find per shape), both impls")
+    ap.add_argument("--resnet-graph", type=int, default=0,
+                    help="resnet50 native, 1 GPU: capture the whole training step in one hipGraph")
     ap.add_argument("--deterministic-conv", type=int, default=0,
                     help="resnet50: torch.backends.cudnn.deterministic (MIOpen solvers without atomics: no "
                          "zero-fill / cast passes around split-K weight-gradient kernels)")
@@ -517,6 +519,34 @@ def make_resnet(args, world, rank, dev, x, y, bucket_mb=None):
                 opt.step()
                 opt.zero_grad()
                 state["loss"] = loss
+
+        if args.resnet_graph and world == 1:
+            # the whole training step (forward, backward, gradient gather, fused SGD)
+            # captured once in a hipGraph and replayed: no per-kernel launch cost for
+            # its ~600 kernels.  Capture happens inside the warm-up (after 3 eager
+            # steps on a side stream: allocator pools, MIOpen solver choice, the 1x1
+            # conv autotune); every replay is one full step on the resident batch.
+            eager = run
+            gstate = {}
+
+            def run(n):
+                if "g" not in gstate:
+                    s_ = torch.cuda.Stream()
+                    s_.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(s_):
+                        k = min(3, n)
+                        eager(k)
+                        n -= k
+                    torch.cuda.current_stream().wait_stream(s_)
+                    arena.prepare_graph_capture()
+                    g_ = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g_):
+                        eager(1)
+                    gstate["g"] = g_
+                for _ in range(n):
+                    gstate["g"].replay()
+
+            info = dict(info, hip_graph=True)
     else:
         m = model
         if world > 1:

@@ -121,7 +121,8 @@ _DT = {torch.float32: 0, torch.bfloat16: 1}
 CHUNK_ELEMS = 16384
 
 
-def build_copy_table(pairs: Sequence[Tuple[torch.Tensor, torch.Tensor]], device=None) -> torch.Tensor:
+def build_copy_table(pairs: Sequence[Tuple[torch.Tensor, torch.Tensor]], device=None,
+                     staging: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Chunk table for :func:`multi_copy`: one row per <=16K-element chunk.
 
     ``pairs`` are (src, dst) tensors of equal numel (fp32 or bf16, contiguous).
@@ -141,9 +142,22 @@ def build_copy_table(pairs: Sequence[Tuple[torch.Tensor, torch.Tensor]], device=
     host = torch.tensor(rows, dtype=torch.int64).reshape(-1, 4)
     if dev.type != "cuda":
         return host
+    if staging is not None:
+        # inside a hipGraph capture (no pinned allocation allowed there): a pinned
+        # buffer reserved beforehand, which the captured copy node re-reads each replay
+        if staging.numel() < host.numel():
+            raise RuntimeError("graph staging buffer too small for the copy table")
+        st = staging[: host.numel()].view(-1, 4)
+        st.copy_(host)
+        return st.to(dev, non_blocking=True)
     # pinned staging + async copy: a pageable H2D copy would block the host until
-    # the stream drains (one such sync per step cost ResNet-50 ~0.5 ms of GPU idle)
-    return host.pin_memory().to(dev, non_blocking=True)
+    # the stream drains (one such sync per step cost ResNet-50 ~0.5 ms of GPU idle).
+    # The staging buffer lives as long as the table: inside a hipGraph capture the
+    # copy becomes a graph node that re-reads it at every replay.
+    pinned = host.pin_memory()
+    table = pinned.to(dev, non_blocking=True)
+    table._rla_pinned = pinned
+    return table
 
 
 def multi_copy(

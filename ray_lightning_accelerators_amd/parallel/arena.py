@@ -70,6 +70,8 @@ class ParamArena:
         self._pver = 0
         self.steal_grads = (dev.type == "cuda") if steal_grads is None else bool(steal_grads)
         self._tables: "OrderedDict[tuple, torch.Tensor]" = OrderedDict()
+        self._graph_tables: List[tuple] = []
+        self._graph_staging: Optional[torch.Tensor] = None
 
     def _shaped(self, flat: torch.Tensor, i: int, like: torch.Tensor, base: int = 0) -> torch.Tensor:
         o, n = self.offsets[i]
@@ -206,8 +208,14 @@ class ParamArena:
             key = tuple(moved) + tuple(s.data_ptr() for s, _ in pairs)
             table = self._tables.get(key)
             if table is None:
-                table = build_copy_table(pairs)
+                capturing = torch.cuda.is_current_stream_capturing()
+                if capturing and self._graph_staging is None:
+                    raise RuntimeError("ParamArena: call prepare_graph_capture() before capturing a step")
+                table = build_copy_table(pairs, staging=self._graph_staging if capturing else None)
                 self._tables[key] = table
+                if capturing:
+                    self._graph_tables.append((table, self._graph_staging))  # replayed: never evicted
+                    self._graph_staging = None
                 if len(self._tables) > 64:  # address sets are stable under the caching allocator
                     self._tables.popitem(last=False)
             multi_copy(pairs, table=table)
@@ -217,6 +225,14 @@ class ParamArena:
                     d.copy_(s)
         for i in moved:
             self.params[i].grad = self.grad_view(i)
+
+    def prepare_graph_capture(self) -> None:
+        """Reserve the pinned staging buffer the next captured step's gradient-gather
+        table is built in (pinned memory cannot be allocated during a capture)."""
+        from ..ops.optim import CHUNK_ELEMS
+
+        rows = sum((n + CHUNK_ELEMS - 1) // CHUNK_ELEMS for _, n in self.offsets)
+        self._graph_staging = torch.empty(rows * 4, dtype=torch.int64).pin_memory()
 
     def zero_grad(self) -> None:
         if self.steal_grads:

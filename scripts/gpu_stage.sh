@@ -44,6 +44,8 @@ for st in "$@"; do
       run tune_warm 300 python scripts/bench_tune.py --trials 8 --warm 8 ;;
     trainerprof)  # host profile of the worker's fit (cProfile, rank 0)
       RLA_PROFILE_EPOCHS="$R/$O/trainer_epochs_prof" run trainer_prof 300 python bench.py --via trainer --trainer-epochs 6 ;;
+    rn50graph)
+      run rn50_graph 600 python bench.py --model resnet50 --steps 30 --warmup 10 --resnet-graph 1 ;;
     rn50ops)
       run rn50_ops 300 python -u scripts/rn50_op_profile.py ;;
     conv1x1)
