@@ -1152,12 +1152,15 @@ __device__ __forceinline__ bool dp_owner_step(const MLP3Args& a, int unit, int o
 }
 
 // One-launch DP: this launch's generation, read with the step state at kernel start
-// (a scalar load -- the kernel boundary's cache invalidation covers it), so no block
+// (the kernel boundary's cache invalidation covers it), so no block
 // waits on a dependent global load and a barrier before its exchange; the end
 // needs no barrier either (every thread holds the same value; timeouts go straight
 // to the host-mapped error word).
 __device__ __forceinline__ uint32_t dp_gen_now(const MLP3Args& a) {
-  return ((const __attribute__((address_space(4))) uint32_t*)(a.dp_gen))[blockIdx.x] + 1u;
+  // a VECTOR load issued with the other tail-role prefetches at kernel start: a
+  // scalar load here shares lgkmcnt with every LDS access of the head pass, whose
+  // first waits then also waited for this (cold) load
+  return a.dp_gen[blockIdx.x] + 1u;
 }
 __device__ __forceinline__ void dp_end_nosync(const MLP3Args& a, uint32_t gen, int fail) {
   if (threadIdx.x == 0) a.dp_gen[blockIdx.x] = gen;

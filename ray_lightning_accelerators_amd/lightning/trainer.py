@@ -220,6 +220,7 @@ class Trainer:
         self._has_val_loop = False
         self._fused = None
         self._pending_log = None
+        self._staged_logs: List[dict] = []  # deferred log rows whose host copy is in flight
         self._log_dir: Optional[str] = None
         self._train_dl_src = self._val_dl_src = self._test_dl_src = None
         self._results: Dict[str, Dict[str, list]] = {}
@@ -599,6 +600,8 @@ class Trainer:
         if self.logger is None or not self.logged_metrics or not self.is_global_zero:
             return
         metrics = dict(self.logged_metrics)
+        if not defer:
+            self._drain_staged_logs(wait=True)  # earlier steps' rows first
         if defer and any(isinstance(v, torch.Tensor) and v.is_cuda for v in metrics.values()):
             # a device-side copy (no host sync): a logged tensor the module later
             # changes in place must still be written with its value at log time
@@ -610,9 +613,58 @@ class Trainer:
             return
         self.logger.log_metrics(metrics, step=self.global_step)
 
+    def _stage_pending_log(self) -> None:
+        """Start the host transfer of the deferred snapshots WITHOUT waiting: one
+        concatenation + one async copy into pinned memory per dtype, an event behind
+        them; the rows are written by :meth:`_drain_staged_logs` once it completed --
+        the validation end no longer holds the next epoch's first dispatch for the
+        logger's file writes (~0.5 ms of GPU idle per epoch, profiles/r3_trainer)."""
+        pending = self._pending_log or []
+        if not pending:
+            return
+        self._pending_log = None
+        dev_vals = [(i, k, v) for i, (snap, _) in enumerate(pending) for k, v in snap.items()
+                    if isinstance(v, torch.Tensor) and v.is_cuda]
+        st = {"pending": pending, "groups": [], "event": None}
+        if dev_vals:
+            groups: Dict[torch.dtype, list] = {}
+            for e in dev_vals:
+                groups.setdefault(e[2].dtype, []).append(e)
+            for dtype, ents in groups.items():
+                flat = torch.cat([v.reshape(-1) for _, _, v in ents])
+                host = torch.empty(flat.shape, dtype=flat.dtype, pin_memory=True)
+                host.copy_(flat, non_blocking=True)
+                st["groups"].append((ents, host))
+            st["event"] = torch.cuda.Event()
+            st["event"].record()
+        self._staged_logs.append(st)
+
+    def _drain_staged_logs(self, wait: bool) -> None:
+        """Write staged rows in step order, as far as their copies completed (``wait``: all)."""
+        while self._staged_logs:
+            st = self._staged_logs[0]
+            ev = st["event"]
+            if ev is not None and not ev.query():
+                if not wait:
+                    return
+                ev.synchronize()
+            pending = st["pending"]
+            for ents, host in st["groups"]:
+                vals = host.double().tolist()
+                off = 0
+                for i, k, v in ents:
+                    n = v.numel()
+                    pending[i][0][k] = vals[off] if n == 1 else host[off: off + n].reshape(v.shape).clone()
+                    off += n
+            for snap, step in pending:
+                self.logger.log_metrics(snap, step=step)
+            self._staged_logs.pop(0)
+
     def _write_pending_log(self, block: bool = True) -> None:
         """Write the deferred snapshots in step order (``block``, or once more than
         1024 are held), their device values fetched by one batched transfer."""
+        if block:
+            self._drain_staged_logs(wait=True)
         pending = self._pending_log or []
         if not pending or (not block and len(pending) <= 1024):
             return
@@ -717,8 +769,13 @@ class Trainer:
         if was_training:
             model.train()
         if not self.running_sanity_check:
-            self._flush_logger()
-        out = [{k: float(v) for k, v in metrics.items()}]
+            if self.on_gpu and self.training and self.logger is not None and self.is_global_zero:
+                # rows go out asynchronously; written while the next chunks run
+                self._flush_logger(defer=True)
+                self._stage_pending_log()
+            else:
+                self._flush_logger()
+        out = [_floats(metrics)]
         mark("eval_done", stage=stage)
         return out
 
@@ -934,6 +991,8 @@ class Trainer:
             self.profiler.stop("run_training_batch")
             if b == 0:
                 mark("first_chunk_dispatched", epoch=self.current_epoch)
+            if self._staged_logs:
+                self._drain_staged_logs(wait=False)  # the previous validation's rows, if copied
             self.global_step += k
             epoch_outputs.extend(outs)
             for cb in self.callbacks:
@@ -1109,6 +1168,17 @@ class Trainer:
         d["_ckpt_writer"] = None
         d["accelerator_backend"] = None
         return d
+
+
+def _floats(metrics: Dict[str, Any]) -> Dict[str, float]:
+    """Metric dict -> Python floats with ONE device->host transfer for the device values."""
+    dev = [(k, v) for k, v in metrics.items() if isinstance(v, torch.Tensor) and v.is_cuda and v.numel() == 1]
+    out = {k: float(v) for k, v in metrics.items() if not (isinstance(v, torch.Tensor) and v.is_cuda
+                                                           and v.numel() == 1)}
+    if dev:
+        vals = torch.stack([v.detach().reshape(()).double() for _, v in dev]).cpu().tolist()
+        out.update({k: x for (k, _), x in zip(dev, vals)})
+    return {k: out[k] for k in metrics}
 
 
 def _to_cpu(obj):
