@@ -76,9 +76,10 @@ class RLAConfig:
     # the next fit on the same GPUs takes them over (runtime actor reuse)
     reuse_workers: bool = True
     # Trainer: fused resident steps issued per host dispatch when nothing observes
-    # single batches (chunks also end at log / validation / max_steps boundaries);
-    # 1 = one dispatch per batch.  Capped by the fused step's stats ring (64).
-    steps_per_dispatch: int = 64
+    # single batches (chunks also end at validation / max_steps boundaries, and at log
+    # points unless the fused step reports them itself); 1 = one dispatch per batch.
+    # Capped by the fused step's stats ring (half of its 4,096 rows).
+    steps_per_dispatch: int = 1024
     # torch.distributed backend of GPU workers: auto = RCCL ("nccl"); "gloo" only
     # for rehearsing N ranks on ONE device (RCCL refuses duplicate GPUs)
     pg_backend: str = "auto"

@@ -164,6 +164,7 @@ class Trainer:
         self.weights_summary = weights_summary
         self.fused_step = fused_step
         self.steps_per_dispatch = steps_per_dispatch  # None: RLAConfig.steps_per_dispatch
+        self._chunks_span_logs = False
         self.profiler = resolve_profiler(profiler)
         self.profiler_summary = ""
         if deterministic:
@@ -971,6 +972,10 @@ class Trainer:
         every = max(1, self.log_every_n_steps)
         bsz = int(getattr(self._fused, "_B", 0))
         validated = False
+        # the fused step reports every log point of a chunk itself (ring views): the
+        # chunk need not end at each one (35 cuts -> 1-2 per MNIST epoch)
+        spans = bool(getattr(self._fused, "chunk_spans_log_points", False)) and self.logger is not None
+        self._chunks_span_logs = spans
         # RLA_CHUNK_TIMING=1 (diagnostic): host time per chunk vs the GPU time
         # between chunk-end events, reported at the epoch end (which syncs anyway)
         timing = [] if os.environ.get("RLA_CHUNK_TIMING") == "1" and torch.cuda.is_available() else None
@@ -982,7 +987,8 @@ class Trainer:
             while True:
                 e += 1
                 gs = self.global_step + (e - b)
-                if (e >= n or e - b >= chunk or gs % every == 0 or self._should_validate(e - 1, False)
+                if (e >= n or e - b >= chunk or (gs % every == 0 and not spans)
+                        or self._should_validate(e - 1, False)
                         or (self.max_steps is not None and gs >= self.max_steps)):
                     break
             k = e - b
@@ -999,7 +1005,20 @@ class Trainer:
                 fn = getattr(cb, "on_train_chunk_end", None)
                 if fn is not None:
                     fn(self, model, outs, k, k * bsz)
-            if self.global_step % every == 0:
+            if spans:
+                rows = getattr(self._fused, "_last_rows", None)
+                if rows is not None and rows.size(0) == k:
+                    final, current = self.global_step, dict(self.logged_metrics)
+                    for st, met in self._fused.log_points(rows, final - k, every):
+                        self.global_step = st  # the row is written under its own step
+                        self.logged_metrics.update(met)
+                        self._flush_logger(defer=True)
+                    self.global_step = final
+                    self.logged_metrics.clear()
+                    self.logged_metrics.update(current)  # the chunk's last step, as before
+                elif self.global_step % every == 0:
+                    self._flush_logger(defer=True)
+            elif self.global_step % every == 0:
                 self._flush_logger(defer=True)
             if timing is not None:
                 ev = torch.cuda.Event(enable_timing=True)

@@ -371,8 +371,29 @@ class FusedMNISTStep:
 
     @property
     def max_chunk(self) -> int:
-        """Most steps one :meth:`train_chunk` can report per-step losses for."""
-        return int(self.stats.size(0))  # the engine's stats ring has this size
+        """Most steps one :meth:`train_chunk` can report per-step losses for: half the
+        engine's stats ring (a chunk's rows stay valid through the next chunk)."""
+        return ENGINE_STATS_RING // 2
+
+    # the Trainer may run a chunk across several log points: log_points() gives each
+    # one's metrics (views of the stats ring) -- no dispatch cut every 50 steps
+    chunk_spans_log_points = True
+
+    def log_points(self, rows: torch.Tensor, first: int, every: int):
+        """``(global step, metrics)`` for every multiple of ``every`` among the steps
+        ``first + 1 .. first + len(rows)`` whose (loss, correct, count) rows are
+        ``rows`` -- ring views, plus ONE division kernel for all their accuracies."""
+        steps = [first + 1 + i for i in range(rows.size(0)) if (first + 1 + i) % every == 0]
+        if not steps:
+            return []
+        acc = rows[:, 1] / rows[:, 2]
+        out = []
+        for st in steps:
+            i = st - first - 1
+            loss, a = rows[i, 0], acc[i]
+            loss._rla_fresh = a._rla_fresh = True
+            out.append((st, {"ptl/train_loss": loss, "ptl/train_accuracy": a}))
+        return out
 
     def _graph_steps(self) -> int:
         """Steps per captured graph: the Trainer cuts dispatches at multiples of
@@ -380,8 +401,18 @@ class FusedMNISTStep:
         (64; 50 for the default 50) makes a typical chunk ONE replay (a graph
         launch costs the host tens of us; the engine's 1/2/4/... remainder
         graphs cover the chunks cut short by validation or the epoch end)."""
+        if getattr(self.trainer, "_chunks_span_logs", False):
+            # dispatch chunks run across log points: bigger graphs, fewer replays --
+            # the largest power of two within the dispatch chunk and the epoch (<= 256)
+            tr = self.trainer
+            spd = tr.steps_per_dispatch if tr.steps_per_dispatch is not None else get_config().steps_per_dispatch
+            cap = min(256, int(spd), int(getattr(tr, "num_training_batches", 256) or 256))
+            g = 1
+            while g * 2 <= cap:
+                g *= 2
+            return max(g, 1)
         every = max(1, int(getattr(self.trainer, "log_every_n_steps", 50) or 50))
-        for g in range(min(self.max_chunk, every), 3, -1):
+        for g in range(min(64, every), 3, -1):
             if every % g == 0:
                 return g
         return 8
@@ -441,6 +472,7 @@ class FusedMNISTStep:
         self.model.log("ptl/train_loss", loss)
         self.model.log("ptl/train_accuracy", acc)
         self.trainer.callback_metrics["loss"] = loss
+        self._last_rows, self._last_first = rows, first + n_steps - k
         return [{"loss": v} for v in rows[:, 0].unbind(0)]
 
     # ---------------------------------------------------------- validation

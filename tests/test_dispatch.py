@@ -161,15 +161,59 @@ def test_fused_mnist_chunked_dispatch_matches_per_batch(tmpdir):
         assert tr._fused is not None and tr._fused.eng is not None
         assert tr.global_step == 260
         if spd > 1:
-            # the chunks (50, 50, 30 steps) run as replays of the 50-step graph and the
-            # 1/2/4/.../32-step remainder graphs
+            # the chunks (64, 64, 2 steps: they run across the log points, which the fused
+            # step reports itself) are replays of the 64-step graph and the 1/2/.../32-step
+            # remainder graphs
             assert tr._fused.eng._graph is not None and not tr._fused._capture_failed
-            assert tr._fused.eng._graph_steps == 50 and sorted(tr._fused.eng._tail_graphs) == [1, 2, 4, 8, 16, 32]
+            assert tr._fused.eng._graph_steps == 64 and sorted(tr._fused.eng._tail_graphs) == [1, 2, 4, 8, 16, 32]
         res[spd] = ({k: v.detach().cpu().clone() for k, v in model.state_dict().items()},
                     float(tr.callback_metrics["ptl/train_loss"]))
     for k, v in res[1][0].items():
         assert torch.equal(v, res[64][0][k]), k
     assert res[1][1] == res[64][1]
+
+
+class _SpanFused(_FakeFused):
+    """A fused step that reports its chunks' log points itself (like FusedMNISTStep)."""
+
+    max_chunk = 2048
+    chunk_spans_log_points = True
+
+    def train_chunk(self, k):
+        self.chunks.append((self.trainer.global_step, k))
+        self._last_rows = torch.arange(k, dtype=torch.float32).unsqueeze(1).repeat(1, 4) + \
+            float(self.trainer.global_step)
+        self._last_rows[:, 2] = 1.0
+        return [{"loss": torch.tensor(1.0)} for _ in range(k)]
+
+    def log_points(self, rows, first, every):
+        return [(first + 1 + i, {"ptl/train_loss": rows[i, 0], "ptl/train_accuracy": rows[i, 1] / rows[i, 2]})
+                for i in range(rows.size(0)) if (first + 1 + i) % every == 0]
+
+
+def test_chunks_span_log_points_when_the_fused_step_reports_them(tmpdir):
+    """Chunks run across log points; every log point still reaches the logger under
+    its own global step, with that step's values."""
+    class M(_Model):
+        def configure_fused_step(self, trainer):
+            self.fake = _SpanFused(trainer)
+            return self.fake
+
+    model = M()
+    tr = pl.Trainer(default_root_dir=str(tmpdir), max_epochs=1, val_check_interval=1.0, log_every_n_steps=7,
+                    num_sanity_val_steps=0, checkpoint_callback=False, progress_bar_refresh_rate=0,
+                    steps_per_dispatch=1024)
+    rows = []
+    orig = tr.logger.log_metrics
+    tr.logger.log_metrics = lambda metrics, step=None: (rows.append((step, dict(metrics))), orig(metrics, step))
+    assert tr.fit(model) == 1
+    assert model.fake.chunks == [(0, 160)]  # one dispatch for the epoch
+    logged = [(st, m["ptl/train_loss"]) for st, m in rows if "ptl/train_loss" in m]
+    # every log point (the validation-end flush writes the chunk's own last-step logs,
+    # which this fake step does not make)
+    assert [st for st, _ in logged] == list(range(7, 161, 7))
+    for st, v in logged:
+        assert float(v) == float(st - 1)  # row i of the chunk starting at step 0 holds i
 
 
 @pytest.mark.parametrize("shuffle", [True, False])
