@@ -530,6 +530,45 @@ void bn_bwd_apply(Tensor x, optional<Tensor> y, Tensor dy, Tensor coef, bool rel
                            ssp);
 }
 
+// dW of an NHWC bf16 convolution (csrc/conv_wgrad.hip): dy [N, OH, OW, Cout] and
+// x [N, H, W, Cin] as contiguous NHWC memory; returns fp32 [Cout, KH, KW, Cin]
+// (the channels_last weight's memory order).
+Tensor conv_wgrad(Tensor dy, Tensor x, int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t OH, int64_t OW,
+                  int64_t Cout, int64_t KH, int64_t KW, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+                  int64_t splits) {
+  TORCH_CHECK(dy.is_cuda() && x.is_cuda(), "conv_wgrad: GPU tensors");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "conv_wgrad: bf16 inputs");
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous(), "conv_wgrad: contiguous NHWC memory");
+  TORCH_CHECK(Cout % 64 == 0 && Cin % 64 == 0 && Cout > 0 && Cin > 0, "conv_wgrad: channels must be multiples of 64");
+  TORCH_CHECK(N > 0 && H > 0 && W > 0 && OH > 0 && OW > 0 && KH > 0 && KW > 0 && sh > 0 && sw > 0 && ph >= 0 &&
+                  pw >= 0, "conv_wgrad: bad geometry");
+  TORCH_CHECK((H + 2 * ph - KH) / sh + 1 == OH && (W + 2 * pw - KW) / sw + 1 == OW, "conv_wgrad: output size mismatch");
+  TORCH_CHECK(dy.numel() == N * OH * OW * Cout, "conv_wgrad: dy has ", dy.numel(), " elements");
+  TORCH_CHECK(x.numel() == N * H * W * Cin, "conv_wgrad: x has ", x.numel(), " elements");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "conv_wgrad: 16-byte aligned inputs");
+  TORCH_CHECK(N * std::max(OH * OW, H * W) < (int64_t(1) << 31) / 4, "conv_wgrad: too many rows");
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  rla::WgradGeom g{(int)N, (int)H, (int)W, (int)Cin, (int)OH, (int)OW, (int)Cout, (int)KH, (int)KW,
+                   (int)sh, (int)sw, (int)ph, (int)pw};
+  const rla::WgradPlan plan = rla::wgrad_plan(g, (int)splits);
+  Tensor out = at::empty({Cout, KH, KW, Cin}, x.options().dtype(at::kFloat));
+  Tensor part;
+  if (plan.splits > 1) part = at::empty({(int64_t)plan.splits * Cout * KH * KW * Cin}, out.options());
+  rla::launch_wgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                    out.data_ptr<float>(), plan.splits > 1 ? part.data_ptr<float>() : nullptr, g, plan, cur_stream(x));
+  return out;
+}
+
+std::vector<int64_t> conv_wgrad_plan(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t OH, int64_t OW,
+                                     int64_t Cout, int64_t KH, int64_t KW, int64_t sh, int64_t sw, int64_t ph,
+                                     int64_t pw, int64_t splits) {
+  rla::WgradGeom g{(int)N, (int)H, (int)W, (int)Cin, (int)OH, (int)OW, (int)Cout, (int)KH, (int)KW,
+                   (int)sh, (int)sw, (int)ph, (int)pw};
+  const rla::WgradPlan p = rla::wgrad_plan(g, (int)splits);
+  return {p.wa, p.wb, p.splits, p.rows_per_split};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -567,5 +606,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd_apply", &bn_bwd_apply, "fused BN backward apply: dx (+ dres = relu-masked dy)", py::arg("x"),
         py::arg("y"), py::arg("dy"), py::arg("coef"), py::arg("relu"), py::arg("dx"), py::arg("dres"),
         py::arg("dy2") = py::none(), py::arg("ss") = py::none());
+  m.def("conv_wgrad", &conv_wgrad, "NHWC bf16 conv weight gradient on MFMA -> fp32 [Cout, KH, KW, Cin]",
+        py::arg("dy"), py::arg("x"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("OH"),
+        py::arg("OW"), py::arg("Cout"), py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"), py::arg("ph"),
+        py::arg("pw"), py::arg("splits") = 0);
+  m.def("conv_wgrad_plan", &conv_wgrad_plan, "the wgrad kernel's (wa, wb, splits, rows_per_split)");
   m.attr("ARCH") = "gfx950";
 }

@@ -1,0 +1,311 @@
+// Weight gradient of NHWC bf16 convolutions on the MFMA units (gfx950).
+//
+//   dW[co][r][s][ci] = sum over m = (n, oh, ow) of dy[m][co] * x[n][oh*sh - ph + r][ow*sw - pw + s][ci]
+//
+// i.e. for every filter tap (r, s) a GEMM  dy^T . x_shifted  whose reduction
+// dimension is the huge N*OH*OW row index and whose output is the small
+// [Cout, Cin] weight slice.  Why a kernel of our own (profiles/r3_rn50):
+// MIOpen's NHWC wrw solvers cost ~80 us per ResNet-50 1x1 layer whatever its
+// size (an fp32 workspace zero-fill, split-K atomics, a bf16 -> fp32 cast kernel;
+// 2-6x the HBM floor of reading dy and x once), and hipBLASLt's dy^T . x with
+// K = N*H*W = 401,408 runs at ~650 us.  The work is HBM-bound (arithmetic
+// intensity Cout*Cin/(Cout+Cin) <= 128 flop/B against ~300 at the MFMA/HBM
+// ridge), so the design goal is one read of dy and x at full bandwidth:
+//
+//   * grid = (output tiles x taps, S row splits); a workgroup (4 waves) owns a
+//     [TCO x TCI] output tile (4 wave tiles of 64x64, or fewer wave tiles with
+//     the reduction split across the waves) over a contiguous range of rows;
+//   * rows stream through LDS in stages of KB rows: every thread loads 16-byte
+//     row chunks of dy / x (coalesced: the row-major NHWC rows ARE the GEMM's k
+//     axis), one stage ahead in registers, and writes them to a double-buffered
+//     LDS image [row][channel] padded by 64 B per row;
+//   * both MFMA operands are k-strided in that image (k = row), so they are read
+//     with ds_read_b64_tr_b16 (hardware transpose: lane i of a 16-lane group gets
+//     channel i of 4 consecutive rows); two reads form one 8-row fragment of
+//     v_mfma_f32_32x32x16_bf16.  The 64-B pad puts the 4 rows of a 32-lane half
+//     on disjoint 16-bank windows (conflict-free);
+//   * S > 1: fp32 partial tiles [S][Cout][taps][Cin], summed in split order by a
+//     small reduce kernel (deterministic; no atomics, no zero-fill).
+//
+// Output layout [Cout][KH][KW][Cin] = the channels_last weight's memory order,
+// so the fp32 result IS the master gradient (no cast, no re-layout).
+// Requires Cout % 64 == 0, Cin % 64 == 0 and 16-byte aligned bases (checked by
+// the binding).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace rla {
+namespace {
+
+typedef __attribute__((address_space(3))) bf16x4 lds_b4;
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWgThreads = 256;
+constexpr int kWgPad = 32;  // bf16 elements (64 B) of padding per LDS row
+
+__device__ __forceinline__ bf16x4 tr4(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4*)(p));
+}
+
+__device__ __forceinline__ bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// source row of x for output row m and tap (r, s); -1 = zero padding
+template <bool GEN>
+__device__ __forceinline__ int64_t x_row(int64_t m, const WgradGeom& g, int r, int s) {
+  if (!GEN) return m;
+  // 32-bit index math (the binding bounds every row count below 2^29)
+  const int mi = (int)m, ohw = g.OH * g.OW;
+  const int n = mi / ohw;
+  const int rem = mi - n * ohw;
+  const int oh = rem / g.OW, ow = rem - oh * g.OW;
+  const int ih = oh * g.sh - g.ph + r, iw = ow * g.sw - g.pw + s;
+  if (ih < 0 || ih >= g.H || iw < 0 || iw >= g.W) return -1;
+  return (int64_t)((n * g.H + ih) * g.W + iw);
+}
+
+template <int WA, int WB, bool GEN>
+__global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t* __restrict__ dy,
+                                                           const uint16_t* __restrict__ x, float* __restrict__ out,
+                                                           WgradGeom g, int64_t M, int64_t rows_per_split,
+                                                           int tiles_co, int tiles_ci) {
+  constexpr int NWT = WA * WB;          // wave tiles per workgroup tile
+  constexpr int KS = 4 / NWT;           // waves sharing one wave tile (reduction split)
+  constexpr int KB = KS == 4 ? 64 : 32;  // rows per stage: every wave gets >= 1 k-step of 16
+  constexpr int TCO = 64 * WA, TCI = 64 * WB;
+  constexpr int SA = TCO + kWgPad, SB = TCI + kWgPad;
+  constexpr int NA = KB * TCO / 8 / kWgThreads, NB = KB * TCI / 8 / kWgThreads;
+  constexpr int STAGE = KB * (SA + SB);  // bf16 elements per LDS buffer
+  constexpr int KSTEPS = KB / 16 / KS;   // k-steps of 16 rows per wave per stage
+  static_assert(NA >= 1 && NB >= 1 && KSTEPS >= 1, "tile / stage shape");
+  static_assert(2 * STAGE * 2 >= (KS - 1) * NWT * 4 * 16 * 64 * 4, "LDS reuse for the reduction");
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int taps = g.KH * g.KW;
+  int b = blockIdx.x;
+  const int tci = b % tiles_ci;
+  b /= tiles_ci;
+  const int tco = b % tiles_co;
+  const int tap = b / tiles_co;
+  const int r = tap / g.KW, s = tap - (tap / g.KW) * g.KW;
+  const int co0 = tco * TCO, ci0 = tci * TCI;
+  const int64_t mb = (int64_t)blockIdx.y * rows_per_split;
+  const int64_t me = mb + rows_per_split < M ? mb + rows_per_split : M;
+  const int nst = (int)((me - mb + KB - 1) / KB);
+
+  // this thread's 16-byte chunks of a stage: dy rows (TCO channels) and x rows (TCI)
+  u32x4 ra[NA], rb[NB];
+  auto load = [&](int64_t m0) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int c = tid + i * kWgThreads, row = c / (TCO / 8), col = (c % (TCO / 8)) * 8;
+      const int64_t m = m0 + row;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (m < me) v = *reinterpret_cast<const u32x4*>(dy + m * g.Cout + co0 + col);
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int c = tid + i * kWgThreads, row = c / (TCI / 8), col = (c % (TCI / 8)) * 8;
+      const int64_t m = m0 + row;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (m < me) {
+        const int64_t xr = x_row<GEN>(m, g, r, s);
+        if (xr >= 0) v = *reinterpret_cast<const u32x4*>(x + xr * g.Cin + ci0 + col);
+      }
+      rb[i] = v;
+    }
+  };
+  auto store = [&](int buf) {
+    __bf16* A = lds + buf * STAGE;
+    __bf16* B = A + KB * SA;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int c = tid + i * kWgThreads, row = c / (TCO / 8), col = (c % (TCO / 8)) * 8;
+      *reinterpret_cast<u32x4*>(A + row * SA + col) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int c = tid + i * kWgThreads, row = c / (TCI / 8), col = (c % (TCI / 8)) * 8;
+      *reinterpret_cast<u32x4*>(B + row * SB + col) = rb[i];
+    }
+  };
+
+  // wave tile and reduction share of this wave
+  const int wt = wave % NWT, ks = wave / NWT;
+  const int wco = (wt / WB) * 64, wci = (wt % WB) * 64;
+  // transposed-read lane roles: group gq of 16 lanes; lane 4q+p addresses row q, channels 4p..4p+3
+  const int gq = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int cho = 16 * (gq & 1) + 4 * p;  // channel offset inside a 32-channel block
+  const int rwo = 8 * (gq >> 1) + q;      // row offset inside a 16-row k-step
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc[i][j][k] = 0.f;
+
+  if (nst > 0) {
+    load(mb);
+    store(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < nst; ++it) {
+    const bool more = it + 1 < nst;
+    if (more) load(mb + (int64_t)(it + 1) * KB);  // in flight under this stage's MFMAs
+    const __bf16* A = lds + (it & 1) * STAGE;
+    const __bf16* B = A + KB * SA;
+#pragma unroll
+    for (int kk = 0; kk < KSTEPS; ++kk) {
+      const int rw = (kk * KS + ks) * 16 + rwo;
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const __bf16* pa = A + rw * SA + wco + 32 * i + cho;
+        fa[i] = cat8(tr4(pa), tr4(pa + 4 * SA));
+        const __bf16* pb = B + rw * SB + wci + 32 * i + cho;
+        fb[i] = cat8(tr4(pb), tr4(pb + 4 * SB));
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) store((it + 1) & 1);  // the other buffer: last read before the previous barrier
+    __syncthreads();
+  }
+
+  // reduction split: waves ks > 0 hand their tiles to ks == 0 through LDS (fixed order)
+  if constexpr (KS > 1) {
+    float* red = reinterpret_cast<float*>(lds);  // every wave passed the loop's last barrier
+    if (ks > 0) {
+      float* d = red + ((ks - 1) * NWT + wt) * 4 * 16 * 64;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int k = 0; k < 16; ++k) d[((i * 2 + j) * 16 + k) * 64 + lane] = acc[i][j][k];
+    }
+    __syncthreads();
+    if (ks > 0) return;
+#pragma unroll
+    for (int o = 1; o < KS; ++o) {
+      const float* d = red + ((o - 1) * NWT + wt) * 4 * 16 * 64;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int k = 0; k < 16; ++k) acc[i][j][k] += d[((i * 2 + j) * 16 + k) * 64 + lane];
+    }
+  }
+
+  // D of 32x32x16: column = lane & 31 (ci), row = (k & 3) + 8 (k >> 2) + 4 (lane >> 5) (co)
+  float* o = out + (int64_t)blockIdx.y * ((int64_t)g.Cout * taps * g.Cin);
+  const int64_t rs = (int64_t)taps * g.Cin;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ci = ci0 + wci + 32 * j + (lane & 31);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int co = co0 + wco + 32 * i + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
+        o[co * rs + (int64_t)tap * g.Cin + ci] = acc[i][j][k];
+      }
+    }
+}
+
+// out[i] = sum over splits of part[s][i], in split order (float4 per thread)
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                           int64_t n, int S) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= n) return;
+  float4 acc = *reinterpret_cast<const float4*>(part + i);
+  for (int k = 1; k < S; ++k) {
+    const float4 v = *reinterpret_cast<const float4*>(part + (int64_t)k * n + i);
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  *reinterpret_cast<float4*>(out + i) = acc;
+}
+
+template <int WA, int WB>
+void launch_tile(const uint16_t* dy, const uint16_t* x, float* out, const WgradGeom& g, int64_t M, int64_t rps,
+                 int S, bool gen, hipStream_t st) {
+  const int tco = g.Cout / (64 * WA), tci = g.Cin / (64 * WB);
+  const dim3 grid(tco * tci * g.KH * g.KW, S), block(kWgThreads);
+  if (gen)
+    hipLaunchKernelGGL((wgrad_kernel<WA, WB, true>), grid, block, 0, st, dy, x, out, g, M, rps, tco, tci);
+  else
+    hipLaunchKernelGGL((wgrad_kernel<WA, WB, false>), grid, block, 0, st, dy, x, out, g, M, rps, tco, tci);
+}
+
+}  // namespace
+
+WgradPlan wgrad_plan(const WgradGeom& g, int splits) {
+  WgradPlan p{};
+  // workgroup tile (in 64-channel wave tiles): 4 wave tiles when the weight is
+  // big enough, with the larger side along the larger channel count
+  if (g.Cout % 128 == 0 && g.Cin % 128 == 0) { p.wa = 2; p.wb = 2; }
+  else if (g.Cout % 256 == 0) { p.wa = 4; p.wb = 1; }
+  else if (g.Cin % 256 == 0) { p.wa = 1; p.wb = 4; }
+  else if (g.Cout % 128 == 0) { p.wa = 2; p.wb = 1; }
+  else if (g.Cin % 128 == 0) { p.wa = 1; p.wb = 2; }
+  else { p.wa = 1; p.wb = 1; }
+  const int64_t M = (int64_t)g.N * g.OH * g.OW;
+  const int kb = p.wa * p.wb == 1 ? 64 : 32;
+  const int64_t tiles = (int64_t)(g.Cout / (64 * p.wa)) * (g.Cin / (64 * p.wb)) * g.KH * g.KW;
+  int64_t S = splits;
+  if (S <= 0) {
+    // ~1024 workgroups (4 per CU) ...
+    S = (1024 + tiles - 1) / tiles;
+    // ... but >= 8 stages per split, and the fp32 partials (written + re-read by the
+    // reduce) at most ~1/8 of the bytes of dy and x
+    const int64_t max_rows = (M + 8 * kb - 1) / (8 * kb);
+    if (S > max_rows) S = max_rows;
+    const double in_bytes = 2.0 * (double)M * (g.Cout + (double)g.Cin * g.KH * g.KW);
+    const double part_bytes = 8.0 * (double)g.Cout * g.Cin * g.KH * g.KW;  // write + read per split
+    const int64_t max_part = (int64_t)(in_bytes / 8.0 / part_bytes);
+    if (S > max_part) S = max_part;
+  }
+  if (S < 1) S = 1;
+  int64_t rps = (M + S - 1) / S;
+  rps = (rps + kb - 1) / kb * kb;
+  p.rows_per_split = rps;
+  p.splits = (int)((M + rps - 1) / rps);
+  if (p.splits < 1) p.splits = 1;
+  return p;
+}
+
+void launch_wgrad(const uint16_t* dy, const uint16_t* x, float* out, float* part, const WgradGeom& g,
+                  const WgradPlan& p, hipStream_t st) {
+  const int64_t M = (int64_t)g.N * g.OH * g.OW;
+  const bool gen = !(g.KH == 1 && g.KW == 1 && g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0 && g.H == g.OH &&
+                     g.W == g.OW);
+  float* dst = p.splits > 1 ? part : out;
+  const int key = p.wa * 10 + p.wb;
+  switch (key) {
+    case 22: launch_tile<2, 2>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st); break;
+    case 41: launch_tile<4, 1>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st); break;
+    case 14: launch_tile<1, 4>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st); break;
+    case 21: launch_tile<2, 1>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st); break;
+    case 12: launch_tile<1, 2>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st); break;
+    default: launch_tile<1, 1>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st); break;
+  }
+  if (p.splits > 1) {
+    const int64_t n = (int64_t)g.Cout * g.KH * g.KW * g.Cin;
+    const int64_t blocks = (n / 4 + 255) / 256;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, part, out, n, p.splits);
+  }
+}
+
+}  // namespace rla

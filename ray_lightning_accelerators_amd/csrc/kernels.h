@@ -217,3 +217,25 @@ bool mlp_supported(int L1, int L2);
 int launch_mlp_adam(const MLPAdamArgs& a, hipStream_t stream);
 
 }  // namespace rla
+
+namespace rla {
+// ---------------------------------------------------------------------------
+// Weight gradient of NHWC bf16 convolutions on MFMA (csrc/conv_wgrad.hip):
+// dW [Cout][KH][KW][Cin] fp32 = sum over output rows of dy x shifted x.
+// Cout % 64 == 0, Cin % 64 == 0.
+// ---------------------------------------------------------------------------
+struct WgradGeom {
+  int N, H, W, Cin;   // x  [N, H, W, Cin]
+  int OH, OW, Cout;   // dy [N, OH, OW, Cout]
+  int KH, KW, sh, sw, ph, pw;
+};
+struct WgradPlan {
+  int wa, wb;              // workgroup tile = (64 wa) x (64 wb) channels
+  int splits;              // row splits (> 1: fp32 partials + a reduce kernel)
+  int64_t rows_per_split;
+};
+WgradPlan wgrad_plan(const WgradGeom& g, int splits);  // splits <= 0: automatic
+// part: splits * Cout * KH * KW * Cin floats when plan.splits > 1 (else unused)
+void launch_wgrad(const uint16_t* dy, const uint16_t* x, float* out, float* part, const WgradGeom& g,
+                  const WgradPlan& p, hipStream_t stream);
+}  // namespace rla

@@ -40,6 +40,11 @@ def _mode() -> str:
     return os.environ.get("RLA_CONV1X1", "auto")
 
 
+def _wmode() -> str:
+    """``RLA_CONV_WGRAD``: backend of the weight gradients (auto: timed per shape)."""
+    return os.environ.get("RLA_CONV_WGRAD", "auto")
+
+
 def _time(fn, reps: int = 3) -> float:
     """Device time of ``reps`` calls.  The device is held by a spin kernel while the
     host enqueues them, so the calls run back to back: a backend's host-side cost
@@ -56,9 +61,13 @@ def _time(fn, reps: int = 3) -> float:
     return s.elapsed_time(e)
 
 
-def _pick(op: str, key: Tuple[int, int, int], cands) -> str:
+def _pick(op: str, key: Tuple[int, ...], cands) -> str:
     mode = _mode()
-    if mode in ("miopen", "gemm"):
+    if op.startswith("wgrad"):
+        # RLA_CONV_WGRAD picks the weight-gradient backend; RLA_CONV1X1=miopen|gemm
+        # still pins the 1x1 layers' wgrad when it is left on auto
+        mode = _wmode() if _wmode() != "auto" or op != "wgrad" else mode
+    if mode in cands:
         return mode
     k = (op,) + key
     c = _choice.get(k)
@@ -75,6 +84,26 @@ def _pick(op: str, key: Tuple[int, int, int], cands) -> str:
 def choices() -> Dict[str, Dict[str, float]]:
     """The autotuned backends so far: ``"op M Cin Cout" -> {backend: us, ..., "pick": name}``."""
     return {" ".join(map(str, k)): dict(_timings.get(k, {}), pick=c) for k, c in _choice.items()}
+
+
+def wgrad_ok(cin: int, cout: int) -> bool:
+    """Shapes the MFMA weight-gradient kernel covers (csrc/conv_wgrad.hip)."""
+    return cin % 64 == 0 and cout % 64 == 0 and os.environ.get("RLA_CONV_WGRAD", "auto") != "off"
+
+
+def wgrad_hip(dy: torch.Tensor, x: torch.Tensor, kernel_size, stride, padding, splits: int = 0) -> torch.Tensor:
+    """Weight gradient of an NHWC bf16 convolution on the MFMA kernel: ``dy`` [N, Cout,
+    OH, OW] and ``x`` [N, Cin, H, W], both channels_last bf16; returns the fp32
+    gradient [Cout, Cin, KH, KW] with channels_last strides (the kernel writes the
+    [Cout, KH, KW, Cin] memory order directly)."""
+    from . import require
+
+    n, cin, h, w = x.shape
+    cout, oh, ow = dy.size(1), dy.size(2), dy.size(3)
+    kh, kw = kernel_size
+    out = require().conv_wgrad(dy.permute(0, 2, 3, 1), x.permute(0, 2, 3, 1), n, h, w, cin, oh, ow, cout, kh, kw,
+                               stride[0], stride[1], padding[0], padding[1], splits)
+    return out.permute(0, 3, 1, 2)
 
 
 def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
@@ -127,12 +156,17 @@ class _Conv1x1Fn(torch.autograd.Function):
             else:
                 dx = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, False, False])[0]
         if ctx.needs_input_grad[1]:
-            be = _pick("wgrad", ctx.key, {
+            cands = {
                 "gemm": lambda: torch.ops.aten.mm.dtype(dy2.t(), x2, torch.float32),
                 "miopen": lambda: _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
                                             [False, True, False])[1].float(),
-            })
-            if be == "gemm":
+            }
+            if wgrad_ok(cin, cout):
+                cands["hip"] = lambda: wgrad_hip(dy, x, (1, 1), (1, 1), (0, 0))
+            be = _pick("wgrad", ctx.key, cands)
+            if be == "hip":
+                dw = wgrad_hip(dy, x, (1, 1), (1, 1), (0, 0))
+            elif be == "gemm":
                 dw = torch.ops.aten.mm.dtype(dy2.t(), x2, torch.float32).view(cout, cin, 1, 1)
             else:
                 dw = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
@@ -166,3 +200,55 @@ class Conv1x1NHWC(nn.Conv2d):
             return _Conv1x1Fn.apply(x, self.weight, bf16_weight(self.weight))
         stats["fallback"] += 1
         return F.conv2d(x, self.weight)
+
+
+class _ConvNHWCFn(torch.autograd.Function):
+    """KxK (or strided) bf16 NHWC convolution: MIOpen forward and dgrad, the weight
+    gradient from MIOpen or the MFMA kernel (``wgrad_hip``), picked per shape on
+    device time.  The weight gradient reaches the fp32 master weight in fp32."""
+
+    @staticmethod
+    def forward(ctx, x, weight, wb, stride, padding):
+        y = _conv(x, wb, None, list(stride), list(padding), [1, 1], False, [0, 0], 1)
+        ctx.save_for_backward(x, wb)
+        ctx.geo = (tuple(stride), tuple(padding))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wb = ctx.saved_tensors
+        stride, padding = ctx.geo
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = _conv_bwd(dy, x, wb, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
+                           [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            cout, cin, kh, kw = wb.shape
+            key = (x.size(0) * dy.size(2) * dy.size(3), cin, cout, kh, kw, stride[0], padding[0])
+            be = _pick("wgrad_kxk", key, {
+                "miopen": lambda: _conv_bwd(dy, x, wb, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
+                                            [False, True, False])[1].float(),
+                "hip": lambda: wgrad_hip(dy, x, (kh, kw), stride, padding),
+            })
+            if be == "hip":
+                dw = wgrad_hip(dy, x, (kh, kw), stride, padding)
+            else:
+                dw = _conv_bwd(dy, x, wb, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
+                               [False, True, False])[1].float()
+        return dx, dw, None, None, None
+
+
+def kxk_fast_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    return (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and x.numel() > 0
+            and x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
+            and conv.padding_mode == "zeros" and isinstance(conv.padding, tuple)
+            and wgrad_ok(conv.in_channels, conv.out_channels))
+
+
+def conv_nhwc(x: torch.Tensor, conv: nn.Conv2d, wb: torch.Tensor) -> torch.Tensor:
+    """``conv(x)`` with the bf16 weight ``wb`` (the arena shadow), the weight gradient
+    going to ``conv.weight`` in fp32."""
+    stats["fast"] += 1
+    return _ConvNHWCFn.apply(x, conv.weight, wb, conv.stride, conv.padding)

@@ -70,6 +70,16 @@ class ConvBF16(nn.Conv2d):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if x.is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16 \
                 and self.padding_mode == "zeros":
+            wb = bf16_weight(self.weight)
+            if wb is not None and torch.is_grad_enabled() and self.weight.requires_grad:
+                from .conv import conv_nhwc, kxk_fast_ok
+
+                xb = x.to(torch.bfloat16)
+                if kxk_fast_ok(xb, self):
+                    # MIOpen forward / dgrad, weight gradient from the MFMA kernel when
+                    # it is the faster one (ops/conv.py)
+                    stats["shadow"] += 1
+                    return conv_nhwc(xb, self, wb)
             w = bf16_param(self.weight)
             if w is not None:
                 b = self.bias.to(torch.bfloat16) if self.bias is not None else None
