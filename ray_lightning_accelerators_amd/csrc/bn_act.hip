@@ -173,15 +173,17 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restri
     const int64_t rs = 2 * (int64_t)C;
     const float* q = part + c;
     int p = sl;
-    for (; p + 3 * kFinSlices < nparts; p += 4 * kFinSlices) {
-      float v[8];
+    // 8 partial rows in flight per thread: the small-C layers' finalize runs on one
+    // or two blocks and is latency-bound on these loads
+    for (; p + 7 * kFinSlices < nparts; p += 8 * kFinSlices) {
+      float v[16];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         v[2 * u] = q[(p + u * kFinSlices) * rs];
         v[2 * u + 1] = q[(p + u * kFinSlices) * rs + C];
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         a += v[2 * u];
         b += v[2 * u + 1];
       }

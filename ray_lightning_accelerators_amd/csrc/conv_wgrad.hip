@@ -12,7 +12,8 @@
 // intensity Cout*Cin/(Cout+Cin) <= 128 flop/B against ~300 at the MFMA/HBM
 // ridge), so the design goal is one read of dy and x at full bandwidth:
 //
-//   * grid = (output tiles x taps, S row splits); a workgroup (4 waves) owns a
+//   * grid = output tiles x taps x S row splits, in an XCD-aware order (the tiles of
+//     one split share an XCD's L2); a workgroup (4 waves) owns a
 //     [TCO x TCI] output tile (4 wave tiles of 64x64, or fewer wave tiles with
 //     the reduction split across the waves) over a contiguous range of rows;
 //   * rows stream through LDS in stages of KB rows: every thread loads 16-byte
@@ -73,7 +74,7 @@ template <int WA, int WB, bool GEN>
 __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t* __restrict__ dy,
                                                            const uint16_t* __restrict__ x, float* __restrict__ out,
                                                            WgradGeom g, int64_t M, int64_t rows_per_split,
-                                                           int tiles_co, int tiles_ci) {
+                                                           int tiles_co, int tiles_ci, int splits) {
   constexpr int NWT = WA * WB;          // wave tiles per workgroup tile
   constexpr int KS = 4 / NWT;           // waves sharing one wave tile (reduction split)
   constexpr int KB = KS == 4 ? 64 : 32;  // rows per stage: every wave gets >= 1 k-step of 16
@@ -88,14 +89,25 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t* __res
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int taps = g.KH * g.KW;
-  int b = blockIdx.x;
+  // XCD-aware order (1-D grid): workgroups are dispatched round-robin over the 8
+  // XCDs, so hardware block L runs on XCD L % 8.  Logical block q = xcd * per + L / 8
+  // (per = blocks per XCD) gives each XCD a contiguous run of (split, tile) pairs:
+  // every tile x tap of one row split runs on the SAME XCD at about the same time,
+  // and their re-reads of the split's dy / x rows hit that XCD's L2 instead of
+  // going to HBM / the shared MALL once per tile.
+  const int ntile = tiles_co * tiles_ci * taps;
+  const int total = ntile * splits, per = (total + 7) / 8;
+  const int lq = (int)(blockIdx.x % 8u) * per + (int)(blockIdx.x / 8u);
+  if (lq >= total) return;  // padding blocks of the last XCD
+  const int split = lq / ntile;
+  int b = lq - split * ntile;
   const int tci = b % tiles_ci;
   b /= tiles_ci;
   const int tco = b % tiles_co;
   const int tap = b / tiles_co;
   const int r = tap / g.KW, s = tap - (tap / g.KW) * g.KW;
   const int co0 = tco * TCO, ci0 = tci * TCI;
-  const int64_t mb = (int64_t)blockIdx.y * rows_per_split;
+  const int64_t mb = (int64_t)split * rows_per_split;
   const int64_t me = mb + rows_per_split < M ? mb + rows_per_split : M;
   const int nst = (int)((me - mb + KB - 1) / KB);
 
@@ -210,7 +222,7 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t* __res
   }
 
   // D of 32x32x16: column = lane & 31 (ci), row = (k & 3) + 8 (k >> 2) + 4 (lane >> 5) (co)
-  float* o = out + (int64_t)blockIdx.y * ((int64_t)g.Cout * taps * g.Cin);
+  float* o = out + (int64_t)split * ((int64_t)g.Cout * taps * g.Cin);
   const int64_t rs = (int64_t)taps * g.Cin;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -225,14 +237,37 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t* __res
     }
 }
 
-// out[i] = sum over splits of part[s][i], in split order (float4 per thread)
+// out = sum over splits of part[s]: a block owns kRedCols float4 columns; thread
+// group j (of 256 / kRedCols) sums splits j, j + G, j + 2G, ... and the group sums
+// are combined in group order through LDS -- a fixed order (deterministic), with
+// S / G independent loads per thread instead of a serial chain of S.
+constexpr int kRedCols = 16;
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
                                                            int64_t n, int S) {
-  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (i >= n) return;
-  float4 acc = *reinterpret_cast<const float4*>(part + i);
-  for (int k = 1; k < S; ++k) {
-    const float4 v = *reinterpret_cast<const float4*>(part + (int64_t)k * n + i);
+  constexpr int G = 256 / kRedCols;
+  __shared__ float4 sh[G][kRedCols];
+  const int c = threadIdx.x % kRedCols, j = threadIdx.x / kRedCols;
+  const int64_t i = ((int64_t)blockIdx.x * kRedCols + c) * 4;
+  float4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (i < n) {
+    int k = j;
+    for (; k + 3 * G < S; k += 4 * G) {  // 4 loads in flight
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(part + (int64_t)(k + u * G) * n + i);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
+    }
+    for (; k < S; k += G) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (int64_t)k * n + i);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  sh[j][c] = acc;
+  __syncthreads();
+  if (j != 0 || i >= n) return;
+  for (int g = 1; g < G; ++g) {
+    const float4 v = sh[g][c];
     acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
   }
   *reinterpret_cast<float4*>(out + i) = acc;
@@ -242,11 +277,12 @@ template <int WA, int WB>
 void launch_tile(const uint16_t* dy, const uint16_t* x, float* out, const WgradGeom& g, int64_t M, int64_t rps,
                  int S, bool gen, hipStream_t st) {
   const int tco = g.Cout / (64 * WA), tci = g.Cin / (64 * WB);
-  const dim3 grid(tco * tci * g.KH * g.KW, S), block(kWgThreads);
+  const int total = tco * tci * g.KH * g.KW * S;
+  const dim3 grid((unsigned)((total + 7) / 8 * 8)), block(kWgThreads);
   if (gen)
-    hipLaunchKernelGGL((wgrad_kernel<WA, WB, true>), grid, block, 0, st, dy, x, out, g, M, rps, tco, tci);
+    hipLaunchKernelGGL((wgrad_kernel<WA, WB, true>), grid, block, 0, st, dy, x, out, g, M, rps, tco, tci, S);
   else
-    hipLaunchKernelGGL((wgrad_kernel<WA, WB, false>), grid, block, 0, st, dy, x, out, g, M, rps, tco, tci);
+    hipLaunchKernelGGL((wgrad_kernel<WA, WB, false>), grid, block, 0, st, dy, x, out, g, M, rps, tco, tci, S);
 }
 
 }  // namespace
@@ -266,15 +302,15 @@ WgradPlan wgrad_plan(const WgradGeom& g, int splits) {
   const int64_t tiles = (int64_t)(g.Cout / (64 * p.wa)) * (g.Cin / (64 * p.wb)) * g.KH * g.KW;
   int64_t S = splits;
   if (S <= 0) {
-    // ~1024 workgroups (4 per CU) ...
-    S = (1024 + tiles - 1) / tiles;
-    // ... but >= 8 stages per split, and the fp32 partials (written + re-read by the
-    // reduce) at most ~1/8 of the bytes of dy and x
-    const int64_t max_rows = (M + 8 * kb - 1) / (8 * kb);
+    // ~512 workgroups (2 per CU, the loads of 8 waves in flight per CU) ...
+    S = (512 + tiles - 1) / tiles;
+    // ... at least 4 stages per split, and fp32 partials (written, then re-read by
+    // the reduce) of at most half the bytes of dy and x
+    const int64_t max_rows = M / (4 * kb);
     if (S > max_rows) S = max_rows;
-    const double in_bytes = 2.0 * (double)M * (g.Cout + (double)g.Cin * g.KH * g.KW);
-    const double part_bytes = 8.0 * (double)g.Cout * g.Cin * g.KH * g.KW;  // write + read per split
-    const int64_t max_part = (int64_t)(in_bytes / 8.0 / part_bytes);
+    const double in_bytes = 2.0 * (double)M * (g.Cout + (double)g.Cin) * g.KH * g.KW;  // per-tap tiles
+    const double part_bytes = 4.0 * (double)g.Cout * g.Cin * g.KH * g.KW;
+    const int64_t max_part = (int64_t)(0.5 * in_bytes / part_bytes);
     if (S > max_part) S = max_part;
   }
   if (S < 1) S = 1;
@@ -303,7 +339,7 @@ void launch_wgrad(const uint16_t* dy, const uint16_t* x, float* out, float* part
   }
   if (p.splits > 1) {
     const int64_t n = (int64_t)g.Cout * g.KH * g.KW * g.Cin;
-    const int64_t blocks = (n / 4 + 255) / 256;
+    const int64_t blocks = (n / 4 + kRedCols - 1) / kRedCols;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, part, out, n, p.splits);
   }
 }

@@ -145,16 +145,13 @@ class _Conv1x1Fn(torch.autograd.Function):
         dy2, x2 = _nhwc2d(dy), _nhwc2d(x)
         w4 = wb.view(cout, cin, 1, 1)
         dx = dw = None
+        be_d = be_w = None
         if ctx.needs_input_grad[0]:
-            be = _pick("dgrad", ctx.key, {
+            be_d = _pick("dgrad", ctx.key, {
                 "gemm": lambda: torch.mm(dy2, wb),
                 "miopen": lambda: _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
                                             [True, False, False]),
             })
-            if be == "gemm":
-                dx = _from2d(torch.mm(dy2, wb), n, h, w)
-            else:
-                dx = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, False, False])[0]
         if ctx.needs_input_grad[1]:
             cands = {
                 "gemm": lambda: torch.ops.aten.mm.dtype(dy2.t(), x2, torch.float32),
@@ -163,14 +160,22 @@ class _Conv1x1Fn(torch.autograd.Function):
             }
             if wgrad_ok(cin, cout):
                 cands["hip"] = lambda: wgrad_hip(dy, x, (1, 1), (1, 1), (0, 0))
-            be = _pick("wgrad", ctx.key, cands)
-            if be == "hip":
-                dw = wgrad_hip(dy, x, (1, 1), (1, 1), (0, 0))
-            elif be == "gemm":
-                dw = torch.ops.aten.mm.dtype(dy2.t(), x2, torch.float32).view(cout, cin, 1, 1)
-            else:
-                dw = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
-                               [False, True, False])[1].float()
+            be_w = _pick("wgrad", ctx.key, cands)
+        if be_d == "miopen" and be_w == "miopen":
+            # both from MIOpen: one call (its host cost is tens of us per call)
+            dx, dw = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, True, False])[:2]
+            return dx, dw.float(), None
+        if be_d == "gemm":
+            dx = _from2d(torch.mm(dy2, wb), n, h, w)
+        elif be_d == "miopen":
+            dx = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, False, False])[0]
+        if be_w == "hip":
+            dw = wgrad_hip(dy, x, (1, 1), (1, 1), (0, 0))
+        elif be_w == "gemm":
+            dw = torch.ops.aten.mm.dtype(dy2.t(), x2, torch.float32).view(cout, cin, 1, 1)
+        elif be_w == "miopen":
+            dw = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                           [False, True, False])[1].float()
         return dx, dw, None
 
 
@@ -220,9 +225,7 @@ class _ConvNHWCFn(torch.autograd.Function):
         stride, padding = ctx.geo
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = dw = None
-        if ctx.needs_input_grad[0]:
-            dx = _conv_bwd(dy, x, wb, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
-                           [True, False, False])[0]
+        be = None
         if ctx.needs_input_grad[1]:
             cout, cin, kh, kw = wb.shape
             key = (x.size(0) * dy.size(2) * dy.size(3), cin, cout, kh, kw, stride[0], padding[0])
@@ -231,11 +234,16 @@ class _ConvNHWCFn(torch.autograd.Function):
                                             [False, True, False])[1].float(),
                 "hip": lambda: wgrad_hip(dy, x, (kh, kw), stride, padding),
             })
-            if be == "hip":
-                dw = wgrad_hip(dy, x, (kh, kw), stride, padding)
-            else:
-                dw = _conv_bwd(dy, x, wb, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
-                               [False, True, False])[1].float()
+        if be == "miopen":
+            # MIOpen for both gradients: one call, as F.conv2d's autograd makes it
+            mask = [bool(ctx.needs_input_grad[0]), True, False]
+            dx, dw = _conv_bwd(dy, x, wb, None, list(stride), list(padding), [1, 1], False, [0, 0], 1, mask)[:2]
+            return dx, dw.float(), None, None, None
+        if ctx.needs_input_grad[0]:
+            dx = _conv_bwd(dy, x, wb, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
+                           [True, False, False])[0]
+        if be == "hip":
+            dw = wgrad_hip(dy, x, (kh, kw), stride, padding)
         return dx, dw, None, None, None
 
 

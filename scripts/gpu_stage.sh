@@ -9,6 +9,7 @@
 # pmc (counter passes of the default step, one pass per run), bench20 (driver-shaped
 # bench), share2 (N = 2 rehearsals with both ranks on the one GPU), corners (Tune
 # search-space corners), selftest (native comm self-test, plain + host ASan/UBSan),
+# wgrad (conv weight-gradient kernel tests + probe), rn50b (native ResNet-50 bench),
 # rn50 (ResNet-50 bench, native + stock torch; --deterministic-conv
 # is not run: MIOpen's atomic-free solvers compile for > 3 min without output), rn50prof (its kernel stats)
 set -o pipefail
@@ -44,6 +45,12 @@ for st in "$@"; do
       run tune_warm 300 python scripts/bench_tune.py --trials 8 --warm 8 ;;
     trainerprof)  # host profile of the worker's fit (cProfile, rank 0)
       RLA_PROFILE_EPOCHS="$R/$O/trainer_epochs_prof" run trainer_prof 300 python bench.py --via trainer --trainer-epochs 6 ;;
+    wgrad)  # MFMA conv weight-gradient kernel: numerics + per-shape timing vs MIOpen / hipBLASLt
+      run pytest_wgrad 300 $PYT tests/test_conv_wgrad.py
+      run wgrad_probe 300 python -u scripts/wgrad_probe.py ;;
+    rn50b)  # native ResNet-50 bench: eager and whole-step hipGraph
+      run rn50_base 600 python bench.py --model resnet50 --steps 30 --warmup 10
+      run rn50_graph 600 python bench.py --model resnet50 --steps 30 --warmup 10 --resnet-graph 1 ;;
     rn50graph)
       run rn50_graph 600 python bench.py --model resnet50 --steps 30 --warmup 10 --resnet-graph 1 ;;
     rn50ops)
