@@ -104,8 +104,9 @@ def parse(argv=None):
                     help="resnet50: comma list of bucket caps (MiB) measured in one run, e.g. 1,2,4,8,16,25")
     ap.add_argument("--benchmark-algos", type=int, default=1,
                     help="resnet50: torch.backends.cudnn.benchmark (MIOpen find per shape), both impls")
-    ap.add_argument("--resnet-graph", type=int, default=0,
-                    help="resnet50 native, 1 GPU: capture the whole training step in one hipGraph")
+    ap.add_argument("--resnet-graph", type=int, default=1,
+                    help="resnet50 native, 1 GPU: capture the whole training step in one hipGraph (default; "
+                         "0 = eager launches, host-bound at ~17 ms/step: profiles/r3_wgrad/rn50_host.log)")
     ap.add_argument("--deterministic-conv", type=int, default=0,
                     help="resnet50: torch.backends.cudnn.deterministic (MIOpen solvers without atomics: no "
                          "zero-fill / cast passes around split-K weight-gradient kernels)")

@@ -18,7 +18,7 @@
 //     the reduction split across the waves) over a contiguous range of rows;
 //   * rows stream through LDS in stages of KB rows: every thread loads 16-byte
 //     row chunks of dy / x (coalesced: the row-major NHWC rows ARE the GEMM's k
-//     axis), one stage ahead in registers, and writes them to a double-buffered
+//     axis), two stages ahead in registers, and writes them to a double-buffered
 //     LDS image [row][channel] padded by 64 B per row;
 //   * both MFMA operands are k-strided in that image (k = row), so they are read
 //     with ds_read_b64_tr_b16 (hardware transpose: lane i of a 16-lane group gets
@@ -111,41 +111,49 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t* __res
   const int64_t me = mb + rows_per_split < M ? mb + rows_per_split : M;
   const int nst = (int)((me - mb + KB - 1) / KB);
 
-  // this thread's 16-byte chunks of a stage: dy rows (TCO channels) and x rows (TCI)
-  u32x4 ra[NA], rb[NB];
-  auto load = [&](int64_t m0) {
+  // this thread's 16-byte chunks of a stage: dy rows (TCO channels) and x rows (TCI),
+  // in one of two register sets (stage k lives in set k & 1: two stages in flight)
+  // Branch-free: out-of-range rows (past the split, or zero padding of x) load a
+  // valid clamped row and are zeroed at the LDS store through a validity mask, so
+  // the waitcnt pass sees straight-line loads and waits only for the older set.
+  struct Set {
+    u32x4 a[NA], b[NB];
+    uint32_t ok;  // bit i: a[i] valid; bit NA + i: b[i] valid
+  };
+  static_assert(NA + NB <= 32, "validity mask");
+  auto load = [&](Set& st, int64_t m0) {
+    st.ok = 0u;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int c = tid + i * kWgThreads, row = c / (TCO / 8), col = (c % (TCO / 8)) * 8;
       const int64_t m = m0 + row;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (m < me) v = *reinterpret_cast<const u32x4*>(dy + m * g.Cout + co0 + col);
-      ra[i] = v;
+      const bool ok = m < me;
+      st.a[i] = *reinterpret_cast<const u32x4*>(dy + (ok ? m : mb) * g.Cout + co0 + col);
+      st.ok |= ok ? (1u << i) : 0u;
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int c = tid + i * kWgThreads, row = c / (TCI / 8), col = (c % (TCI / 8)) * 8;
       const int64_t m = m0 + row;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (m < me) {
-        const int64_t xr = x_row<GEN>(m, g, r, s);
-        if (xr >= 0) v = *reinterpret_cast<const u32x4*>(x + xr * g.Cin + ci0 + col);
-      }
-      rb[i] = v;
+      const int64_t xr = x_row<GEN>(m < me ? m : mb, g, r, s);
+      const bool ok = m < me && xr >= 0;
+      st.b[i] = *reinterpret_cast<const u32x4*>(x + (ok ? xr : 0) * g.Cin + ci0 + col);
+      st.ok |= ok ? (1u << (NA + i)) : 0u;
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](const Set& st, int buf) {
     __bf16* A = lds + buf * STAGE;
     __bf16* B = A + KB * SA;
+    const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int c = tid + i * kWgThreads, row = c / (TCO / 8), col = (c % (TCO / 8)) * 8;
-      *reinterpret_cast<u32x4*>(A + row * SA + col) = ra[i];
+      *reinterpret_cast<u32x4*>(A + row * SA + col) = (st.ok >> i) & 1u ? st.a[i] : z;
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int c = tid + i * kWgThreads, row = c / (TCI / 8), col = (c % (TCI / 8)) * 8;
-      *reinterpret_cast<u32x4*>(B + row * SB + col) = rb[i];
+      *reinterpret_cast<u32x4*>(B + row * SB + col) = (st.ok >> (NA + i)) & 1u ? st.b[i] : z;
     }
   };
 
@@ -165,15 +173,8 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t* __res
 #pragma unroll
       for (int k = 0; k < 16; ++k) acc[i][j][k] = 0.f;
 
-  if (nst > 0) {
-    load(mb);
-    store(0);
-  }
-  __syncthreads();
-  for (int it = 0; it < nst; ++it) {
-    const bool more = it + 1 < nst;
-    if (more) load(mb + (int64_t)(it + 1) * KB);  // in flight under this stage's MFMAs
-    const __bf16* A = lds + (it & 1) * STAGE;
+  auto compute = [&](int buf) {
+    const __bf16* A = lds + buf * STAGE;
     const __bf16* B = A + KB * SA;
 #pragma unroll
     for (int kk = 0; kk < KSTEPS; ++kk) {
@@ -191,8 +192,34 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t* __res
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-    if (more) store((it + 1) & 1);  // the other buffer: last read before the previous barrier
+  };
+  // stage `it` from LDS buffer it & 1 while stages it + 1 (set nxt, landing) and
+  // it + 2 (set cur, issued here: cur's stage went to LDS one step earlier) are in
+  // flight; then stage it + 1 goes to the other buffer, read last before the
+  // previous barrier
+  // Every load and store of the loop is unconditional (a split with an odd stage
+  // count runs one all-zero stage more): a load whose value were used only inside
+  // an `if` would be sunk by the compiler next to that use -- the LDS store that
+  // waits for it -- and the prefetch would be lost.
+  auto step = [&](int it, Set& cur, Set& nxt) {
+    load(cur, mb + (int64_t)(it + 2) * KB);  // past the split's end: masked, harmless
+    __builtin_amdgcn_sched_barrier(0);  // loads stay ahead of the MFMAs
+    compute(it & 1);
+    __builtin_amdgcn_sched_barrier(0);
+    store(nxt, (it + 1) & 1);  // stage it + 1 (past the end: zeros, never read)
     __syncthreads();
+  };
+  Set s0, s1;
+  const int nst2 = (nst + 1) & ~1;
+  if (nst2 > 0) {
+    load(s0, mb);
+    load(s1, mb + KB);
+    store(s0, 0);
+  }
+  __syncthreads();
+  for (int it = 0; it < nst2; it += 2) {  // unrolled by two: the register sets stay static
+    step(it, s0, s1);
+    step(it + 1, s1, s0);
   }
 
   // reduction split: waves ks > 0 hand their tiles to ks == 0 through LDS (fixed order)
@@ -305,7 +332,7 @@ WgradPlan wgrad_plan(const WgradGeom& g, int splits) {
     // ~512 workgroups (2 per CU, the loads of 8 waves in flight per CU) ...
     S = (512 + tiles - 1) / tiles;
     // ... at least 4 stages per split, and fp32 partials (written, then re-read by
-    // the reduce) of at most half the bytes of dy and x
+    // the reduce) of at most half the bytes the tiles read
     const int64_t max_rows = M / (4 * kb);
     if (S > max_rows) S = max_rows;
     const double in_bytes = 2.0 * (double)M * (g.Cout + (double)g.Cin) * g.KH * g.KW;  // per-tap tiles

@@ -46,13 +46,15 @@ for st in "$@"; do
     trainerprof)  # host profile of the worker's fit (cProfile, rank 0)
       RLA_PROFILE_EPOCHS="$R/$O/trainer_epochs_prof" run trainer_prof 300 python bench.py --via trainer --trainer-epochs 6 ;;
     wgrad)  # MFMA conv weight-gradient kernel: numerics + per-shape timing vs MIOpen / hipBLASLt
-      run pytest_wgrad 300 $PYT tests/test_conv_wgrad.py
+      run pytest_wgrad 300 $PYT tests/test_conv_wgrad.py tests/test_bn.py
       run wgrad_probe 300 python -u scripts/wgrad_probe.py ;;
     rn50b)  # native ResNet-50 bench: eager and whole-step hipGraph
       run rn50_base 600 python bench.py --model resnet50 --steps 30 --warmup 10
       run rn50_graph 600 python bench.py --model resnet50 --steps 30 --warmup 10 --resnet-graph 1 ;;
     rn50graph)
       run rn50_graph 600 python bench.py --model resnet50 --steps 30 --warmup 10 --resnet-graph 1 ;;
+    rn50host)  # host cProfile of the eager native ResNet-50 step
+      run rn50_host 300 python -u scripts/rn50_host_prof.py ;;
     rn50ops)
       run rn50_ops 300 python -u scripts/rn50_op_profile.py ;;
     conv1x1)
