@@ -535,8 +535,9 @@ void bn_bwd_apply(Tensor x, optional<Tensor> y, Tensor dy, Tensor coef, bool rel
 // (the channels_last weight's memory order).
 Tensor conv_wgrad(Tensor dy, Tensor x, int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t OH, int64_t OW,
                   int64_t Cout, int64_t KH, int64_t KW, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
-                  int64_t splits) {
+                  int64_t splits, int64_t algo) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda(), "conv_wgrad: GPU tensors");
+  TORCH_CHECK(algo == 0 || algo == 1, "conv_wgrad: algo 0 (auto) or 1 (generic)");
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "conv_wgrad: bf16 inputs");
   TORCH_CHECK(dy.is_contiguous() && x.is_contiguous(), "conv_wgrad: contiguous NHWC memory");
   TORCH_CHECK(Cout % 64 == 0 && Cin % 64 == 0 && Cout > 0 && Cin > 0, "conv_wgrad: channels must be multiples of 64");
@@ -551,7 +552,7 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int64_t N, int64_t H, int64_t W, int64_t 
   const at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   rla::WgradGeom g{(int)N, (int)H, (int)W, (int)Cin, (int)OH, (int)OW, (int)Cout, (int)KH, (int)KW,
                    (int)sh, (int)sw, (int)ph, (int)pw};
-  const rla::WgradPlan plan = rla::wgrad_plan(g, (int)splits);
+  const rla::WgradPlan plan = rla::wgrad_plan(g, (int)splits, (int)algo);
   Tensor out = at::empty({Cout, KH, KW, Cin}, x.options().dtype(at::kFloat));
   Tensor part;
   if (plan.splits > 1) part = at::empty({(int64_t)plan.splits * Cout * KH * KW * Cin}, out.options());
@@ -562,11 +563,11 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int64_t N, int64_t H, int64_t W, int64_t 
 
 std::vector<int64_t> conv_wgrad_plan(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t OH, int64_t OW,
                                      int64_t Cout, int64_t KH, int64_t KW, int64_t sh, int64_t sw, int64_t ph,
-                                     int64_t pw, int64_t splits) {
+                                     int64_t pw, int64_t splits, int64_t algo) {
   rla::WgradGeom g{(int)N, (int)H, (int)W, (int)Cin, (int)OH, (int)OW, (int)Cout, (int)KH, (int)KW,
                    (int)sh, (int)sw, (int)ph, (int)pw};
-  const rla::WgradPlan p = rla::wgrad_plan(g, (int)splits);
-  return {p.wa, p.wb, p.splits, p.rows_per_split};
+  const rla::WgradPlan p = rla::wgrad_plan(g, (int)splits, (int)algo);
+  return {p.kind, p.wa, p.wb, p.splits, p.rows_per_split};
 }
 
 }  // namespace
@@ -609,7 +610,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad", &conv_wgrad, "NHWC bf16 conv weight gradient on MFMA -> fp32 [Cout, KH, KW, Cin]",
         py::arg("dy"), py::arg("x"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("OH"),
         py::arg("OW"), py::arg("Cout"), py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"), py::arg("ph"),
-        py::arg("pw"), py::arg("splits") = 0);
-  m.def("conv_wgrad_plan", &conv_wgrad_plan, "the wgrad kernel's (wa, wb, splits, rows_per_split)");
+        py::arg("pw"), py::arg("splits") = 0, py::arg("algo") = 0);
+  m.def("conv_wgrad_plan", &conv_wgrad_plan, "the wgrad kernel's (kind, wa, wb, splits, rows_per_split)",
+        py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("OH"), py::arg("OW"), py::arg("Cout"),
+        py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
+        py::arg("splits") = 0, py::arg("algo") = 0);
   m.attr("ARCH") = "gfx950";
 }

@@ -56,17 +56,22 @@ __device__ __forceinline__ bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-// source row of x for output row m and tap (r, s); -1 = zero padding
+// source row of x for output row m and tap (r, s), clamped into the image (a
+// padding tap loads a neighbouring pixel: a valid address near the real loads,
+// not one hot dummy row); *pad is set when the tap falls in the zero padding
 template <bool GEN>
-__device__ __forceinline__ int64_t x_row(int64_t m, const WgradGeom& g, int r, int s) {
+__device__ __forceinline__ int64_t x_row(int64_t m, const WgradGeom& g, int r, int s, bool* pad) {
+  *pad = false;
   if (!GEN) return m;
   // 32-bit index math (the binding bounds every row count below 2^29)
   const int mi = (int)m, ohw = g.OH * g.OW;
   const int n = mi / ohw;
   const int rem = mi - n * ohw;
   const int oh = rem / g.OW, ow = rem - oh * g.OW;
-  const int ih = oh * g.sh - g.ph + r, iw = ow * g.sw - g.pw + s;
-  if (ih < 0 || ih >= g.H || iw < 0 || iw >= g.W) return -1;
+  int ih = oh * g.sh - g.ph + r, iw = ow * g.sw - g.pw + s;
+  *pad = ih < 0 || ih >= g.H || iw < 0 || iw >= g.W;
+  ih = ih < 0 ? 0 : (ih >= g.H ? g.H - 1 : ih);
+  iw = iw < 0 ? 0 : (iw >= g.W ? g.W - 1 : iw);
   return (int64_t)((n * g.H + ih) * g.W + iw);
 }
 
@@ -135,9 +140,10 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t* __res
     for (int i = 0; i < NB; ++i) {
       const int c = tid + i * kWgThreads, row = c / (TCI / 8), col = (c % (TCI / 8)) * 8;
       const int64_t m = m0 + row;
-      const int64_t xr = x_row<GEN>(m < me ? m : mb, g, r, s);
-      const bool ok = m < me && xr >= 0;
-      st.b[i] = *reinterpret_cast<const u32x4*>(x + (ok ? xr : 0) * g.Cin + ci0 + col);
+      bool pad;
+      const int64_t xr = x_row<GEN>(m < me ? m : mb, g, r, s, &pad);
+      const bool ok = m < me && !pad;
+      st.b[i] = *reinterpret_cast<const u32x4*>(x + xr * g.Cin + ci0 + col);
       st.ok |= ok ? (1u << (NA + i)) : 0u;
     }
   };
@@ -300,6 +306,169 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   *reinterpret_cast<float4*>(out + i) = acc;
 }
 
+
+// ---------------------------------------------------------------------------
+// 3x3 / stride 1 / pad 1 (ResNet's bottleneck conv2): all nine taps of a 64x64
+// [Cout x Cin] tile in one workgroup, from ONE load of each dy row and a halo
+// tile of x, instead of the generic kernel's nine independent (tap) GEMMs that
+// each re-read dy and x.  A stage is 64 dy rows = R whole output image rows of
+// OWP (>= OW, multiple of 16) pixels; the x tile holds the R + 2 input rows they
+// touch, each with one zero pixel of padding on both sides (OWP + 2 pixels), so
+// tap (r, s) of output pixel (j, p) reads x-tile row (j + r) * (OWP + 2) + p + s:
+// a plain row offset of the same LDS image (transposed reads at any row).  Wave
+// r (0..2) accumulates the three taps (r, 0..2) = 3 x 64x64 fp32 in AGPRs; wave 3
+// only helps load.  Rows outside the image (halo, p >= OW, rows past OH) are
+// zeros, so no tap needs a mask.
+template <int OWP>
+__global__ __launch_bounds__(kWgThreads) void wgrad3x3_kernel(const uint16_t* __restrict__ dy,
+                                                              const uint16_t* __restrict__ x, float* __restrict__ out,
+                                                              WgradGeom g, int stages_per_split, int tiles_co,
+                                                              int tiles_ci, int splits) {
+  constexpr int R = 64 / OWP, XP = OWP + 2, XROWS = (R + 2) * XP;
+  constexpr int SA = 64 + kWgPad, SB = 64 + kWgPad;
+  constexpr int NA = 64 * 8 / kWgThreads;                    // dy chunks per thread
+  constexpr int NB = (XROWS * 8 + kWgThreads - 1) / kWgThreads;  // x chunks per thread
+  constexpr int BROWS = NB * kWgThreads / 8;                  // x-tile rows incl. the unused tail
+  static_assert(OWP % 16 == 0 && 64 % OWP == 0 && NA + NB <= 32, "3x3 stage shape");
+  __shared__ __attribute__((aligned(16))) __bf16 lds[64 * SA + BROWS * SB];
+  __bf16* A = lds;
+  __bf16* B = lds + 64 * SA;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntile = tiles_co * tiles_ci, total = ntile * splits, per = (total + 7) / 8;
+  const int lq = (int)(blockIdx.x % 8u) * per + (int)(blockIdx.x / 8u);  // XCD-aware (see wgrad_kernel)
+  if (lq >= total) return;
+  const int split = lq / ntile, tile = lq - split * ntile;
+  const int co0 = (tile / tiles_ci) * 64, ci0 = (tile % tiles_ci) * 64;
+  const int RB = (g.OH + R - 1) / R, T = g.N * RB;
+  const int s0 = split * stages_per_split;
+  const int s1 = s0 + stages_per_split < T ? s0 + stages_per_split : T;
+
+  struct Set {
+    u32x4 a[NA], b[NB];
+    uint32_t ok;
+  };
+  // Masked chunks load a CLAMPED in-image address next to the valid ones (already
+  // in cache): a shared dummy address (e.g. the tensor base) would have every CU
+  // hammer one L2 channel with its halo / padding / tail chunks.
+  auto load = [&](Set& st, int stage) {
+    const bool live = stage < s1;
+    const int sc = stage < T ? stage : T - 1;
+    const int n = sc / RB, oh0 = (sc - (sc / RB) * RB) * R;
+    st.ok = 0u;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int c = tid + i * kWgThreads, row = c >> 3, col = (c & 7) * 8;
+      const int j = row / OWP, pp = row - (row / OWP) * OWP;
+      const bool ok = live && pp < g.OW && oh0 + j < g.OH;
+      const int oh = oh0 + j < g.OH ? oh0 + j : g.OH - 1, ow = pp < g.OW ? pp : g.OW - 1;
+      st.a[i] = *reinterpret_cast<const u32x4*>(dy + ((int64_t)(n * g.OH + oh) * g.OW + ow) * g.Cout + co0 + col);
+      st.ok |= ok ? (1u << i) : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int c = tid + i * kWgThreads, ri = c >> 3, col = (c & 7) * 8;
+      const int rc = ri < XROWS ? ri : XROWS - 1;
+      const int jr = rc / XP, q = rc - (rc / XP) * XP;
+      const int ih = oh0 - 1 + jr, iw = q - 1;
+      const bool ok = live && ri < XROWS && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+      const int ihc = ih < 0 ? 0 : (ih >= g.H ? g.H - 1 : ih), iwc = iw < 0 ? 0 : (iw >= g.W ? g.W - 1 : iw);
+      st.b[i] = *reinterpret_cast<const u32x4*>(x + ((int64_t)(n * g.H + ihc) * g.W + iwc) * g.Cin + ci0 + col);
+      st.ok |= ok ? (1u << (NA + i)) : 0u;
+    }
+  };
+  auto store = [&](const Set& st) {
+    const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int c = tid + i * kWgThreads, row = c >> 3, col = (c & 7) * 8;
+      *reinterpret_cast<u32x4*>(A + row * SA + col) = (st.ok >> i) & 1u ? st.a[i] : z;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int c = tid + i * kWgThreads, ri = c >> 3, col = (c & 7) * 8;
+      *reinterpret_cast<u32x4*>(B + ri * SB + col) = (st.ok >> (NA + i)) & 1u ? st.b[i] : z;
+    }
+  };
+
+  const int gq = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  const int cho = 16 * (gq & 1) + 4 * p4, rwo = 8 * (gq >> 1) + q4;
+  const int r = wave;  // tap row of this wave (wave 3: loads only)
+  f32x16 acc[3][2][2];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc[t][i][j][k] = 0.f;
+
+  auto compute = [&]() {
+    if (r >= 3) return;  // wave-uniform
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int j = kk * 16 / OWP, p0 = kk * 16 - j * OWP;
+      bf16x8 fa[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const __bf16* pa = A + (kk * 16 + rwo) * SA + 32 * i + cho;
+        fa[i] = cat8(tr4(pa), tr4(pa + 4 * SA));
+      }
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int xb = (j + r) * XP + p0 + t + rwo;
+        bf16x8 fb[2];
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const __bf16* pb = B + xb * SB + 32 * jj + cho;
+          fb[jj] = cat8(tr4(pb), tr4(pb + 4 * SB));
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+            acc[t][i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[jj], acc[t][i][jj], 0, 0, 0);
+      }
+    }
+  };
+  // one LDS image, two register sets: stage `it` goes to LDS while stage it + 1 is
+  // in flight; stage it + 2 is issued before this stage's MFMAs.  Loads and stores
+  // unconditional (stages past the split are masked zeros) so none is sunk.
+  auto step = [&](int it, Set& cur) {
+    store(cur);
+    __syncthreads();
+    load(cur, it + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    compute();
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+  };
+  Set sa, sb;
+  load(sa, s0);
+  load(sb, s0 + 1);
+  for (int it = s0; it < s1; it += 2) {
+    step(it, sa);
+    step(it + 1, sb);
+  }
+
+  if (r >= 3) return;
+  float* o = out + (int64_t)split * ((int64_t)g.Cout * 9 * g.Cin);
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int ci = ci0 + 32 * jj + (lane & 31);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int co = co0 + 32 * i + (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
+          o[((int64_t)co * 9 + r * 3 + t) * g.Cin + ci] = acc[t][i][jj][k];
+        }
+      }
+}
+
 template <int WA, int WB>
 void launch_tile(const uint16_t* dy, const uint16_t* x, float* out, const WgradGeom& g, int64_t M, int64_t rps,
                  int S, bool gen, hipStream_t st) {
@@ -314,8 +483,40 @@ void launch_tile(const uint16_t* dy, const uint16_t* x, float* out, const WgradG
 
 }  // namespace
 
-WgradPlan wgrad_plan(const WgradGeom& g, int splits) {
+bool wgrad3x3_ok(const WgradGeom& g) {
+  return g.KH == 3 && g.KW == 3 && g.sh == 1 && g.sw == 1 && g.ph == 1 && g.pw == 1 && g.H == g.OH &&
+         g.W == g.OW && g.OW <= 64;
+}
+
+int wgrad3x3_owp(int OW) { return OW <= 16 ? 16 : OW <= 32 ? 32 : 64; }
+
+WgradPlan wgrad_plan(const WgradGeom& g, int splits, int algo) {
   WgradPlan p{};
+  if (algo != 1 && wgrad3x3_ok(g)) {
+    // halo kernel: stages of 64 / OWP whole output rows, 64x64 tiles
+    p.kind = 1;
+    p.wa = p.wb = 1;
+    const int R = 64 / wgrad3x3_owp(g.OW);
+    const int64_t T = (int64_t)g.N * ((g.OH + R - 1) / R);
+    const int64_t tiles = (int64_t)(g.Cout / 64) * (g.Cin / 64);
+    int64_t S = splits;
+    if (S <= 0) {
+      S = (384 + tiles - 1) / tiles;  // ~1.5 workgroups per CU (one fits per CU by registers)
+      if (S > T / 4) S = T / 4;       // >= 4 stages per split
+      // fp32 partials (9 taps) at most ~2x the dy + x bytes (the generic kernel
+      // re-reads those 9x; the autotuner picks between the two)
+      const double in_bytes = 2.0 * (double)g.N * g.OH * g.OW * (g.Cout + (double)g.Cin);
+      const int64_t max_part = (int64_t)(2.0 * in_bytes / (4.0 * 9.0 * g.Cout * g.Cin));
+      if (S > max_part) S = max_part;
+    }
+    if (S < 1) S = 1;
+    int64_t sps = (T + S - 1) / S;
+    sps = (sps + 1) & ~(int64_t)1;  // even: the loop runs stages in pairs
+    p.rows_per_split = sps;
+    p.splits = (int)((T + sps - 1) / sps);
+    return p;
+  }
+  p.kind = 0;
   // workgroup tile (in 64-channel wave tiles): 4 wave tiles when the weight is
   // big enough, with the larger side along the larger channel count
   if (g.Cout % 128 == 0 && g.Cin % 128 == 0) { p.wa = 2; p.wb = 2; }
@@ -352,6 +553,18 @@ WgradPlan wgrad_plan(const WgradGeom& g, int splits) {
 void launch_wgrad(const uint16_t* dy, const uint16_t* x, float* out, float* part, const WgradGeom& g,
                   const WgradPlan& p, hipStream_t st) {
   const int64_t M = (int64_t)g.N * g.OH * g.OW;
+  if (p.kind == 1) {
+    float* dst = p.splits > 1 ? part : out;
+    const int tco = g.Cout / 64, tci = g.Cin / 64, total = tco * tci * p.splits;
+    const dim3 grid((unsigned)((total + 7) / 8 * 8)), block(kWgThreads);
+    const int sps = (int)p.rows_per_split, owp = wgrad3x3_owp(g.OW);
+    if (owp == 16)
+      hipLaunchKernelGGL(wgrad3x3_kernel<16>, grid, block, 0, st, dy, x, dst, g, sps, tco, tci, p.splits);
+    else if (owp == 32)
+      hipLaunchKernelGGL(wgrad3x3_kernel<32>, grid, block, 0, st, dy, x, dst, g, sps, tco, tci, p.splits);
+    else
+      hipLaunchKernelGGL(wgrad3x3_kernel<64>, grid, block, 0, st, dy, x, dst, g, sps, tco, tci, p.splits);
+  } else {
   const bool gen = !(g.KH == 1 && g.KW == 1 && g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0 && g.H == g.OH &&
                      g.W == g.OW);
   float* dst = p.splits > 1 ? part : out;
@@ -363,6 +576,7 @@ void launch_wgrad(const uint16_t* dy, const uint16_t* x, float* out, float* part
     case 21: launch_tile<2, 1>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st); break;
     case 12: launch_tile<1, 2>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st); break;
     default: launch_tile<1, 1>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st); break;
+  }
   }
   if (p.splits > 1) {
     const int64_t n = (int64_t)g.Cout * g.KH * g.KW * g.Cin;

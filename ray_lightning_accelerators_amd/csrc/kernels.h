@@ -230,11 +230,13 @@ struct WgradGeom {
   int KH, KW, sh, sw, ph, pw;
 };
 struct WgradPlan {
+  int kind;                // 0 generic (any geometry), 1 3x3 / stride 1 / pad 1 halo kernel
   int wa, wb;              // workgroup tile = (64 wa) x (64 wb) channels
   int splits;              // row splits (> 1: fp32 partials + a reduce kernel)
-  int64_t rows_per_split;
+  int64_t rows_per_split;  // kind 1: stages (64 output rows each) per split
 };
-WgradPlan wgrad_plan(const WgradGeom& g, int splits);  // splits <= 0: automatic
+// splits <= 0: automatic; algo 0: the halo kernel when the geometry allows, 1: generic
+WgradPlan wgrad_plan(const WgradGeom& g, int splits, int algo = 0);
 // part: splits * Cout * KH * KW * Cin floats when plan.splits > 1 (else unused)
 void launch_wgrad(const uint16_t* dy, const uint16_t* x, float* out, float* part, const WgradGeom& g,
                   const WgradPlan& p, hipStream_t stream);

@@ -91,18 +91,20 @@ def wgrad_ok(cin: int, cout: int) -> bool:
     return cin % 64 == 0 and cout % 64 == 0 and os.environ.get("RLA_CONV_WGRAD", "auto") != "off"
 
 
-def wgrad_hip(dy: torch.Tensor, x: torch.Tensor, kernel_size, stride, padding, splits: int = 0) -> torch.Tensor:
+def wgrad_hip(dy: torch.Tensor, x: torch.Tensor, kernel_size, stride, padding, splits: int = 0,
+              algo: int = 0) -> torch.Tensor:
     """Weight gradient of an NHWC bf16 convolution on the MFMA kernel: ``dy`` [N, Cout,
     OH, OW] and ``x`` [N, Cin, H, W], both channels_last bf16; returns the fp32
     gradient [Cout, Cin, KH, KW] with channels_last strides (the kernel writes the
-    [Cout, KH, KW, Cin] memory order directly)."""
+    [Cout, KH, KW, Cin] memory order directly).  ``algo`` 0: the 3x3 / stride-1 /
+    pad-1 halo kernel where it applies, else the generic one; 1: always generic."""
     from . import require
 
     n, cin, h, w = x.shape
     cout, oh, ow = dy.size(1), dy.size(2), dy.size(3)
     kh, kw = kernel_size
     out = require().conv_wgrad(dy.permute(0, 2, 3, 1), x.permute(0, 2, 3, 1), n, h, w, cin, oh, ow, cout, kh, kw,
-                               stride[0], stride[1], padding[0], padding[1], splits)
+                               stride[0], stride[1], padding[0], padding[1], splits, algo)
     return out.permute(0, 3, 1, 2)
 
 
@@ -229,11 +231,15 @@ class _ConvNHWCFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             cout, cin, kh, kw = wb.shape
             key = (x.size(0) * dy.size(2) * dy.size(3), cin, cout, kh, kw, stride[0], padding[0])
-            be = _pick("wgrad_kxk", key, {
+            cands = {
                 "miopen": lambda: _conv_bwd(dy, x, wb, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
                                             [False, True, False])[1].float(),
                 "hip": lambda: wgrad_hip(dy, x, (kh, kw), stride, padding),
-            })
+            }
+            if (kh, kw, tuple(stride), tuple(padding)) == (3, 3, (1, 1), (1, 1)):
+                # "hip" is the halo kernel here; the generic tap-GEMM kernel competes too
+                cands["hip_gen"] = lambda: wgrad_hip(dy, x, (kh, kw), stride, padding, algo=1)
+            be = _pick("wgrad_kxk", key, cands)
         if be == "miopen":
             # MIOpen for both gradients: one call, as F.conv2d's autograd makes it
             mask = [bool(ctx.needs_input_grad[0]), True, False]
@@ -244,6 +250,8 @@ class _ConvNHWCFn(torch.autograd.Function):
                            [True, False, False])[0]
         if be == "hip":
             dw = wgrad_hip(dy, x, (kh, kw), stride, padding)
+        elif be == "hip_gen":
+            dw = wgrad_hip(dy, x, (kh, kw), stride, padding, algo=1)
         return dx, dw, None, None, None
 
 

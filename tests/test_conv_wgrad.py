@@ -15,7 +15,7 @@ from ray_lightning_accelerators_amd.ops.conv import wgrad_hip, wgrad_ok
 pytestmark = pytest.mark.gpu
 
 
-def _case(n, cin, h, w, cout, k, stride, pad, splits=0, seed=0):
+def _case(n, cin, h, w, cout, k, stride, pad, splits=0, seed=0, algo=0):
     g = torch.Generator(device="cuda").manual_seed(seed)
     oh = (h + 2 * pad - k) // stride + 1
     ow = (w + 2 * pad - k) // stride + 1
@@ -23,7 +23,7 @@ def _case(n, cin, h, w, cout, k, stride, pad, splits=0, seed=0):
     dy = torch.randn(n, cout, oh, ow, device="cuda", generator=g).to(torch.bfloat16)
     x = x.contiguous(memory_format=torch.channels_last)
     dy = dy.contiguous(memory_format=torch.channels_last)
-    got = wgrad_hip(dy, x, (k, k), (stride, stride), (pad, pad), splits)
+    got = wgrad_hip(dy, x, (k, k), (stride, stride), (pad, pad), splits, algo)
     ref = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, k, k), dy.float(), stride=stride, padding=pad)
     return got, ref
 
@@ -52,6 +52,21 @@ def test_wgrad_1x1_splits(splits):
 def test_wgrad_kxk(k, stride, pad, h):
     got, ref = _case(2, 64, h, h, 128, k, stride, pad)
     _check(got, ref)
+
+
+@pytest.mark.parametrize("h,w,n,splits", [(7, 7, 4, 0), (14, 14, 3, 0), (28, 28, 2, 0), (56, 56, 2, 0),
+                                          (9, 13, 2, 0), (20, 33, 2, 0), (14, 14, 3, 1), (28, 28, 2, 5)])
+def test_wgrad_3x3_halo(h, w, n, splits):
+    """3x3 / stride 1 / pad 1: the halo kernel (every output-width class: 16, 32 and
+    64-pixel stages; non-square images; one and several splits)."""
+    from ray_lightning_accelerators_amd.ops import require
+
+    plan = require().conv_wgrad_plan(n, h, w, 64, h, w, 128, 3, 3, 1, 1, 1, 1, splits)
+    assert plan[0] == 1  # halo kernel
+    got, ref = _case(n, 64, h, w, 128, 3, 1, 1, splits=splits)
+    _check(got, ref)
+    gen, _ = _case(n, 64, h, w, 128, 3, 1, 1, splits=splits, algo=1)  # generic tap-GEMM kernel
+    _check(gen, ref)
 
 
 def test_wgrad_resnet_layer1_shape():
