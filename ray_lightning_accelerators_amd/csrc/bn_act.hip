@@ -320,12 +320,13 @@ int apply_grid(int64_t M, int C) {
 
 BnPlan bn_plan(int64_t M, int C) {
   const int rpi = kBnThreads / (C >> 3);
-  // >= 16 row iterations per thread, at most 1024 blocks (4 per CU) and 256K partial
-  // floats (1 MB; the wide layers of the last stages got only 64-128 blocks under
-  // the earlier 128K cap -- a quarter of the chip)
+  // >= 16 row iterations per thread, at most 512 blocks (2 per CU: 8 waves with 4-8
+  // rows in flight each keep HBM busy) and 128K partial floats: the finalize kernel
+  // reads the partials with one block per 64 channels, so their count sets its
+  // latency (1024-block partials cost ~5-6 us per finalize, profiles/r3_wgrad)
   int64_t blocks = (M + (int64_t)rpi * 16 - 1) / ((int64_t)rpi * 16);
-  int64_t cap = (int64_t(1) << 18) / C;
-  if (cap > 1024) cap = 1024;
+  int64_t cap = (int64_t(1) << 17) / C;
+  if (cap > 512) cap = 512;
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   BnPlan p;
