@@ -501,7 +501,10 @@ WgradPlan wgrad_plan(const WgradGeom& g, int splits, int algo) {
     const int64_t tiles = (int64_t)(g.Cout / 64) * (g.Cin / 64);
     int64_t S = splits;
     if (S <= 0) {
-      S = (384 + tiles - 1) / tiles;  // ~1.5 workgroups per CU (one fits per CU by registers)
+      // one workgroup per CU (424 registers per lane: one wave per SIMD) in ONE round:
+      // 359 workgroups ran as 256 + 103 (profiles/r3_wgrad/pmc_halo.log: 33% MFMA-busy
+      // waves, the second round on 40% of the chip)
+      S = 256 / tiles;
       if (S > T / 4) S = T / 4;       // >= 4 stages per split
       // fp32 partials (9 taps) at most ~2x the dy + x bytes (the generic kernel
       // re-reads those 9x; the autotuner picks between the two)
