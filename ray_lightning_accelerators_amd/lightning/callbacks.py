@@ -18,6 +18,8 @@ from typing import Any, Dict, Optional
 
 import torch
 
+from ..utils.timeline import mark
+
 from .utilities import log, rank_zero_warn
 
 
@@ -155,26 +157,50 @@ class ModelCheckpoint(Callback):
         if self.dirpath is None:
             self.on_pretrain_routine_start(trainer, pl_module)
         metrics = dict(trainer.callback_metrics)
+        mark("ckpt_cb_begin")
         key = self._monitor_key(metrics)
         self.monitor = key
         top_k = self.save_top_k if self.save_top_k is not None else 1
+        if key is not None and top_k != -1 and key not in metrics:
+            rank_zero_warn(f"ModelCheckpoint(monitor={key!r}) not found in logged metrics")
+            return
+        defer = self.filename is None and getattr(trainer, "deferred_checkpoints_ok", lambda: False)()
+        if defer:
+            # the decision needs the monitored value, which is still being computed
+            # on the device: snapshot the state there and decide / write in the
+            # background once it is known -- the epoch end does not wait for the
+            # device (trainer.defer_checkpoint); the default file name has no metrics
+            filepath = self.format_checkpoint_name(epoch, step, {})
+            value = metrics.get(key) if key is not None else None
+            self.last_global_step_saved = step
+
+            def job(resolve, vals):
+                ckpt = resolve()
+                self._decide(trainer, epoch, step, key, top_k, filepath, vals[0],
+                             lambda path: trainer.write_checkpoint(ckpt, path))
+
+            trainer.defer_checkpoint(job, self.save_weights_only, [value])
+            return
         filepath = self.format_checkpoint_name(epoch, step, metrics)
+        value = _scalar(metrics[key]) if key is not None and top_k != -1 else None
+        mark("ckpt_metric_read")
+        self._decide(trainer, epoch, step, key, top_k, filepath, value, lambda path: self._save(trainer, path))
+
+    def _decide(self, trainer, epoch, step, key, top_k, filepath, value, save) -> None:
+        """Top-k bookkeeping + writes for one save point (``value``: the monitored metric)."""
         if key is None or top_k == -1:
-            self._save(trainer, filepath)
+            save(filepath)
             if self.best_model_path and self.best_model_path != filepath and top_k != -1:
                 self._remove(trainer, self.best_model_path)
             self.best_model_path = filepath
         else:
-            if key not in metrics:
-                rank_zero_warn(f"ModelCheckpoint(monitor={key!r}) not found in logged metrics")
-                return
-            current = torch.as_tensor(_scalar(metrics[key]))
+            current = torch.as_tensor(float(value))
             if not torch.isfinite(current):
                 current = torch.tensor(math.inf if self.mode == "min" else -math.inf)
             self.current_score = current
             if top_k > 0 and self._is_better(current):
                 prev = self.best_model_path
-                self._save(trainer, filepath)
+                save(filepath)
                 self.best_model_score = current
                 self.best_model_path = filepath
                 self.best_k_models = {filepath: current}
@@ -185,7 +211,7 @@ class ModelCheckpoint(Callback):
                     log.warning(f"Epoch {epoch}: {key} reached {float(current):.5f}; saved {filepath}")
         if self.save_last:
             last = os.path.join(self.dirpath, self.CHECKPOINT_NAME_LAST + self.FILE_EXTENSION)
-            self._save(trainer, last)
+            save(last)
             self.last_model_path = last
         self.last_global_step_saved = step
 

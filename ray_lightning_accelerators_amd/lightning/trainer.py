@@ -43,8 +43,10 @@ class _CheckpointConnector:
     def __init__(self, trainer: "Trainer"):
         self.trainer = trainer
 
-    def dump_checkpoint(self, weights_only: bool = False) -> dict:
-        """The Lightning checkpoint dict (PL 1.1 layout; callback keys are class names)."""
+    def dump_checkpoint(self, weights_only: bool = False, staged: bool = False) -> dict:
+        """The Lightning checkpoint dict (PL 1.1 layout; callback keys are class names).
+        ``staged``: device state goes into device-side snapshots (``_Staged``; no
+        host sync) that :func:`_resolve_staged` turns into host tensors later."""
         t = self.trainer
         model = t.get_model()
         ckpt: Dict[str, Any] = {
@@ -59,9 +61,9 @@ class _CheckpointConnector:
                 if st is not None:
                     cb_states[cb.state_key] = st
             ckpt["callbacks"] = cb_states
-            ckpt["optimizer_states"] = [t._optimizer_state_dict(o) for o in t.optimizers]
+            ckpt["optimizer_states"] = [t._optimizer_state_dict(o, staged) for o in t.optimizers]
             ckpt["lr_schedulers"] = [s["scheduler"].state_dict() for s in t.lr_schedulers]
-        ckpt["state_dict"] = t._model_state_dict(model)
+        ckpt["state_dict"] = t._model_state_dict(model, staged)
         hp = dict(model.hparams) if getattr(model, "hparams", None) else {}
         if hp:
             ckpt[LightningModule.CHECKPOINT_HYPER_PARAMS_NAME] = "hparams"
@@ -326,7 +328,10 @@ class Trainer:
         """``blocking=False`` (ModelCheckpoint): the checkpoint dict is built now and
         written by the background writer (``RLAConfig.async_checkpoint``); a
         blocking save first drains earlier background writes (file order kept)."""
+        self.wait_deferred()  # earlier background saves first (one writer, file order kept)
+        mark("ckpt_dump_begin")
         ckpt = self.checkpoint_connector.dump_checkpoint(weights_only)
+        mark("ckpt_dumped")
         if not self.is_global_zero:
             return
         if not blocking and get_config().async_checkpoint:
@@ -337,9 +342,19 @@ class Trainer:
             if w.ready() or getattr(self, "_ckpt_writer", None) is w:
                 self._ckpt_writer = w
                 w.save(ckpt, filepath)
+                mark("ckpt_handed_off")
                 return
         self.wait_checkpoints()
         atomic_save(ckpt, filepath)
+
+    def write_checkpoint(self, ckpt: dict, filepath: str) -> None:
+        """Write an already-built checkpoint dict (the deferred saves' path): through
+        the writer process when it is up, else in place."""
+        w = getattr(self, "_ckpt_writer", None)
+        if w is not None and w.alive():
+            w.save(ckpt, filepath)
+        else:
+            atomic_save(ckpt, filepath)
 
     def file_op(self, fn, *args) -> None:
         """Run a checkpoint-file operation (e.g. a top-k removal) after the pending
@@ -352,6 +367,7 @@ class Trainer:
 
     def wait_checkpoints(self) -> None:
         """Block until every background checkpoint write has landed (re-raises a failed one)."""
+        self.wait_deferred()
         w = getattr(self, "_ckpt_writer", None)
         if w is not None:
             w.wait()
@@ -439,6 +455,9 @@ class Trainer:
             self.run_train()
         finally:
             self.wait_checkpoints()  # every checkpoint file is on disk when fit returns
+        f = self._fused
+        if f is not None and hasattr(f, "check"):
+            f.check(blocking=True)  # the epoch-end checks trail by one epoch: the last one here
         model.teardown("fit")
         return None
 
@@ -776,7 +795,9 @@ class Trainer:
                 self._stage_pending_log()
             else:
                 self._flush_logger()
-        out = [_floats(metrics)]
+        # inside fit nobody reads the returned floats: no host sync for them (the
+        # epoch end then never waits for the device; validate()/test() do convert)
+        out = [metrics] if (self.training and not self.running_sanity_check) else [_floats(metrics)]
         mark("eval_done", stage=stage)
         return out
 
@@ -939,7 +960,7 @@ class Trainer:
         # means a block overwrote state another block was still reading)
         f = getattr(self, "_fused", None)
         if f is not None and hasattr(f, "check"):
-            f.check()
+            f.check(blocking=False)  # the previous epoch's flag: no device sync here
 
     def _dispatch_chunk(self, model: LightningModule) -> int:
         """Steps per host dispatch of the fused resident step (1 = one per batch).
@@ -1165,12 +1186,13 @@ class Trainer:
                 self._fused.on_lr_change()
 
     # ---------------------------------------------------------------- state
-    def _model_state_dict(self, model: LightningModule) -> Dict[str, torch.Tensor]:
+    def _model_state_dict(self, model: LightningModule, staged: bool = False):
         if self._fused is not None:
             self._fused.sync_params_to_module()
-        return _to_cpu(dict(model.state_dict()))
+        sd = dict(model.state_dict())
+        return _Staged(sd) if staged else _to_cpu(sd)
 
-    def _optimizer_state_dict(self, opt) -> dict:
+    def _optimizer_state_dict(self, opt, staged: bool = False):
         if self._fused is not None and hasattr(self._fused, "optimizer_state_dict"):
             return self._fused.optimizer_state_dict()
         if self._fused is not None and hasattr(self._fused, "sync_optimizer_state"):
@@ -1178,13 +1200,50 @@ class Trainer:
             # state lives on its owner rank until consolidated (collective; every
             # rank dumps the checkpoint)
             self._fused.sync_optimizer_state()
-        return _to_cpu(opt.state_dict())
+        sd = opt.state_dict()
+        return _Staged(sd) if staged else _to_cpu(sd)
+
+    # ------------------------------------------------- deferred checkpoints
+    def deferred_checkpoints_ok(self) -> bool:
+        """Whether ModelCheckpoint may hand its epoch-end save to the background
+        (``_DeferredCheckpoints``): rank 0 of a single-rank GPU fit whose checkpoint
+        writer is configured (``RLA_DEFER_CKPT=0`` turns it off).  At world > 1 every
+        rank dumps the checkpoint (collective state consolidation), so it stays inline."""
+        if os.environ.get("RLA_DEFER_CKPT", "1") == "0" or not get_config().async_checkpoint:
+            return False
+        if not (self.on_gpu and torch.cuda.is_available() and self.is_global_zero):
+            return False
+        # (without the writer process the background thread pickles the file itself)
+        return getattr(self, "world_size", 1) == 1 and self._fused is not None
+
+    def defer_checkpoint(self, job, weights_only: bool, values=()):
+        """Snapshot the checkpoint state ON THE DEVICE now (stream-ordered copies, no
+        host sync) and queue ``job(resolve, values)`` for the background thread, which
+        runs it once the device has produced that state: ``resolve()`` returns the
+        host checkpoint dict, ``values`` (device scalars, e.g. the monitored metric)
+        arrive as floats.  The training loop keeps dispatching meanwhile."""
+        mark("ckpt_stage_begin")
+        q = getattr(self, "_deferred", None)
+        if q is None:
+            q = self._deferred = _DeferredCheckpoints()
+        q.drain_done()  # earlier decisions (best model path / score) are in place
+        ckpt = self.checkpoint_connector.dump_checkpoint(weights_only, staged=True)
+        vals = [v.detach().reshape(()).double().clone() if isinstance(v, torch.Tensor) and v.is_cuda else v
+                for v in values]
+        q.submit(ckpt, vals, job)
+        mark("ckpt_staged")
+
+    def wait_deferred(self) -> None:
+        q = getattr(self, "_deferred", None)
+        if q is not None:
+            q.wait()
 
     def __getstate__(self):
         d = self.__dict__.copy()
         d["_fused"] = None
         d["_pending_log"] = None
         d["_ckpt_writer"] = None
+        d["_deferred"] = None
         d["accelerator_backend"] = None
         return d
 
@@ -1249,3 +1308,137 @@ def _to_cpu(obj):
         return o
 
     return rebuild(obj)
+
+
+class _Staged:
+    """A (nested) state dict whose device tensors were copied into device-side flat
+    buffers (one per device / dtype, stream-ordered: no host sync) and whose host
+    tensors were cloned, at staging time; :meth:`host` makes the host copy."""
+
+    def __init__(self, obj):
+        leaves: List[torch.Tensor] = []
+        self._cpu: Dict[int, torch.Tensor] = {}
+
+        def collect(o):
+            if isinstance(o, torch.Tensor):
+                if o.device.type != "cpu" and o.numel() > 0:
+                    leaves.append(o)
+                elif id(o) not in self._cpu:
+                    self._cpu[id(o)] = o.detach().clone()  # e.g. Adam's step: changes in place
+            elif isinstance(o, dict):
+                for v in o.values():
+                    collect(v)
+            elif isinstance(o, (list, tuple)):
+                for v in o:
+                    collect(v)
+
+        collect(obj)
+        self._obj = obj
+        seen: Dict[int, bool] = {}
+        groups: Dict[tuple, List[torch.Tensor]] = {}
+        for t in leaves:
+            if id(t) not in seen:
+                seen[id(t)] = True
+                groups.setdefault((t.device, t.dtype), []).append(t)
+        self._groups = [(ts, torch.cat([t.detach().reshape(-1) for t in ts]) if len(ts) > 1 else
+                         ts[0].detach().reshape(-1).clone()) for ts in groups.values()]
+
+    def host(self):
+        host: Dict[int, torch.Tensor] = dict(self._cpu)
+        for ts, flat in self._groups:
+            hflat = flat.cpu()
+            off = 0
+            for t in ts:
+                n = t.numel()
+                host[id(t)] = hflat[off: off + n].view(t.shape).clone()  # own storage (see _to_cpu)
+                off += n
+
+        def rebuild(o):
+            if isinstance(o, torch.Tensor):
+                return host[id(o)] if id(o) in host else o.detach().cpu()
+            if isinstance(o, dict):
+                return {k: rebuild(v) for k, v in o.items()}
+            if isinstance(o, (list, tuple)):
+                return type(o)(rebuild(v) for v in o)
+            return o
+
+        out = rebuild(self._obj)
+        self._groups, self._obj = [], None
+        return out
+
+
+def _resolve_staged(o):
+    if isinstance(o, _Staged):
+        return o.host()
+    if isinstance(o, dict):
+        return {k: _resolve_staged(v) for k, v in o.items()}
+    if isinstance(o, list):
+        return [_resolve_staged(v) for v in o]
+    return o
+
+
+class _DeferredCheckpoints:
+    """One background thread that finishes staged checkpoint saves in order.
+
+    The main thread stages the state on the device and records an event; the
+    thread makes its device-to-host copies on its OWN stream after waiting for
+    that event only -- so neither the copies nor the wait queue behind the next
+    epoch's work the main thread keeps dispatching (on the default stream a D2H
+    copy would wait for all of it), and the main thread never blocks at the epoch
+    end.  ``job`` decides (ModelCheckpoint's top-k on the now-known metric), writes
+    through the checkpoint writer process and removes superseded files, in
+    submission order.  Errors re-raise on the next :meth:`wait` / ``drain_done``."""
+
+    def __init__(self):
+        import queue
+        import threading
+
+        self._q: "queue.Queue" = queue.Queue()
+        self._err: Optional[BaseException] = None
+        self._pending = 0
+        self._cv = threading.Condition()
+        self._stream = torch.cuda.Stream()
+        self._t = threading.Thread(target=self._loop, name="rla-deferred-ckpt", daemon=True)
+        self._t.start()
+
+    def submit(self, ckpt, values, job) -> None:
+        ev = torch.cuda.Event()
+        ev.record()
+        with self._cv:
+            self._pending += 1
+        self._q.put((ckpt, values, job, ev))
+
+    def _loop(self) -> None:
+        while True:
+            item = self._q.get()
+            if item is None:
+                return
+            ckpt, values, job, ev = item
+            try:
+                with torch.cuda.stream(self._stream):
+                    self._stream.wait_event(ev)
+                    vals = [float(v.cpu()) if isinstance(v, torch.Tensor) else v for v in values]
+                    job(lambda: _resolve_staged(ckpt), vals)
+            except BaseException as e:  # surfaced on the main thread
+                self._err = e
+            finally:
+                del ckpt, values, item
+                with self._cv:
+                    self._pending -= 1
+                    self._cv.notify_all()
+
+    def _raise(self) -> None:
+        if self._err is not None:
+            e, self._err = self._err, None
+            raise RuntimeError(f"deferred checkpoint save failed: {e!r}") from e
+
+    def drain_done(self) -> None:
+        """Wait for the queued saves (their device state was produced long ago when
+        the next one is staged: this returns at once in steady state)."""
+        self.wait()
+
+    def wait(self) -> None:
+        with self._cv:
+            while self._pending:
+                self._cv.wait()
+        self._raise()

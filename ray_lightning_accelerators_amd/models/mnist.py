@@ -540,10 +540,11 @@ class FusedMNISTStep:
         tot = part.sum(0) / n
         return {"val_loss": tot[0], "val_accuracy": tot[1]}
 
-    def check(self) -> None:
-        """Raise if the engine's in-launch hand-off ever timed out (epoch end)."""
+    def check(self, blocking: bool = True) -> None:
+        """Raise if the engine's in-launch hand-off ever timed out (epoch end:
+        ``blocking=False`` checks the previous epoch's asynchronously copied flag)."""
         if self.eng is not None:
-            self.eng.check()
+            self.eng.check(blocking)
 
     def sync_optimizer_state(self) -> None:
         """Owner protocol: consolidate the Adam state before it is read (collective)."""

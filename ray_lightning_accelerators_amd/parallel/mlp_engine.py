@@ -222,11 +222,33 @@ class FusedMLPEngine:
         """Host edits of the device state go to both copies (current / advanced)."""
         self.counters[5:10].copy_(self.counters[0:5])
 
-    def check(self) -> None:
+    def check(self, blocking: bool = True) -> None:
         """Raise if a one-launch step's in-launch hand-off ever timed out (a block
-        polled past its bound: the step it belongs to is not trustworthy)."""
-        if self.native and int(self.hand[16].item()) != 0:
-            raise RuntimeError("fused MLP one-launch step: an in-launch hand-off timed out")
+        polled past its bound: the step it belongs to is not trustworthy).
+        ``blocking=False`` (the Trainer's epoch ends): the flag is copied to pinned
+        host memory asynchronously and the copy made at the PREVIOUS call is the one
+        checked -- no device sync at an epoch boundary, detection one epoch late; a
+        blocking call at the end of the fit reads the current value."""
+        if not self.native:
+            return
+        prev = getattr(self, "_hand_probe", None)
+        if prev is not None:
+            buf, ev = prev
+            ev.synchronize()  # enqueued one epoch ago: long complete
+            self._hand_probe = None
+            if int(buf[0]) != 0:
+                raise RuntimeError("fused MLP one-launch step: an in-launch hand-off timed out")
+        if blocking:
+            if int(self.hand[16].item()) != 0:
+                raise RuntimeError("fused MLP one-launch step: an in-launch hand-off timed out")
+            return
+        buf = getattr(self, "_hand_pin", None)
+        if buf is None:
+            buf = self._hand_pin = torch.zeros(1, dtype=self.hand.dtype, pin_memory=True)
+        buf.copy_(self.hand[16:17], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._hand_probe = (buf, ev)
 
     def set_step(self, step: int) -> None:
         self.counters[0] = int(step)

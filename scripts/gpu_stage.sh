@@ -62,6 +62,8 @@ for st in "$@"; do
     tunetl)  # cold sweep with the cross-process start-up timeline
       RLA_TIMELINE="$R/$O/tune_timeline.jsonl" run tune_tl 300 python scripts/bench_tune.py --trials 6
       python scripts/timeline_report.py "$O/tune_timeline.jsonl" --merged > "$O/tune_timeline.txt" 2>&1 || true ;;
+    trainertests)  # Trainer / checkpoint GPU tests
+      run pytest_trainer 600 $PYT tests/test_checkpoint_writer.py tests/test_dispatch.py tests/test_fused_validation.py tests/test_trainer.py -m gpu ;;
     trainer)
       RLA_TIMELINE="$R/$O/trainer_timeline.jsonl" run trainer 300 python bench.py --via trainer --trainer-epochs 6
       python scripts/timeline_report.py "$O/trainer_timeline.jsonl" > "$O/trainer_timeline.txt" 2>&1 || true ;;

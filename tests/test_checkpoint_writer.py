@@ -129,3 +129,54 @@ def test_process_checkpoint_writer_matches_atomic_save(tmp_path):
         w.save(ck, "/proc/definitely/not/writable.ckpt")
         w.wait()
     w.close()
+
+
+@pytest.mark.gpu
+def test_deferred_checkpoints_match_inline(tmp_path, monkeypatch):
+    """ModelCheckpoint's epoch-end save deferred to the background (device snapshot,
+    decision once the monitored val_loss is known, no host sync at the epoch end)
+    writes the same files with the same contents as the inline save of an
+    identical, deterministic fit (fused MNIST step on the GPU)."""
+    import torch
+
+    from ray_lightning_accelerators_amd import lightning as pl
+    from ray_lightning_accelerators_amd.lightning.callbacks import ModelCheckpoint
+    from ray_lightning_accelerators_amd.lightning.utilities import load_checkpoint
+    from ray_lightning_accelerators_amd.models.mnist import MNISTClassifier
+
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+
+    def fit(defer: str, root):
+        monkeypatch.setenv("RLA_DEFER_CKPT", defer)
+        torch.manual_seed(0)
+        model = MNISTClassifier({"layer_1": 32, "layer_2": 64, "lr": 1e-3, "batch_size": 32})
+        ckpt = ModelCheckpoint(dirpath=str(root), save_last=True)
+        trainer = pl.Trainer(default_root_dir=str(root), max_epochs=3, gpus=1, progress_bar_refresh_rate=0,
+                             callbacks=[ckpt], limit_train_batches=120, limit_val_batches=20)
+        assert trainer.fit(model) == 1
+        deferred = getattr(trainer, "_deferred", None) is not None
+        files = sorted(p.name for p in root.iterdir() if p.suffix == ".ckpt")
+        return trainer, ckpt, files, deferred
+
+    t_in, c_in, f_in, d_in = fit("0", tmp_path / "inline")
+    t_df, c_df, f_df, d_df = fit("1", tmp_path / "deferred")
+    assert not d_in and d_df, "the deferred path was not taken"
+    assert f_in == f_df and "last.ckpt" in f_df
+    assert os.path.basename(c_in.best_model_path) == os.path.basename(c_df.best_model_path)
+    sa, sb = c_in.best_model_score, c_df.best_model_score
+    assert (sa is None and sb is None) or float(sa) == float(sb)
+    for name in f_in:
+        a = load_checkpoint(str(tmp_path / "inline" / name))
+        b = load_checkpoint(str(tmp_path / "deferred" / name))
+        assert a["epoch"] == b["epoch"] and a["global_step"] == b["global_step"]
+        for k in a["state_dict"]:
+            assert torch.equal(a["state_dict"][k], b["state_dict"][k]), (name, k)
+        sa, sb = a["optimizer_states"][0]["state"], b["optimizer_states"][0]["state"]
+        for i in sa:
+            for k in sa[i]:
+                assert torch.equal(torch.as_tensor(sa[i][k]), torch.as_tensor(sb[i][k])), (name, i, k)
+    # the last checkpoint holds the final weights
+    last = load_checkpoint(str(tmp_path / "deferred" / "last.ckpt"))
+    for k, v in t_df.get_model().state_dict().items():
+        assert torch.equal(last["state_dict"][k], v.detach().cpu()), k
