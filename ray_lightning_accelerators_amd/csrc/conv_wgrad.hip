@@ -75,7 +75,7 @@ __device__ __forceinline__ int64_t x_row(int64_t m, const WgradGeom& g, int r, i
   return (int64_t)((n * g.H + ih) * g.W + iw);
 }
 
-template <int WA, int WB, bool GEN>
+template <int WA, int WB, bool GEN, int DEPTH = 4>
 __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t* __restrict__ dy,
                                                            const uint16_t* __restrict__ x, float* __restrict__ out,
                                                            WgradGeom g, int64_t M, int64_t rows_per_split,
@@ -207,25 +207,27 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t* __res
   // count runs one all-zero stage more): a load whose value were used only inside
   // an `if` would be sunk by the compiler next to that use -- the LDS store that
   // waits for it -- and the prefetch would be lost.
+  // DEPTH register sets: stage k lives in set k % DEPTH, so DEPTH - 1 stages are
+  // in flight while one is computed (4: the latency-bound small-row layers)
   auto step = [&](int it, Set& cur, Set& nxt) {
-    load(cur, mb + (int64_t)(it + 2) * KB);  // past the split's end: masked, harmless
+    load(cur, mb + (int64_t)(it + DEPTH) * KB);  // past the split's end: masked, harmless
     __builtin_amdgcn_sched_barrier(0);  // loads stay ahead of the MFMAs
     compute(it & 1);
     __builtin_amdgcn_sched_barrier(0);
     store(nxt, (it + 1) & 1);  // stage it + 1 (past the end: zeros, never read)
     __syncthreads();
   };
-  Set s0, s1;
-  const int nst2 = (nst + 1) & ~1;
-  if (nst2 > 0) {
-    load(s0, mb);
-    load(s1, mb + KB);
-    store(s0, 0);
+  Set st[DEPTH];
+  const int nstd = (nst + DEPTH - 1) / DEPTH * DEPTH;
+  if (nstd > 0) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) load(st[d], mb + (int64_t)d * KB);
+    store(st[0], 0);
   }
   __syncthreads();
-  for (int it = 0; it < nst2; it += 2) {  // unrolled by two: the register sets stay static
-    step(it, s0, s1);
-    step(it + 1, s1, s0);
+  for (int it = 0; it < nstd; it += DEPTH) {  // unrolled by DEPTH: the register sets stay static
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) step(it + d, st[d], st[(d + 1) % DEPTH]);
   }
 
   // reduction split: waves ks > 0 hand their tiles to ks == 0 through LDS (fixed order)
