@@ -180,3 +180,30 @@ def test_deferred_checkpoints_match_inline(tmp_path, monkeypatch):
     last = load_checkpoint(str(tmp_path / "deferred" / "last.ckpt"))
     for k, v in t_df.get_model().state_dict().items():
         assert torch.equal(last["state_dict"][k], v.detach().cpu()), k
+
+
+def test_staged_state_is_a_snapshot():
+    """_Staged (the deferred checkpoint's state) copies at staging time: later
+    in-place updates -- Adam's CPU step counter, parameters -- do not leak into the
+    host dict it produces, and its layout equals _to_cpu's."""
+    from ray_lightning_accelerators_amd.lightning.trainer import _resolve_staged, _Staged, _to_cpu
+
+    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    w = torch.arange(6.0, device=dev).view(2, 3)
+    b = torch.ones(3, device=dev, dtype=torch.float64)
+    step = torch.tensor(5.0)
+    sd = {"state": {0: {"exp_avg": w, "step": step}, 1: {"exp_avg": b}}, "param_groups": [{"lr": 0.1}],
+          "w": w}
+    expect = {k: v.clone() for k, v in _to_cpu({"w": w, "b": b}).items()}  # (CPU: _to_cpu aliases)
+    staged = {"optimizer_states": [_Staged(sd)], "epoch": 3}
+    w.add_(100.0)
+    b.mul_(7.0)
+    step.fill_(9.0)
+    got = _resolve_staged(staged)
+    assert got["epoch"] == 3
+    host = got["optimizer_states"][0]
+    assert torch.equal(host["state"][0]["exp_avg"], expect["w"])
+    assert torch.equal(host["state"][1]["exp_avg"], expect["b"])
+    assert float(host["state"][0]["step"]) == 5.0
+    assert host["param_groups"] == [{"lr": 0.1}]
+    assert host["state"][0]["exp_avg"].device.type == "cpu"
