@@ -75,7 +75,7 @@ __device__ __forceinline__ int64_t x_row(int64_t m, const WgradGeom& g, int r, i
   return (int64_t)((n * g.H + ih) * g.W + iw);
 }
 
-template <int WA, int WB, bool GEN, int DEPTH = 4>
+template <int WA, int WB, bool GEN, int DEPTH = 2>
 __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t* __restrict__ dy,
                                                            const uint16_t* __restrict__ x, float* __restrict__ out,
                                                            WgradGeom g, int64_t M, int64_t rows_per_split,
@@ -208,7 +208,8 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t* __res
   // an `if` would be sunk by the compiler next to that use -- the LDS store that
   // waits for it -- and the prefetch would be lost.
   // DEPTH register sets: stage k lives in set k % DEPTH, so DEPTH - 1 stages are
-  // in flight while one is computed (4: the latency-bound small-row layers)
+  // in flight while one is computed (2: four measured no faster -- equal on 1x1,
+  // up to 20 % slower on the strided / 3x3 generic shapes, profiles/r3_wgrad/wgrad_probe_depth4.log)
   auto step = [&](int it, Set& cur, Set& nxt) {
     load(cur, mb + (int64_t)(it + DEPTH) * KB);  // past the split's end: masked, harmless
     __builtin_amdgcn_sched_barrier(0);  // loads stay ahead of the MFMAs
