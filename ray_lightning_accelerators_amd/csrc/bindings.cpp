@@ -570,6 +570,14 @@ std::vector<int64_t> conv_wgrad_plan(int64_t N, int64_t H, int64_t W, int64_t Ci
   return {p.kind, p.wa, p.wb, p.splits, p.rows_per_split};
 }
 
+Tensor dp_pack_roundtrip(Tensor x, int64_t tag) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous(), "x: contiguous fp32 on the GPU");
+  Tensor y = at::empty_like(x);
+  TORCH_CHECK(rla::dp_pack_roundtrip(x.data_ptr<float>(), y.data_ptr<float>(), x.numel(), (int)tag, cur_stream(x)) == 0,
+              "dp_pack_roundtrip: bad arguments");
+  return y;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -589,6 +597,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp_eval", &mlp_eval, "fused MNIST-MLP forward + NLL/accuracy");
   m.def("mlp3", &mlp3, "fused MNIST-MLP step v3 (pipelined layer 1): kind 0 step, 1 head, 2 tail-grad, "
         "3 tail-adam, 4 prime, 5 step with the in-kernel xGMI exchange, 6 one-launch step (B <= 32)");
+  m.def("dp_pack_roundtrip", &dp_pack_roundtrip, "packed DP exchange wire form of fp32 pairs, encoded + decoded");
   m.def("mlp3_hand_words", [](int64_t l1, int64_t l2) { return rla::mlp3_hand_words((int)l1, (int)l2); });
   m.def("mlp3_dp_area_floats", []() { return rla::comm::kDpUnitAreaFloats; },
         "aux receive-area stride (floats) of the one-launch step's packed / owner protocols");

@@ -209,6 +209,8 @@ enum MLP3Kind { kMLP3Step = 0, kMLP3Head = 1, kMLP3TailGrad = 2, kMLP3TailAdam =
 int64_t mlp3_hand_words(int L1, int L2);  // int64 words of the one-launch step's hand-off buffer
 int launch_mlp3(const MLP3Args& a, int kind, hipStream_t stream);
 int mlp3_act_rows(int L1, int L2);
+// the packed DP exchange's wire form of fp32 pairs, encoded and decoded (tests)
+int dp_pack_roundtrip(const float* x, float* y, int64_t n, int tag, hipStream_t stream);
 
 // returns 0 on success, -1 if (L1, L2) has no compiled instantiation
 int launch_mlp_train_step(const MLPStepArgs& a, hipStream_t stream);

@@ -984,9 +984,19 @@ __device__ __forceinline__ float dp_sum1(const MLP3Args& a, int slot, int64_t id
 // ---------------------------------------------------------------------------
 typedef unsigned long long u64;
 
+// v0's wire form: rounded to a multiple of 4 ulp, never carried into the exponent
+// (a mantissa within 2 ulp of all-ones truncates: FLT_MAX stays finite), non-finite
+// values kept non-finite -- an infinity keeps a zero mantissa above the tag bits
+// (the reader masks them off), a NaN gets its quiet bit so the tag cannot turn it
+// into an infinity.
+__device__ __forceinline__ uint32_t pk_round(float v) {
+  const uint32_t b = __float_as_uint(v), man = b & 0x7fffffu;
+  uint32_t r = man >= 0x7ffffeu ? b : b + 2u;
+  if ((b & 0x7f800000u) == 0x7f800000u) r = man ? (b | 0x400000u) : b;
+  return r & ~3u;
+}
 __device__ __forceinline__ u64 pk2(float v0, float v1, uint32_t tag) {
-  const uint32_t b0 = ((__float_as_uint(v0) + 2u) & ~3u) | tag;
-  return ((u64)__float_as_uint(v1) << 32) | (u64)b0;
+  return ((u64)__float_as_uint(v1) << 32) | (u64)(pk_round(v0) | tag);
 }
 __device__ __forceinline__ float pk_lo(u64 w) { return __uint_as_float((uint32_t)w & ~3u); }
 __device__ __forceinline__ float pk_hi(u64 w) { return __uint_as_float((uint32_t)(w >> 32)); }
@@ -1791,7 +1801,25 @@ int dispatch3(const MLP3Args& a, int kind, hipStream_t stream) {
 
 static_assert(fits3<kHeadRows, 128, 256>(), "v3 head LDS budget");
 
+__global__ void dp_pack_roundtrip_kernel(const float* x, float* y, int64_t n, uint32_t tag) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (2 * i + 1 < n + 1) {
+    const float v0 = x[2 * i], v1 = 2 * i + 1 < n ? x[2 * i + 1] : 0.f;
+    const u64 w = pk2(v0, v1, tag);
+    y[2 * i] = ((uint32_t)w & 3u) == tag ? pk_lo(w) : __builtin_nanf("");
+    if (2 * i + 1 < n) y[2 * i + 1] = pk_hi(w);
+  }
+}
+
 }  // namespace
+
+int dp_pack_roundtrip(const float* x, float* y, int64_t n, int tag, hipStream_t stream) {
+  if (n <= 0 || tag < 0 || tag > 3) return -1;
+  const int64_t pairs = (n + 1) / 2;
+  hipLaunchKernelGGL(dp_pack_roundtrip_kernel, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, stream, x, y, n,
+                     (uint32_t)tag);
+  return 0;
+}
 
 int mlp3_act_rows(int L1, int L2) { return L1 + 2 * L2 + 16; }
 int64_t mlp3_hand_words(int, int) { return kHandWords; }

@@ -176,8 +176,16 @@ class ModelCheckpoint(Callback):
 
             def job(resolve, vals):
                 ckpt = resolve()
-                self._decide(trainer, epoch, step, key, top_k, filepath, vals[0],
-                             lambda path: trainer.write_checkpoint(ckpt, path))
+
+                def write(path):
+                    # the dict was dumped before this save point's decision: its
+                    # ModelCheckpoint entry is refreshed with the decided state
+                    if "callbacks" in ckpt:
+                        ckpt["callbacks"] = dict(ckpt["callbacks"])
+                        ckpt["callbacks"][self.state_key] = self.on_save_checkpoint(trainer, None)
+                    trainer.write_checkpoint(ckpt, path)
+
+                self._decide(trainer, epoch, step, key, top_k, filepath, vals[0], write)
 
             trainer.defer_checkpoint(job, self.save_weights_only, [value])
             return
@@ -187,12 +195,18 @@ class ModelCheckpoint(Callback):
         self._decide(trainer, epoch, step, key, top_k, filepath, value, lambda path: self._save(trainer, path))
 
     def _decide(self, trainer, epoch, step, key, top_k, filepath, value, save) -> None:
-        """Top-k bookkeeping + writes for one save point (``value``: the monitored metric)."""
+        """Top-k bookkeeping + writes for one save point (``value``: the monitored metric).
+
+        As PL 1.1.7's ``_update_best_and_save``: the best / current fields are
+        updated BEFORE the file is written, so the checkpoint's own
+        ``callbacks[ModelCheckpoint]`` entry names this file as the best one and
+        carries this save point's score (a resume from it restores them)."""
         if key is None or top_k == -1:
-            save(filepath)
-            if self.best_model_path and self.best_model_path != filepath and top_k != -1:
-                self._remove(trainer, self.best_model_path)
+            prev = self.best_model_path
             self.best_model_path = filepath
+            save(filepath)
+            if prev and prev != filepath and top_k != -1:
+                self._remove(trainer, prev)
         else:
             current = torch.as_tensor(float(value))
             if not torch.isfinite(current):
@@ -200,11 +214,11 @@ class ModelCheckpoint(Callback):
             self.current_score = current
             if top_k > 0 and self._is_better(current):
                 prev = self.best_model_path
-                save(filepath)
                 self.best_model_score = current
                 self.best_model_path = filepath
                 self.best_k_models = {filepath: current}
                 self.kth_best_model_path = filepath
+                save(filepath)
                 if prev and prev != filepath:
                     self._remove(trainer, prev)
                 if self.verbose:

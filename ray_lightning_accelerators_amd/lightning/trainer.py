@@ -351,6 +351,15 @@ class Trainer:
         """Write an already-built checkpoint dict (the deferred saves' path): through
         the writer process when it is up, else in place."""
         w = getattr(self, "_ckpt_writer", None)
+        if w is None and get_config().async_checkpoint:
+            # the writer process started for this worker (ddp_train pre-warms it):
+            # pickling and file I/O leave this process's GIL; later removals
+            # (file_op) and wait_checkpoints order behind these writes
+            from . import utilities as _u
+
+            pw = _u._process_writer  # never started here (a spawn from this thread)
+            if pw is not None and pw.alive() and pw.ready():
+                self._ckpt_writer = w = pw
         if w is not None and w.alive():
             w.save(ckpt, filepath)
         else:
@@ -777,6 +786,8 @@ class Trainer:
         metrics.update(self._reduce_epoch_metrics(f"{stage}_epoch_end"))
         self.call_hook(f"on_{stage}_epoch_end")
         mark("eval_epoch_end_hooks", stage=stage)
+        if stage == "validation" and not self.running_sanity_check:
+            self._consolidate_optimizer_state()
         self.call_hook(f"on_{stage}_end")
         mark("eval_end_hooks", stage=stage)
         if stage == "validation" and getattr(self, "world_size", 1) > 1:
@@ -1195,13 +1206,27 @@ class Trainer:
     def _optimizer_state_dict(self, opt, staged: bool = False):
         if self._fused is not None and hasattr(self._fused, "optimizer_state_dict"):
             return self._fused.optimizer_state_dict()
-        if self._fused is not None and hasattr(self._fused, "sync_optimizer_state"):
+        if (self._fused is not None and hasattr(self._fused, "sync_optimizer_state")
+                and getattr(self, "_opt_state_synced_step", None) != self.global_step):
             # fused data-parallel step with the owner protocol: every element's Adam
             # state lives on its owner rank until consolidated (collective; every
-            # rank dumps the checkpoint)
+            # rank dumps the checkpoint).  At validation ends it already ran on every
+            # rank (_consolidate_optimizer_state): ModelCheckpoint's per-rank save
+            # decision cannot strand a rank inside this collective.
             self._fused.sync_optimizer_state()
         sd = opt.state_dict()
         return _Staged(sd) if staged else _to_cpu(sd)
+
+    def _consolidate_optimizer_state(self) -> None:
+        """Validation end at world > 1: the owner-protocol Adam state is consolidated
+        on EVERY rank before the checkpoint callbacks run (a collective at a point
+        every rank reaches), so a checkpoint dump on only some ranks needs none."""
+        if (getattr(self, "world_size", 1) > 1 and self._fused is not None
+                and hasattr(self._fused, "sync_optimizer_state") and self.training
+                and any(hasattr(cb, "best_model_path") or "Checkpoint" in type(cb).__name__
+                        for cb in self.callbacks)):
+            self._fused.sync_optimizer_state()
+            self._opt_state_synced_step = self.global_step
 
     # ------------------------------------------------- deferred checkpoints
     def deferred_checkpoints_ok(self) -> bool:

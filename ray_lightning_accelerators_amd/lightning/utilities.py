@@ -287,13 +287,15 @@ class ProcessCheckpointWriter:
             shm.unlink()
             raise
         self._pending.append(shm)
-        self._conn.send(("save", skel, metas, shm.name, filepath))
+        # absolute: the writer process keeps the directory it started in, while this
+        # process changes it (a recycled worker per assignment, a Tune trial per trial)
+        self._conn.send(("save", skel, metas, shm.name, os.path.abspath(filepath)))
 
     def submit(self, fn, *args) -> None:
         """File operations after the pending writes (only removals are shipped)."""
         if getattr(fn, "__name__", "") == "_remove_file" and len(args) == 1:
             self._pending.append(None)
-            self._conn.send(("remove", args[0]))
+            self._conn.send(("remove", os.path.abspath(args[0])))
         else:
             self.wait()
             fn(*args)

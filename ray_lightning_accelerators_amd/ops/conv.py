@@ -46,6 +46,7 @@ def _wmode() -> str:
 
 
 _REPS = 3
+_DETERMINISTIC_ORDER = ("hip", "hip_gen", "gemm", "miopen")
 
 
 def _time(fn, reps: int = _REPS) -> float:
@@ -72,6 +73,13 @@ def _pick(op: str, key: Tuple[int, ...], cands) -> str:
         mode = _wmode() if _wmode() != "auto" or op != "wgrad" else mode
     if mode in cands:
         return mode
+    if torch.are_deterministic_algorithms_enabled():
+        # Trainer(deterministic=True): no timing (two runs could pick different
+        # kernels that round differently), and never MIOpen's split-K-atomic wgrad:
+        # the MFMA kernel (fixed-order split reduction), else the GEMM
+        for name in _DETERMINISTIC_ORDER:
+            if name in cands:
+                return name
     k = (op,) + key
     c = _choice.get(k)
     if c is None and torch.cuda.is_current_stream_capturing():

@@ -131,6 +131,33 @@ def test_process_checkpoint_writer_matches_atomic_save(tmp_path):
     w.close()
 
 
+def test_process_writer_follows_cwd_changes(tmp_path, monkeypatch):
+    """one writer process serves a recycled worker across fits / Tune
+    trials that chdir into their own directory; relative checkpoint paths (and
+    top-k removals) resolve against the TRAINING process's current directory."""
+    import os
+
+    from ray_lightning_accelerators_amd.lightning.utilities import ProcessCheckpointWriter
+
+    w = ProcessCheckpointWriter()
+
+    def _remove_file(p):
+        os.remove(p)
+
+    try:
+        for trial in ("trial_a", "trial_b"):
+            d = tmp_path / trial
+            (d / "ckpt").mkdir(parents=True)
+            monkeypatch.chdir(d)
+            w.save({"epoch": 1, "w": torch.ones(3)}, os.path.join("ckpt", "e0.ckpt"))
+            w.save({"epoch": 2, "w": torch.ones(3)}, os.path.join("ckpt", "e1.ckpt"))
+            w.submit(_remove_file, os.path.join("ckpt", "e0.ckpt"))
+            w.wait()
+            assert sorted(os.listdir(d / "ckpt")) == ["e1.ckpt"], trial
+    finally:
+        w.close()
+
+
 @pytest.mark.gpu
 def test_deferred_checkpoints_match_inline(tmp_path, monkeypatch):
     """ModelCheckpoint's epoch-end save deferred to the background (device snapshot,
@@ -170,6 +197,13 @@ def test_deferred_checkpoints_match_inline(tmp_path, monkeypatch):
         a = load_checkpoint(str(tmp_path / "inline" / name))
         b = load_checkpoint(str(tmp_path / "deferred" / name))
         assert a["epoch"] == b["epoch"] and a["global_step"] == b["global_step"]
+        # the callback state (PL 1.1: decided BEFORE the dump) agrees on both paths
+        ca, cb = a["callbacks"]["ModelCheckpoint"], b["callbacks"]["ModelCheckpoint"]
+        assert os.path.basename(ca["best_model_path"]) == os.path.basename(cb["best_model_path"]), name
+        for k in ("best_model_score", "current_score"):
+            assert (ca[k] is None and cb[k] is None) or float(ca[k]) == float(cb[k]), (name, k)
+        if name != "last.ckpt":
+            assert os.path.basename(cb["best_model_path"]) == name
         for k in a["state_dict"]:
             assert torch.equal(a["state_dict"][k], b["state_dict"][k]), (name, k)
         sa, sb = a["optimizer_states"][0]["state"], b["optimizer_states"][0]["state"]

@@ -572,3 +572,34 @@ def test_mlp3_300_step_trajectory_vs_fp32_torch_adam():
     # bf16 path does from the same init and batches, and well inside the travel
     assert drift < 1.5 * drift_ac + 0.02 and drift < 0.3, (drift, drift_ac, per)
     assert abs(loss_k - loss_r) < 0.05 * loss_r + 0.02, (loss_k, loss_r)
+
+
+@gpu
+def test_dp_packed_wire_keeps_non_finite_and_max_finite():
+    """the packed exchange's 2-bit tag rides in v0's low mantissa bits.
+    Inf must stay Inf, NaN stay NaN (not become Inf), FLT_MAX stay finite (no carry
+    into the exponent), every finite value within 2 ulp of fp32 (truncation near
+    the top of a binade: 3 ulp) and the second value of a pair bit-exact."""
+    from ray_lightning_accelerators_amd import ops
+
+    C = ops.require()
+    fmax = torch.finfo(torch.float32).max
+    special = [float("inf"), -float("inf"), float("nan"), fmax, -fmax, 0.0, -0.0, 1e-45, 1.0,
+               torch.nextafter(torch.tensor(2.0), torch.tensor(0.0)).item()]
+    nan_low = torch.tensor([0x7F800001, 0x7F800003, 0xFF800002], dtype=torch.int32).view(torch.float32)
+    x = torch.cat([torch.tensor(special), nan_low, torch.randn(4096) * 1e3]).cuda()
+    for tag in range(4):
+        # every value in the encoded (even) position, then in the plain (odd) one
+        even = torch.stack([x, torch.zeros_like(x)], 1).reshape(-1).contiguous()
+        y = C.dp_pack_roundtrip(even, tag)[0::2]
+        assert not torch.isnan(y[~torch.isnan(x)]).any(), "a tag mismatch or a finite value became NaN"
+        assert torch.isnan(y[torch.isnan(x)]).all(), "a NaN lost its NaN-ness"
+        inf = torch.isinf(x)
+        assert torch.equal(y[inf], x[inf])
+        fin = torch.isfinite(x)
+        assert torch.isfinite(y[fin]).all(), "a finite value carried into the exponent"
+        ulp = (torch.nextafter(x[fin].abs(), torch.tensor(float("inf"), device=x.device)) - x[fin].abs())
+        assert ((y[fin] - x[fin]).abs() <= 3 * ulp).all()
+        odd = torch.stack([torch.zeros_like(x), x], 1).reshape(-1).contiguous()
+        y1 = C.dp_pack_roundtrip(odd, tag)[1::2]
+        assert torch.equal(y1.view(torch.int32), x.view(torch.int32))

@@ -187,6 +187,45 @@ def test_model_checkpoint_monitor_explicit(tmpdir):
     assert float(mc.best_model_score) == 2.0
 
 
+def test_new_best_checkpoint_names_itself_and_resume_keeps_score(tmpdir):
+    """PL 1.1.7 _update_best_and_save: the best / current fields are set BEFORE the
+    dump, so a new-best file's callbacks[ModelCheckpoint] names that file and its
+    score (reference tune.py:138 ships this dict; tests/utils.py:129-134 reloads it);
+    resuming from it restores the best score and path."""
+    class M(BoringModel):
+        def validation_step(self, batch, batch_idx):
+            self.log("score", torch.tensor(float(self.current_epoch) + 0.5))
+            return super().validation_step(batch, batch_idx)
+
+    mc = ModelCheckpoint(dirpath=str(tmpdir), monitor="score", mode="max", save_last=True)
+    trainer = pl.Trainer(default_root_dir=str(tmpdir), max_epochs=3, limit_train_batches=1, limit_val_batches=1,
+                         callbacks=[mc])
+    trainer.fit(M())
+    trainer.wait_checkpoints()
+    best = mc.best_model_path
+    ck = load_checkpoint(best)["callbacks"]["ModelCheckpoint"]
+    assert ck["best_model_path"] == best
+    assert float(ck["best_model_score"]) == 2.5 and float(ck["current_score"]) == 2.5
+    last = load_checkpoint(os.path.join(str(tmpdir), "last.ckpt"))["callbacks"]["ModelCheckpoint"]
+    assert last["best_model_path"] == best
+    # resume: the restored callback keeps the best score / path of the file
+    mc2 = ModelCheckpoint(dirpath=str(tmpdir), monitor="score", mode="max")
+    t2 = pl.Trainer(default_root_dir=str(tmpdir), max_epochs=3, limit_train_batches=1, limit_val_batches=1,
+                    callbacks=[mc2], resume_from_checkpoint=best)
+    t2.fit(M())
+    assert float(mc2.best_model_score) == 2.5 and mc2.best_model_path == best
+
+
+def test_model_checkpoint_without_monitor_names_itself(tmpdir):
+    mc = ModelCheckpoint(dirpath=str(tmpdir))
+    trainer = pl.Trainer(default_root_dir=str(tmpdir), max_epochs=2, limit_train_batches=1, limit_val_batches=0,
+                         callbacks=[mc], logger=False)
+    trainer.fit(BoringModel())
+    trainer.wait_checkpoints()
+    ck = load_checkpoint(mc.best_model_path)["callbacks"]["ModelCheckpoint"]
+    assert ck["best_model_path"] == mc.best_model_path
+
+
 def test_async_checkpoint_writes_land_before_fit_returns(tmpdir, monkeypatch):
     """RLAConfig.async_checkpoint: ModelCheckpoint's writes (and its top-k removals)
     run on the background writer, in order; every file is complete when fit returns."""
@@ -220,3 +259,28 @@ def test_async_checkpoint_writes_land_before_fit_returns(tmpdir, monkeypatch):
 def test_seed_everything_env(bad):
     s = pl.seed_everything(42)
     assert s == 42 and os.environ["PL_GLOBAL_SEED"] == "42"
+
+
+def test_owner_state_consolidated_at_validation_end_not_in_dump(tmpdir):
+    """under the owner exchange protocol the Adam-state consolidation is a
+    collective.  It runs on EVERY rank at validation end (before ModelCheckpoint,
+    whose per-rank save decision may differ); the dump itself then skips it."""
+    class FakeFused:
+        calls = 0
+
+        def sync_optimizer_state(self):
+            FakeFused.calls += 1
+
+    trainer = pl.Trainer(default_root_dir=str(tmpdir), max_epochs=1, callbacks=[ModelCheckpoint()])
+    trainer._fused = FakeFused()
+    trainer.world_size = 2
+    trainer.training = True
+    trainer.global_step = 7
+    opt = torch.optim.Adam([torch.nn.Parameter(torch.zeros(2))])
+    trainer._consolidate_optimizer_state()
+    assert FakeFused.calls == 1
+    trainer._optimizer_state_dict(opt)
+    assert FakeFused.calls == 1, "dump re-ran the collective at the consolidated step"
+    trainer.global_step = 8
+    trainer._optimizer_state_dict(opt)
+    assert FakeFused.calls == 2
