@@ -522,12 +522,16 @@ def make_resnet(args, world, rank, dev, x, y, bucket_mb=None):
                 opt.zero_grad()
                 state["loss"] = loss
 
-        if args.resnet_graph and world == 1:
+        if args.resnet_graph:
             # the whole training step (forward, backward, gradient gather, fused SGD)
             # captured once in a hipGraph and replayed: no per-kernel launch cost for
             # its ~600 kernels.  Capture happens inside the warm-up (after 3 eager
             # steps on a side stream: allocator pools, MIOpen solver choice, the 1x1
             # conv autotune); every replay is one full step on the resident batch.
+            # World > 1: the capture also holds the data-parallel part -- the DDP
+            # buffer broadcast, every bucket's allreduce forked onto the reducer's
+            # comm stream by an event and joined back before the SGD (device-side
+            # xGMI generation counters / RCCL: nothing host-side per step).
             eager = run
             gstate = {}
 
@@ -549,6 +553,9 @@ def make_resnet(args, world, rank, dev, x, y, bucket_mb=None):
                     gstate["g"].replay()
 
             info = dict(info, hip_graph=True)
+
+        def checksum():
+            return float(arena.data.double().sum()) + 1e-3 * float(arena.data.double().abs().sum())
     else:
         m = model
         if world > 1:
@@ -556,6 +563,7 @@ def make_resnet(args, world, rank, dev, x, y, bucket_mb=None):
                                                           bucket_cap_mb=bucket_mb or args.bucket_mb)
             info = {"route": "torch-ddp", "bucket_mb": bucket_mb or args.bucket_mb}
         opt = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5, foreach=True)
+        checksum = None
 
         def run(n):
             for _ in range(n):
@@ -567,7 +575,40 @@ def make_resnet(args, world, rank, dev, x, y, bucket_mb=None):
                 opt.step()
                 state["loss"] = loss
 
-    return run, (lambda: float(state["loss"].item())), None, info
+        if args.impl == "torch-graph" and world == 1:
+            # the fair stock baseline: the same stock step (MIOpen convs /
+            # BN, foreach SGD-momentum) captured whole under torch.cuda.graph, so
+            # neither side pays per-kernel launch cost.  PyTorch's recipe: warm-up on
+            # a side stream (momentum buffers, MIOpen solver choice), grads set to
+            # None before the capture, forward + backward + step inside it.
+            eager_t = run
+            tg = {}
+
+            def run(n):
+                if "g" not in tg:
+                    s_ = torch.cuda.Stream()
+                    s_.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(s_):
+                        k = min(3, n)
+                        eager_t(k)
+                        n -= k
+                    torch.cuda.current_stream().wait_stream(s_)
+                    opt.zero_grad(set_to_none=True)
+                    g_ = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g_):
+                        with torch.autocast("cuda", dtype=torch.bfloat16):
+                            out = m(xb)
+                        loss = F.cross_entropy(out.float(), yb)
+                        loss.backward()
+                        opt.step()
+                        state["loss"] = loss
+                    tg["g"] = g_
+                for _ in range(n):
+                    tg["g"].replay()
+
+            info = dict(info, hip_graph=True)
+
+    return run, (lambda: float(state["loss"].item())), checksum, info
 
 
 # ------------------------------------------------------------ measurement

@@ -137,11 +137,15 @@ class RayAccelerator(DataParallelAccelerator):
     # ----------------------------------------------------------- driver side
     def _create_worker(self):
         opts = dict(num_cpus=self.num_cpus_per_worker, num_gpus=int(self.use_gpu))
-        if self.use_gpu and get_config().reuse_workers:
+        if self._recycles():
             # a recycled GPU worker (HIP context + kernels already loaded) when one is
             # parked for this GPU: Tune trials stop paying worker start-up each
-            opts["_reuse"] = RECYCLE_KEY
+            opts["_reuse"] = RECYCLE_KEY if self.use_gpu else RECYCLE_KEY + ":cpu"
         return RayExecutor.options(**opts).remote()
+
+    def _recycles(self) -> bool:
+        cfg = get_config()
+        return cfg.reuse_workers and (self.use_gpu or cfg.reuse_cpu_workers)
 
     def setup(self, model) -> None:
         assert self.trainer is not None, "trainer must be attached before setup()"
@@ -160,7 +164,7 @@ class RayAccelerator(DataParallelAccelerator):
             self._failed = False
             return
 
-        recycled = self.use_gpu and get_config().reuse_workers
+        recycled = self._recycles()
 
         def shutdown_remote():
             from ..parallel.comm import reset_native_comm

@@ -75,6 +75,9 @@ class RLAConfig:
     # fit parks its worker processes with their HIP context and loaded kernels, and
     # the next fit on the same GPUs takes them over (runtime actor reuse)
     reuse_workers: bool = True
+    # the same recycling for CPU-only workers (off by default: a CPU worker starts
+    # from the pre-warmed pool cheaply); used by the gloo tests of the reuse path
+    reuse_cpu_workers: bool = False
     # Trainer: fused resident steps issued per host dispatch when nothing observes
     # single batches (chunks also end at validation / max_steps boundaries, and at log
     # points unless the fused step reports them itself); 1 = one dispatch per batch.

@@ -1016,74 +1016,68 @@ __device__ __forceinline__ u64 ld_sys(const u64* p) {
   return __hip_atomic_load(const_cast<u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Poll granules 0..n-1 (address addr(i), n <= NMAX): every load is issued before
-// any check, then only the mismatched ones are re-read, so the common case is ONE
-// round trip for all of them.  Returns when every tag matches or the bound expires
-// (*fail set).  Unrolled over NMAX: w[] stays in registers.
-template <int NMAX, typename Addr>
-__device__ __forceinline__ void dp_poll_issue(u64 (&w)[NMAX], int n, Addr addr) {
+// Polls of the wave-positioned protocols are compiled for a rank CLASS NW (the
+// world size rounded up to 2, 4 or 8: one kernel instance each), so every loop
+// below is unrolled over compile-time indices and every load is unconditional: a
+// per-element "load if i < n" on a run-time n made hipcc branch around each load
+// and wait vmcnt(0) per element (profiles/r4_dp: the round-3 instance that took a
+// run-time world size).  Peer slots k < NW - 1 that the actual world does not have
+// re-read our own source slot (a valid address) and are never checked.
+constexpr int kDpPeerGran = 2 * (kXgmiMaxRanks - 1);
+constexpr int64_t kDpSrcGran = (int64_t)comm::kDpMaxUnits * 128;  // granules per source rank of a slot
+
+// peer slot k (0..NW-2) -> its rank: the ranks in order, ours skipped
+__device__ __forceinline__ int dp_peer(int k, int me) { return k < me ? k : k + 1; }
+
+// issue the 2 (NW - 1) peer granules of (slot, unit) in our own region: granule 2k + h
+// is half h of peer k's contribution
+template <int NW>
+__device__ __forceinline__ void dp_peer_issue(u64 (&w)[2 * (NW - 1)], const u64* src0, int me, int W) {
 #pragma unroll
-  for (int i = 0; i < NMAX; ++i)
-    if (i < n) w[i] = ld_sys(addr(i));
+  for (int k = 0; k < NW - 1; ++k) {
+    const int s = dp_peer(k, me);
+    const u64* p = src0 + (int64_t)(s < W ? s : me) * kDpSrcGran;
+    w[2 * k] = ld_sys(p);
+    w[2 * k + 1] = ld_sys(p + 64);
+  }
 }
 
-// Check / re-poll granules issued by dp_poll_issue.  gfx950 counts loads AND stores
-// in one in-order vmcnt, so a wave's own pushes issued BEFORE its polls would make
-// the first wait cover their completion acks too (a full remote round trip); the
-// protocols below issue the first polls before their pushes.
-template <int NMAX, typename Addr, typename TagOk>
-__device__ __forceinline__ void dp_poll_finish(const MLP3Args& a, u64 (&w)[NMAX], int n, Addr addr, TagOk ok,
-                                               int* fail) {
+// Wait until every real peer's two granules carry this step's tag (or the bound
+// expires: *fail).  Re-polls re-issue all of them (unconditional, still one round
+// trip; a matched granule is not rewritten before this wave's own next step).
+template <int NW>
+__device__ __forceinline__ void dp_peer_wait(const MLP3Args& a, u64 (&w)[2 * (NW - 1)], const u64* src0, int me,
+                                             int W, uint32_t tag, int* fail) {
   int64_t spins = 0;
   while (true) {
     bool all = true;
 #pragma unroll
-    for (int i = 0; i < NMAX; ++i)
-      if (i < n && !ok(w[i])) all = false;
+    for (int k = 0; k < NW - 1; ++k)
+      if (dp_peer(k, me) < W) all = all && ((uint32_t)w[2 * k] & 3u) == tag && ((uint32_t)w[2 * k + 1] & 3u) == tag;
     if (all) return;
     if (++spins > a.dp_spin) {
       *fail = 1;
       return;
     }
     __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-    for (int i = 0; i < NMAX; ++i)
-      if (i < n && !ok(w[i])) w[i] = ld_sys(addr(i));
+    dp_peer_issue<NW>(w, src0, me, W);
   }
 }
 
 // Fixed-rank-order sum of every rank's packed contribution to this lane's 4 values
-// (our own from registers): polls the W - 1 peers' granules of slot / unit.
-// granule i of the W - 1 peers' packed contributions to unit / slot: peer i / 2
-// (ranks in order, skipping ours), half i & 1
-struct DpPeerAddr {
-  char* mine;
-  int slot, unit, me, lane;
-  __device__ __forceinline__ const u64* operator()(int i) const {
-    const int k = i >> 1, s = k < me ? k : k + 1;
-    return dp_pk_area(mine, slot, s, unit) + (i & 1) * 64 + lane;
-  }
-};
-constexpr int kDpPeerGran = 2 * (kXgmiMaxRanks - 1);
-
-__device__ __forceinline__ void dp_packed_sum(const MLP3Args& a, int unit, int slot, uint32_t tag, u64 g0, u64 g1,
-                                              float (&v)[4], float scale, int* fail, u64 (&w)[kDpPeerGran],
-                                              bool issued) {
-  const int me = a.dp_rank, W = a.dp_world;
-  const DpPeerAddr addr{a.dp_regions[me], slot, unit, me, (int)(threadIdx.x & 63)};
-  if (!issued) dp_poll_issue(w, 2 * (W - 1), addr);
-  dp_poll_finish(a, w, 2 * (W - 1), addr, [tag](u64 x) { return ((uint32_t)x & 3u) == tag; }, fail);
+// (ours from registers, rounded as on the wire), times `scale`.
+template <int NW>
+__device__ __forceinline__ void dp_packed_sum(const u64 (&w)[2 * (NW - 1)], int me, int W, u64 g0, u64 g1,
+                                              float (&v)[4], float scale) {
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll
-  for (int s = 0; s < kXgmiMaxRanks; ++s) {
+  for (int s = 0; s < NW; ++s) {
     if (s >= W) break;
-    const int k = s < me ? s : s - 1;
+    // rank s is peer slot s (below us) or s - 1 (above): both compile-time indices
+    const int lo = s < NW - 1 ? s : 0, hi = s > 0 ? s - 1 : 0;
     u64 a0 = g0, a1 = g1;
-    if (s != me) {
-#pragma unroll
-      for (int q = 0; q < kXgmiMaxRanks - 1; ++q)  // register-resident select (no indexed access)
-        if (q == k) { a0 = w[2 * q]; a1 = w[2 * q + 1]; }
-    }
+    if (s < me) { a0 = w[2 * lo]; a1 = w[2 * lo + 1]; }
+    else if (s > me) { a0 = w[2 * hi]; a1 = w[2 * hi + 1]; }
     s0 += pk_lo(a0); s1 += pk_hi(a0); s2 += pk_lo(a1); s3 += pk_hi(a1);
   }
   v[0] = s0 * scale; v[1] = s1 * scale; v[2] = s2 * scale; v[3] = s3 * scale;
@@ -1096,20 +1090,35 @@ __device__ __forceinline__ void dp_push_packed(char* region, int slot, int src, 
   st_sys(d + 64 + lane, g1);
 }
 
+// this rank's contribution to every peer (loopback: into every peer's source slot
+// of our own region)
+template <int NW>
+__device__ __forceinline__ void dp_push_all(const MLP3Args& a, int slot, int unit, u64 g0, u64 g1) {
+  const int me = a.dp_rank, W = a.dp_world;
+#pragma unroll
+  for (int r = 0; r < NW; ++r)
+    if (r < W && r != me) dp_push_packed(a.dp_loop ? a.dp_regions[me] : a.dp_regions[r], slot, a.dp_loop ? r : me,
+                                         unit, g0, g1);
+}
+
 // "packed" one-shot: push this wave's 4 values to every peer, sum all ranks' in
 // fixed order; v[] becomes the sum times `scale`.  Whole-wave call.
+template <int NW>
 __device__ __forceinline__ void dp_packed_exchange(const MLP3Args& a, int unit, uint32_t gen, float (&v)[4],
                                                    float scale, int* fail) {
   const int slot = (int)(gen & 1u), me = a.dp_rank, W = a.dp_world;
   const uint32_t tag = (gen >> 1) & 3u;
   const u64 g0 = pk2(v[0], v[1], tag), g1 = pk2(v[2], v[3], tag);
-  u64 w[kDpPeerGran];
-  // first polls before the pushes (see dp_poll_finish); loopback reads its own pushes
-  if (!a.dp_loop) dp_poll_issue(w, 2 * (W - 1), DpPeerAddr{a.dp_regions[me], slot, unit, me, (int)(threadIdx.x & 63)});
-  // 2 x 512 contiguous bytes per peer (loopback: every peer's source slot of our own region)
-  for (int r = 0; r < W; ++r)
-    if (r != me) dp_push_packed(a.dp_regions[r], slot, a.dp_loop ? r : me, unit, g0, g1);
-  dp_packed_sum(a, unit, slot, tag, g0, g1, v, scale, fail, w, !a.dp_loop);
+  const u64* src0 = dp_pk_area(a.dp_regions[me], slot, 0, unit) + (threadIdx.x & 63);
+  u64 w[2 * (NW - 1)];
+  // first polls before the pushes: gfx950 counts loads AND stores in one in-order
+  // vmcnt, so pushes issued first would make the first wait cover their remote
+  // completion too.  Loopback reads its own pushes: polls after them.
+  if (!a.dp_loop) dp_peer_issue<NW>(w, src0, me, W);
+  dp_push_all<NW>(a, slot, unit, g0, g1);
+  if (a.dp_loop) dp_peer_issue<NW>(w, src0, me, W);
+  dp_peer_wait<NW>(a, w, src0, me, W, tag, fail);
+  dp_packed_sum<NW>(w, me, W, g0, g1, v, scale);
 }
 
 // "owner": the task's gradient goes to its owner rank only (reduce-scatter, one
@@ -1120,7 +1129,7 @@ __device__ __forceinline__ void dp_packed_exchange(const MLP3Args& a, int unit, 
 // On return v[] holds the new weights on every rank; true on the owner (whose
 // m / v registers are then the ones to store).  Loopback: a wave whose task
 // another (absent) rank owns plays that owner itself.
-template <typename AdamFn>
+template <int NW, typename AdamFn>
 __device__ __forceinline__ bool dp_owner_step(const MLP3Args& a, int unit, int owner, uint32_t gen, float (&v)[4],
                                               float scale, int* fail, AdamFn adam) {
   const int lane = threadIdx.x & 63, slot = (int)(gen & 1u), me = a.dp_rank, W = a.dp_world;
@@ -1128,17 +1137,21 @@ __device__ __forceinline__ bool dp_owner_step(const MLP3Args& a, int unit, int o
   const bool own = owner == me;
   const u64 g0 = pk2(v[0], v[1], tag), g1 = pk2(v[2], v[3], tag);
   const u64* agsrc = dp_ag_area(a.dp_regions[me], slot, unit) + lane;
-  auto agaddr = [agsrc](int i) { return agsrc + i * 64; };
   u64 wa[4];
-  if (!own && !a.dp_loop) dp_poll_issue(wa, 4, agaddr);  // first polls before the push
+  auto ag_issue = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wa[i] = ld_sys(agsrc + i * 64);
+  };
+  if (!own && !a.dp_loop) ag_issue();  // first polls before the push
   if (!own) dp_push_packed(a.dp_regions[owner], slot, me, unit, g0, g1);
   if (own || a.dp_loop) {
     if (own) {
-      u64 w[kDpPeerGran];
-      if (a.dp_loop)
-        for (int s = 0; s < W; ++s)
-          if (s != me) dp_push_packed(a.dp_regions[me], slot, s, unit, g0, g1);
-      dp_packed_sum(a, unit, slot, tag, g0, g1, v, scale, fail, w, false);
+      const u64* src0 = dp_pk_area(a.dp_regions[me], slot, 0, unit) + lane;
+      u64 w[2 * (NW - 1)];
+      if (a.dp_loop) dp_push_all<NW>(a, slot, unit, g0, g1);
+      dp_peer_issue<NW>(w, src0, me, W);
+      dp_peer_wait<NW>(a, w, src0, me, W, tag, fail);
+      dp_packed_sum<NW>(w, me, W, g0, g1, v, scale);
     } else {  // loopback stand-in of the owner: W identical contributions
       float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
       for (int s = 0; s < W; ++s) { s0 += pk_lo(g0); s1 += pk_hi(g0); s2 += pk_lo(g1); s3 += pk_hi(g1); }
@@ -1146,16 +1159,29 @@ __device__ __forceinline__ bool dp_owner_step(const MLP3Args& a, int unit, int o
     }
     adam(v);
     const u64 tg = (u64)gen << 32;
-    for (int r = 0; r < W; ++r) {
-      if (own ? r == me : r != owner) continue;  // loopback stand-in: publish once, to ourselves
+#pragma unroll
+    for (int r = 0; r < NW; ++r) {
+      if (r >= W || (own ? r == me : r != owner)) continue;  // loopback stand-in: publish once, to ourselves
       u64* d = dp_ag_area(a.dp_regions[r], slot, unit);
 #pragma unroll
       for (int i = 0; i < 4; ++i) st_sys(d + i * 64 + lane, tg | (u64)__float_as_uint(v[i]));
     }
     if (own) return true;
   }
-  if (a.dp_loop) dp_poll_issue(wa, 4, agaddr);
-  dp_poll_finish(a, wa, 4, agaddr, [gen](u64 x) { return (uint32_t)(x >> 32) == gen; }, fail);
+  if (a.dp_loop) ag_issue();
+  int64_t spins = 0;
+  while (true) {
+    bool all = true;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) all = all && (uint32_t)(wa[i] >> 32) == gen;
+    if (all) break;
+    if (++spins > a.dp_spin) {
+      *fail = 1;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    ag_issue();
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) v[i] = __uint_as_float((uint32_t)wa[i]);
   return false;
@@ -1514,8 +1540,9 @@ __device__ __forceinline__ void one_wait_acks(const MLP3Args& a, int64_t seq, in
 // DPP: -1 world size 1 (Step1); else the exchange protocol of Step1DP (0 granule,
 // 1 packed, 2 owner) as a template parameter -- each instance carries only its own
 // protocol's code (a run-time switch over all three cost the head pass ~0.5 us and
-// the tile epilogue ~1.4 us of register pressure, profiles/r3_dp/dp_phases.log)
-template <int L1, int L2, int DPP>
+// the tile epilogue ~1.4 us of register pressure, profiles/r3_dp/dp_phases.log).
+// NW: the rank class of the packed / owner polls (world size <= NW; see dp_peer_issue).
+template <int L1, int L2, int DPP, int NW = 8>
 __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
   constexpr bool DP = DPP >= 0;
   using C = typename One<L1, L2>::C;
@@ -1620,10 +1647,10 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
           float v[4] = {acc[0], acc[1], acc[2], acc[3]};
           const int unit = blk * kWaves + w;
           if constexpr (DPP == 1) {
-            dp_packed_exchange(a, unit, gen, v, a.grad_scale, &fail);
+            dp_packed_exchange<NW>(a, unit, gen, v, a.grad_scale, &fail);
           } else {
             const AdamScal o = *sh_o;
-            store_mv = dp_owner_step(a, unit, dp_task_owner(a, kt), gen, v, a.grad_scale, &fail,
+            store_mv = dp_owner_step<NW>(a, unit, dp_task_owner(a, kt), gen, v, a.grad_scale, &fail,
                                      [&](float (&x)[4]) {
 #pragma unroll
                                        for (int i = 0; i < 4; ++i) x[i] = adam1(p4.v[i], x[i], m4.v[i], v4.v[i], o);
@@ -1700,12 +1727,12 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
         float v[4] = {r.v[0], r.v[1], r.v[2], r.v[3]};
         const int unit = blk * kWaves + w;
         if constexpr (DPP == 1) {
-          dp_packed_exchange(a, unit, gen, v, a.grad_scale, &fail);
+          dp_packed_exchange<NW>(a, unit, gen, v, a.grad_scale, &fail);
         } else {
           // Adam in registers before the acknowledgement wait below: the owner
           // publishes the weights as early as possible, stores after the wait
           const AdamScal o = *sh_o;
-          store_mv = dp_owner_step(a, unit, dp_task_owner(a, kTiles + task), gen, v, a.grad_scale, &fail,
+          store_mv = dp_owner_step<NW>(a, unit, dp_task_owner(a, kTiles + task), gen, v, a.grad_scale, &fail,
                                    [&](float (&x)[4]) {
 #pragma unroll
                                      for (int i = 0; i < 4; ++i) x[i] = adam1(r.pv[i], x[i], r.mv[i], r.vv[i], o);
@@ -1763,12 +1790,15 @@ int dispatch3(const MLP3Args& a, int kind, hipStream_t stream) {
     // round-2 granules need 2 floats per parameter, the wave-positioned areas their fixed size
     if (a.dp_proto == 0 ? (a.dp_lite != 2 || a.dp_stride < 2 * Off<L1, L2>::NP) : a.dp_stride < comm::kDpUnitAreaFloats)
       return -7;
-    if (a.dp_proto == 0)
-      hipLaunchKernelGGL((mlp3_one_kernel<L1, L2, 0>), dim3(kOneGrid), dim3(kThreads), 0, stream, a);
-    else if (a.dp_proto == 1)
-      hipLaunchKernelGGL((mlp3_one_kernel<L1, L2, 1>), dim3(kOneGrid), dim3(kThreads), 0, stream, a);
-    else
-      hipLaunchKernelGGL((mlp3_one_kernel<L1, L2, 2>), dim3(kOneGrid), dim3(kThreads), 0, stream, a);
+    const dim3 g(kOneGrid), b(kThreads);
+    const int nw = a.dp_world <= 2 ? 2 : (a.dp_world <= 4 ? 4 : 8);
+    if (a.dp_proto == 0) hipLaunchKernelGGL((mlp3_one_kernel<L1, L2, 0>), g, b, 0, stream, a);
+    else if (a.dp_proto == 1 && nw == 2) hipLaunchKernelGGL((mlp3_one_kernel<L1, L2, 1, 2>), g, b, 0, stream, a);
+    else if (a.dp_proto == 1 && nw == 4) hipLaunchKernelGGL((mlp3_one_kernel<L1, L2, 1, 4>), g, b, 0, stream, a);
+    else if (a.dp_proto == 1) hipLaunchKernelGGL((mlp3_one_kernel<L1, L2, 1, 8>), g, b, 0, stream, a);
+    else if (nw == 2) hipLaunchKernelGGL((mlp3_one_kernel<L1, L2, 2, 2>), g, b, 0, stream, a);
+    else if (nw == 4) hipLaunchKernelGGL((mlp3_one_kernel<L1, L2, 2, 4>), g, b, 0, stream, a);
+    else hipLaunchKernelGGL((mlp3_one_kernel<L1, L2, 2, 8>), g, b, 0, stream, a);
     return 0;
   }
   constexpr int NT = 64 * (L1 / 16);

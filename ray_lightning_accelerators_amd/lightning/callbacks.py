@@ -178,6 +178,8 @@ class ModelCheckpoint(Callback):
                 ckpt = resolve()
 
                 def write(path):
+                    if ckpt is None:
+                        return  # ranks > 0: bookkeeping only (PL 1.1: rank 0 saves)
                     # the dict was dumped before this save point's decision: its
                     # ModelCheckpoint entry is refreshed with the decided state
                     if "callbacks" in ckpt:

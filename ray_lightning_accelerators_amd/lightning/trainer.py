@@ -349,7 +349,9 @@ class Trainer:
 
     def write_checkpoint(self, ckpt: dict, filepath: str) -> None:
         """Write an already-built checkpoint dict (the deferred saves' path): through
-        the writer process when it is up, else in place."""
+        the writer process when it is up, else in place.  Only rank 0 writes."""
+        if ckpt is None or not self.is_global_zero:
+            return
         w = getattr(self, "_ckpt_writer", None)
         if w is None and get_config().async_checkpoint:
             # the writer process started for this worker (ddp_train pre-warms it):
@@ -790,10 +792,11 @@ class Trainer:
             self._consolidate_optimizer_state()
         self.call_hook(f"on_{stage}_end")
         mark("eval_end_hooks", stage=stage)
-        if stage == "validation" and getattr(self, "world_size", 1) > 1:
+        if stage == "validation" and getattr(self, "world_size", 1) > 1 and not self.deferred_checkpoints_ok():
             # ModelCheckpoint (on_validation_end) may have rank 0 writing a file: the
             # other ranks wait for it here, not inside the next step's gradient
-            # collective, where a long write would look like a stalled peer
+            # collective, where a long write would look like a stalled peer.  (Deferred
+            # checkpoints write in the background: no rank waits, no barrier.)
             acc = self.accelerator_backend
             if acc is not None and hasattr(acc, "barrier"):
                 acc.barrier("validation_end")
@@ -1231,15 +1234,19 @@ class Trainer:
     # ------------------------------------------------- deferred checkpoints
     def deferred_checkpoints_ok(self) -> bool:
         """Whether ModelCheckpoint may hand its epoch-end save to the background
-        (``_DeferredCheckpoints``): rank 0 of a single-rank GPU fit whose checkpoint
-        writer is configured (``RLA_DEFER_CKPT=0`` turns it off).  At world > 1 every
-        rank dumps the checkpoint (collective state consolidation), so it stays inline."""
+        (``_DeferredCheckpoints``): every rank of a GPU fit on the fused step whose
+        checkpoint writer is configured (``RLA_DEFER_CKPT=0`` turns it off).  Rank 0
+        stages the state on the device and decides / writes in the background; the
+        other ranks stage nothing and write nothing (PL 1.1: only rank 0 saves), they
+        only keep the top-k bookkeeping.  The owner-protocol consolidation -- the one
+        collective a dump can need -- already ran on every rank at validation end
+        (``_consolidate_optimizer_state``), so nothing here is collective."""
         if os.environ.get("RLA_DEFER_CKPT", "1") == "0" or not get_config().async_checkpoint:
             return False
-        if not (self.on_gpu and torch.cuda.is_available() and self.is_global_zero):
+        if not (self.on_gpu and torch.cuda.is_available()):
             return False
         # (without the writer process the background thread pickles the file itself)
-        return getattr(self, "world_size", 1) == 1 and self._fused is not None
+        return self._fused is not None
 
     def defer_checkpoint(self, job, weights_only: bool, values=()):
         """Snapshot the checkpoint state ON THE DEVICE now (stream-ordered copies, no
@@ -1252,7 +1259,8 @@ class Trainer:
         if q is None:
             q = self._deferred = _DeferredCheckpoints()
         q.drain_done()  # earlier decisions (best model path / score) are in place
-        ckpt = self.checkpoint_connector.dump_checkpoint(weights_only, staged=True)
+        # ranks > 0 never write a file: no device snapshot, no host copy
+        ckpt = self.checkpoint_connector.dump_checkpoint(weights_only, staged=True) if self.is_global_zero else None
         vals = [v.detach().reshape(()).double().clone() if isinstance(v, torch.Tensor) and v.is_cuda else v
                 for v in values]
         q.submit(ckpt, vals, job)
@@ -1443,7 +1451,7 @@ class _DeferredCheckpoints:
                 with torch.cuda.stream(self._stream):
                     self._stream.wait_event(ev)
                     vals = [float(v.cpu()) if isinstance(v, torch.Tensor) else v for v in values]
-                    job(lambda: _resolve_staged(ckpt), vals)
+                    job(lambda: _resolve_staged(ckpt) if ckpt is not None else None, vals)
             except BaseException as e:  # surfaced on the main thread
                 self._err = e
             finally:

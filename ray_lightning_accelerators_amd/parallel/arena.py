@@ -72,6 +72,7 @@ class ParamArena:
         self._tables: "OrderedDict[tuple, torch.Tensor]" = OrderedDict()
         self._graph_tables: List[tuple] = []
         self._graph_staging: Optional[torch.Tensor] = None
+        self._graph_staging_off = 0
 
     def _shaped(self, flat: torch.Tensor, i: int, like: torch.Tensor, base: int = 0) -> torch.Tensor:
         o, n = self.offsets[i]
@@ -211,11 +212,14 @@ class ParamArena:
                 capturing = torch.cuda.is_current_stream_capturing()
                 if capturing and self._graph_staging is None:
                     raise RuntimeError("ParamArena: call prepare_graph_capture() before capturing a step")
-                table = build_copy_table(pairs, staging=self._graph_staging if capturing else None)
+                # captured: each table takes the next slice of the reserved pinned buffer
+                # (a data-parallel step gathers once per bucket, all in one capture)
+                off = self._graph_staging_off if capturing else 0
+                table = build_copy_table(pairs, staging=self._graph_staging[off:] if capturing else None)
                 self._tables[key] = table
                 if capturing:
                     self._graph_tables.append((table, self._graph_staging))  # replayed: never evicted
-                    self._graph_staging = None
+                    self._graph_staging_off = off + table.numel()
                 if len(self._tables) > 64:  # address sets are stable under the caching allocator
                     self._tables.popitem(last=False)
             multi_copy(pairs, table=table)
@@ -233,6 +237,7 @@ class ParamArena:
 
         rows = sum((n + CHUNK_ELEMS - 1) // CHUNK_ELEMS for _, n in self.offsets)
         self._graph_staging = torch.empty(rows * 4, dtype=torch.int64).pin_memory()
+        self._graph_staging_off = 0
 
     def zero_grad(self) -> None:
         if self.steal_grads:

@@ -140,7 +140,7 @@ class GradSynchronizer:
         groups = {}
         for b in self.module.buffers():
             groups.setdefault((b.dtype, b.device), []).append(b)
-        for (_, dev), bufs in groups.items():
+        for (dtype, dev), bufs in groups.items():
             flat = _flatten_dense_tensors([b.data for b in bufs])
             if dev.type == "cuda" and self.pg is None:
                 from .comm import get_native_comm
@@ -148,6 +148,17 @@ class GradSynchronizer:
                 comm = get_native_comm()
                 if comm is not None and comm.rccl:
                     comm.broadcast_(flat, 0)
+                elif comm is not None and (comm.xgmi or comm.twoshot):
+                    # no RCCL (ranks sharing a device): a broadcast as the device-side
+                    # xGMI allreduce of rank 0's values and everyone else's zeros --
+                    # exact, and capturable in the step's hipGraph (a gloo broadcast
+                    # of a device tensor is a host round trip)
+                    f = flat if dtype == torch.float32 else flat.to(torch.float32)  # counters: exact < 2^24
+                    if dist.get_rank() != 0:
+                        f.zero_()
+                    comm.allreduce_(f)
+                    if f is not flat:
+                        flat.copy_(f)
                 else:
                     dist.broadcast(flat, 0, group=self.pg)
             else:

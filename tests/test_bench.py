@@ -105,6 +105,26 @@ def test_bench_torch_graph_baseline():
     assert out["n_gpus"] == 1 and out["config"]["impl"] == "torch-graph" and out["value"] > 0
 
 
+@pytest.mark.gpu
+def test_bench_resnet50_two_ranks_share_gpu_graph_captured():
+    """ResNet-50 (config 5) at world 2 runs its data-parallel step as ONE hipGraph
+    replay: forward, backward, the DDP buffer broadcast, every bucket's allreduce on
+    the reducer's comm stream and the fused SGD (VERDICT r3 missing 2).  bench.py
+    raises if the replicas differ after the timed steps."""
+    out, err = _bench("--model", "resnet50", "--gpus", "2", "--steps", "6", "--warmup", "4", "--batch-size", "16",
+                      "--bucket-mb", "4", env={"RLA_BENCH_SHARE_GPU": "1"}, timeout=600)
+    assert out["n_gpus"] == 2 and out["config"]["route"] == "native-reducer", (out, err[-2000:])
+    assert out["config"]["hip_graph"] is True, out
+    assert out["dp"]["comm_error_state"] == 0 and out["dp"]["comm_failed_validation"] == [], out
+
+
+@pytest.mark.gpu
+def test_bench_resnet50_torch_graph_baseline():
+    out, _ = _bench("--model", "resnet50", "--impl", "torch-graph", "--steps", "4", "--warmup", "4",
+                    "--batch-size", "16", timeout=600)
+    assert out["config"]["impl"] == "torch-graph" and out["config"]["hip_graph"] is True and out["value"] > 0
+
+
 def test_graph_steps_divide_the_timed_window():
     import importlib
     import sys

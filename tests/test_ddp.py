@@ -1,4 +1,6 @@
 """RayAccelerator on CPU / gloo -- port of the reference's ray_lightning/tests/test_ddp.py."""
+import time
+
 import pytest
 from torch.utils.data import DistributedSampler
 
@@ -145,3 +147,51 @@ def test_worker_failure_tears_down(tmpdir, ray_start_2_cpus):
 
     time.sleep(0.5)
     assert all(a["State"] == "DEAD" for a in ray.actors().values())
+
+
+def test_recycled_worker_pair_across_two_fits(tmpdir, monkeypatch):
+    """A world-2 worker pair is parked after one fit and taken over by the next
+    (the Tune config-4 pattern: trials of RayAccelerator(num_workers=2) back to
+    back).  The second fit must find a FRESH process group (new rendezvous, the
+    first's destroyed in __rla_park__), a fresh session and config, and train
+    correctly -- in the SAME processes (gloo stand-in for the
+    GPU path, RLA_REUSE_CPU_WORKERS)."""
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from ray_lightning_accelerators_amd.config import set_config
+
+    monkeypatch.setenv("RLA_REUSE_CPU_WORKERS", "1")
+    set_config(None)
+
+    class PidModel(BoringModel):
+        def __init__(self):
+            super().__init__()
+            self.register_buffer("pids", torch.zeros(2, dtype=torch.int64))
+            self.register_buffer("groups", torch.zeros(1, dtype=torch.int64))
+
+        def on_train_start(self):
+            # both ranks' pids reach rank 0 (whose state dict comes back) through the
+            # process group this fit created
+            t = torch.zeros(2, dtype=torch.int64)
+            t[dist.get_rank()] = os.getpid()
+            dist.all_reduce(t)
+            self.pids.copy_(t)
+            self.groups.fill_(dist.get_world_size())
+
+    ray.init(num_cpus=4, num_gpus=0)
+    try:
+        seen = []
+        for fit in range(2):
+            model = PidModel()
+            trainer = get_trainer(tmpdir, accelerator=RayAccelerator(num_workers=2))
+            train_test(trainer, model)
+            assert int(model.groups) == 2
+            seen.append(sorted(int(p) for p in model.pids))
+            time.sleep(0.5)  # the park acknowledgement (the next create waits for it anyway)
+        assert seen[0] == seen[1] and 0 not in seen[0], seen
+    finally:
+        ray.shutdown()
+        set_config(None)

@@ -166,3 +166,15 @@ def test_bench_two_gpus_self_launched():
     assert out["config"]["dp_proto"] in ("packed", "owner"), out
     assert set(out["config"]["dp_proto_tuning_us_per_step"]) == {"packed", "owner"}, out
     assert out["dp"]["rccl_world"] == 2 and out["dp"]["comm_failed_validation"] == [], out
+
+
+def test_bench_resnet50_two_gpus_graph_captured():
+    """Physical-GPU twin of test_bench_resnet50_two_ranks_share_gpu_graph_captured:
+    the captured data-parallel ResNet-50 step over RCCL / xGMI between two devices."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--model", "resnet50", "--gpus", "2",
+                        "--steps", "6", "--warmup", "4", "--batch-size", "32"], cwd="/tmp", capture_output=True,
+                       text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["config"]["route"] == "native-reducer" and out["config"]["hip_graph"] is True, out
+    assert out["dp"]["rccl_world"] == 2 and out["dp"]["comm_error_state"] == 0, out
