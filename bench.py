@@ -98,6 +98,9 @@ def parse(argv=None):
     ap.add_argument("--lr", type=float, default=1e-1)
     ap.add_argument("--graph-steps", type=int, default=8,
                     help="optimizer steps per captured hipGraph (native, torch-graph); 0 = eager launches")
+    ap.add_argument("--launch", choices=["graph", "loop"], default="graph",
+                    help="mnist native one-launch step: 'graph' replays hipGraphs of --graph-steps steps; "
+                         "'loop' issues the timed window's launches back to back from one C++ call")
     ap.add_argument("--n-data", type=int, default=55000)
     ap.add_argument("--trainer-epochs", type=int, default=4, help="--via trainer: epochs (the first is warm-up)")
     ap.add_argument("--bucket-mb", type=float, default=8.0, help="resnet50 DDP bucket cap (MiB)")
@@ -251,6 +254,9 @@ def make_native(args, world, rank, dev, x, y, force_split=False):
         route = f"split-{get_native_comm(create=False).route(eng.comm_buffer)}"  # oneshot / rccl / torch
     graphed = False
     gsteps = graph_steps_for(args.graph_steps, args.steps)
+    if args.launch == "loop" and eng._loop_ok():
+        eng.launch_loop = True
+        gsteps = 0  # no capture: run() issues each window from one C++ launch loop
     tuned = None
     if eng.one_launch_dp and args.dp_proto == "auto" and gsteps > 0:
         tuned = tune_dp_proto(eng, world, rank, dev, gsteps)
@@ -268,7 +274,8 @@ def make_native(args, world, rank, dev, x, y, force_split=False):
 
     one = eng.native and (eng.one_launch_dp if world > 1 else eng.one_launch)
     info = {"route": route, "hip_graph_steps": gsteps if graphed else 0,
-            "step_kernel": ("one-launch" if one else "head+tail") if eng.native else "torch-cpu"}
+            "step_kernel": ("one-launch" if one else "head+tail") if eng.native else "torch-cpu",
+            "step_launch": "cpp-loop" if eng.launch_loop else ("hip-graph" if graphed else "eager")}
     if eng.dp_ctx is not None:
         info["dp_proto"] = eng.dp_proto
         if tuned is not None:

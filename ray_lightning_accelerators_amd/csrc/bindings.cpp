@@ -175,8 +175,9 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
           bool advance_step, double lr,
           double beta1, double beta2, double eps, double weight_decay, double grad_scale, optional<Tensor> lr_t,
           bool adamw, optional<Tensor> stamps, std::vector<int64_t> dp_ctx, optional<Tensor> head_part,
-          optional<Tensor> hand, int64_t dp_proto, bool dp_loop) {
+          optional<Tensor> hand, int64_t dp_proto, bool dp_loop, int64_t repeat) {
   TORCH_CHECK(kind >= 0 && kind <= 7, "mlp3: bad kind ", kind);
+  TORCH_CHECK(repeat >= 1, "mlp3: repeat must be >= 1");
   TORCH_CHECK(rla::mlp_supported((int)L1, (int)L2), "no fused MLP kernel for layer sizes ", L1, "/", L2);
   TORCH_CHECK(B >= 1 && B <= 256, "fused MLP step supports 1 <= batch <= 256");
   const int64_t np = mlp_param_count(L1, L2);
@@ -282,7 +283,12 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
     }
     TORCH_CHECK(!dp_loop || kind == rla::kMLP3Step1DP, "loopback is a one-launch-step diagnostic");
   }
-  TORCH_CHECK(rla::launch_mlp3(a, (int)kind, cur_stream(params)) == 0, "fused MLP v3 launch failed");
+  // repeat: the same launch back to back (every step's state lives on the device:
+  // counters, rings, generations), issued from this C++ loop -- one host call for a
+  // window of steps, a few us of launch work each against ~8 us of GPU time
+  const hipStream_t st = cur_stream(params);
+  for (int64_t i = 0; i < repeat; ++i)
+    TORCH_CHECK(rla::launch_mlp3(a, (int)kind, st) == 0, "fused MLP v3 launch failed");
 }
 
 void mlp_adam(Tensor params, Tensor grads, Tensor exp_avg, Tensor exp_avg_sq, Tensor shadow, int64_t L1,

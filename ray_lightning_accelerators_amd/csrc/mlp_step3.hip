@@ -1193,10 +1193,12 @@ __device__ __forceinline__ bool dp_owner_step(const MLP3Args& a, int unit, int o
 // needs no barrier either (every thread holds the same value; timeouts go straight
 // to the host-mapped error word).
 __device__ __forceinline__ uint32_t dp_gen_now(const MLP3Args& a) {
-  // a VECTOR load issued with the other tail-role prefetches at kernel start: a
-  // scalar load here shares lgkmcnt with every LDS access of the head pass, whose
-  // first waits then also waited for this (cold) load
-  return a.dp_gen[blockIdx.x] + 1u;
+  // a SCALAR load, issued with the step-state loads (ld_state) it is waited for
+  // together with.  (Round 3 used a vector load here; hipcc proves the value
+  // uniform, moves it to an SGPR with v_readfirstlane and waits vmcnt(0) for it
+  // right at kernel start, ahead of every prefetch: +0.7-1 us on the head pass of
+  // every exchange-capable instance, profiles/r4_dp.)
+  return ((const __attribute__((address_space(4))) uint32_t*)(a.dp_gen))[blockIdx.x] + 1u;
 }
 __device__ __forceinline__ void dp_end_nosync(const MLP3Args& a, uint32_t gen, int fail) {
   if (threadIdx.x == 0) a.dp_gen[blockIdx.x] = gen;
@@ -1582,7 +1584,10 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
   r.kind = -1;
   const int task = (blk - 1 - kTiles) * kWaves + w;
   if (small) small_compute<L1, L2, true>(a, true, task, r);  // setup + Adam state prefetch
-  const float lr_now = a.lr_ptr ? a.lr_ptr[0] : a.lr;
+  // the device learning rate through the SCALAR path: as a vector load, the f64 bias
+  // corrections below (thread 0) waited vmcnt(0) for it -- i.e. for every prologue
+  // prefetch -- before wave 0 issued a single head-pass load (profiles/r4_dp)
+  const float lr_now = a.lr_ptr ? ((const __attribute__((address_space(4))) float*)(a.lr_ptr))[0] : a.lr;
   // wave 0 of a tile: row (lane & 31) of X[t] (parked by the previous step) and the
   // sample index of row (lane & 31) of the NEXT batch (its pixels load after the head pass)
   __bf16* XR = reinterpret_cast<__bf16*>(a.xring);

@@ -24,7 +24,7 @@ from torch.utils.data import Dataset
 
 from ..lightning import LightningModule
 from ..ops.bn import BatchNormAct2d
-from ..ops.conv import Conv1x1NHWC
+from ..ops.conv import Conv1x1NHWC, GradFork
 from ..ops.pool import MaxPool2dNHWC
 from ..ops.shadow import ConvBF16
 
@@ -65,6 +65,13 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
+        if self.fused_bn and self.downsample is not None:
+            # conv1 and the downsample conv both read x: their input gradients meet in
+            # one tensor (ops.conv.GradFork) instead of an autograd add of two
+            fork = GradFork()
+            idt = self.downsample[1](self.downsample[0](x, fork=fork))
+            out = self.bn2(self.conv2(self.bn1(self.conv1(x, fork=fork))))
+            return self.bn3(self.conv3(out), idt, residual_is_ancestor=False)
         idt = x if self.downsample is None else self.downsample(x)
         if self.fused_bn:
             out = self.bn2(self.conv2(self.bn1(self.conv1(x))))

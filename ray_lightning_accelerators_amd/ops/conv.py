@@ -22,7 +22,7 @@ odd alignment) runs the stock convolution.  ``RLA_CONV1X1=miopen|gemm|auto``.
 from __future__ import annotations
 
 import os
-from typing import Dict, Tuple
+from typing import Dict, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -132,9 +132,51 @@ def _from2d(t2: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
     return t2.view(n, h, w, t2.size(1)).permute(0, 3, 1, 2)
 
 
+class GradFork:
+    """Two convolutions reading the SAME input (a bottleneck's conv1 and its
+    downsample conv): their input gradients meet in ONE tensor instead of two
+    tensors and an autograd add kernel (``CUDAFunctor_add<bf16>``,
+    ~200 us per ResNet-50 step).  Whichever backward runs first parks its full dgrad
+    here and returns None for the input; the second accumulates its contribution
+    INTO that tensor -- a GEMM with beta = 1 (stride 1), or a GEMM on the
+    subsampled rows plus an add into every s-th pixel only (stride s > 1) -- and
+    returns the sum.  Order-independent; autograd sees None + sum.  Only when BOTH
+    consumers took a fast path (each registers in its forward): with one consumer on a
+    stock fallback, the fast one returns its own gradient and autograd adds as usual."""
+
+    __slots__ = ("dx", "users")
+
+    def __init__(self):
+        self.dx: Optional[torch.Tensor] = None
+        self.users = 0
+
+
+def _fork_dx(fork: Optional[GradFork], full, accumulate) -> Optional[torch.Tensor]:
+    """``full()``: this op's dgrad as a new tensor; ``accumulate(d)``: add it into ``d``."""
+    if fork is None or fork.users < 2:
+        return full()
+    if fork.dx is None:
+        fork.dx = full()
+        return None
+    d, fork.dx = fork.dx, None
+    if accumulate is None:
+        d.add_(full())  # no fused form for this op: a plain add (still one tensor less)
+    else:
+        accumulate(d)
+    return d
+
+
+def _acc_dgrad(d: torch.Tensor, dy2: torch.Tensor, wb: torch.Tensor) -> None:
+    """d += dy . W for a stride-1 1x1 conv: in the GEMM (beta = 1) on d's NHWC view."""
+    if d.permute(0, 2, 3, 1).is_contiguous():
+        _nhwc2d(d).addmm_(dy2, wb)
+    else:
+        d.add_(_from2d(torch.mm(dy2, wb), d.size(0), d.size(2), d.size(3)))
+
+
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, shadow=None):
+    def forward(ctx, x, weight, shadow=None, fork=None):
         n, cin, h, w = x.shape
         cout = weight.size(0)
         # the arena's bf16 shadow (ops/shadow.py) when there is one: no cast kernel
@@ -151,6 +193,9 @@ class _Conv1x1Fn(torch.autograd.Function):
             y = _conv(x, wb.view(cout, cin, 1, 1), None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
         ctx.save_for_backward(x, wb)
         ctx.key = key
+        ctx.fork = fork
+        if fork is not None:
+            fork.users += 1
         return y
 
     @staticmethod
@@ -163,7 +208,11 @@ class _Conv1x1Fn(torch.autograd.Function):
         w4 = wb.view(cout, cin, 1, 1)
         dx = dw = None
         be_d = be_w = None
-        if ctx.needs_input_grad[0]:
+        fork = ctx.fork if ctx.needs_input_grad[0] else None
+        if fork is not None and fork.users >= 2 and fork.dx is not None:
+            # second of a forked pair: dx += dy . W in the GEMM itself (beta = 1)
+            dx = _fork_dx(fork, None, lambda d: _acc_dgrad(d, dy2, wb))
+        elif ctx.needs_input_grad[0]:
             be_d = _pick("dgrad", ctx.key, {
                 "gemm": lambda: torch.mm(dy2, wb),
                 "miopen": lambda: _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
@@ -178,14 +227,15 @@ class _Conv1x1Fn(torch.autograd.Function):
             if wgrad_ok(cin, cout):
                 cands["hip"] = lambda: wgrad_hip(dy, x, (1, 1), (1, 1), (0, 0))
             be_w = _pick("wgrad", ctx.key, cands)
-        if be_d == "miopen" and be_w == "miopen":
+        if be_d == "miopen" and be_w == "miopen" and fork is None:
             # both from MIOpen: one call (its host cost is tens of us per call)
             dx, dw = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, True, False])[:2]
-            return dx, dw.float(), None
+            return dx, dw.float(), None, None
         if be_d == "gemm":
-            dx = _from2d(torch.mm(dy2, wb), n, h, w)
+            dx = _fork_dx(fork, lambda: _from2d(torch.mm(dy2, wb), n, h, w), None)
         elif be_d == "miopen":
-            dx = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, False, False])[0]
+            dx = _fork_dx(fork, lambda: _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                                  [True, False, False])[0], None)
         if be_w == "hip":
             dw = wgrad_hip(dy, x, (1, 1), (1, 1), (0, 0))
         elif be_w == "gemm":
@@ -193,7 +243,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         elif be_w == "miopen":
             dw = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
                            [False, True, False])[1].float()
-        return dx, dw, None
+        return dx, dw, None, None
 
 
 def fast_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
@@ -212,14 +262,14 @@ class Conv1x1NHWC(nn.Conv2d):
     def __init__(self, in_channels: int, out_channels: int, device=None, dtype=None):
         super().__init__(in_channels, out_channels, 1, 1, 0, bias=False, device=device, dtype=dtype)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, fork: Optional[GradFork] = None) -> torch.Tensor:
         if torch.is_autocast_enabled("cuda") and x.is_cuda and x.dtype == torch.float32:
             x = x.to(torch.bfloat16)
         if fast_ok(x, self) and _mode() != "off":
             stats["fast"] += 1
             from .shadow import bf16_weight
 
-            return _Conv1x1Fn.apply(x, self.weight, bf16_weight(self.weight))
+            return _Conv1x1Fn.apply(x, self.weight, bf16_weight(self.weight), fork)
         stats["fallback"] += 1
         return F.conv2d(x, self.weight)
 
@@ -230,10 +280,13 @@ class _ConvNHWCFn(torch.autograd.Function):
     device time.  The weight gradient reaches the fp32 master weight in fp32."""
 
     @staticmethod
-    def forward(ctx, x, weight, wb, stride, padding):
+    def forward(ctx, x, weight, wb, stride, padding, fork=None):
         y = _conv(x, wb, None, list(stride), list(padding), [1, 1], False, [0, 0], 1)
         ctx.save_for_backward(x, wb)
         ctx.geo = (tuple(stride), tuple(padding))
+        ctx.fork = fork
+        if fork is not None:
+            fork.users += 1
         return y
 
     @staticmethod
@@ -243,6 +296,20 @@ class _ConvNHWCFn(torch.autograd.Function):
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = dw = None
         be = None
+        fork = ctx.fork if ctx.needs_input_grad[0] else None
+        if fork is not None and fork.users >= 2 and fork.dx is not None and wb.shape[2:] == (1, 1) \
+                and padding == (0, 0):
+            # second of a forked pair, strided 1x1: GEMM over the output pixels, added
+            # into every stride-th input pixel of the parked dgrad (1/s^2 of it)
+            cout, cin = wb.shape[:2]
+            g2 = torch.mm(_nhwc2d(dy), wb.reshape(cout, cin))
+
+            def acc(d):
+                view = d[:, :, ::stride[0], ::stride[1]]
+                view.add_(_from2d(g2, dy.size(0), dy.size(2), dy.size(3)))
+
+            dx = _fork_dx(fork, None, acc)
+            fork = None  # the input gradient is settled
         if ctx.needs_input_grad[1]:
             cout, cin, kh, kw = wb.shape
             key = (x.size(0) * dy.size(2) * dy.size(3), cin, cout, kh, kw, stride[0], padding[0])
@@ -255,19 +322,22 @@ class _ConvNHWCFn(torch.autograd.Function):
                 # "hip" is the halo kernel here; the generic tap-GEMM kernel competes too
                 cands["hip_gen"] = lambda: wgrad_hip(dy, x, (kh, kw), stride, padding, algo=1)
             be = _pick("wgrad_kxk", key, cands)
+        need_dx = bool(ctx.needs_input_grad[0]) and dx is None
         if be == "miopen":
             # MIOpen for both gradients: one call, as F.conv2d's autograd makes it
-            mask = [bool(ctx.needs_input_grad[0]), True, False]
-            dx, dw = _conv_bwd(dy, x, wb, None, list(stride), list(padding), [1, 1], False, [0, 0], 1, mask)[:2]
-            return dx, dw.float(), None, None, None
-        if ctx.needs_input_grad[0]:
-            dx = _conv_bwd(dy, x, wb, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
-                           [True, False, False])[0]
+            mask = [need_dx, True, False]
+            dxm, dw = _conv_bwd(dy, x, wb, None, list(stride), list(padding), [1, 1], False, [0, 0], 1, mask)[:2]
+            if need_dx:
+                dx = _fork_dx(fork, lambda: dxm, None)
+            return dx, dw.float(), None, None, None, None
+        if need_dx:
+            dx = _fork_dx(fork, lambda: _conv_bwd(dy, x, wb, None, list(stride), list(padding), [1, 1], False,
+                                                  [0, 0], 1, [True, False, False])[0], None)
         if be == "hip":
             dw = wgrad_hip(dy, x, (kh, kw), stride, padding)
         elif be == "hip_gen":
             dw = wgrad_hip(dy, x, (kh, kw), stride, padding, algo=1)
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
 def kxk_fast_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
@@ -278,8 +348,8 @@ def kxk_fast_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
             and wgrad_ok(conv.in_channels, conv.out_channels))
 
 
-def conv_nhwc(x: torch.Tensor, conv: nn.Conv2d, wb: torch.Tensor) -> torch.Tensor:
+def conv_nhwc(x: torch.Tensor, conv: nn.Conv2d, wb: torch.Tensor, fork: Optional[GradFork] = None) -> torch.Tensor:
     """``conv(x)`` with the bf16 weight ``wb`` (the arena shadow), the weight gradient
-    going to ``conv.weight`` in fp32."""
+    going to ``conv.weight`` in fp32 (``fork``: see :class:`GradFork`)."""
     stats["fast"] += 1
-    return _ConvNHWCFn.apply(x, conv.weight, wb, conv.stride, conv.padding)
+    return _ConvNHWCFn.apply(x, conv.weight, wb, conv.stride, conv.padding, fork)

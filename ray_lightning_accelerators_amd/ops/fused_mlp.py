@@ -245,8 +245,10 @@ def mlp3_launch(
     hand: Optional[torch.Tensor] = None,
     dp_proto: int = -1,
     dp_loop: bool = False,
+    repeat: int = 1,
 ) -> None:
-    """One v3 launch (GPU only).  ``kind``: MLP3_STEP (head + fused tail, world size 1),
+    """One v3 launch (GPU only; ``repeat``: that many identical launches back to back
+    from one C++ loop -- every step's state lives on the device).  ``kind``: MLP3_STEP (head + fused tail, world size 1),
     MLP3_HEAD / MLP3_TAIL_GRAD (gradients, before the allreduce), MLP3_TAIL_ADAM
     (Adam with ``grad_scale`` + next-step layer-1 partial, after it), MLP3_PRIME
     (layer-1 pre-activations of the pending batch from the current weights; the
@@ -267,7 +269,7 @@ def mlp3_launch(
         int(kind), x_u8, labels, order, counters, int(n_batches), int(B), int(L1), int(L2), params, grads, exp_avg,
         exp_avg_sq, shadow, dh1t, xring, h1pre, act, yring, stats, bool(advance_step), float(lr), float(betas[0]),
         float(betas[1]), float(eps), float(weight_decay), float(grad_scale), lr_tensor, bool(adamw), stamps,
-        [int(v) for v in (dp_ctx or ())], head_part, hand, int(dp_proto), bool(dp_loop),
+        [int(v) for v in (dp_ctx or ())], head_part, hand, int(dp_proto), bool(dp_loop), int(repeat),
     )
 
 

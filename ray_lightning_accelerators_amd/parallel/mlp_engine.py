@@ -153,6 +153,9 @@ class FusedMLPEngine:
         self._graph = None
         self._graph_steps = 0
         self._tail_graphs: Dict[int, "torch.cuda.CUDAGraph"] = {}  # remainder sizes (powers of two)
+        # run(): a window of one-launch steps as back-to-back launches from ONE C++
+        # call instead of hipGraph replays (see _run_loop; RLA_MLP_LAUNCH_LOOP=1)
+        self.launch_loop = os.environ.get("RLA_MLP_LAUNCH_LOOP", "0") == "1"
         self._primed = False
         self._host_epochs = False
         self.x_u8 = self.labels = self.order = None
@@ -375,7 +378,9 @@ class FusedMLPEngine:
             fused_mlp.mlp3_launch(fused_mlp.MLP3_PRIME, **self._kw3())
         self._primed = True
 
-    def _device_step(self) -> None:
+    def _device_step(self, repeat: int = 1) -> None:
+        """One step (``repeat``: that many back-to-back launches; one-launch kinds only)."""
+        assert repeat == 1 or self._loop_ok()
         if self.x_u8 is None:
             raise RuntimeError("set_data() first")
         if not self._primed:
@@ -386,12 +391,12 @@ class FusedMLPEngine:
             kw = self._kw3()
             if self.world_size == 1 and not self.dp_loop:
                 kind = fused_mlp.MLP3_STEP1 if self.one_launch else fused_mlp.MLP3_STEP
-                fused_mlp.mlp3_launch(kind, stats=self.stats, **kw)
+                fused_mlp.mlp3_launch(kind, stats=self.stats, repeat=repeat, **kw)
             elif self.dp_ctx is not None:
                 kind = fused_mlp.MLP3_STEP1_DP if self.one_launch_dp else fused_mlp.MLP3_STEP_DP
                 fused_mlp.mlp3_launch(kind, stats=self.stats, grad_scale=1.0 / self.dp_ctx[0],
                                       dp_ctx=self.dp_ctx, dp_proto=fused_mlp.DP_PROTOS.get(self.dp_proto, -1),
-                                      dp_loop=self.dp_loop, **kw)
+                                      dp_loop=self.dp_loop, repeat=repeat, **kw)
                 self._stepped_owner = self._stepped_owner or (self.one_launch_dp and self.dp_proto == "owner")
             else:
                 fused_mlp.mlp3_launch(fused_mlp.MLP3_HEAD, stats=self.stats, **kw)
@@ -508,7 +513,18 @@ class FusedMLPEngine:
         self._device_step()
         self._advance_host(1)
 
+    def _loop_ok(self) -> bool:
+        """A step is ONE launch (world 1 one-launch, or the one-launch DP step)."""
+        if not self.native:
+            return False
+        if self.world_size == 1 and not self.dp_loop:
+            return self.one_launch
+        return self.dp_ctx is not None and self.one_launch_dp
+
     def run(self, n_steps: int) -> None:
+        if self.launch_loop and self._loop_ok():
+            self._run_loop(n_steps)
+            return
         done = 0
         while done < n_steps:
             g, k = self._pick_graph(n_steps - done)
@@ -516,6 +532,23 @@ class FusedMLPEngine:
                 g.replay()
             else:
                 self._device_step()
+            self._advance_host(k)
+            done += k
+
+    def _run_loop(self, n_steps: int) -> None:
+        """``launch_loop``: the window's one-launch steps issued by ONE C++ call that
+        launches the kernel back to back (no hipGraph).  A graph replay costs ~10-16 us
+        of fixed host + dispatch time per replay (MI355X_MICROARCH.md
+        'graph-replay-floor'); back-to-back launches from an idle stream start in
+        ~3-5 us and then stay ahead of the ~8 us GPU step (host launch ~3.5 us each),
+        so a short timed window pays less fixed cost.  Chunks stop at epoch ends, where
+        the host refills the next epoch's order buffer (as the graph path does)."""
+        if not self._primed:
+            self.prime()
+        done = 0
+        while done < n_steps:
+            k = min(n_steps - done, self.n_batches - self.step_in_epoch)
+            self._device_step(repeat=k)
             self._advance_host(k)
             done += k
 

@@ -1,0 +1,64 @@
+"""GradFork: a bottleneck's conv1 and downsample conv accumulate their input
+gradients into ONE tensor (ops/conv.py) -- the gradient equals autograd's sum."""
+import pytest
+import torch
+
+from ray_lightning_accelerators_amd.ops import conv as C
+
+gpu = pytest.mark.gpu
+
+
+def test_fork_dx_order_independent_cpu():
+    a, b = torch.randn(2, 8, 4, 4), torch.randn(2, 8, 4, 4)
+    for first, second in ((a, b), (b, a)):
+        f = C.GradFork()
+        f.users = 2
+        assert C._fork_dx(f, lambda: first.clone(), None) is None
+        out = C._fork_dx(f, lambda: second.clone(), None)
+        assert torch.allclose(out, a + b) and f.dx is None
+    f = C.GradFork()
+    f.users = 1  # the other consumer is on a stock path: no parking
+    assert torch.equal(C._fork_dx(f, lambda: a, None), a)
+
+
+@gpu
+@pytest.mark.parametrize("stride", [1, 2])
+def test_forked_convs_match_autograd_sum(stride):
+    """conv1 (1x1, stride 1, GEMM / MIOpen) and the downsample conv (1x1, stride s)
+    on the same input: x.grad with the fork equals the plain two-branch autograd sum
+    (fp32 reference of the same bf16 ops), for both backward orders."""
+    from ray_lightning_accelerators_amd.ops.shadow import ConvBF16
+
+    torch.manual_seed(0)
+    dev = torch.device("cuda", 0)
+    cin, width, cout = 64, 64, 256
+    c1 = C.Conv1x1NHWC(cin, width).to(dev)
+    ds = (C.Conv1x1NHWC(cin, cout) if stride == 1 else ConvBF16(cin, cout, 1, stride, bias=False)).to(dev)
+    x0 = torch.randn(4, cin, 16, 16, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+    def run(use_fork, swap):
+        x = x0.clone().requires_grad_(True)
+        fork = C.GradFork() if use_fork else None
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            if swap:
+                a = c1(x, fork=fork)
+                b = ds(x, fork=fork)
+            else:
+                b = ds(x, fork=fork)
+                a = c1(x, fork=fork)
+        g = torch.Generator(device=dev).manual_seed(1)
+        ga = torch.randn(a.shape, device=dev, generator=g)
+        gb = torch.randn(b.shape, device=dev, generator=g)
+        (a.float() * ga.float()).sum().add_((b.float() * gb.float()).sum()).backward()
+        if use_fork:
+            assert fork.users == 2 and fork.dx is None
+        return x.grad.float(), c1.weight.grad.clone(), ds.weight.grad.clone()
+
+    for swap in (False, True):
+        c1.weight.grad = ds.weight.grad = None
+        ref = run(False, swap)
+        c1.weight.grad = ds.weight.grad = None
+        got = run(True, swap)
+        err = (got[0] - ref[0]).norm() / ref[0].norm()
+        assert err < 2e-2, err  # bf16 dgrad outputs, different rounding points
+        assert torch.allclose(got[1], ref[1]) and torch.allclose(got[2], ref[2])

@@ -586,7 +586,7 @@ def test_dp_packed_wire_keeps_non_finite_and_max_finite():
     fmax = torch.finfo(torch.float32).max
     special = [float("inf"), -float("inf"), float("nan"), fmax, -fmax, 0.0, -0.0, 1e-45, 1.0,
                torch.nextafter(torch.tensor(2.0), torch.tensor(0.0)).item()]
-    nan_low = torch.tensor([0x7F800001, 0x7F800003, 0xFF800002], dtype=torch.int32).view(torch.float32)
+    nan_low = torch.tensor([0x7F800001, 0x7F800003, 0xFF800002 - (1 << 32)], dtype=torch.int32).view(torch.float32)
     x = torch.cat([torch.tensor(special), nan_low, torch.randn(4096) * 1e3]).cuda()
     for tag in range(4):
         # every value in the encoded (even) position, then in the plain (odd) one
