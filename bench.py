@@ -65,13 +65,14 @@ RESNET_METRIC = "images/sec (whole node), ResNet-50 synthetic ImageNet 224px"
 # (BASELINE.md "Our MI355X measurements"; the reference publishes no numbers).
 # vs_baseline divides by the FASTER stock implementation.
 STOCK_BASELINE = {
-    "torch": 53015.0,        # eager nn.Linear + torch.optim.Adam (profiles/r1_first/bench_torch.jsonl)
+    "torch": 45378.2,        # eager nn.Linear + torch.optim.Adam (profiles/r3_stock; r1: 53,015)
     "torch-graph": 166204.1,  # the same step under torch.cuda.graph, 8 steps/graph (profiles/r3_stock; r2: 165,417)
 }
 # where each hard-coded number was measured (printed in the JSON next to it;
 # ``--compare-stock`` re-measures the eager stock step inside the same job)
 STOCK_BASELINE_SOURCE = {
-    "torch": "profiles/r1_first/bench_torch.jsonl (round 1, one MI355X, 2000 steps)",
+    "torch": "profiles/r3_stock/bench_torch.log (round 3 re-measurement, one MI355X, 2000 steps; "
+             "round 1: 53,015 in profiles/r1_first/bench_torch.jsonl)",
     "torch-graph": "profiles/r3_stock/bench_torch_graph.log (round 3 re-measurement, one MI355X, 2000 steps; "
                    "round 2: 165,417 in profiles/r2_c03)",
 }

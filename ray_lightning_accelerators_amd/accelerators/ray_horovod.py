@@ -96,9 +96,13 @@ class HorovodRayExecutor:
                 "HOROVOD_CONTROLLER": "gloo", "HOROVOD_CPU_OPERATIONS": "gloo",
             }
             if self.use_gpu:
-                vis = ",".join(host_gpus[ip])
+                # the host's GPUs, each once (a rehearsal ledger can list one device for
+                # several slots); RLA_HVD_DEVICE: this slot's index among them
+                ids = list(dict.fromkeys(host_gpus[ip]))
+                vis = ",".join(ids)
                 env.update({"HIP_VISIBLE_DEVICES": vis, "CUDA_VISIBLE_DEVICES": vis,
-                            "HOROVOD_GPU_OPERATIONS": "NCCL", "RLA_HVD_USE_GPU": "1"})
+                            "HOROVOD_GPU_OPERATIONS": "NCCL", "RLA_HVD_USE_GPU": "1",
+                            "RLA_HVD_DEVICE": ids.index(host_gpus[ip][lr]) if lr < len(host_gpus[ip]) else lr})
             env.update(extra_env_vars or {})
             envs.append(env)
         ray.get([w.set_env_vars.remote(e) for w, e in zip(self.workers, envs)])
@@ -221,7 +225,9 @@ class HorovodRayAccelerator(Accelerator):
         rank_zero_only_state.rank = hvd.rank()
         log_config(hvd.rank(), self.config)
         if self.use_gpu:
-            trainer.root_gpu = hvd.local_rank()
+            # the slot's device among the host's visible GPUs (== local rank on a real
+            # node; 0 for every slot of a one-device rehearsal ledger)
+            trainer.root_gpu = int(os.environ.get("RLA_HVD_DEVICE", hvd.local_rank()))
             torch.cuda.set_device(trainer.root_gpu)
             self.root_device = torch.device("cuda", trainer.root_gpu)
         else:

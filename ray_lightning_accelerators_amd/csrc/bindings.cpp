@@ -395,6 +395,24 @@ const float* bn_ss(const optional<Tensor>& ss, int64_t C) {
   return ss->data_ptr<float>();
 }
 
+// Ticket counters of the BN partial kernels' second reduction level: one zeroed
+// buffer per device, allocated outside any stream capture (hipMalloc is not
+// capturable; a capture that finds none yet runs the single-level partials) and
+// reset in-kernel by each group's last block.  Launches on one stream never
+// overlap, so every call can reuse the same tickets.
+int* bn_tickets(int device, hipStream_t stream) {
+  static int* bufs[64] = {};
+  if (device < 0 || device >= 64) return nullptr;
+  if (bufs[device]) return bufs[device];
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+  int* p = nullptr;
+  if (hipMalloc(reinterpret_cast<void**>(&p), 4096 * sizeof(int)) != hipSuccess) return nullptr;
+  if (hipMemset(p, 0, 4096 * sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
+  bufs[device] = p;
+  return p;
+}
+
 Tensor bn_partial(Tensor x, optional<Tensor> y, optional<Tensor> dy, int64_t C, int64_t mode, bool relu,
                   optional<Tensor> nbt, optional<Tensor> dy2, optional<Tensor> ss) {
   const int64_t M = bn_rows(x, "x", C);
@@ -416,16 +434,26 @@ Tensor bn_partial(Tensor x, optional<Tensor> y, optional<Tensor> dy, int64_t C, 
   const rla::BnPlan plan = rla::bn_plan(M, (int)C);
   Tensor part = at::empty({plan.blocks, 2, C}, x.options().dtype(at::kFloat));
   int64_t* nbtp = mode == 0 ? ptr_or_null<int64_t>(nbt, "num_batches_tracked", at::kLong, 1) : nullptr;
+  // second reduction level in the partial kernel: the finalize reads `groups` fp64
+  // rows (returned instead of the per-block fp32 partials)
+  rla::BnLevel2 lv{nullptr, nullptr};
+  Tensor rows;
+  int* tickets = plan.group > 1 ? bn_tickets(x.device().index(), cur_stream(x)) : nullptr;
+  if (tickets) {
+    rows = at::empty({plan.groups, 2, C}, x.options().dtype(at::kDouble));
+    lv = rla::BnLevel2{rows.data_ptr<double>(), tickets};
+  }
   rla::launch_bn_partial(reinterpret_cast<const uint16_t*>(x.data_ptr()), yp, dyp, M, (int)C, (int)mode, relu,
                          plan, part.data_ptr<float>(), nbtp, cur_stream(x), mode == 1 ? bn_dy2(x, dy2, C) : nullptr,
-                         mode == 1 && relu ? bn_ss(ss, C) : nullptr);
-  return part;
+                         mode == 1 && relu ? bn_ss(ss, C) : nullptr, lv);
+  return tickets ? rows : part;
 }
 
 Tensor bn_finalize(Tensor part, double count, optional<Tensor> weight, optional<Tensor> bias,
                    optional<Tensor> running_mean, optional<Tensor> running_var, optional<Tensor> nbt,
                    double momentum, double eps) {
-  check_dev(part, "partials", at::kFloat);
+  const bool l2 = part.scalar_type() == at::kDouble;  // second-level rows of bn_partial
+  check_dev(part, "partials", l2 ? at::kDouble : at::kFloat);
   TORCH_CHECK(part.dim() == 3 && part.size(1) == 2, "partials must be [blocks, 2, C]");
   const int64_t C = part.size(2);
   TORCH_CHECK(count > 0, "fused BN: count must be > 0");
@@ -435,25 +463,36 @@ Tensor bn_finalize(Tensor part, double count, optional<Tensor> weight, optional<
   const int64_t* nbtp = ptr_or_null<const int64_t>(nbt, "num_batches_tracked", at::kLong, 1);
   TORCH_CHECK(momentum >= 0 || nbtp, "cumulative averaging (momentum=None) needs num_batches_tracked");
   const at::hip::HIPGuardMasqueradingAsCUDA guard(part.device());
-  Tensor stats = at::empty({4, C}, part.options());
-  rla::launch_bn_finalize(part.data_ptr<float>(), (int)part.size(0), (int)C, count, f32_vec(weight, "weight", C),
-                          f32_vec(bias, "bias", C), rm, rv, nbtp, (float)momentum, (float)eps,
-                          stats.data_ptr<float>(), cur_stream(part));
+  Tensor stats = at::empty({4, C}, part.options().dtype(at::kFloat));
+  if (l2)
+    rla::launch_bn_finalize64(part.data_ptr<double>(), (int)part.size(0), (int)C, count, f32_vec(weight, "weight", C),
+                              f32_vec(bias, "bias", C), rm, rv, nbtp, (float)momentum, (float)eps,
+                              stats.data_ptr<float>(), cur_stream(part));
+  else
+    rla::launch_bn_finalize(part.data_ptr<float>(), (int)part.size(0), (int)C, count, f32_vec(weight, "weight", C),
+                            f32_vec(bias, "bias", C), rm, rv, nbtp, (float)momentum, (float)eps,
+                            stats.data_ptr<float>(), cur_stream(part));
   return stats;
 }
 
 Tensor bn_bwd_finalize(Tensor part, double count, optional<Tensor> weight, Tensor mean, Tensor invstd) {
-  check_dev(part, "partials", at::kFloat);
+  const bool l2 = part.scalar_type() == at::kDouble;
+  check_dev(part, "partials", l2 ? at::kDouble : at::kFloat);
   TORCH_CHECK(part.dim() == 3 && part.size(1) == 2, "partials must be [blocks, 2, C]");
   const int64_t C = part.size(2);
   check_dev(mean, "mean", at::kFloat);
   check_dev(invstd, "invstd", at::kFloat);
   TORCH_CHECK(mean.numel() == C && invstd.numel() == C, "mean / invstd must have C elements");
   const at::hip::HIPGuardMasqueradingAsCUDA guard(part.device());
-  Tensor coef = at::empty({5, C}, part.options());
-  rla::launch_bn_bwd_finalize(part.data_ptr<float>(), (int)part.size(0), (int)C, count,
-                              f32_vec(weight, "weight", C), mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                              coef.data_ptr<float>(), cur_stream(part));
+  Tensor coef = at::empty({5, C}, part.options().dtype(at::kFloat));
+  if (l2)
+    rla::launch_bn_bwd_finalize64(part.data_ptr<double>(), (int)part.size(0), (int)C, count,
+                                  f32_vec(weight, "weight", C), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                                  coef.data_ptr<float>(), cur_stream(part));
+  else
+    rla::launch_bn_bwd_finalize(part.data_ptr<float>(), (int)part.size(0), (int)C, count,
+                                f32_vec(weight, "weight", C), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                                coef.data_ptr<float>(), cur_stream(part));
   return coef;
 }
 

@@ -69,13 +69,29 @@ __device__ __forceinline__ f8 relu_mask(f8 d, f8 y) {
 // the two into a new tensor first (ops/bn.py, fold_residual_grad)
 // RECOMP (backward, ReLU without residual): the mask is x*scale+shift > 0 recomputed
 // from the forward statistics `ss` ([4, C]: mean, invstd, scale, shift) -- y is not read
+// L2 (two-level reduction, bn_plan's `group` > 1): the partial rows are stored
+// write-through (sc1); one lane per block takes a ticket on its group's counter
+// (agent scope, after every wave drained its stores); the block that draws the
+// group's last ticket sums the group's rows in block order in fp64 (sc1 loads, the
+// guide's write-through + ticket hand-off, MI355X_MICROARCH.md §visibility) into row
+// `group index` of `l2` and resets the counter.  bn_finalize then reads a handful
+// of fp64 rows instead of up to 512 fp32 rows -- its small-C launches were ONE
+// block streaming 256 KB of partials (~5 us).  Deterministic:
+// fixed order at both levels.
+struct BnL2 {
+  double* rows;   // [ceil(blocks / group), 2, C]
+  int* cnt;       // [ceil(blocks / group)] zero-initialised tickets (reset by each last arriver)
+  int group;      // blocks per group (1: no second level)
+};
+
 template <int MODE, bool RELU, bool DY2 = false, bool RECOMP = false>
 __global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(const uint16_t* __restrict__ x,
                                                                 const uint16_t* __restrict__ y,
                                                                 const uint16_t* __restrict__ dy, int64_t M, int C,
                                                                 int64_t rows_per_blk, float* __restrict__ part,
                                                                 int64_t* nbt, const uint16_t* __restrict__ dy2 = nullptr,
-                                                                const float* __restrict__ ss = nullptr) {
+                                                                const float* __restrict__ ss = nullptr,
+                                                                BnL2 l2 = BnL2{nullptr, nullptr, 1}) {
   // forward: one input stream, so twice the rows in flight per thread
   constexpr int U = MODE == 0 ? 8 : 4;
   __shared__ float sh[2][kBnThreads * 8];
@@ -147,8 +163,46 @@ __global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(const uint16_t* 
       a += sh[0][r * C + c];
       b += sh[1][r * C + c];
     }
-    out[c] = a;
-    out[C + c] = b;
+    if (l2.group > 1) {  // write-through: read by another block of this launch
+      __hip_atomic_store(out + c, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(out + C + c, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      out[c] = a;
+      out[C + c] = b;
+    }
+  }
+  if (l2.group <= 1) return;
+  __shared__ int sh_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drained
+  __syncthreads();
+  const int grp = (int)blockIdx.x / l2.group;
+  const int g0 = grp * l2.group;
+  const int gsz = (int)gridDim.x - g0 < l2.group ? (int)gridDim.x - g0 : l2.group;
+  if (tid == 0) {
+    const int t = __hip_atomic_fetch_add(l2.cnt + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sh_last = t == gsz - 1;
+    if (sh_last) __hip_atomic_store(l2.cnt + grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!sh_last) return;
+  const float* rows = part + (int64_t)g0 * 2 * C;
+  double* dst = l2.rows + (int64_t)grp * 2 * C;
+  for (int c = tid; c < 2 * C; c += kBnThreads) {
+    double acc = 0.0;
+    int k = 0;
+    for (; k + 8 <= gsz; k += 8) {  // 8 loads in flight
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = __hip_atomic_load(const_cast<float*>(rows + (int64_t)(k + u) * 2 * C + c), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += (double)v[u];
+    }
+    for (; k < gsz; ++k)
+      acc += (double)__hip_atomic_load(const_cast<float*>(rows + (int64_t)k * 2 * C + c), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+    dst[c] = acc;
   }
 }
 
@@ -157,8 +211,8 @@ __global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(const uint16_t* 
 // flight per thread, fp64 accumulation; the slices are combined through LDS.
 constexpr int kFinSlices = 16;
 
-template <bool BWD>
-__global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restrict__ part, int nparts, int C,
+template <bool BWD, typename P = float>
+__global__ __launch_bounds__(1024) void bn_finalize_kernel(const P* __restrict__ part, int nparts, int C,
                                                            double count, const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, float* running_mean,
                                                            float* running_var, const int64_t* nbt, float momentum,
@@ -171,12 +225,12 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restri
   double a = 0.0, b = 0.0;
   if (c < C) {
     const int64_t rs = 2 * (int64_t)C;
-    const float* q = part + c;
+    const P* q = part + c;
     int p = sl;
     // 8 partial rows in flight per thread: the small-C layers' finalize runs on one
     // or two blocks and is latency-bound on these loads
     for (; p + 7 * kFinSlices < nparts; p += 8 * kFinSlices) {
-      float v[16];
+      P v[16];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         v[2 * u] = q[(p + u * kFinSlices) * rs];
@@ -333,40 +387,47 @@ BnPlan bn_plan(int64_t M, int C) {
   p.rows_per_blk = (M + blocks - 1) / blocks;
   p.blocks = (int)((M + p.rows_per_blk - 1) / p.rows_per_blk);
   if (p.blocks < 1) p.blocks = 1;
+  // second level: groups whose rows (group x 2C fp32) one block sums in ~1 us
+  // (<= 32 KB); only where the finalize would otherwise stream many rows
+  int g = 4096 / C;
+  if (g > p.blocks) g = p.blocks;
+  p.group = p.blocks > 16 && g > 1 ? g : 1;
+  p.groups = (p.blocks + p.group - 1) / p.group;
   return p;
 }
 
 void launch_bn_partial(const uint16_t* x, const uint16_t* y, const uint16_t* dy, int64_t M, int C, int mode,
                        bool relu, const BnPlan& plan, float* part, int64_t* nbt, hipStream_t s, const uint16_t* dy2,
-                       const float* ss) {
+                       const float* ss, BnLevel2 lv) {
   const dim3 grid(plan.blocks), block(kBnThreads);
+  const BnL2 L{lv.rows, lv.tickets, lv.rows ? plan.group : 1};
   if (mode == 1 && relu && ss) {
     if (dy2)
       hipLaunchKernelGGL((bn_partial_kernel<1, true, true, true>), grid, block, 0, s, x, y, dy, M, C,
-                         plan.rows_per_blk, part, nullptr, dy2, ss);
+                         plan.rows_per_blk, part, nullptr, dy2, ss, L);
     else
       hipLaunchKernelGGL((bn_partial_kernel<1, true, false, true>), grid, block, 0, s, x, y, dy, M, C,
-                         plan.rows_per_blk, part, nullptr, nullptr, ss);
+                         plan.rows_per_blk, part, nullptr, nullptr, ss, L);
     return;
   }
   if (mode == 1 && dy2) {
     if (relu)
       hipLaunchKernelGGL((bn_partial_kernel<1, true, true>), grid, block, 0, s, x, y, dy, M, C, plan.rows_per_blk,
-                         part, nullptr, dy2);
+                         part, nullptr, dy2, nullptr, L);
     else
       hipLaunchKernelGGL((bn_partial_kernel<1, false, true>), grid, block, 0, s, x, y, dy, M, C, plan.rows_per_blk,
-                         part, nullptr, dy2);
+                         part, nullptr, dy2, nullptr, L);
     return;
   }
   if (mode == 0)
     hipLaunchKernelGGL((bn_partial_kernel<0, false>), grid, block, 0, s, x, y, dy, M, C, plan.rows_per_blk, part,
-                       nbt);
+                       nbt, nullptr, nullptr, L);
   else if (relu)
     hipLaunchKernelGGL((bn_partial_kernel<1, true>), grid, block, 0, s, x, y, dy, M, C, plan.rows_per_blk, part,
-                       nullptr);
+                       nullptr, nullptr, nullptr, L);
   else
     hipLaunchKernelGGL((bn_partial_kernel<1, false>), grid, block, 0, s, x, y, dy, M, C, plan.rows_per_blk, part,
-                       nullptr);
+                       nullptr, nullptr, nullptr, L);
 }
 
 void launch_bn_finalize(const float* part, int nparts, int C, double count, const float* gamma,
@@ -380,6 +441,19 @@ void launch_bn_bwd_finalize(const float* part, int nparts, int C, double count, 
                             const float* mean, const float* invstd, float* coef, hipStream_t s) {
   hipLaunchKernelGGL((bn_finalize_kernel<true>), dim3((C + 63) / 64), dim3(1024), 0, s, part, nparts, C, count,
                      gamma, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, mean, invstd, coef);
+}
+
+void launch_bn_finalize64(const double* part, int nparts, int C, double count, const float* gamma,
+                          const float* beta, float* running_mean, float* running_var, const int64_t* nbt,
+                          float momentum, float eps, float* stats, hipStream_t s) {
+  hipLaunchKernelGGL((bn_finalize_kernel<false, double>), dim3((C + 63) / 64), dim3(1024), 0, s, part, nparts, C,
+                     count, gamma, beta, running_mean, running_var, nbt, momentum, eps, nullptr, nullptr, stats);
+}
+
+void launch_bn_bwd_finalize64(const double* part, int nparts, int C, double count, const float* gamma,
+                              const float* mean, const float* invstd, float* coef, hipStream_t s) {
+  hipLaunchKernelGGL((bn_finalize_kernel<true, double>), dim3((C + 63) / 64), dim3(1024), 0, s, part, nparts, C,
+                     count, gamma, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, mean, invstd, coef);
 }
 
 void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* scale, const float* shift, int64_t M,

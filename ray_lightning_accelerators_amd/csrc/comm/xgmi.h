@@ -17,11 +17,12 @@ constexpr int kDpMaxBlocks = 128;
 
 // Wave-positioned areas of the one-launch step's exchange protocols (mlp_step3.hip,
 // "packed" and "owner"): one exchange UNIT per (block, wave) = 64 lanes x 4 values.
-//   packed / reduce-scatter area: [2 slots][kXgmiMaxRanks srcs][kDpMaxUnits][2][64] 8-B granules
+//   packed / reduce-scatter area: [2 slots][kXgmiMaxRanks srcs][kDpMaxUnits][64 lanes][2] 8-B granules
 //     (two values per granule, the tag in the low mantissa bits of the first)
-//   all-gather area:              [2 slots][kDpMaxUnits][4][64] 8-B {generation, fp32} granules
-// Every store instruction of a wave covers 512 contiguous bytes (whole 64-B lines
-// over the link), not 64 scattered arena positions.
+//   all-gather area:              [2 slots][kDpMaxUnits][64 lanes][4] 8-B {generation, fp32} granules
+// A lane's granules are adjacent, so it moves them 16 B per instruction and every
+// store instruction of a wave covers 1 KB contiguous bytes (whole 64-B lines over
+// the link), not 64 scattered arena positions.
 constexpr int kDpMaxUnits = kDpMaxBlocks * 8;
 constexpr int64_t kDpPackedGranules = 2LL * kXgmiMaxRanks * kDpMaxUnits * 128;
 constexpr int64_t kDpGatherGranules = 2LL * kDpMaxUnits * 256;

@@ -57,8 +57,15 @@ constexpr int kBnMaxC = 2048;  // 8 channels per thread x 256 threads per row
 struct BnPlan {
   int64_t rows_per_blk;  // rows each block of the partial kernels reduces
   int blocks;
+  int group;   // > 1: blocks per group of the in-kernel second reduction level (fp64 rows)
+  int groups;  // ceil(blocks / group): rows the finalize reads
 };
 BnPlan bn_plan(int64_t M, int C);
+// second reduction level of the partial kernels (see bn_act.hip BnL2)
+struct BnLevel2 {
+  double* rows;  // [groups, 2, C] or nullptr (single level)
+  int* tickets;  // [groups] zero-initialised, self-resetting
+};
 
 // per-block partial sums part[b][0][c], part[b][1][c]:
 //   mode 0 (forward):  sum x, sum x^2   (nbt, if given, is incremented by block 0)
@@ -66,17 +73,24 @@ BnPlan bn_plan(int64_t M, int C);
 void launch_bn_partial(const uint16_t* x, const uint16_t* y, const uint16_t* dy, int64_t M, int C, int mode,
                        bool relu, const BnPlan& plan, float* part, int64_t* nbt, hipStream_t s,
                        const uint16_t* dy2 = nullptr,   // backward: gradient = dy + dy2
-                       const float* ss = nullptr);      // backward ReLU mask from the fwd stats, not y
+                       const float* ss = nullptr,       // backward ReLU mask from the fwd stats, not y
+                       BnLevel2 l2 = BnLevel2{nullptr, nullptr});
 
 // forward finalize of `nparts` partial rows: stats[0]=mean [1]=invstd [2]=scale [3]=shift ([4, C]);
 // running stats update (momentum < 0: cumulative average over num_batches_tracked)
 void launch_bn_finalize(const float* part, int nparts, int C, double count, const float* gamma,
                         const float* beta, float* running_mean, float* running_var, const int64_t* nbt,
                         float momentum, float eps, float* stats, hipStream_t s);
+// the same from the fp64 rows of the second reduction level
+void launch_bn_finalize64(const double* part, int nparts, int C, double count, const float* gamma,
+                          const float* beta, float* running_mean, float* running_var, const int64_t* nbt,
+                          float momentum, float eps, float* stats, hipStream_t s);
 
 // backward finalize: coef[0]=dgamma [1]=dbeta [2]=A [3]=B [4]=Cc ([5, C]); dx = A*dz + B*x + Cc
 void launch_bn_bwd_finalize(const float* part, int nparts, int C, double count, const float* gamma,
                             const float* mean, const float* invstd, float* coef, hipStream_t s);
+void launch_bn_bwd_finalize64(const double* part, int nparts, int C, double count, const float* gamma,
+                              const float* mean, const float* invstd, float* coef, hipStream_t s);
 
 // y = act(x*scale + shift (+ res))
 void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* scale, const float* shift, int64_t M,

@@ -1001,19 +1001,40 @@ __device__ __forceinline__ u64 pk2(float v0, float v1, uint32_t tag) {
 __device__ __forceinline__ float pk_lo(u64 w) { return __uint_as_float((uint32_t)w & ~3u); }
 __device__ __forceinline__ float pk_hi(u64 w) { return __uint_as_float((uint32_t)(w >> 32)); }
 
-__device__ __forceinline__ u64* dp_pk_area(char* region, int slot, int src, int unit) {
-  return reinterpret_cast<u64*>(region + kXgmiFlagBytes) +
-         (((int64_t)slot * kXgmiMaxRanks + src) * comm::kDpMaxUnits + unit) * 128;
+// Wire layout (round 4): each lane's share of a unit is CONTIGUOUS -- packed /
+// reduce-scatter area: lane l's two granules {g0, g1} at u64 [2l, 2l + 1] of the
+// unit's 1 KB; all-gather area: its four {gen, fp32} granules at u64 [4l, 4l + 3]
+// of 2 KB -- so a lane moves 16 B per instruction (buffer_load / store_dwordx4 sc0
+// sc1) instead of 8 B: half the poll and push instructions, and 16-B system-scope
+// accesses run at the full rate where 8-B ones ran at 0.54-0.70x of it
+// (MI355X_MICROARCH.md, the visibility table).  Each 8-B granule still carries its
+// own tag / generation, so a 16-B access torn between its halves is harmless.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+// byte offsets inside a region
+__device__ __forceinline__ uint32_t dp_pk_off(int slot, int src, int unit) {
+  return (uint32_t)(kXgmiFlagBytes + ((((int64_t)slot * kXgmiMaxRanks + src) * comm::kDpMaxUnits + unit) * 128) * 8);
 }
-__device__ __forceinline__ u64* dp_ag_area(char* region, int slot, int unit) {
-  return reinterpret_cast<u64*>(region + kXgmiFlagBytes) + comm::kDpPackedGranules +
-         ((int64_t)slot * comm::kDpMaxUnits + unit) * 256;
+__device__ __forceinline__ uint32_t dp_ag_off(int slot, int unit) {
+  return (uint32_t)(kXgmiFlagBytes + (comm::kDpPackedGranules + ((int64_t)slot * comm::kDpMaxUnits + unit) * 256) * 8);
 }
-__device__ __forceinline__ void st_sys(u64* p, u64 w) {
-  __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+constexpr uint32_t kDpSrcBytes = (uint32_t)comm::kDpMaxUnits * 128 * 8;  // bytes per source rank of a slot
+static_assert((int64_t)kXgmiFlagBytes + (comm::kDpPackedGranules + comm::kDpGatherGranules) * 8 < (1ll << 31),
+              "32-bit buffer offsets");
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t dp_rsrc(char* region) {
+  // raw buffer over the whole region (gfx9 dword3); offsets stay below 2^31
+  return __builtin_amdgcn_make_buffer_rsrc(region, 0, 0x7fffffff, 0x00020000);
 }
-__device__ __forceinline__ u64 ld_sys(const u64* p) {
-  return __hip_atomic_load(const_cast<u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+constexpr int kSysPolicy = 1 | 16;  // sc0 | sc1: system scope (peer memory over xGMI)
+__device__ __forceinline__ void st_sys2(__amdgpu_buffer_rsrc_t r, uint32_t off, u64 a, u64 b) {
+  const u32x4_t v = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kSysPolicy);
+}
+__device__ __forceinline__ void ld_sys2(__amdgpu_buffer_rsrc_t r, uint32_t off, u64& a, u64& b) {
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kSysPolicy);
+  a = (u64)v[0] | ((u64)v[1] << 32);
+  b = (u64)v[2] | ((u64)v[3] << 32);
 }
 
 // Polls of the wave-positioned protocols are compiled for a rank CLASS NW (the
@@ -1024,21 +1045,20 @@ __device__ __forceinline__ u64 ld_sys(const u64* p) {
 // run-time world size).  Peer slots k < NW - 1 that the actual world does not have
 // re-read our own source slot (a valid address) and are never checked.
 constexpr int kDpPeerGran = 2 * (kXgmiMaxRanks - 1);
-constexpr int64_t kDpSrcGran = (int64_t)comm::kDpMaxUnits * 128;  // granules per source rank of a slot
 
 // peer slot k (0..NW-2) -> its rank: the ranks in order, ours skipped
 __device__ __forceinline__ int dp_peer(int k, int me) { return k < me ? k : k + 1; }
 
 // issue the 2 (NW - 1) peer granules of (slot, unit) in our own region: granule 2k + h
 // is half h of peer k's contribution
+// (src0: byte offset of source rank 0's area of this slot / unit, plus this lane's 16 B)
 template <int NW>
-__device__ __forceinline__ void dp_peer_issue(u64 (&w)[2 * (NW - 1)], const u64* src0, int me, int W) {
+__device__ __forceinline__ void dp_peer_issue(u64 (&w)[2 * (NW - 1)], __amdgpu_buffer_rsrc_t mine, uint32_t src0,
+                                              int me, int W) {
 #pragma unroll
   for (int k = 0; k < NW - 1; ++k) {
     const int s = dp_peer(k, me);
-    const u64* p = src0 + (int64_t)(s < W ? s : me) * kDpSrcGran;
-    w[2 * k] = ld_sys(p);
-    w[2 * k + 1] = ld_sys(p + 64);
+    ld_sys2(mine, src0 + (uint32_t)(s < W ? s : me) * kDpSrcBytes, w[2 * k], w[2 * k + 1]);
   }
 }
 
@@ -1046,8 +1066,8 @@ __device__ __forceinline__ void dp_peer_issue(u64 (&w)[2 * (NW - 1)], const u64*
 // expires: *fail).  Re-polls re-issue all of them (unconditional, still one round
 // trip; a matched granule is not rewritten before this wave's own next step).
 template <int NW>
-__device__ __forceinline__ void dp_peer_wait(const MLP3Args& a, u64 (&w)[2 * (NW - 1)], const u64* src0, int me,
-                                             int W, uint32_t tag, int* fail) {
+__device__ __forceinline__ void dp_peer_wait(const MLP3Args& a, u64 (&w)[2 * (NW - 1)], __amdgpu_buffer_rsrc_t mine,
+                                             uint32_t src0, int me, int W, uint32_t tag, int* fail) {
   int64_t spins = 0;
   while (true) {
     bool all = true;
@@ -1060,7 +1080,7 @@ __device__ __forceinline__ void dp_peer_wait(const MLP3Args& a, u64 (&w)[2 * (NW
       return;
     }
     __builtin_amdgcn_s_sleep(1);
-    dp_peer_issue<NW>(w, src0, me, W);
+    dp_peer_issue<NW>(w, mine, src0, me, W);
   }
 }
 
@@ -1084,10 +1104,7 @@ __device__ __forceinline__ void dp_packed_sum(const u64 (&w)[2 * (NW - 1)], int 
 }
 
 __device__ __forceinline__ void dp_push_packed(char* region, int slot, int src, int unit, u64 g0, u64 g1) {
-  const int lane = threadIdx.x & 63;
-  u64* d = dp_pk_area(region, slot, src, unit);
-  st_sys(d + lane, g0);
-  st_sys(d + 64 + lane, g1);
+  st_sys2(dp_rsrc(region), dp_pk_off(slot, src, unit) + 16u * (threadIdx.x & 63), g0, g1);
 }
 
 // this rank's contribution to every peer (loopback: into every peer's source slot
@@ -1107,17 +1124,23 @@ template <int NW>
 __device__ __forceinline__ void dp_packed_exchange(const MLP3Args& a, int unit, uint32_t gen, float (&v)[4],
                                                    float scale, int* fail) {
   const int slot = (int)(gen & 1u), me = a.dp_rank, W = a.dp_world;
+  if (W == 1) {  // (uniform) nothing to exchange
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] *= scale;
+    return;
+  }
   const uint32_t tag = (gen >> 1) & 3u;
   const u64 g0 = pk2(v[0], v[1], tag), g1 = pk2(v[2], v[3], tag);
-  const u64* src0 = dp_pk_area(a.dp_regions[me], slot, 0, unit) + (threadIdx.x & 63);
+  const __amdgpu_buffer_rsrc_t mine = dp_rsrc(a.dp_regions[me]);
+  const uint32_t src0 = dp_pk_off(slot, 0, unit) + 16u * (threadIdx.x & 63);
   u64 w[2 * (NW - 1)];
   // first polls before the pushes: gfx950 counts loads AND stores in one in-order
   // vmcnt, so pushes issued first would make the first wait cover their remote
   // completion too.  Loopback reads its own pushes: polls after them.
-  if (!a.dp_loop) dp_peer_issue<NW>(w, src0, me, W);
+  if (!a.dp_loop) dp_peer_issue<NW>(w, mine, src0, me, W);
   dp_push_all<NW>(a, slot, unit, g0, g1);
-  if (a.dp_loop) dp_peer_issue<NW>(w, src0, me, W);
-  dp_peer_wait<NW>(a, w, src0, me, W, tag, fail);
+  if (a.dp_loop) dp_peer_issue<NW>(w, mine, src0, me, W);
+  dp_peer_wait<NW>(a, w, mine, src0, me, W, tag, fail);
   dp_packed_sum<NW>(w, me, W, g0, g1, v, scale);
 }
 
@@ -1133,24 +1156,31 @@ template <int NW, typename AdamFn>
 __device__ __forceinline__ bool dp_owner_step(const MLP3Args& a, int unit, int owner, uint32_t gen, float (&v)[4],
                                               float scale, int* fail, AdamFn adam) {
   const int lane = threadIdx.x & 63, slot = (int)(gen & 1u), me = a.dp_rank, W = a.dp_world;
+  if (W == 1) {  // (uniform) every task is ours and there is nothing to exchange
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] *= scale;
+    adam(v);
+    return true;
+  }
   const uint32_t tag = (gen >> 1) & 3u;
   const bool own = owner == me;
   const u64 g0 = pk2(v[0], v[1], tag), g1 = pk2(v[2], v[3], tag);
-  const u64* agsrc = dp_ag_area(a.dp_regions[me], slot, unit) + lane;
+  const __amdgpu_buffer_rsrc_t mine = dp_rsrc(a.dp_regions[me]);
+  const uint32_t agsrc = dp_ag_off(slot, unit) + 32u * lane;
   u64 wa[4];
   auto ag_issue = [&]() {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) wa[i] = ld_sys(agsrc + i * 64);
+    ld_sys2(mine, agsrc, wa[0], wa[1]);
+    ld_sys2(mine, agsrc + 16u, wa[2], wa[3]);
   };
   if (!own && !a.dp_loop) ag_issue();  // first polls before the push
   if (!own) dp_push_packed(a.dp_regions[owner], slot, me, unit, g0, g1);
   if (own || a.dp_loop) {
     if (own) {
-      const u64* src0 = dp_pk_area(a.dp_regions[me], slot, 0, unit) + lane;
+      const uint32_t src0 = dp_pk_off(slot, 0, unit) + 16u * lane;
       u64 w[2 * (NW - 1)];
       if (a.dp_loop) dp_push_all<NW>(a, slot, unit, g0, g1);
-      dp_peer_issue<NW>(w, src0, me, W);
-      dp_peer_wait<NW>(a, w, src0, me, W, tag, fail);
+      dp_peer_issue<NW>(w, mine, src0, me, W);
+      dp_peer_wait<NW>(a, w, mine, src0, me, W, tag, fail);
       dp_packed_sum<NW>(w, me, W, g0, g1, v, scale);
     } else {  // loopback stand-in of the owner: W identical contributions
       float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
@@ -1162,9 +1192,10 @@ __device__ __forceinline__ bool dp_owner_step(const MLP3Args& a, int unit, int o
 #pragma unroll
     for (int r = 0; r < NW; ++r) {
       if (r >= W || (own ? r == me : r != owner)) continue;  // loopback stand-in: publish once, to ourselves
-      u64* d = dp_ag_area(a.dp_regions[r], slot, unit);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) st_sys(d + i * 64 + lane, tg | (u64)__float_as_uint(v[i]));
+      const __amdgpu_buffer_rsrc_t dr = dp_rsrc(a.dp_regions[r]);
+      const uint32_t off = dp_ag_off(slot, unit) + 32u * lane;
+      st_sys2(dr, off, tg | (u64)__float_as_uint(v[0]), tg | (u64)__float_as_uint(v[1]));
+      st_sys2(dr, off + 16u, tg | (u64)__float_as_uint(v[2]), tg | (u64)__float_as_uint(v[3]));
     }
     if (own) return true;
   }

@@ -207,6 +207,40 @@ class Accelerator:
         return torch.device("cpu")
 
 
+_fits_in_process = 0
+
+
+def _worker_diag(trainer) -> None:
+    """``RLA_WORKER_DIAG_DIR``: one JSON line per fit and rank (worker reuse audit,
+    scripts/bench_tune.py --diag): process id, how many fits this process has run
+    (> 1: a recycled worker), the native communicator this fit used (a fresh one per
+    fit: its Python id and bring-up state) and how often the fused step's exchange
+    region was re-armed in it."""
+    global _fits_in_process
+    _fits_in_process += 1
+    d = os.environ.get("RLA_WORKER_DIAG_DIR")
+    if not d:
+        return
+    import json
+
+    from ..parallel.comm import get_native_comm
+
+    comm = get_native_comm(create=False)
+    eng = getattr(getattr(trainer, "_fused", None), "eng", None)
+    rec = {"pid": os.getpid(), "fit_in_process": _fits_in_process, "rank": trainer.global_rank,
+           "world": trainer.world_size, "cwd": os.getcwd(),
+           "comm_id": comm.serial if comm is not None else None,
+           "comm": comm.describe() if comm is not None else None,
+           "comm_error_state": int(comm._c.error_state()) if comm is not None else None,
+           "dp_region_rearms": getattr(comm, "rearms", 0) if comm is not None else 0,
+           "fused_dp": bool(eng is not None and eng.dp_ctx is not None and eng.one_launch_dp),
+           "dp_proto": getattr(eng, "dp_proto", None) if eng is not None else None,
+           "global_step": trainer.global_step}
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, f"fit_{os.getpid()}_{_fits_in_process}_r{trainer.global_rank}.json"), "w") as f:
+        json.dump(rec, f)
+
+
 class DataParallelAccelerator(Accelerator):
     """Shared worker-side flow of process-per-device data parallelism.
 
@@ -302,6 +336,7 @@ class DataParallelAccelerator(Accelerator):
         mark("model_on_device", rank=t.global_rank)
         results = t._run(model)
         mark("run_end", rank=t.global_rank)
+        _worker_diag(t)
         self.transfer_distrib_spawn_state_on_fit_end(model, results)
         mark("state_handed_back", rank=t.global_rank)
         return results

@@ -61,6 +61,8 @@ class NativeCommunicator:
     """RCCL + xGMI communicator of this rank.  ``allreduce_(t)`` sums in place on
     the current stream (graph-capturable); ``average=True`` divides by world."""
 
+    _serials = 0
+
     def __init__(self, group=None, device: Optional[int] = None, use_rccl: bool = True,
                  use_xgmi: bool = True, xgmi_bytes: Optional[int] = None, validate: bool = True,
                  spin_limit: Optional[int] = None, watchdog_ms: Optional[int] = None,
@@ -68,6 +70,8 @@ class NativeCommunicator:
         """Unset knobs come from :func:`~ray_lightning_accelerators_amd.config.get_config`
         (``allreduce_algo="rccl"`` disables the xGMI path, ``"oneshot"`` forbids RCCL for
         buckets that fit the one-shot area)."""
+        NativeCommunicator._serials += 1
+        self.serial = NativeCommunicator._serials  # unique per process (worker reuse audit)
         cfg = get_config()
         self.algo = cfg.allreduce_algo
         xgmi_bytes = cfg.xgmi_bytes if xgmi_bytes is None else xgmi_bytes
@@ -303,6 +307,7 @@ class NativeCommunicator:
         dist.barrier(group=self.group)
         self._c.aux_rearm()
         dist.barrier(group=self.group)
+        self.rearms = getattr(self, "rearms", 0) + 1
 
     # ------------------------------------------------------- collectives
     def allreduce_(self, t: torch.Tensor, average: bool = False, bf16_wire: bool = False) -> torch.Tensor:

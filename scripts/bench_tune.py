@@ -35,7 +35,14 @@ def main():
     ap.add_argument("--share-gpu", type=int, default=0,
                     help="rehearsal: a virtual N-GPU ledger whose devices all map to GPU 0 (config 4's 4 trials x "
                          "2 workers on a 1-GPU box; gloo process groups, xGMI protocol over same-device IPC)")
+    ap.add_argument("--diag", action="store_true",
+                    help="worker reuse audit: every fit writes its process / communicator record "
+                         "(RLA_WORKER_DIAG_DIR); checked per trial and summarised in the JSON")
     args = ap.parse_args()
+    diag_dir = None
+    if args.diag:
+        diag_dir = tempfile.mkdtemp(prefix="rla_diag_")
+        os.environ["RLA_WORKER_DIAG_DIR"] = diag_dir
     gpu = bool(args.use_gpu)
     if gpu:
         import torch
@@ -64,12 +71,52 @@ def main():
         shutdown_s = time.perf_counter() - t1
     df = analysis.results_df
     iters = [int(v) for v in df["training_iteration"]] if "training_iteration" in df else []
+    audit = None
+    if diag_dir:
+        audit = _audit(diag_dir, analysis, args)
     print(json.dumps({
         "metric": "Tune sweep trials/hour (tune_mnist, RayAccelerator workers)",
         "value": round(args.trials / wall * 3600.0, 1), "unit": "trials/hour", "trials": args.trials,
         "workers_per_trial": args.workers, "gpus": n_gpus, "epochs_per_trial": args.epochs,
         "wall_s": round(wall, 2), "runtime_shutdown_s": round(shutdown_s, 2), "pool_warm_s": args.warm, "virtual_gpus_on_one": args.share_gpu, "s_per_trial": round(wall / args.trials, 2), "reports_per_trial": iters,
-        "best_config": analysis.best_config, "data": "synthetic"}), flush=True)
+        "best_config": analysis.best_config, "data": "synthetic", "reuse_audit": audit}), flush=True)
+    if audit is not None and not audit["ok"]:
+        raise SystemExit(f"worker reuse audit failed: {audit['problems']}")
+
+
+def _audit(diag_dir, analysis, args):
+    """Per trial: max_epochs reports and a checkpoint; per fit: every rank on a fresh
+    communicator (a new object, no error, rank / world as the trial's), the exchange
+    region re-armed; plus how many fits recycled processes served."""
+    import glob
+
+    recs = [json.load(open(p)) for p in sorted(glob.glob(os.path.join(diag_dir, "*.json")))]
+    problems = []
+    for t in analysis.trials:
+        if len(t.results) != args.epochs:
+            problems.append(f"{t.trial_id}: {len(t.results)} reports, expected {args.epochs}")
+        if not t.checkpoint or not os.path.exists(t.checkpoint):
+            problems.append(f"{t.trial_id}: no checkpoint")
+    comm_ids = {}
+    for r in recs:
+        if r["world"] != args.workers:
+            problems.append(f"fit {r}: world {r['world']}")
+        if args.workers > 1 and args.use_gpu:
+            if r["comm_id"] is None or r["comm_error_state"] != 0:
+                problems.append(f"pid {r['pid']} fit {r['fit_in_process']}: communicator {r['comm']}")
+            if r["fused_dp"] and r["dp_region_rearms"] < 1:
+                problems.append(f"pid {r['pid']} fit {r['fit_in_process']}: exchange region never re-armed")
+            key = (r["pid"], r["comm_id"])
+            if key in comm_ids:
+                problems.append(f"pid {r['pid']}: communicator reused across fits {comm_ids[key]} and "
+                                f"{r['fit_in_process']}")
+            comm_ids[key] = r["fit_in_process"]
+    recycled = sum(1 for r in recs if r["fit_in_process"] > 1)
+    return {"ok": not problems, "problems": problems[:10], "fits": len(recs), "processes": len({r["pid"] for r in recs}),
+            "fits_on_recycled_workers": recycled, "max_fits_per_process": max((r["fit_in_process"] for r in recs),
+                                                                            default=0),
+            "fused_dp_fits": sum(1 for r in recs if r["fused_dp"]),
+            "dp_protos": sorted({r["dp_proto"] for r in recs if r["dp_proto"]})}
 
 
 if __name__ == "__main__":

@@ -28,12 +28,17 @@ def test_forked_convs_match_autograd_sum(stride):
     on the same input: x.grad with the fork equals the plain two-branch autograd sum
     (fp32 reference of the same bf16 ops), for both backward orders."""
     from ray_lightning_accelerators_amd.ops.shadow import ConvBF16
+    from ray_lightning_accelerators_amd.parallel.arena import ParamArena
 
     torch.manual_seed(0)
     dev = torch.device("cuda", 0)
     cin, width, cout = 64, 64, 256
     c1 = C.Conv1x1NHWC(cin, width).to(dev)
     ds = (C.Conv1x1NHWC(cin, cout) if stride == 1 else ConvBF16(cin, cout, 1, stride, bias=False)).to(dev)
+    pair = torch.nn.ModuleList([c1, ds]).to(memory_format=torch.channels_last)
+    # ConvBF16 takes its native (fork-aware) path only with an arena bf16 shadow
+    arena = ParamArena(pair)
+    arena.enable_bf16_shadow(pair)
     x0 = torch.randn(4, cin, 16, 16, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
 
     def run(use_fork, swap):
