@@ -68,6 +68,16 @@ STOCK_BASELINE = {
     "torch": 45378.2,        # eager nn.Linear + torch.optim.Adam (profiles/r3_stock; r1: 53,015)
     "torch-graph": 166204.1,  # the same step under torch.cuda.graph, 8 steps/graph (profiles/r3_stock; r2: 165,417)
 }
+# ResNet-50 (batch 128, bf16 autocast, channels_last, SGD-momentum) on one MI355X:
+# stock torchvision-layout model, eager and under torch.cuda.graph
+RESNET_STOCK_BASELINE = {
+    "torch": 6010.3,        # profiles/r4_rn/rn50_torch.log
+    "torch-graph": 6021.4,  # profiles/r4_rn/rn50_torch_graph.log
+}
+RESNET_STOCK_SOURCE = {
+    "torch": "profiles/r4_rn/rn50_torch.log (round 4, one MI355X, 30 steps)",
+    "torch-graph": "profiles/r4_rn/rn50_torch_graph.log (round 4, one MI355X, 30 steps)",
+}
 # where each hard-coded number was measured (printed in the JSON next to it;
 # ``--compare-stock`` re-measures the eager stock step inside the same job)
 STOCK_BASELINE_SOURCE = {
@@ -729,8 +739,9 @@ def run_rank(args):
     if rank == 0:
         default_cfg = (args.layer_1, args.layer_2, args.batch_size) == (32, 64, 32)
         base_impl, base = None, None
-        if not rn and default_cfg and dev.type == "cuda":
-            known = {k: v for k, v in STOCK_BASELINE.items() if v}
+        rn_default = rn and args.batch_size == 128 and getattr(args, "impl", "native") == "native"
+        if (rn_default or (not rn and default_cfg)) and dev.type == "cuda":
+            known = {k: v for k, v in (RESNET_STOCK_BASELINE if rn else STOCK_BASELINE).items() if v}
             if known:
                 base_impl = max(known, key=known.get)
                 base = known[base_impl]
@@ -751,7 +762,8 @@ def run_rank(args):
             "vs_baseline": (round(value / base, 3) if base else None),
             "baseline_impl": base_impl,
             "baseline_value": base,
-            "baseline_source": STOCK_BASELINE_SOURCE.get((base_impl or "").split(" ")[0]),
+            "baseline_source": (RESNET_STOCK_SOURCE if rn else STOCK_BASELINE_SOURCE).get(
+                (base_impl or "").split(" ")[0]),
             "dtype": "bf16" if dev.type == "cuda" else "fp32",
             "data": "synthetic",
             "config": {

@@ -26,7 +26,7 @@ import torch
 from ..config import RLAConfig, log_config, set_config
 from .. import horovod as hvd
 from .. import runtime as ray
-from ..lightning.accelerators import Accelerator
+from ..lightning.accelerators import Accelerator, _worker_diag
 from ..lightning.utilities import rank_zero_only_state, seed_everything
 from ..session import finish_session, init_session, shutdown_session
 from ..util import Queue, process_results
@@ -237,6 +237,7 @@ class HorovodRayAccelerator(Accelerator):
         try:
             results = trainer._run(model)
             hvd.join()
+            _worker_diag(trainer)
         finally:
             finish_session()
         if hvd.rank() != 0:

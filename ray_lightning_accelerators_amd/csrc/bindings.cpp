@@ -5,6 +5,9 @@
 // built for (an out-of-bounds access can reset every GPU of the host).
 #include <torch/extension.h>
 #include <cstdlib>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
@@ -414,7 +417,7 @@ int* bn_tickets(int device, hipStream_t stream) {
 }
 
 Tensor bn_partial(Tensor x, optional<Tensor> y, optional<Tensor> dy, int64_t C, int64_t mode, bool relu,
-                  optional<Tensor> nbt, optional<Tensor> dy2, optional<Tensor> ss) {
+                  optional<Tensor> nbt, optional<Tensor> dy2, optional<Tensor> ss, optional<Tensor> dout) {
   const int64_t M = bn_rows(x, "x", C);
   TORCH_CHECK(M > 0, "fused BN: empty input");
   TORCH_CHECK(mode == 0 || mode == 1, "fused BN: mode 0 (forward) or 1 (backward)");
@@ -429,6 +432,13 @@ Tensor bn_partial(Tensor x, optional<Tensor> y, optional<Tensor> dy, int64_t C, 
       bn_same(x, *y, "y", C);
       yp = reinterpret_cast<const uint16_t*>(y->data_ptr());
     }
+  }
+  uint16_t* doutp = nullptr;
+  if (dout.has_value() && dout->defined()) {
+    TORCH_CHECK(mode == 1, "dout: backward partial only");
+    TORCH_CHECK(!(ss.has_value() && ss->defined()), "dout: y-masked (residual) layers only");
+    bn_same(x, *dout, "dout", C);
+    doutp = reinterpret_cast<uint16_t*>(dout->data_ptr());
   }
   const at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const rla::BnPlan plan = rla::bn_plan(M, (int)C);
@@ -445,7 +455,7 @@ Tensor bn_partial(Tensor x, optional<Tensor> y, optional<Tensor> dy, int64_t C, 
   }
   rla::launch_bn_partial(reinterpret_cast<const uint16_t*>(x.data_ptr()), yp, dyp, M, (int)C, (int)mode, relu,
                          plan, part.data_ptr<float>(), nbtp, cur_stream(x), mode == 1 ? bn_dy2(x, dy2, C) : nullptr,
-                         mode == 1 && relu ? bn_ss(ss, C) : nullptr, lv);
+                         mode == 1 && relu ? bn_ss(ss, C) : nullptr, lv, doutp);
   return tickets ? rows : part;
 }
 
@@ -615,6 +625,45 @@ std::vector<int64_t> conv_wgrad_plan(int64_t N, int64_t H, int64_t W, int64_t Ci
   return {p.kind, p.wa, p.wb, p.splits, p.rows_per_split};
 }
 
+// 3x3 / stride 1 / pad 1 NHWC bf16 convolution (csrc/conv3x3.hip): x [N, H, W, Cin]
+// and w [Cout, 3, 3, Cin] as contiguous memory; returns y as contiguous [N, H, W, Cout]
+Tensor conv3x3(Tensor x, Tensor w, int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout) {
+  TORCH_CHECK(x.is_cuda() && w.is_cuda(), "conv3x3: GPU tensors");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "conv3x3: bf16 inputs");
+  TORCH_CHECK(x.is_contiguous() && w.is_contiguous(), "conv3x3: contiguous NHWC / [Cout,3,3,Cin] memory");
+  TORCH_CHECK(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0, "conv3x3: bad geometry");
+  TORCH_CHECK(x.numel() == N * H * W * Cin, "conv3x3: x has ", x.numel(), " elements");
+  TORCH_CHECK(w.numel() == Cout * 9 * Cin, "conv3x3: w has ", w.numel(), " elements");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+              "conv3x3: 16-byte aligned inputs");
+  TORCH_CHECK(N * (H + 2) * (W + 2) < (int64_t(1) << 30), "conv3x3: too many pixels");
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  rla::Conv3x3Geom g{(int)N, (int)H, (int)W, (int)Cin, (int)Cout, 0};
+  static std::map<std::tuple<int64_t, int64_t, int64_t>, int> vrows_cache;
+  static std::mutex mu;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto key = std::make_tuple(N, H, W);
+    auto it = vrows_cache.find(key);
+    if (it == vrows_cache.end()) it = vrows_cache.emplace(key, rla::conv3x3_vrows(g)).first;
+    g.vrows = it->second;
+  }
+  TORCH_CHECK(rla::conv3x3_ok(g), "conv3x3: unsupported shape (Cin % 16, Cout % 64, halo tile size)");
+  Tensor y = at::empty({N, H, W, Cout}, x.options());
+  TORCH_CHECK(rla::launch_conv3x3(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                  reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                                  reinterpret_cast<uint16_t*>(y.data_ptr()), g, cur_stream(x)),
+              "conv3x3: launch refused");
+  return y;
+}
+
+bool conv3x3_supported(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout) {
+  rla::Conv3x3Geom g{(int)N, (int)H, (int)W, (int)Cin, (int)Cout, 0};
+  if (N <= 0 || H <= 0 || W <= 0 || N * (H + 2) * (W + 2) >= (int64_t(1) << 30)) return false;
+  g.vrows = rla::conv3x3_vrows(g);
+  return rla::conv3x3_ok(g);
+}
+
 Tensor dp_pack_roundtrip(Tensor x, int64_t tag) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous(), "x: contiguous fp32 on the GPU");
   Tensor y = at::empty_like(x);
@@ -652,7 +701,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp_param_count", &mlp_param_count);
   m.def("bn_partial", &bn_partial, "fused BN: per-block partial sums (mode 0 fwd stats, 1 bwd dz/dz*x)",
         py::arg("x"), py::arg("y"), py::arg("dy"), py::arg("C"), py::arg("mode"), py::arg("relu"), py::arg("nbt"),
-        py::arg("dy2") = py::none(), py::arg("ss") = py::none());
+        py::arg("dy2") = py::none(), py::arg("ss") = py::none(), py::arg("dout") = py::none());
   m.def("bn_finalize", &bn_finalize, "fused BN: mean/invstd/scale/shift + running stats from partials");
   m.def("bn_bwd_finalize", &bn_bwd_finalize, "fused BN backward: dgamma/dbeta + dx coefficients");
   m.def("bn_apply", &bn_apply, "fused BN apply: y = act(x*scale + shift (+res))");
@@ -669,5 +718,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("OH"), py::arg("OW"), py::arg("Cout"),
         py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
         py::arg("splits") = 0, py::arg("algo") = 0);
+  m.def("conv3x3", &conv3x3, "3x3 / stride 1 / pad 1 NHWC bf16 convolution on MFMA -> [N, H, W, Cout]",
+        py::arg("x"), py::arg("w"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"));
+  m.def("conv3x3_supported", &conv3x3_supported, "shapes the 3x3 MFMA convolution covers");
   m.attr("ARCH") = "gfx950";
 }

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "kernels.h"
 
@@ -36,6 +37,13 @@ __device__ __forceinline__ f8 ld8(const uint16_t* p) {
 
 __device__ __forceinline__ void st8(uint16_t* p, f8 v) {
   *reinterpret_cast<u8x16*>(p) = __builtin_bit_cast(u8x16, __builtin_convertvector(v, b8));
+}
+
+// store v as bf16 and return the stored (rounded) values
+__device__ __forceinline__ f8 st8r(uint16_t* p, f8 v) {
+  const b8 b = __builtin_convertvector(v, b8);
+  *reinterpret_cast<u8x16*>(p) = __builtin_bit_cast(u8x16, b);
+  return __builtin_convertvector(b, f8);
 }
 
 __device__ __forceinline__ f8 splat(float v) {
@@ -69,6 +77,10 @@ __device__ __forceinline__ f8 relu_mask(f8 d, f8 y) {
 // the two into a new tensor first (ops/bn.py, fold_residual_grad)
 // RECOMP (backward, ReLU without residual): the mask is x*scale+shift > 0 recomputed
 // from the forward statistics `ss` ([4, C]: mean, invstd, scale, shift) -- y is not read
+// WD (backward with a residual: the layer's dres IS the masked incoming gradient d):
+// the partial pass writes d once, rounded to bf16, and sums the rounded values; the
+// apply pass then reads x and d only (dx = A d + B x + C) -- 2 streams fewer than
+// re-reading y, dy and dy2 there and writing dres again.
 // L2 (two-level reduction, bn_plan's `group` > 1): the partial rows are stored
 // write-through (sc1); one lane per block takes a ticket on its group's counter
 // (agent scope, after every wave drained its stores); the block that draws the
@@ -84,14 +96,15 @@ struct BnL2 {
   int group;      // blocks per group (1: no second level)
 };
 
-template <int MODE, bool RELU, bool DY2 = false, bool RECOMP = false>
+template <int MODE, bool RELU, bool DY2 = false, bool RECOMP = false, bool WD = false>
 __global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(const uint16_t* __restrict__ x,
                                                                 const uint16_t* __restrict__ y,
                                                                 const uint16_t* __restrict__ dy, int64_t M, int C,
                                                                 int64_t rows_per_blk, float* __restrict__ part,
                                                                 int64_t* nbt, const uint16_t* __restrict__ dy2 = nullptr,
                                                                 const float* __restrict__ ss = nullptr,
-                                                                BnL2 l2 = BnL2{nullptr, nullptr, 1}) {
+                                                                BnL2 l2 = BnL2{nullptr, nullptr, 1},
+                                                                uint16_t* __restrict__ dout = nullptr) {
   // forward: one input stream, so twice the rows in flight per thread
   constexpr int U = MODE == 0 ? 8 : 4;
   __shared__ float sh[2][kBnThreads * 8];
@@ -126,6 +139,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(const uint16_t* 
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (MODE == 1 && RECOMP) dv[u] = relu_mask(dv[u], bn_affine(xv[u], sc, sf));
+        if (MODE == 1 && WD) dv[u] = st8r(dout + (px - x) + u * step, dv[u]);
         if (MODE == 0) {
           s += xv[u];
           q += xv[u] * xv[u];
@@ -145,6 +159,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(const uint16_t* 
         f8 d = ld8(dy + off);
         if (DY2) d += ld8(dy2 + off);
         if (RELU) d = relu_mask(d, RECOMP ? bn_affine(xv, sc, sf) : ld8(y + off));
+        if (WD) d = st8r(dout + off, d);
         s += d;
         q += d * xv;
       }
@@ -207,9 +222,13 @@ __global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(const uint16_t* 
 }
 
 // ---------------------------------------------------------------- finalize
-// 64 channels per block x 16 slices of the partial rows (1024 threads), 4 rows in
-// flight per thread, fp64 accumulation; the slices are combined through LDS.
-constexpr int kFinSlices = 16;
+// kFinCh channels per block x kFinSlices slices of the partial rows (1024 threads):
+// each thread sums rows sl, sl + kFinSlices, ... of its channel, 8 in flight, in
+// fp64; the slices are combined by a fixed-order LDS tree.  64 slices: the small-C
+// layers' finalize (C = 64: 512 partial rows) is ONE round of 8 loads per thread
+// over 4 blocks instead of four dependent rounds on one block (~5 us -> ~2 us a
+// launch; 106 launches per ResNet-50 step, profiles/r4_rn).
+constexpr int kFinCh = 16, kFinSlices = 1024 / kFinCh;
 
 template <bool BWD, typename P = float>
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(const P* __restrict__ part, int nparts, int C,
@@ -219,16 +238,14 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const P* __restrict__
                                                            float eps, const float* __restrict__ mean_in,
                                                            const float* __restrict__ invstd_in,
                                                            float* __restrict__ out) {
-  __shared__ double sh[2][kFinSlices][64];
-  const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  __shared__ double sh[2][kFinSlices][kFinCh];
+  const int cl = threadIdx.x % kFinCh, sl = threadIdx.x / kFinCh;
+  const int c = blockIdx.x * kFinCh + cl;
   double a = 0.0, b = 0.0;
   if (c < C) {
     const int64_t rs = 2 * (int64_t)C;
     const P* q = part + c;
     int p = sl;
-    // 8 partial rows in flight per thread: the small-C layers' finalize runs on one
-    // or two blocks and is latency-bound on these loads
     for (; p + 7 * kFinSlices < nparts; p += 8 * kFinSlices) {
       P v[16];
 #pragma unroll
@@ -250,14 +267,17 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const P* __restrict__
   sh[0][sl][cl] = a;
   sh[1][sl][cl] = b;
   __syncthreads();
-  if (sl != 0 || c >= C) return;
-  a = 0.0;
-  b = 0.0;
 #pragma unroll
-  for (int k = 0; k < kFinSlices; ++k) {
-    a += sh[0][k][cl];
-    b += sh[1][k][cl];
+  for (int st = kFinSlices / 2; st >= 1; st >>= 1) {
+    if (sl < st) {
+      sh[0][sl][cl] += sh[0][sl + st][cl];
+      sh[1][sl][cl] += sh[1][sl + st][cl];
+    }
+    __syncthreads();
   }
+  if (sl != 0 || c >= C) return;
+  a = sh[0][0][cl];
+  b = sh[1][0][cl];
   const float g = gamma ? gamma[c] : 1.f;
   if (!BWD) {
     const double mean = a / count;
@@ -389,18 +409,40 @@ BnPlan bn_plan(int64_t M, int C) {
   if (p.blocks < 1) p.blocks = 1;
   // second level: groups whose rows (group x 2C fp32) one block sums in ~1 us
   // (<= 32 KB); only where the finalize would otherwise stream many rows
+  // Off by default (RLA_BN_L2=1 turns it on): the tickets' agent-scope atomics and the
+  // last arriver's fp64 pass lengthened every partial launch by ~5 us while saving
+  // ~1 us of finalize (profiles/r4_rn: forward partials 609 -> 900 us per step)
+  static const bool l2_on = [] {
+    const char* e = getenv("RLA_BN_L2");
+    return e && e[0] == '1';
+  }();
   int g = 4096 / C;
   if (g > p.blocks) g = p.blocks;
-  p.group = p.blocks > 16 && g > 1 ? g : 1;
+  p.group = l2_on && p.blocks > 16 && g > 1 ? g : 1;
   p.groups = (p.blocks + p.group - 1) / p.group;
   return p;
 }
 
 void launch_bn_partial(const uint16_t* x, const uint16_t* y, const uint16_t* dy, int64_t M, int C, int mode,
                        bool relu, const BnPlan& plan, float* part, int64_t* nbt, hipStream_t s, const uint16_t* dy2,
-                       const float* ss, BnLevel2 lv) {
+                       const float* ss, BnLevel2 lv, uint16_t* dout) {
   const dim3 grid(plan.blocks), block(kBnThreads);
   const BnL2 L{lv.rows, lv.tickets, lv.rows ? plan.group : 1};
+  if (mode == 1 && dout) {  // residual layer: d written here (y-mask or none)
+    if (relu && dy2)
+      hipLaunchKernelGGL((bn_partial_kernel<1, true, true, false, true>), grid, block, 0, s, x, y, dy, M, C,
+                         plan.rows_per_blk, part, nullptr, dy2, nullptr, L, dout);
+    else if (relu)
+      hipLaunchKernelGGL((bn_partial_kernel<1, true, false, false, true>), grid, block, 0, s, x, y, dy, M, C,
+                         plan.rows_per_blk, part, nullptr, nullptr, nullptr, L, dout);
+    else if (dy2)
+      hipLaunchKernelGGL((bn_partial_kernel<1, false, true, false, true>), grid, block, 0, s, x, y, dy, M, C,
+                         plan.rows_per_blk, part, nullptr, dy2, nullptr, L, dout);
+    else
+      hipLaunchKernelGGL((bn_partial_kernel<1, false, false, false, true>), grid, block, 0, s, x, y, dy, M, C,
+                         plan.rows_per_blk, part, nullptr, nullptr, nullptr, L, dout);
+    return;
+  }
   if (mode == 1 && relu && ss) {
     if (dy2)
       hipLaunchKernelGGL((bn_partial_kernel<1, true, true, true>), grid, block, 0, s, x, y, dy, M, C,
@@ -433,26 +475,26 @@ void launch_bn_partial(const uint16_t* x, const uint16_t* y, const uint16_t* dy,
 void launch_bn_finalize(const float* part, int nparts, int C, double count, const float* gamma,
                         const float* beta, float* running_mean, float* running_var, const int64_t* nbt,
                         float momentum, float eps, float* stats, hipStream_t s) {
-  hipLaunchKernelGGL((bn_finalize_kernel<false>), dim3((C + 63) / 64), dim3(1024), 0, s, part, nparts, C, count,
+  hipLaunchKernelGGL((bn_finalize_kernel<false>), dim3((C + kFinCh - 1) / kFinCh), dim3(1024), 0, s, part, nparts, C, count,
                      gamma, beta, running_mean, running_var, nbt, momentum, eps, nullptr, nullptr, stats);
 }
 
 void launch_bn_bwd_finalize(const float* part, int nparts, int C, double count, const float* gamma,
                             const float* mean, const float* invstd, float* coef, hipStream_t s) {
-  hipLaunchKernelGGL((bn_finalize_kernel<true>), dim3((C + 63) / 64), dim3(1024), 0, s, part, nparts, C, count,
+  hipLaunchKernelGGL((bn_finalize_kernel<true>), dim3((C + kFinCh - 1) / kFinCh), dim3(1024), 0, s, part, nparts, C, count,
                      gamma, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, mean, invstd, coef);
 }
 
 void launch_bn_finalize64(const double* part, int nparts, int C, double count, const float* gamma,
                           const float* beta, float* running_mean, float* running_var, const int64_t* nbt,
                           float momentum, float eps, float* stats, hipStream_t s) {
-  hipLaunchKernelGGL((bn_finalize_kernel<false, double>), dim3((C + 63) / 64), dim3(1024), 0, s, part, nparts, C,
+  hipLaunchKernelGGL((bn_finalize_kernel<false, double>), dim3((C + kFinCh - 1) / kFinCh), dim3(1024), 0, s, part, nparts, C,
                      count, gamma, beta, running_mean, running_var, nbt, momentum, eps, nullptr, nullptr, stats);
 }
 
 void launch_bn_bwd_finalize64(const double* part, int nparts, int C, double count, const float* gamma,
                               const float* mean, const float* invstd, float* coef, hipStream_t s) {
-  hipLaunchKernelGGL((bn_finalize_kernel<true, double>), dim3((C + 63) / 64), dim3(1024), 0, s, part, nparts, C,
+  hipLaunchKernelGGL((bn_finalize_kernel<true, double>), dim3((C + kFinCh - 1) / kFinCh), dim3(1024), 0, s, part, nparts, C,
                      count, gamma, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, mean, invstd, coef);
 }
 

@@ -1,0 +1,263 @@
+// 3x3 / stride 1 / pad 1 NHWC bf16 convolution on the MFMA units (gfx950):
+//
+//   y[n][oh][ow][co] = sum over r, s, ci of x[n][oh + r - 1][ow + s - 1][ci] * w[co][r][s][ci]
+//
+// ResNet-50's bottleneck conv2 (13 of its 16 3x3 layers are stride 1).  The same
+// kernel is the layer's input gradient: dx = conv3x3(dy, w') with
+// w'[ci][r][s][co] = w[co][2 - r][2 - s][ci] (ops/conv.py builds w').  Why a kernel
+// of our own (profiles/r3_final/kernel_stats_rn50.csv): the library forward and
+// data-gradient kernels of these layers run at ~300-550 TFLOP/s, and MIOpen's dgrad
+// adds SubTensorOp / fill passes around them; every one of these layers is the
+// same 29.6 GFLOP at batch 128, so the whole family is ~0.95 TFLOP per step.
+//
+// Implicit GEMM  D[co][m] = W[co][(tap, ci)] . X[(tap, ci)][m]  over m = output pixel:
+//   * workgroup = 4 waves, tile = 256 consecutive output pixels x 64 output channels;
+//     wave w owns pixels [64 w, 64 w + 64) x all 64 channels = 2 x 2 blocks of
+//     v_mfma_f32_32x32x16_bf16 (A = weights: co x ci, B = pixels: ci x m);
+//   * the reduction runs in chunks of 16 input channels (one MFMA k-step per tap);
+//     a chunk's operands are staged in LDS: the x HALO image of the tile -- every
+//     input row the 256 pixels touch, in a virtual padded layout [n][H + 2][W + 2]
+//     whose zero rows / columns ARE the padding -- and the 9 taps x 64 channels of w.
+//     Tap (r, s) of pixel (n, oh, ow) reads halo row (n (H + 2) + oh + r - v0),
+//     column ow + s: every tap is a per-lane address into the SAME image, so x is
+//     fetched once per chunk instead of once per tap (an im2col would read it 9x);
+//   * LDS rows are 48 B (16 channels + 16 B pad): ds_read_b128 of 32 consecutive
+//     pixels (or channels) lands on 16 distinct 16-B bank windows (3 is odd), i.e.
+//     conflict-free (MI355X_MICROARCH.md, ds_read_b128 lane groups);
+//   * two LDS buffers and two register sets: chunk k + 1 goes from registers to the
+//     other buffer while chunk k is multiplied, chunk k + 3 is in flight from HBM/L2;
+//     one barrier per chunk.  Loads are unconditional (masked chunks read a clamped
+//     in-image address and store zeros) so the compiler cannot sink them;
+//   * grid in an XCD-aware order: the output-channel tiles of one pixel tile and
+//     neighbouring pixel tiles run on the same XCD, so the halo / weight re-reads hit
+//     that XCD's L2.
+// Epilogue: D of 32x32x16 gives a lane one pixel and 4 consecutive output channels
+// per 4 accumulator values: 8-byte bf16 stores.
+// Requires Cin % 16 == 0, Cout % 64 == 0, 16-byte aligned bases (checked by the binding).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace rla {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kCvThreads = 256;
+constexpr int kTM = 256;        // output pixels per workgroup tile
+constexpr int kTN = 64;         // output channels per workgroup tile
+constexpr int kKC = 16;         // input channels per chunk (one k-step of 16)
+constexpr int kRow = 24;        // bf16 per LDS row: 16 channels + 8 pad (48 B)
+constexpr int kWChunks = 9 * kTN * 2;  // 16-byte pieces of a chunk's weights
+constexpr int kNW = (kWChunks + kCvThreads - 1) / kCvThreads;
+constexpr int kMaxNX = 6;       // halo pieces per thread (host checks the shape fits)
+// LDS buffer: halo rows for kMaxNX pieces per thread, then weight rows for kNW; every
+// thread's stores land in it unconditionally (surplus pieces go to unused rows), so
+// no load is used only under a branch (the compiler would sink it to the use)
+constexpr int kXRows = kMaxNX * kCvThreads / 2, kWRows = kNW * kCvThreads / 2;
+constexpr int kBufElems = (kXRows + kWRows) * kRow;
+
+template <int NX>
+struct CvSet {
+  u32x4 x[NX], w[kNW];
+  uint32_t ok;  // bit i: x[i] valid (weights are always in range)
+};
+
+template <int NX>
+__global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __restrict__ x,
+                                                             const uint16_t* __restrict__ w,
+                                                             uint16_t* __restrict__ y, Conv3x3Geom g) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * kBufElems];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int WP = g.W + 2, HP = g.H + 2;
+  const int64_t M = (int64_t)g.N * g.H * g.W;
+  const int tiles_m = (int)((M + kTM - 1) / kTM), tiles_n = g.Cout / kTN;
+  const int total = tiles_m * tiles_n, per = (total + 7) / 8;
+  const int lq = (int)(blockIdx.x % 8u) * per + (int)(blockIdx.x / 8u);
+  if (lq >= total) return;  // padding blocks of the last XCD
+  const int tm = lq / tiles_n, tn = lq - tm * tiles_n;
+  const int64_t m0 = (int64_t)tm * kTM;
+  const int co0 = tn * kTN;
+  const int hw = g.H * g.W;
+  // first virtual halo row of the tile: output row (n0, oh0) needs rows oh0-1.. = virtual n0*HP + oh0
+  const int n0 = (int)(m0 / hw), oh0 = (int)((m0 - (int64_t)n0 * hw) / g.W);
+  const int v0 = n0 * HP + oh0;
+  const int xpieces = g.vrows * WP * 2;  // 16-byte pieces of the chunk's halo image
+  const int nchunks = g.Cin / kKC;
+
+  auto load = [&](CvSet<NX>& st, int chunk) {
+    const int cc = chunk < nchunks ? chunk : nchunks - 1;  // past the end: a valid re-read, never stored
+    const int ci0 = cc * kKC;
+    st.ok = 0u;
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int p = tid + i * kCvThreads;
+      const int pc = p < xpieces ? p : xpieces - 1;
+      const int pix = pc >> 1, h = pc & 1;
+      const int vr = pix / WP, q = pix - vr * WP;
+      const int v = v0 + vr;
+      const int n = v / HP, ih = v - n * HP - 1, iw = q - 1;
+      const bool ok = p < xpieces && n < g.N && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+      const int nc = n < g.N ? n : g.N - 1;
+      const int ihc = ih < 0 ? 0 : (ih >= g.H ? g.H - 1 : ih), iwc = iw < 0 ? 0 : (iw >= g.W ? g.W - 1 : iw);
+      st.x[i] = *reinterpret_cast<const u32x4*>(x + ((int64_t)(nc * g.H + ihc) * g.W + iwc) * g.Cin + ci0 + h * 8);
+      st.ok |= ok ? (1u << i) : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < kNW; ++i) {
+      const int p = tid + i * kCvThreads;
+      const int pc = p < kWChunks ? p : kWChunks - 1;
+      const int h = pc & 1, rest = pc >> 1, co = rest % kTN, tap = rest / kTN;
+      st.w[i] = *reinterpret_cast<const u32x4*>(w + ((int64_t)(co0 + co) * 9 + tap) * g.Cin + ci0 + h * 8);
+    }
+  };
+  auto store = [&](const CvSet<NX>& st, int buf) {
+    __bf16* X = lds + buf * kBufElems;
+    __bf16* Wt = X + kXRows * kRow;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int p = tid + i * kCvThreads;  // p >= xpieces: a row past the image, never read
+      *reinterpret_cast<u32x4*>(X + (p >> 1) * kRow + (p & 1) * 8) = (st.ok >> i) & 1u ? st.x[i] : z;
+    }
+#pragma unroll
+    for (int i = 0; i < kNW; ++i) {
+      const int p = tid + i * kCvThreads;  // row p / 2 = tap * kTN + co (>= 9 kTN: unused)
+      *reinterpret_cast<u32x4*>(Wt + (p >> 1) * kRow + (p & 1) * 8) = st.w[i];
+    }
+  };
+
+  // this lane's two pixels (B columns) as halo-image positions of tap (0, 0)
+  const int kg = (lane >> 5) * 8;  // k-group: channels 8 (lane / 32) .. + 7 of the chunk
+  int bpos[2];
+#pragma unroll
+  for (int jb = 0; jb < 2; ++jb) {
+    int64_t m = m0 + wave * 64 + jb * 32 + (lane & 31);
+    if (m >= M) m = M - 1;  // tail pixels compute a duplicate, never stored
+    const int n = (int)(m / hw), rem = (int)(m - (int64_t)n * hw);
+    const int oh = rem / g.W, ow = rem - oh * g.W;
+    bpos[jb] = (n * HP + oh - v0) * WP + ow;
+  }
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc[i][j][k] = 0.f;
+
+  auto compute = [&](int buf) {
+    const __bf16* X = lds + buf * kBufElems;
+    const __bf16* Wt = X + kXRows * kRow;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int r = tap / 3, s = tap - (tap / 3) * 3;
+      const int toff = r * WP + s;
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        fa[i] = *reinterpret_cast<const bf16x8*>(Wt + (tap * kTN + i * 32 + (lane & 31)) * kRow + kg);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8*>(X + (bpos[j] + toff) * kRow + kg);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // chunk k: global -> register set k & 1 -> LDS buffer k & 1.  At iteration `it`
+  // set (it + 1) & 1 holds chunk it + 1 (issued two iterations earlier) and goes to
+  // the buffer the previous iteration finished reading; the set is then reloaded with
+  // chunk it + 3.  One barrier per chunk.
+  CvSet<NX> sa, sb;
+  load(sa, 0);
+  load(sb, 1);
+  store(sa, 0);
+  __syncthreads();
+  load(sa, 2);
+  for (int it = 0; it < nchunks; it += 2) {
+    // even chunk `it` from buffer 0; chunk it + 1 (set b) -> buffer 1
+    compute(0);
+    store(sb, 1);
+    __syncthreads();
+    load(sb, it + 3);
+    if (it + 1 >= nchunks) break;  // uniform
+    compute(1);
+    store(sa, 0);
+    __syncthreads();
+    load(sa, it + 4);
+  }
+
+  // D[co][m]: lane -> pixel (lane & 31) of block j; accumulator k -> channel
+  // (k & 3) + 8 (k >> 2) + 4 (lane >> 5) of block i
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t m = m0 + wave * 64 + j * 32 + (lane & 31);
+    if (m >= M) continue;
+    uint16_t* yo = y + m * g.Cout + co0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int co = i * 32 + 8 * q + 4 * (lane >> 5);
+        bf16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (__bf16)acc[i][j][4 * q + e];
+        *reinterpret_cast<bf16x4*>(yo + co) = v;
+      }
+  }
+}
+
+}  // namespace
+
+int conv3x3_vrows(const Conv3x3Geom& g) {
+  // the most virtual halo rows any tile of kTM consecutive pixels touches
+  const int64_t M = (int64_t)g.N * g.H * g.W;
+  const int hw = g.H * g.W, HP = g.H + 2;
+  int best = 0;
+  for (int64_t m0 = 0; m0 < M; m0 += kTM) {
+    const int64_t m1 = (m0 + kTM < M ? m0 + kTM : M) - 1;
+    const int n0 = (int)(m0 / hw), oh0 = (int)((m0 % hw) / g.W);
+    const int n1 = (int)(m1 / hw), oh1 = (int)((m1 % hw) / g.W);
+    const int rows = (n1 * HP + oh1 + 2) - (n0 * HP + oh0) + 1;
+    if (rows > best) best = rows;
+  }
+  return best;
+}
+
+int conv3x3_pieces_per_thread(const Conv3x3Geom& g) {
+  return (g.vrows * (g.W + 2) * 2 + kCvThreads - 1) / kCvThreads;
+}
+
+bool conv3x3_ok(const Conv3x3Geom& g) {
+  return g.N > 0 && g.H > 0 && g.W > 0 && g.Cin % kKC == 0 && g.Cout % kTN == 0 && g.vrows > 0 &&
+         conv3x3_pieces_per_thread(g) <= kMaxNX && (int64_t)g.N * (g.H + 2) < (1ll << 30) &&
+         (int64_t)g.N * g.H * g.W * (g.Cin > g.Cout ? g.Cin : g.Cout) < (1ll << 40);
+}
+
+bool launch_conv3x3(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, hipStream_t st) {
+  if (!conv3x3_ok(g)) return false;
+  const int64_t M = (int64_t)g.N * g.H * g.W;
+  const int tiles = (int)((M + kTM - 1) / kTM) * (g.Cout / kTN);
+  const dim3 grid((unsigned)((tiles + 7) / 8 * 8)), block(kCvThreads);
+  switch (conv3x3_pieces_per_thread(g)) {
+    case 1: case 2: case 3: case 4:
+      hipLaunchKernelGGL(conv3x3_kernel<4>, grid, block, 0, st, x, w, y, g);
+      return true;
+    case 5:
+      hipLaunchKernelGGL(conv3x3_kernel<5>, grid, block, 0, st, x, w, y, g);
+      return true;
+    default:
+      hipLaunchKernelGGL(conv3x3_kernel<6>, grid, block, 0, st, x, w, y, g);
+      return true;
+  }
+}
+
+}  // namespace rla

@@ -74,7 +74,8 @@ void launch_bn_partial(const uint16_t* x, const uint16_t* y, const uint16_t* dy,
                        bool relu, const BnPlan& plan, float* part, int64_t* nbt, hipStream_t s,
                        const uint16_t* dy2 = nullptr,   // backward: gradient = dy + dy2
                        const float* ss = nullptr,       // backward ReLU mask from the fwd stats, not y
-                       BnLevel2 l2 = BnLevel2{nullptr, nullptr});
+                       BnLevel2 l2 = BnLevel2{nullptr, nullptr},
+                       uint16_t* dout = nullptr);       // backward: also write d = masked dy (+dy2), bf16
 
 // forward finalize of `nparts` partial rows: stats[0]=mean [1]=invstd [2]=scale [3]=shift ([4, C]);
 // running stats update (momentum < 0: cumulative average over num_batches_tracked)
@@ -256,4 +257,17 @@ WgradPlan wgrad_plan(const WgradGeom& g, int splits, int algo = 0);
 // part: splits * Cout * KH * KW * Cin floats when plan.splits > 1 (else unused)
 void launch_wgrad(const uint16_t* dy, const uint16_t* x, float* out, float* part, const WgradGeom& g,
                   const WgradPlan& p, hipStream_t stream);
+
+// ---------------------------------------------------------------------------
+// 3x3 / stride 1 / pad 1 NHWC bf16 convolution on MFMA (csrc/conv3x3.hip):
+// y [N, H, W, Cout] = conv(x [N, H, W, Cin], w [Cout][3][3][Cin]); also the input
+// gradient with the flipped, transposed weight.  Cin % 16 == 0, Cout % 64 == 0.
+// ---------------------------------------------------------------------------
+struct Conv3x3Geom {
+  int N, H, W, Cin, Cout;
+  int vrows;  // halo rows of the largest pixel tile (conv3x3_vrows)
+};
+int conv3x3_vrows(const Conv3x3Geom& g);
+bool conv3x3_ok(const Conv3x3Geom& g);
+bool launch_conv3x3(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, hipStream_t stream);
 }  // namespace rla

@@ -8,9 +8,10 @@ activations (ResNet-50 under bf16 autocast) it runs the gfx950 kernels of
 
   forward   partial sums (1 read of x) -> finalize ([C]; running stats and
             num_batches_tracked updated in-kernel) -> apply (read x [+res], write y)
-  backward  partial sums (read x, dy [, y]) -> finalize -> apply (write dx [+dres])
+  backward  partial sums (read x, dy [, y]) -> finalize -> apply (write dx)
             (without a residual the ReLU mask is recomputed from x and the
-            forward's scale/shift, so y is not re-read)
+            forward's scale/shift, so y is not re-read; with one, the partial
+            pass writes dres = the masked gradient and the apply reads x, dres)
 
 which replaces MIOpen's six batch-norm kernels per layer plus the separate
 ReLU, residual-add and ReLU-backward passes (profiles/r1_resnet50_v2).
@@ -120,7 +121,11 @@ class _BNActFn(torch.autograd.Function):
         if ctx.slot is not None and ctx.slot.dres is not None:
             dy2, ctx.slot.dres = _nhwc(ctx.slot.dres), None
             fold_stats["folded"] += 1
-        part = mod.bn_partial(xv, yv, dyv, C, 1, ctx.relu, None, dy2, ss)
+        # residual layer: dres is the masked incoming gradient d itself -- the partial
+        # pass writes it, and the apply pass reads x and d only (csrc/bn_act.hip, WD)
+        dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
+        part = mod.bn_partial(xv, yv, dyv, C, 1, ctx.relu, None, dy2, ss,
+                              _nhwc(dres) if dres is not None else None)
         local = None
         if ctx.group is not None:
             local = mod.bn_bwd_finalize(part, ctx.count, weight, mean, invstd)  # local dgamma / dbeta
@@ -128,9 +133,10 @@ class _BNActFn(torch.autograd.Function):
             dist.all_reduce(part, group=ctx.group)
         coef = mod.bn_bwd_finalize(part, ctx.count, weight, mean, invstd)
         dx = torch.empty_like(x, memory_format=torch.channels_last)
-        dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
-        mod.bn_bwd_apply(xv, yv, dyv, coef, ctx.relu, _nhwc(dx), _nhwc(dres) if dres is not None else None, dy2,
-                         ss)
+        if dres is not None:
+            mod.bn_bwd_apply(xv, None, _nhwc(dres), coef, False, _nhwc(dx), None)
+        else:
+            mod.bn_bwd_apply(xv, yv, dyv, coef, ctx.relu, _nhwc(dx), None, dy2, ss)
         if ctx.sink is not None:
             ctx.sink.dres, dres = dres, None  # the producer's backward consumes it
         wsrc = local if local is not None else coef

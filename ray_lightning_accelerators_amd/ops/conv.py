@@ -21,6 +21,7 @@ odd alignment) runs the stock convolution.  ``RLA_CONV1X1=miopen|gemm|auto``.
 """
 from __future__ import annotations
 
+import functools
 import os
 from typing import Dict, Optional, Tuple
 
@@ -121,6 +122,44 @@ def wgrad_hip(dy: torch.Tensor, x: torch.Tensor, kernel_size, stride, padding, s
     out = require().conv_wgrad(dy.permute(0, 2, 3, 1), x.permute(0, 2, 3, 1), n, h, w, cin, oh, ow, cout, kh, kw,
                                stride[0], stride[1], padding[0], padding[1], splits, algo)
     return out.permute(0, 3, 1, 2)
+
+
+def conv3x3_ok(x: torch.Tensor, wb: torch.Tensor, stride, padding) -> bool:
+    """3x3 / stride 1 / pad 1 layers the MFMA convolution kernel covers (csrc/conv3x3.hip)."""
+    if tuple(wb.shape[2:]) != (3, 3) or tuple(stride) != (1, 1) or tuple(padding) != (1, 1):
+        return False
+    if os.environ.get("RLA_CONV3X3", "auto") == "off":
+        return False
+    n, cin, h, w = x.shape
+    cout = wb.size(0)
+    return (cin % 64 == 0 and cout % 64 == 0 and wb.is_contiguous(memory_format=torch.channels_last)
+            and _conv3x3_shape_ok(n, h, w, cin, cout))
+
+
+@functools.lru_cache(maxsize=256)
+def _conv3x3_shape_ok(n: int, h: int, w: int, cin: int, cout: int) -> bool:
+    from . import require
+
+    return bool(require().conv3x3_supported(n, h, w, cin, cout))
+
+
+def conv3x3_hip(x: torch.Tensor, wb: torch.Tensor) -> torch.Tensor:
+    """``conv2d(x, wb, stride=1, padding=1)`` on the MFMA kernel: ``x`` [N, Cin, H, W]
+    channels_last bf16, ``wb`` [Cout, Cin, 3, 3] channels_last bf16 (its memory IS the
+    kernel's [Cout][3][3][Cin]); returns [N, Cout, H, W] channels_last."""
+    from . import require
+
+    n, cin, h, w = x.shape
+    cout = wb.size(0)
+    y = require().conv3x3(x.permute(0, 2, 3, 1), wb.permute(0, 2, 3, 1), n, h, w, cin, cout)
+    return y.permute(0, 3, 1, 2)
+
+
+def conv3x3_dgrad_hip(dy: torch.Tensor, wb: torch.Tensor) -> torch.Tensor:
+    """Input gradient of a 3x3 / stride 1 / pad 1 convolution = the same convolution
+    of ``dy`` with the weight flipped in both taps and transposed in channels."""
+    wt = wb.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+    return conv3x3_hip(dy, wt)
 
 
 def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
@@ -281,7 +320,18 @@ class _ConvNHWCFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, wb, stride, padding, fork=None):
-        y = _conv(x, wb, None, list(stride), list(padding), [1, 1], False, [0, 0], 1)
+        ctx.c3 = conv3x3_ok(x, wb, stride, padding)
+        be = "miopen"
+        if ctx.c3:
+            key = (x.size(0) * x.size(2) * x.size(3), x.size(1), wb.size(0), 3, 3, 1, 1)
+            be = _pick("fwd_kxk", key, {
+                "miopen": lambda: _conv(x, wb, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1),
+                "hip": lambda: conv3x3_hip(x, wb),
+            })
+        if be == "hip":
+            y = conv3x3_hip(x, wb)
+        else:
+            y = _conv(x, wb, None, list(stride), list(padding), [1, 1], False, [0, 0], 1)
         ctx.save_for_backward(x, wb)
         ctx.geo = (tuple(stride), tuple(padding))
         ctx.fork = fork
@@ -323,6 +373,18 @@ class _ConvNHWCFn(torch.autograd.Function):
                 cands["hip_gen"] = lambda: wgrad_hip(dy, x, (kh, kw), stride, padding, algo=1)
             be = _pick("wgrad_kxk", key, cands)
         need_dx = bool(ctx.needs_input_grad[0]) and dx is None
+        be_d = None
+        if need_dx and ctx.c3:
+            cout, cin = wb.shape[:2]
+            key = (x.size(0) * x.size(2) * x.size(3), cin, cout, 3, 3, 1, 1)
+            be_d = _pick("dgrad_kxk", key, {
+                "miopen": lambda: _conv_bwd(dy, x, wb, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                                            [True, False, False])[0],
+                "hip": lambda: conv3x3_dgrad_hip(dy, wb),
+            })
+        if be_d == "hip":
+            dx = _fork_dx(fork, lambda: conv3x3_dgrad_hip(dy, wb), None)
+            need_dx = False
         if be == "miopen":
             # MIOpen for both gradients: one call, as F.conv2d's autograd makes it
             mask = [need_dx, True, False]

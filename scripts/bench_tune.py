@@ -61,6 +61,7 @@ def main():
         ray.init(num_cpus=ncpu, num_gpus=n_gpus)
     time.sleep(args.warm)  # a long-lived cluster has its worker pool warm; 0 = cold start counted
     t0 = time.perf_counter()
+    _progress(t0, diag_dir)
     try:
         analysis = ray_ddp_tune.tune_mnist(os.path.join(tempfile.gettempdir(), "mnist_data_"), args.trials,
                                            args.epochs, args.workers, gpu)
@@ -82,6 +83,22 @@ def main():
         "best_config": analysis.best_config, "data": "synthetic", "reuse_audit": audit}), flush=True)
     if audit is not None and not audit["ok"]:
         raise SystemExit(f"worker reuse audit failed: {audit['problems']}")
+
+
+def _progress(t0, diag_dir, every_s: float = 15.0):
+    """A progress line on stderr every ``every_s`` (elapsed, fits finished so far):
+    a long sweep keeps telling the caller it is alive, and a stall shows where."""
+    import glob
+    import threading
+
+    def run():
+        while True:
+            time.sleep(every_s)
+            fits = len(glob.glob(os.path.join(diag_dir, "*.json"))) if diag_dir else None
+            print(f"[bench_tune] {time.perf_counter() - t0:.0f} s, fits recorded: {fits}", file=sys.stderr,
+                  flush=True)
+
+    threading.Thread(target=run, daemon=True).start()
 
 
 def _audit(diag_dir, analysis, args):

@@ -1,0 +1,101 @@
+"""3x3 / stride 1 / pad 1 NHWC convolution on MFMA (csrc/conv3x3.hip): forward and
+input gradient against an fp32 PyTorch reference of the same bf16 operands."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+gpu = pytest.mark.gpu
+
+# (N, H, W, Cin, Cout): ResNet-50's stride-1 conv2 shapes at small batch, plus tiles
+# that cross image boundaries (H*W not a multiple of 256, tiny images) and a tail
+SHAPES = [
+    (2, 56, 56, 64, 64),
+    (2, 28, 28, 128, 128),
+    (3, 14, 14, 256, 256),
+    (5, 7, 7, 512, 512),
+    (3, 5, 9, 16, 64),
+    (1, 3, 3, 32, 128),
+    (7, 11, 13, 48, 64),
+]
+
+
+def _rel(a, b):
+    return float((a.float() - b).norm() / b.norm().clamp_min(1e-30))
+
+
+@gpu
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv3x3_forward_matches_fp32(shape):
+    from ray_lightning_accelerators_amd import ops
+    from ray_lightning_accelerators_amd.ops.conv import conv3x3_hip
+
+    n, h, w, cin, cout = shape
+    torch.manual_seed(0)
+    dev = torch.device("cuda", 0)
+    x = torch.randn(n, cin, h, w, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wb = (torch.randn(cout, cin, 3, 3, device=dev) / (3 * cin ** 0.5)).to(torch.bfloat16)
+    wb = wb.contiguous(memory_format=torch.channels_last)
+    assert ops.require().conv3x3_supported(n, h, w, cin, cout)
+    y = conv3x3_hip(x, wb)
+    ref = F.conv2d(x.float(), wb.float(), padding=1)
+    assert y.shape == ref.shape and y.dtype == torch.bfloat16
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(y, ref) < 8e-3, _rel(y, ref)  # bf16 output rounding (2^-9 relative)
+    assert float((y.float() - ref).abs().max()) < 0.05 * float(ref.abs().max())
+
+
+@gpu
+@pytest.mark.parametrize("shape", SHAPES[:4] + SHAPES[-1:])
+def test_conv3x3_dgrad_matches_fp32(shape):
+    from ray_lightning_accelerators_amd.ops.conv import conv3x3_dgrad_hip
+
+    n, h, w, cin, cout = shape
+    if cout % 64 or cin % 64:  # the dgrad swaps the channel roles: Cin becomes the tile side
+        pytest.skip("dgrad needs Cin % 64 == 0")
+    torch.manual_seed(1)
+    dev = torch.device("cuda", 0)
+    x = torch.randn(n, cin, h, w, device=dev, requires_grad=True)
+    wb = (torch.randn(cout, cin, 3, 3, device=dev) / (3 * cin ** 0.5)).to(torch.bfloat16)
+    wb = wb.contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(n, cout, h, w, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    F.conv2d(x, wb.float(), padding=1).backward(dy.float())
+    dx = conv3x3_dgrad_hip(dy, wb)
+    assert dx.shape == x.shape
+    assert _rel(dx, x.grad) < 8e-3, _rel(dx, x.grad)
+
+
+@gpu
+def test_conv_bf16_layer_routes_through_kernel(monkeypatch):
+    """ConvBF16 with an arena shadow: RLA_CONV3X3 auto-times the kernel against
+    MIOpen per shape; forced to the kernel, the layer's output and input gradient
+    match MIOpen's (both bf16 convolutions of the same operands)."""
+    from ray_lightning_accelerators_amd.ops import conv as C
+    from ray_lightning_accelerators_amd.ops.shadow import ConvBF16
+    from ray_lightning_accelerators_amd.parallel.arena import ParamArena
+
+    torch.manual_seed(0)
+    dev = torch.device("cuda", 0)
+    m = torch.nn.ModuleList([ConvBF16(64, 64, 3, 1, 1, bias=False)]).to(dev).to(memory_format=torch.channels_last)
+    arena = ParamArena(m)
+    arena.enable_bf16_shadow(m)
+    x0 = torch.randn(4, 64, 20, 20, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    calls = {"n": 0}
+    real = C.conv3x3_hip
+
+    def counting(*a, **k):
+        calls["n"] += 1
+        return real(*a, **k)
+
+    monkeypatch.setattr(C, "conv3x3_hip", counting)
+    outs = {}
+    for mode in ("hip", "miopen"):
+        monkeypatch.setenv("RLA_CONV1X1", mode)  # _pick honours a pinned backend name
+        x = x0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = m[0](x)
+        y.float().square().sum().backward()
+        outs[mode] = (y.detach().float(), x.grad.float())
+        if mode == "hip":
+            assert calls["n"] >= 2  # forward + dgrad
+    assert _rel(outs["hip"][0], outs["miopen"][0]) < 1e-2
+    assert _rel(outs["hip"][1], outs["miopen"][1]) < 2e-2
