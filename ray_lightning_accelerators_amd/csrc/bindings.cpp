@@ -626,8 +626,9 @@ std::vector<int64_t> conv_wgrad_plan(int64_t N, int64_t H, int64_t W, int64_t Ci
 }
 
 // 3x3 / stride 1 / pad 1 NHWC bf16 convolution (csrc/conv3x3.hip): x [N, H, W, Cin]
-// and w [Cout, 3, 3, Cin] as contiguous memory; returns y as contiguous [N, H, W, Cout]
-Tensor conv3x3(Tensor x, Tensor w, int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout) {
+// and w [Cout, 3, 3, Cin] as contiguous memory; returns y as contiguous [N, H, W, Cout].
+// flip: the input gradient -- x = dy, w = the forward weight [Cin][3][3][Cout]
+Tensor conv3x3(Tensor x, Tensor w, int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, bool flip) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda(), "conv3x3: GPU tensors");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "conv3x3: bf16 inputs");
   TORCH_CHECK(x.is_contiguous() && w.is_contiguous(), "conv3x3: contiguous NHWC / [Cout,3,3,Cin] memory");
@@ -652,7 +653,7 @@ Tensor conv3x3(Tensor x, Tensor w, int64_t N, int64_t H, int64_t W, int64_t Cin,
   Tensor y = at::empty({N, H, W, Cout}, x.options());
   TORCH_CHECK(rla::launch_conv3x3(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                                   reinterpret_cast<const uint16_t*>(w.data_ptr()),
-                                  reinterpret_cast<uint16_t*>(y.data_ptr()), g, cur_stream(x)),
+                                  reinterpret_cast<uint16_t*>(y.data_ptr()), g, flip, cur_stream(x)),
               "conv3x3: launch refused");
   return y;
 }
@@ -719,7 +720,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
         py::arg("splits") = 0, py::arg("algo") = 0);
   m.def("conv3x3", &conv3x3, "3x3 / stride 1 / pad 1 NHWC bf16 convolution on MFMA -> [N, H, W, Cout]",
-        py::arg("x"), py::arg("w"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"));
+        py::arg("x"), py::arg("w"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"),
+        py::arg("flip") = false);
   m.def("conv3x3_supported", &conv3x3_supported, "shapes the 3x3 MFMA convolution covers");
   m.attr("ARCH") = "gfx950";
 }

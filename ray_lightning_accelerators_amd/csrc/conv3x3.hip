@@ -50,16 +50,24 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 constexpr int kCvThreads = 256;
 constexpr int kTM = 256;        // output pixels per workgroup tile
 constexpr int kTN = 64;         // output channels per workgroup tile
-constexpr int kKC = 16;         // input channels per chunk (one k-step of 16)
-constexpr int kRow = 24;        // bf16 per LDS row: 16 channels + 8 pad (48 B)
-constexpr int kWChunks = 9 * kTN * 2;  // 16-byte pieces of a chunk's weights
-constexpr int kNW = (kWChunks + kCvThreads - 1) / kCvThreads;
+constexpr int kKC = 16;         // reduction channels per chunk (one k-step of 16)
+constexpr int kRow = 24;        // bf16 per halo / weight row: 16 channels + 8 pad (48 B)
+constexpr int kFRow = 96;       // FLIP weight rows: 64 output channels + 32 pad (wgrad's tr-read image)
+constexpr int kWPieces = 9 * kTN * 2;  // 16-byte pieces of a chunk's weights (both layouts)
+constexpr int kNW = (kWPieces + kCvThreads - 1) / kCvThreads;
 constexpr int kMaxNX = 6;       // halo pieces per thread (host checks the shape fits)
-// LDS buffer: halo rows for kMaxNX pieces per thread, then weight rows for kNW; every
-// thread's stores land in it unconditionally (surplus pieces go to unused rows), so
-// no load is used only under a branch (the compiler would sink it to the use)
-constexpr int kXRows = kMaxNX * kCvThreads / 2, kWRows = kNW * kCvThreads / 2;
-constexpr int kBufElems = (kXRows + kWRows) * kRow;
+// LDS buffer: halo rows for kMaxNX pieces per thread, then the weights (kNW pieces
+// per thread in either layout); every thread's stores land in it unconditionally
+// (surplus pieces go to unused rows), so no load is used only under a branch (the
+// compiler would sink it to the use)
+constexpr int kXElems = kMaxNX * kCvThreads / 2 * kRow;
+constexpr int kWElems = (kNW * kCvThreads / 2 * kRow) > (kNW * kCvThreads / 8 * kFRow)
+                            ? (kNW * kCvThreads / 2 * kRow) : (kNW * kCvThreads / 8 * kFRow);
+constexpr int kBufElems = kXElems + kWElems;
+
+__device__ __forceinline__ bf16x4 tr4(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(p));
+}
 
 template <int NX>
 struct CvSet {
@@ -67,7 +75,20 @@ struct CvSet {
   uint32_t ok;  // bit i: x[i] valid (weights are always in range)
 };
 
-template <int NX>
+// FLIP (input gradient): w is the FORWARD weight [Cr][3][3][Co] of the layer whose
+// input gradient this is -- Cr (= g.Cin here) its output channels, Co (= g.Cout)
+// its input channels -- read as w'[co][t][k] = w[k][8 - t][co] with no re-layout
+// kernel: a chunk's pieces are 8 consecutive co of one (k, tap) row, staged as
+// [tap][k][co] and read as A fragments by transposed LDS reads (ds_read_b64_tr_b16).
+//
+// Persistent: gridDim.x workgroups (the CU count), each walks its tiles' chunks as
+// ONE stream -- the next tile's first chunks are in flight while this tile's last
+// ones are multiplied and its results stored -- so the per-tile pipeline fill is paid
+// once per workgroup, not once per tile.  Tiles are dealt XCD by XCD: XCD x (hardware
+// block L runs on XCD L % 8) owns a contiguous tile range, its workgroups take every
+// (G / 8)-th tile of it, so tiles running together share halo rows and weights in
+// that XCD's L2.
+template <int NX, bool FLIP, int DEPTH = 4>
 __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __restrict__ x,
                                                              const uint16_t* __restrict__ w,
                                                              uint16_t* __restrict__ y, Conv3x3Geom g) {
@@ -75,22 +96,39 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int WP = g.W + 2, HP = g.H + 2;
   const int64_t M = (int64_t)g.N * g.H * g.W;
-  const int tiles_m = (int)((M + kTM - 1) / kTM), tiles_n = g.Cout / kTN;
-  const int total = tiles_m * tiles_n, per = (total + 7) / 8;
-  const int lq = (int)(blockIdx.x % 8u) * per + (int)(blockIdx.x / 8u);
-  if (lq >= total) return;  // padding blocks of the last XCD
-  const int tm = lq / tiles_n, tn = lq - tm * tiles_n;
-  const int64_t m0 = (int64_t)tm * kTM;
-  const int co0 = tn * kTN;
   const int hw = g.H * g.W;
-  // first virtual halo row of the tile: output row (n0, oh0) needs rows oh0-1.. = virtual n0*HP + oh0
-  const int n0 = (int)(m0 / hw), oh0 = (int)((m0 - (int64_t)n0 * hw) / g.W);
-  const int v0 = n0 * HP + oh0;
-  const int xpieces = g.vrows * WP * 2;  // 16-byte pieces of the chunk's halo image
+  const int tiles_m = (int)((M + kTM - 1) / kTM), tiles_n = g.Cout / kTN;
+  const int total = tiles_m * tiles_n;
+  const int per = (total + 7) / 8, gx = (int)(gridDim.x / 8u);
+  const int xcd = (int)(blockIdx.x % 8u), slot = (int)(blockIdx.x / 8u);
+  const int t_lo = xcd * per + slot, t_hi = (xcd + 1) * per < total ? (xcd + 1) * per : total;
+  const int ntiles = t_lo < t_hi ? (t_hi - t_lo + gx - 1) / gx : 0;
+  if (ntiles == 0) return;
   const int nchunks = g.Cin / kKC;
+  const int nst = ntiles * nchunks;
+  const int xpieces = g.vrows * WP * 2;  // 16-byte pieces of a chunk's halo image
 
-  auto load = [&](CvSet<NX>& st, int chunk) {
-    const int cc = chunk < nchunks ? chunk : nchunks - 1;  // past the end: a valid re-read, never stored
+  // tile of stream stage `st` (clamped: stages past the end re-load the last one)
+  auto tile_of = [&](int st, int* chunk) {
+    const int sc = st < nst ? st : nst - 1;
+    const int i = sc / nchunks;
+    *chunk = sc - i * nchunks;
+    return t_lo + i * gx;
+  };
+  auto tile_org = [&](int tile, int64_t* m0, int* co0, int* v0) {
+    const int tm = tile / tiles_n;
+    *co0 = (tile - tm * tiles_n) * kTN;
+    *m0 = (int64_t)tm * kTM;
+    const int n0 = (int)(*m0 / hw), oh0 = (int)((*m0 - (int64_t)n0 * hw) / g.W);
+    *v0 = n0 * HP + oh0;  // first virtual halo row (the padded layout [n][H + 2][W + 2])
+  };
+
+  auto load = [&](CvSet<NX>& st, int stage) {
+    int cc;
+    const int tile = tile_of(stage, &cc);
+    int64_t m0;
+    int co0, v0;
+    tile_org(tile, &m0, &co0, &v0);
     const int ci0 = cc * kKC;
     st.ok = 0u;
 #pragma unroll
@@ -110,14 +148,20 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
 #pragma unroll
     for (int i = 0; i < kNW; ++i) {
       const int p = tid + i * kCvThreads;
-      const int pc = p < kWChunks ? p : kWChunks - 1;
-      const int h = pc & 1, rest = pc >> 1, co = rest % kTN, tap = rest / kTN;
-      st.w[i] = *reinterpret_cast<const u32x4*>(w + ((int64_t)(co0 + co) * 9 + tap) * g.Cin + ci0 + h * 8);
+      const int pc = p < kWPieces ? p : kWPieces - 1;
+      if (FLIP) {
+        // piece = (tap, k, group of 8 co): w[ci0 + k][8 - tap][co0 + 8 grp]
+        const int tap = pc >> 7, k = (pc >> 3) & 15, grp = pc & 7;
+        st.w[i] = *reinterpret_cast<const u32x4*>(w + ((int64_t)(ci0 + k) * 9 + (8 - tap)) * g.Cout + co0 + grp * 8);
+      } else {
+        const int h = pc & 1, rest = pc >> 1, co = rest % kTN, tap = rest / kTN;
+        st.w[i] = *reinterpret_cast<const u32x4*>(w + ((int64_t)(co0 + co) * 9 + tap) * g.Cin + ci0 + h * 8);
+      }
     }
   };
   auto store = [&](const CvSet<NX>& st, int buf) {
     __bf16* X = lds + buf * kBufElems;
-    __bf16* Wt = X + kXRows * kRow;
+    __bf16* Wt = X + kXElems;
     const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int i = 0; i < NX; ++i) {
@@ -126,42 +170,60 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
     }
 #pragma unroll
     for (int i = 0; i < kNW; ++i) {
-      const int p = tid + i * kCvThreads;  // row p / 2 = tap * kTN + co (>= 9 kTN: unused)
-      *reinterpret_cast<u32x4*>(Wt + (p >> 1) * kRow + (p & 1) * 8) = st.w[i];
+      const int p = tid + i * kCvThreads;  // pieces past 9 taps land in unused rows
+      if (FLIP)
+        *reinterpret_cast<u32x4*>(Wt + (p >> 3) * kFRow + (p & 7) * 8) = st.w[i];
+      else
+        *reinterpret_cast<u32x4*>(Wt + (p >> 1) * kRow + (p & 1) * 8) = st.w[i];
     }
   };
 
-  // this lane's two pixels (B columns) as halo-image positions of tap (0, 0)
   const int kg = (lane >> 5) * 8;  // k-group: channels 8 (lane / 32) .. + 7 of the chunk
+  // transposed-read roles (FLIP A operand): group gq of 16 lanes, lane 4q+p -> row q, channels 4p..4p+3
+  const int gq = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  const int cho = 16 * (gq & 1) + 4 * p4, rwo = 8 * (gq >> 1) + q4;
   int bpos[2];
+  auto set_tile = [&](int tile) {  // this lane's two pixels as halo positions of tap (0, 0)
+    int64_t m0;
+    int co0, v0;
+    tile_org(tile, &m0, &co0, &v0);
 #pragma unroll
-  for (int jb = 0; jb < 2; ++jb) {
-    int64_t m = m0 + wave * 64 + jb * 32 + (lane & 31);
-    if (m >= M) m = M - 1;  // tail pixels compute a duplicate, never stored
-    const int n = (int)(m / hw), rem = (int)(m - (int64_t)n * hw);
-    const int oh = rem / g.W, ow = rem - oh * g.W;
-    bpos[jb] = (n * HP + oh - v0) * WP + ow;
-  }
+    for (int jb = 0; jb < 2; ++jb) {
+      int64_t m = m0 + wave * 64 + jb * 32 + (lane & 31);
+      if (m >= M) m = M - 1;  // tail pixels compute a duplicate, never stored
+      const int n = (int)(m / hw), rem = (int)(m - (int64_t)n * hw);
+      const int oh = rem / g.W, ow = rem - oh * g.W;
+      bpos[jb] = (n * HP + oh - v0) * WP + ow;
+    }
+  };
 
   f32x16 acc[2][2];
+  auto zero = [&]() {
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int k = 0; k < 16; ++k) acc[i][j][k] = 0.f;
+        for (int k = 0; k < 16; ++k) acc[i][j][k] = 0.f;
+  };
 
   auto compute = [&](int buf) {
     const __bf16* X = lds + buf * kBufElems;
-    const __bf16* Wt = X + kXRows * kRow;
+    const __bf16* Wt = X + kXElems;
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int r = tap / 3, s = tap - (tap / 3) * 3;
       const int toff = r * WP + s;
       bf16x8 fa[2], fb[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        fa[i] = *reinterpret_cast<const bf16x8*>(Wt + (tap * kTN + i * 32 + (lane & 31)) * kRow + kg);
+      for (int i = 0; i < 2; ++i) {
+        if (FLIP) {
+          const __bf16* pa = Wt + (tap * 16 + rwo) * kFRow + i * 32 + cho;
+          fa[i] = __builtin_shufflevector(tr4(pa), tr4(pa + 4 * kFRow), 0, 1, 2, 3, 4, 5, 6, 7);
+        } else {
+          fa[i] = *reinterpret_cast<const bf16x8*>(Wt + (tap * kTN + i * 32 + (lane & 31)) * kRow + kg);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         fb[j] = *reinterpret_cast<const bf16x8*>(X + (bpos[j] + toff) * kRow + kg);
@@ -172,46 +234,61 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
     }
   };
 
-  // chunk k: global -> register set k & 1 -> LDS buffer k & 1.  At iteration `it`
-  // set (it + 1) & 1 holds chunk it + 1 (issued two iterations earlier) and goes to
-  // the buffer the previous iteration finished reading; the set is then reloaded with
-  // chunk it + 3.  One barrier per chunk.
-  CvSet<NX> sa, sb;
-  load(sa, 0);
-  load(sb, 1);
-  store(sa, 0);
-  __syncthreads();
-  load(sa, 2);
-  for (int it = 0; it < nchunks; it += 2) {
-    // even chunk `it` from buffer 0; chunk it + 1 (set b) -> buffer 1
-    compute(0);
-    store(sb, 1);
-    __syncthreads();
-    load(sb, it + 3);
-    if (it + 1 >= nchunks) break;  // uniform
-    compute(1);
-    store(sa, 0);
-    __syncthreads();
-    load(sa, it + 4);
-  }
-
   // D[co][m]: lane -> pixel (lane & 31) of block j; accumulator k -> channel
   // (k & 3) + 8 (k >> 2) + 4 (lane >> 5) of block i
+  auto epilogue = [&](int tile) {
+    int64_t m0;
+    int co0, v0;
+    tile_org(tile, &m0, &co0, &v0);
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int64_t m = m0 + wave * 64 + j * 32 + (lane & 31);
-    if (m >= M) continue;
-    uint16_t* yo = y + m * g.Cout + co0;
+    for (int j = 0; j < 2; ++j) {
+      const int64_t m = m0 + wave * 64 + j * 32 + (lane & 31);
+      if (m < M) {
+        uint16_t* yo = y + m * g.Cout + co0;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int co = i * 32 + 8 * q + 4 * (lane >> 5);
-        bf16x4 v;
+          for (int q = 0; q < 4; ++q) {
+            const int co = i * 32 + 8 * q + 4 * (lane >> 5);
+            bf16x4 v;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (__bf16)acc[i][j][4 * q + e];
-        *reinterpret_cast<bf16x4*>(yo + co) = v;
+            for (int e = 0; e < 4; ++e) v[e] = (__bf16)acc[i][j][4 * q + e];
+            *reinterpret_cast<bf16x4*>(yo + co) = v;
+          }
       }
+    }
+  };
+
+  // stage k of the stream: global -> register set k % DEPTH -> LDS buffer k & 1.  At
+  // iteration `it` set (it + 1) % DEPTH holds stage it + 1 (issued DEPTH - 1
+  // iterations earlier: the loads of DEPTH - 1 stages are in flight behind every
+  // stage's MFMAs) and goes to the buffer the previous iteration finished reading;
+  // the set is then reloaded with stage it + 1 + DEPTH.  One barrier per stage.
+  auto step = [&](int it, int buf, CvSet<NX>& nxt) {
+    int cc;
+    const int tile = tile_of(it, &cc);
+    if (cc == 0) {
+      set_tile(tile);
+      zero();
+    }
+    compute(buf);
+    store(nxt, buf ^ 1);
+    __syncthreads();
+    load(nxt, it + 1 + DEPTH);
+    if (cc == nchunks - 1) epilogue(tile);
+  };
+  CvSet<NX> sets[DEPTH];
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d) load(sets[d], d);
+  store(sets[0], 0);
+  __syncthreads();
+  load(sets[0], DEPTH);
+  for (int it = 0; it < nst; it += DEPTH) {  // unrolled by DEPTH: the register sets stay static
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      if (it + d >= nst) break;  // uniform
+      step(it + d, d & 1, sets[(d + 1) % DEPTH]);
+    }
   }
 }
 
@@ -242,22 +319,48 @@ bool conv3x3_ok(const Conv3x3Geom& g) {
          (int64_t)g.N * g.H * g.W * (g.Cin > g.Cout ? g.Cin : g.Cout) < (1ll << 40);
 }
 
-bool launch_conv3x3(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, hipStream_t st) {
+static int cu_count() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
+template <bool FLIP>
+static void launch_nx(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, hipStream_t st,
+                      dim3 grid) {
+  const dim3 block(kCvThreads);
+  switch (conv3x3_pieces_per_thread(g)) {
+    case 1: case 2: case 3: case 4:
+      hipLaunchKernelGGL((conv3x3_kernel<4, FLIP>), grid, block, 0, st, x, w, y, g);
+      break;
+    case 5:
+      hipLaunchKernelGGL((conv3x3_kernel<5, FLIP>), grid, block, 0, st, x, w, y, g);
+      break;
+    default:
+      hipLaunchKernelGGL((conv3x3_kernel<6, FLIP>), grid, block, 0, st, x, w, y, g);
+      break;
+  }
+}
+
+bool launch_conv3x3(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, bool flip,
+                    hipStream_t st) {
   if (!conv3x3_ok(g)) return false;
   const int64_t M = (int64_t)g.N * g.H * g.W;
   const int tiles = (int)((M + kTM - 1) / kTM) * (g.Cout / kTN);
-  const dim3 grid((unsigned)((tiles + 7) / 8 * 8)), block(kCvThreads);
-  switch (conv3x3_pieces_per_thread(g)) {
-    case 1: case 2: case 3: case 4:
-      hipLaunchKernelGGL(conv3x3_kernel<4>, grid, block, 0, st, x, w, y, g);
-      return true;
-    case 5:
-      hipLaunchKernelGGL(conv3x3_kernel<5>, grid, block, 0, st, x, w, y, g);
-      return true;
-    default:
-      hipLaunchKernelGGL(conv3x3_kernel<6>, grid, block, 0, st, x, w, y, g);
-      return true;
-  }
+  // persistent: one workgroup per CU (the LDS image holds one per CU), or one per tile
+  int blocks = cu_count();
+  if (blocks > tiles) blocks = tiles;
+  const dim3 grid((unsigned)((blocks + 7) / 8 * 8));
+  if (flip)
+    launch_nx<true>(x, w, y, g, st, grid);
+  else
+    launch_nx<false>(x, w, y, g, st, grid);
+  return true;
 }
 
 }  // namespace rla

@@ -269,5 +269,8 @@ struct Conv3x3Geom {
 };
 int conv3x3_vrows(const Conv3x3Geom& g);
 bool conv3x3_ok(const Conv3x3Geom& g);
-bool launch_conv3x3(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, hipStream_t stream);
+// flip: input gradient -- x is dy [N, H, W, Cin], w the FORWARD weight [Cin][3][3][Cout]
+// (Cin = the forward's output channels), y is dx [N, H, W, Cout]
+bool launch_conv3x3(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, bool flip,
+                    hipStream_t stream);
 }  // namespace rla

@@ -68,15 +68,21 @@ class _FusionState:
         self.synchronized = False
         # GPU ranks: the C++ fusion engine (csrc/comm/fusion_engine.cpp) packs,
         # allreduces (xGMI one-shot / RCCL) and unpacks each bucket on its own
-        # thread + comm stream.  Created here, where every rank is in lock-step.
+        # thread + high-priority comm stream.  The communicator is brought up here,
+        # where every rank is in lock-step; the engine itself (no collective in it)
+        # only at the first bucket launch: a step that never runs autograd (the fused
+        # MNIST step exchanges gradients inside its kernel) never creates its stream
+        # -- an idle high-priority queue per rank made the hardware scheduler
+        # time-slice two ranks sharing one GPU (Trainer.fit rehearsal, 12.8 -> 59 us
+        # a step, profiles/r4_share2).
         self.engine = None
+        self._engine_comm = None
+        self._threshold = threshold_bytes
         if (size() > 1 and compression is Compression.none and params and params[0].is_cuda
                 and get_config().hvd_native):
             from ..parallel.comm import get_native_comm
 
-            comm = get_native_comm()
-            if comm is not None:
-                self.engine = comm.fusion_engine(threshold_bytes)
+            self._engine_comm = get_native_comm()
         self.hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
 
     def _add(self, ps):
@@ -122,6 +128,8 @@ class _FusionState:
         for p in b.params:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
+        if self.engine is None and self._engine_comm is not None:
+            self.engine = self._engine_comm.fusion_engine(self._threshold)
         if self.engine is not None and all(p.grad.dtype == torch.float32 and p.grad.is_contiguous()
                                            for p in b.params):
             scale = 1.0 / size() if self.op == Average else 1.0

@@ -308,6 +308,15 @@ class DataParallelAccelerator(Accelerator):
         self.sync.broadcast_parameters(0)
 
     def ddp_train(self, process_idx: int, model):
+        from ..utils.faults import hang_watch_start, hang_watch_stop
+
+        watch = hang_watch_start(f"fit{_fits_in_process + 1}")
+        try:
+            return self._ddp_train(process_idx, model)
+        finally:
+            hang_watch_stop(watch)
+
+    def _ddp_train(self, process_idx: int, model):
         t = self.trainer
         set_config(self.config)  # every rank runs the driver-resolved knobs
         if "PL_GLOBAL_SEED" in os.environ:

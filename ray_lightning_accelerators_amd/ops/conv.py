@@ -157,9 +157,14 @@ def conv3x3_hip(x: torch.Tensor, wb: torch.Tensor) -> torch.Tensor:
 
 def conv3x3_dgrad_hip(dy: torch.Tensor, wb: torch.Tensor) -> torch.Tensor:
     """Input gradient of a 3x3 / stride 1 / pad 1 convolution = the same convolution
-    of ``dy`` with the weight flipped in both taps and transposed in channels."""
-    wt = wb.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
-    return conv3x3_hip(dy, wt)
+    of ``dy`` with the weight flipped in both taps and transposed in channels; the
+    kernel reads the forward weight that way itself (no re-layout kernel)."""
+    from . import require
+
+    n, cout, h, w = dy.shape
+    cin = wb.size(1)
+    dx = require().conv3x3(dy.permute(0, 2, 3, 1), wb.permute(0, 2, 3, 1), n, h, w, cout, cin, True)
+    return dx.permute(0, 3, 1, 2)
 
 
 def _nhwc2d(t: torch.Tensor) -> torch.Tensor:

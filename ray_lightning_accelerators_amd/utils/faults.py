@@ -35,3 +35,33 @@ def maybe_inject(rank: int, global_step: int) -> None:
     if kind == "exit":
         os._exit(13)
     raise InjectedFault(f"injected fault on rank {rank} at step {global_step}")
+
+
+def hang_watch_start(tag: str):
+    """``RLA_HANG_DUMP_DIR``: every thread's Python stack is written to
+    ``<dir>/stacks_<pid>_<tag>.txt`` every ``RLA_HANG_DUMP_S`` seconds (default 60)
+    until :func:`hang_watch_stop` -- a worker stuck in a rendezvous, a collective or a
+    device wait names the call it is in (scripts/bench_tune.py --diag-dir)."""
+    d = os.environ.get("RLA_HANG_DUMP_DIR")
+    if not d:
+        return None
+    import faulthandler
+
+    os.makedirs(d, exist_ok=True)
+    f = open(os.path.join(d, f"stacks_{os.getpid()}_{tag}.txt"), "w")
+    faulthandler.dump_traceback_later(float(os.environ.get("RLA_HANG_DUMP_S", "60")), repeat=True, file=f)
+    return f
+
+
+def hang_watch_stop(f) -> None:
+    if f is None:
+        return
+    import faulthandler
+
+    faulthandler.cancel_dump_traceback_later()
+    f.close()
+    try:
+        if os.path.getsize(f.name) == 0:
+            os.remove(f.name)  # finished in time: nothing to keep
+    except OSError:
+        pass

@@ -38,11 +38,18 @@ def main():
     ap.add_argument("--diag", action="store_true",
                     help="worker reuse audit: every fit writes its process / communicator record "
                          "(RLA_WORKER_DIAG_DIR); checked per trial and summarised in the JSON")
+    ap.add_argument("--diag-dir", default=None,
+                    help="where --diag records go (default: a temp dir); workers also dump their "
+                         "stacks there when a fit runs > 60 s (RLA_HANG_DUMP_DIR)")
     args = ap.parse_args()
     diag_dir = None
-    if args.diag:
-        diag_dir = tempfile.mkdtemp(prefix="rla_diag_")
+    if args.diag or args.diag_dir:
+        args.diag = True
+        diag_dir = args.diag_dir or tempfile.mkdtemp(prefix="rla_diag_")
+        os.makedirs(diag_dir, exist_ok=True)
+        diag_dir = os.path.abspath(diag_dir)
         os.environ["RLA_WORKER_DIAG_DIR"] = diag_dir
+        os.environ.setdefault("RLA_HANG_DUMP_DIR", diag_dir)
     gpu = bool(args.use_gpu)
     if gpu:
         import torch

@@ -21,6 +21,7 @@ args = ap.parse_args()
 conv = torch.ops.aten.convolution
 conv_bwd = torch.ops.aten.convolution_backward
 dev = torch.device("cuda", 0)
+torch.backends.cudnn.benchmark = True  # MIOpen find, as in the model (bench.py)
 
 
 def timed(fn, reps):

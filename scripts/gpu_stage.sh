@@ -40,7 +40,7 @@ for st in "$@"; do
     recycle)
       run pytest_recycle 300 $PYT tests/test_ddp_gpu.py tests/test_runtime.py -k "recycl" ;;
     tuneaudit)  # config 4 (2 workers sharing the GPU, recycled) with per-fit worker diagnostics audited
-      run tune_audit 600 python -u scripts/bench_tune.py --workers 2 --share-gpu 8 --trials 8 --epochs 2 --diag ;;
+      run tune_audit 240 python -u scripts/bench_tune.py --workers 2 --share-gpu 8 --trials 8 --epochs 2 --diag-dir "$R/$O/tune_diag" ;;
     tune)
       run tune_cold 300 python scripts/bench_tune.py --trials 4
       run tune_cold16 300 python scripts/bench_tune.py --trials 16

@@ -271,7 +271,9 @@ def _gpu_worker(rank, world, port, q, mode):
             model = make()
             opt = hvd.DistributedOptimizer(torch.optim.SGD(model.parameters(), lr=0.1),
                                            named_parameters=model.named_parameters())
-            res["native_engine"] = opt._hvd_state.engine is not None
+            # the engine comes up at the first bucket launch (lazily: a step without
+            # autograd never creates its stream); the communicator is bound now
+            res["native_engine"] = opt._hvd_state._engine_comm is not None
             for _ in range(3):
                 x, y = data(rank)
                 opt.zero_grad()
@@ -290,6 +292,7 @@ def _gpu_worker(rank, world, port, q, mode):
             comm.check()
             res["match"] = all(bool(torch.allclose(a, b, atol=1e-5)) for a, b in
                                zip(model.parameters(), ref.parameters()))
+            res["native_engine"] = res["native_engine"] and opt._hvd_state.engine is not None
             res["batches"] = opt._hvd_state.engine.batches_executed if res["native_engine"] else 0
         elif mode in ("reducer", "reducer_check"):
             # GradSynchronizer on the C++ reducer: several in-order buckets, averaged grads
