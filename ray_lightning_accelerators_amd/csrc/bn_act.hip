@@ -395,13 +395,12 @@ int apply_grid(int64_t M, int C) {
 BnPlan bn_plan(int64_t M, int C) {
   const int rpi = kBnThreads / (C >> 3);
   // >= 16 row iterations per thread, at most 512 blocks (2 per CU: 8 waves with 4-8
-  // rows in flight each keep HBM busy) and 128K partial floats: the finalize kernel
-  // reads the partials with one block per 64 channels, so their count sets its
-  // latency (1024-block partials cost ~5-6 us per finalize, profiles/r3_wgrad)
+  // rows in flight each keep HBM busy).  Round 3 also capped the partial table at
+  // 128K floats for the finalize's sake -- which left the wide layers on a fraction
+  // of the chip (C = 2048: 64 blocks on 256 CUs); the 64-slice finalize reads up to
+  // 512 rows in one round, so every width now gets the full grid.
   int64_t blocks = (M + (int64_t)rpi * 16 - 1) / ((int64_t)rpi * 16);
-  int64_t cap = (int64_t(1) << 17) / C;
-  if (cap > 512) cap = 512;
-  if (blocks > cap) blocks = cap;
+  if (blocks > 512) blocks = 512;
   if (blocks < 1) blocks = 1;
   BnPlan p;
   p.rows_per_blk = (M + blocks - 1) / blocks;

@@ -123,14 +123,19 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
     *v0 = n0 * HP + oh0;  // first virtual halo row (the padded layout [n][H + 2][W + 2])
   };
 
-  auto load = [&](CvSet<NX>& st, int stage) {
-    int cc;
-    const int tile = tile_of(stage, &cc);
+  // Load-side tile state: every thread's piece offsets (elements, without the
+  // chunk's channel offset) and halo validity, computed once per tile -- the
+  // per-chunk loads are then one add each.  (Recomputing the halo geometry per
+  // chunk cost two runtime integer divisions per piece, ~1K VALU cycles a stage at
+  // one wave per SIMD: the MFMAs ran at ~15 % of the step, profiles/r4_rn.)
+  int ld_tile = -1;
+  int xoff[NX], woff[kNW];
+  uint32_t xok = 0u;
+  auto load_geom = [&](int tile) {
     int64_t m0;
     int co0, v0;
     tile_org(tile, &m0, &co0, &v0);
-    const int ci0 = cc * kKC;
-    st.ok = 0u;
+    xok = 0u;
 #pragma unroll
     for (int i = 0; i < NX; ++i) {
       const int p = tid + i * kCvThreads;
@@ -142,8 +147,8 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
       const bool ok = p < xpieces && n < g.N && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
       const int nc = n < g.N ? n : g.N - 1;
       const int ihc = ih < 0 ? 0 : (ih >= g.H ? g.H - 1 : ih), iwc = iw < 0 ? 0 : (iw >= g.W ? g.W - 1 : iw);
-      st.x[i] = *reinterpret_cast<const u32x4*>(x + ((int64_t)(nc * g.H + ihc) * g.W + iwc) * g.Cin + ci0 + h * 8);
-      st.ok |= ok ? (1u << i) : 0u;
+      xoff[i] = ((nc * g.H + ihc) * g.W + iwc) * g.Cin + h * 8;
+      xok |= ok ? (1u << i) : 0u;
     }
 #pragma unroll
     for (int i = 0; i < kNW; ++i) {
@@ -152,12 +157,27 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
       if (FLIP) {
         // piece = (tap, k, group of 8 co): w[ci0 + k][8 - tap][co0 + 8 grp]
         const int tap = pc >> 7, k = (pc >> 3) & 15, grp = pc & 7;
-        st.w[i] = *reinterpret_cast<const u32x4*>(w + ((int64_t)(ci0 + k) * 9 + (8 - tap)) * g.Cout + co0 + grp * 8);
+        woff[i] = (k * 9 + (8 - tap)) * g.Cout + co0 + grp * 8;
       } else {
         const int h = pc & 1, rest = pc >> 1, co = rest % kTN, tap = rest / kTN;
-        st.w[i] = *reinterpret_cast<const u32x4*>(w + ((int64_t)(co0 + co) * 9 + tap) * g.Cin + ci0 + h * 8);
+        woff[i] = ((co0 + co) * 9 + tap) * g.Cin + h * 8;
       }
     }
+  };
+  auto load = [&](CvSet<NX>& st, int stage) {
+    int cc;
+    const int tile = tile_of(stage, &cc);
+    if (tile != ld_tile) {  // uniform: the stage stream crossed into a new tile
+      load_geom(tile);
+      ld_tile = tile;
+    }
+    const int ci0 = cc * kKC;
+    const int wstep = FLIP ? ci0 * 9 * g.Cout : ci0;
+    st.ok = xok;
+#pragma unroll
+    for (int i = 0; i < NX; ++i) st.x[i] = *reinterpret_cast<const u32x4*>(x + xoff[i] + ci0);
+#pragma unroll
+    for (int i = 0; i < kNW; ++i) st.w[i] = *reinterpret_cast<const u32x4*>(w + woff[i] + wstep);
   };
   auto store = [&](const CvSet<NX>& st, int buf) {
     __bf16* X = lds + buf * kBufElems;
@@ -314,9 +334,11 @@ int conv3x3_pieces_per_thread(const Conv3x3Geom& g) {
 }
 
 bool conv3x3_ok(const Conv3x3Geom& g) {
+  // 32-bit element offsets into x, y and w (the kernel's per-tile piece tables)
   return g.N > 0 && g.H > 0 && g.W > 0 && g.Cin % kKC == 0 && g.Cout % kTN == 0 && g.vrows > 0 &&
          conv3x3_pieces_per_thread(g) <= kMaxNX && (int64_t)g.N * (g.H + 2) < (1ll << 30) &&
-         (int64_t)g.N * g.H * g.W * (g.Cin > g.Cout ? g.Cin : g.Cout) < (1ll << 40);
+         (int64_t)g.N * g.H * g.W * (g.Cin > g.Cout ? g.Cin : g.Cout) < (1ll << 31) &&
+         (int64_t)g.Cin * 9 * g.Cout < (1ll << 31);
 }
 
 static int cu_count() {
