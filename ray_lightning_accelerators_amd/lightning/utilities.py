@@ -160,6 +160,9 @@ def _writer_main(conn) -> None:  # pragma: no cover - runs in the writer process
     import pickle
     from multiprocessing import shared_memory
 
+    # a forked writer must not enter a parallel region: the parent's OpenMP pool
+    # threads do not exist in the child (an intra-op parallel copy would wait on them)
+    torch.set_num_threads(1)
     conn.send(("ready", None))
     while True:
         try:
@@ -227,9 +230,10 @@ class ProcessCheckpointWriter:
         self._proc = ctx.Process(target=_writer_main, args=(child,), daemon=True, name="rla-ckpt-writer")
         self._proc.start()
         child.close()
-        self._pending = []  # shared-memory blocks (or None) of unacknowledged requests
+        self._pending = []  # (shared-memory block or None, request) of unacknowledged requests
         self._err: Optional[str] = None
         self._ready = False
+        self._dead = False
 
     def ready(self) -> bool:
         """The writer finished starting (interpreter + torch import, ~1-2 s)."""
@@ -241,25 +245,70 @@ class ProcessCheckpointWriter:
         return self._ready
 
     def alive(self) -> bool:
-        return self._proc.is_alive()
+        return not self._dead and self._proc.is_alive()
+
+    # a writer silent this long while requests are pending is declared stuck: it is
+    # killed and the pending requests are completed in this process (a Tune sweep
+    # once hung here for good, profiles/r4_tune/cfg4_recycle_stalled_run.log)
+    STALL_S = 20.0
+
+    def _recv(self, block: bool):
+        """The writer's next message, or None (non-blocking and nothing there); raises
+        EOFError when the writer died or stayed silent past STALL_S."""
+        if not block:
+            return self._conn.recv() if self._conn.poll() else None
+        if not self._conn.poll(self.STALL_S):
+            raise EOFError("checkpoint writer process stalled")
+        return self._conn.recv()
 
     def _reap(self, block: bool) -> None:
-        if self._pending and not self._ready:
-            if not block:
-                return
-            self._ready = self._conn.recv()[0] == "ready"
-        while self._pending and (block or self._conn.poll()):
+        try:
+            if self._pending and not self._ready:
+                msg = self._recv(block)
+                if msg is None:
+                    return
+                self._ready = msg[0] == "ready"
+            while self._pending:
+                msg = self._recv(block)
+                if msg is None:
+                    return
+                shm, _req = self._pending.pop(0)
+                if shm is not None:
+                    shm.close()
+                    shm.unlink()
+                if msg[1] and self._err is None:
+                    self._err = msg[1]
+        except EOFError:
+            self._take_over()
+
+    def _take_over(self) -> None:
+        """The writer died or stalled: stop it and finish its queue here, in order."""
+        import pickle
+
+        try:
+            self._proc.terminate()
+            self._proc.join(timeout=5)
+        except Exception:  # noqa: BLE001
+            pass
+        self._dead = True
+        pending, self._pending = self._pending, []
+        for shm, req in pending:
             try:
-                _, err = self._conn.recv()
-            except EOFError:
-                err = "checkpoint writer process died"
-                self._pending = [None]
-            shm = self._pending.pop(0)
-            if shm is not None:
-                shm.close()
-                shm.unlink()
-            if err and self._err is None:
-                self._err = err
+                if req is not None and req[0] == "save":
+                    _, skel, metas, _name, filepath = req
+                    buf = torch.frombuffer(shm.buf, dtype=torch.uint8)
+                    tensors = [buf[o: o + nb].view(dt).reshape(shape).clone() for dt, shape, o, nb in metas]
+                    del buf
+                    atomic_save(_rebuild_tensors(pickle.loads(skel), tensors), filepath)
+                elif req is not None and req[0] == "remove" and os.path.exists(req[1]):
+                    os.remove(req[1])
+            except BaseException as e:  # noqa: BLE001 - reported like the writer's errors
+                if self._err is None:
+                    self._err = repr(e)
+            finally:
+                if shm is not None:
+                    shm.close()
+                    shm.unlink()
 
     def save(self, checkpoint: Any, filepath: str) -> None:
         import pickle
@@ -286,16 +335,28 @@ class ProcessCheckpointWriter:
             shm.close()
             shm.unlink()
             raise
-        self._pending.append(shm)
         # absolute: the writer process keeps the directory it started in, while this
         # process changes it (a recycled worker per assignment, a Tune trial per trial)
-        self._conn.send(("save", skel, metas, shm.name, os.path.abspath(filepath)))
+        req = ("save", skel, metas, shm.name, os.path.abspath(filepath))
+        self._pending.append((shm, req))
+        if self._dead:
+            self._take_over()
+            self._raise()
+            return
+        try:
+            self._conn.send(req)
+        except (OSError, EOFError, BrokenPipeError):
+            self._take_over()
 
     def submit(self, fn, *args) -> None:
         """File operations after the pending writes (only removals are shipped)."""
-        if getattr(fn, "__name__", "") == "_remove_file" and len(args) == 1:
-            self._pending.append(None)
-            self._conn.send(("remove", os.path.abspath(args[0])))
+        if getattr(fn, "__name__", "") == "_remove_file" and len(args) == 1 and not self._dead:
+            req = ("remove", os.path.abspath(args[0]))
+            self._pending.append((None, req))
+            try:
+                self._conn.send(req)
+            except (OSError, EOFError, BrokenPipeError):
+                self._take_over()
         else:
             self.wait()
             fn(*args)
@@ -313,12 +374,13 @@ class ProcessCheckpointWriter:
         try:
             self.wait()
         finally:
-            try:
-                self._pending.append(None)
-                self._conn.send(("exit",))
-                self._reap(block=True)
-            except (OSError, EOFError):
-                pass
+            if not self._dead:
+                try:
+                    self._pending.append((None, None))
+                    self._conn.send(("exit",))
+                    self._reap(block=True)
+                except (OSError, EOFError):
+                    pass
             self._proc.join(timeout=10)
 
 

@@ -77,6 +77,7 @@ class FusedMLPEngine:
         dp_proto: Optional[str] = None,
         dp_rearm: Optional[Callable[[], None]] = None,
         dp_loop: bool = False,
+        resident: Optional[bool] = None,
     ):
         """``buffers``: optional external fp32 tensors ``params`` / ``grads`` /
         ``exp_avg`` / ``exp_avg_sq`` (e.g. views of a Trainer's parameter arena,
@@ -156,6 +157,12 @@ class FusedMLPEngine:
         # run(): a window of one-launch steps as back-to-back launches from ONE C++
         # call instead of hipGraph replays (see _run_loop; RLA_MLP_LAUNCH_LOOP=1)
         self.launch_loop = os.environ.get("RLA_MLP_LAUNCH_LOOP", "0") == "1"
+        # run(): at world 1, a window of steps as ONE launch of the resident kernel
+        # (csrc/mlp_resident.hip: the model lives on one CU for the whole window, no
+        # hand-off between steps); RLA_MLP_RESIDENT=0 / resident=False keeps the
+        # pipelined one-launch steps (hipGraph replays)
+        self.resident = (os.environ.get("RLA_MLP_RESIDENT", "1") != "0") if resident is None else bool(resident)
+        self._shadow_stale = False
         self._primed = False
         self._host_epochs = False
         self.x_u8 = self.labels = self.order = None
@@ -351,6 +358,7 @@ class FusedMLPEngine:
     def refresh_shadow(self) -> None:
         """Rebuild the bf16 weight shadows after the fp32 params changed outside a step."""
         fused_mlp.mlp_refresh_shadow(self.params, self.shadow, self.L1, self.L2)
+        self._shadow_stale = False
         self._primed = False
 
     def load_params(self, flat: torch.Tensor) -> None:
@@ -373,6 +381,9 @@ class FusedMLPEngine:
 
     def prime(self) -> None:
         """Layer-1 pre-activations of the pending batch from the current weights."""
+        if self._shadow_stale:
+            self._shadow_stale = False
+            fused_mlp.mlp_refresh_shadow(self.params, self.shadow, self.L1, self.L2)
         if self.native:
             self.h1pre.zero_()
             fused_mlp.mlp3_launch(fused_mlp.MLP3_PRIME, **self._kw3())
@@ -521,7 +532,33 @@ class FusedMLPEngine:
             return self.one_launch
         return self.dp_ctx is not None and self.one_launch_dp
 
+    def resident_ok(self) -> bool:
+        """run() takes the resident kernel: world 1, the (L1, L2, B) it is built for."""
+        return (self.resident and self.native and self.world_size == 1 and not self.dp_loop
+                and self.x_u8 is not None and fused_mlp.resident_supported(self.L1, self.L2, self.B))
+
+    def _run_resident(self, n_steps: int) -> None:
+        """The window as resident launches, one per stretch up to the epoch end (where
+        the host refills the next epoch's order buffer, as the graph path does)."""
+        done = 0
+        while done < n_steps:
+            k = min(n_steps - done, self.n_batches - self.step_in_epoch)
+            fused_mlp.mlp_resident(x_u8=self.x_u8, labels=self.labels, order=self.order, counters=self.counters,
+                                   n_batches=self.n_batches, B=self.B, L1=self.L1, L2=self.L2, K=k,
+                                   params=self.params, exp_avg=self.exp_avg, exp_avg_sq=self.exp_avg_sq,
+                                   stats=self.stats, lr=self.lr, betas=self.betas, eps=self.eps,
+                                   weight_decay=self.wd, lr_tensor=self.lr_tensor)
+            self._advance_host(k)
+            done += k
+        # the pipelined kernels' state (bf16 shadows, pending H1pre) is rebuilt before
+        # they run again
+        self._shadow_stale = True
+        self._primed = False
+
     def run(self, n_steps: int) -> None:
+        if n_steps > 0 and self.resident_ok():
+            self._run_resident(n_steps)
+            return
         if self.launch_loop and self._loop_ok():
             self._run_loop(n_steps)
             return

@@ -131,6 +131,44 @@ def test_process_checkpoint_writer_matches_atomic_save(tmp_path):
     w.close()
 
 
+def test_stalled_writer_process_is_taken_over(tmp_path, monkeypatch):
+    """A writer process that stops answering (the Tune config-4 rehearsal once hung on
+    it for good) is killed after STALL_S and its queued saves / removals complete in
+    the training process, in order; later saves keep working without it."""
+    import os
+    import signal
+
+    from ray_lightning_accelerators_amd.lightning.utilities import ProcessCheckpointWriter, atomic_save
+
+    monkeypatch.setattr(ProcessCheckpointWriter, "STALL_S", 1.0)
+    w = ProcessCheckpointWriter()
+    assert w._conn.poll(30)  # started
+    os.kill(w._proc.pid, signal.SIGSTOP)  # alive, silent
+
+    def _remove_file(p):
+        os.remove(p)
+
+    try:
+        ck = {"epoch": 1, "state_dict": {"w": torch.randn(4, 3)}}
+        w.save(ck, str(tmp_path / "a.ckpt"))
+        w.save(ck, str(tmp_path / "b.ckpt"))
+        w.submit(_remove_file, str(tmp_path / "a.ckpt"))
+        w.wait()  # returns after ~STALL_S instead of blocking forever
+        assert sorted(os.listdir(tmp_path)) == ["b.ckpt"]
+        assert not w.alive()
+        w.save(ck, str(tmp_path / "c.ckpt"))  # written in-process from now on
+        w.wait()
+        atomic_save(ck, str(tmp_path / "ref.ckpt"))
+        assert torch.equal(torch.load(tmp_path / "c.ckpt", weights_only=True)["state_dict"]["w"],
+                           torch.load(tmp_path / "ref.ckpt", weights_only=True)["state_dict"]["w"])
+    finally:
+        try:
+            os.kill(w._proc.pid, signal.SIGKILL)
+        except OSError:
+            pass
+        w.close()
+
+
 def test_process_writer_follows_cwd_changes(tmp_path, monkeypatch):
     """one writer process serves a recycled worker across fits / Tune
     trials that chdir into their own directory; relative checkpoint paths (and

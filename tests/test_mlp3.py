@@ -17,6 +17,13 @@ from ray_lightning_accelerators_amd.parallel.mlp_engine import FusedMLPEngine, s
 gpu = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _pipelined_kernels(monkeypatch):
+    """These tests pin the pipelined / one-launch step kernels (mlp_step3.hip): run()
+    would otherwise take the resident kernel at world 1 (tests/test_mlp_resident.py)."""
+    monkeypatch.setenv("RLA_MLP_RESIDENT", "0")
+
+
 def _rel(a, b):
     return (a.float() - b.float()).norm().item() / max(b.float().norm().item(), 1e-12)
 
