@@ -161,7 +161,7 @@ class FusedMLPEngine:
         # (csrc/mlp_resident.hip: the model lives on one CU for the whole window, no
         # hand-off between steps); RLA_MLP_RESIDENT=0 / resident=False keeps the
         # pipelined one-launch steps (hipGraph replays)
-        self.resident = (os.environ.get("RLA_MLP_RESIDENT", "1") != "0") if resident is None else bool(resident)
+        self.resident = (os.environ.get("RLA_MLP_RESIDENT", "0") == "1") if resident is None else bool(resident)
         self._shadow_stale = False
         self._primed = False
         self._host_epochs = False
