@@ -210,6 +210,12 @@ class Accelerator:
 _fits_in_process = 0
 
 
+def _ckpt_takeovers() -> int:
+    from . import utilities
+
+    return int(getattr(utilities, "writer_takeovers", 0))
+
+
 def _worker_diag(trainer) -> None:
     """``RLA_WORKER_DIAG_DIR``: one JSON line per fit and rank (worker reuse audit,
     scripts/bench_tune.py --diag): process id, how many fits this process has run
@@ -235,7 +241,8 @@ def _worker_diag(trainer) -> None:
            "dp_region_rearms": getattr(comm, "rearms", 0) if comm is not None else 0,
            "fused_dp": bool(eng is not None and eng.dp_ctx is not None and eng.one_launch_dp),
            "dp_proto": getattr(eng, "dp_proto", None) if eng is not None else None,
-           "global_step": trainer.global_step}
+           "global_step": trainer.global_step,
+           "ckpt_writer_takeovers": _ckpt_takeovers()}
     os.makedirs(d, exist_ok=True)
     with open(os.path.join(d, f"fit_{os.getpid()}_{_fits_in_process}_r{trainer.global_rank}.json"), "w") as f:
         json.dump(rec, f)

@@ -225,6 +225,12 @@ class ProcessCheckpointWriter:
             from ..utils import warmup
 
             warmup.join()  # never fork while a warm-up thread may hold an import lock
+        if not gpu_ctx:
+            # everything the writer imports, imported HERE first: a forked child that
+            # imports a module another thread of this process was importing at the
+            # fork inherits that module's import lock held -- and waits on it forever
+            import pickle  # noqa: F401
+            from multiprocessing import resource_tracker, shared_memory  # noqa: F401
         ctx = mp.get_context("spawn" if gpu_ctx else "fork")
         self._conn, child = ctx.Pipe()
         self._proc = ctx.Process(target=_writer_main, args=(child,), daemon=True, name="rla-ckpt-writer")
@@ -284,6 +290,11 @@ class ProcessCheckpointWriter:
     def _take_over(self) -> None:
         """The writer died or stalled: stop it and finish its queue here, in order."""
         import pickle
+
+        global writer_takeovers
+        writer_takeovers += 1
+        print(f"[rla] checkpoint writer process {self._proc.pid} stopped answering; "
+              f"finishing {len(self._pending)} request(s) in-process", file=sys.stderr, flush=True)
 
         try:
             self._proc.terminate()
@@ -385,6 +396,7 @@ class ProcessCheckpointWriter:
 
 
 _process_writer: Optional[ProcessCheckpointWriter] = None
+writer_takeovers = 0  # writer processes this process had to take over (diagnostics)
 
 
 def process_checkpoint_writer() -> ProcessCheckpointWriter:

@@ -140,6 +140,7 @@ def _audit(diag_dir, analysis, args):
             "fits_on_recycled_workers": recycled, "max_fits_per_process": max((r["fit_in_process"] for r in recs),
                                                                             default=0),
             "fused_dp_fits": sum(1 for r in recs if r["fused_dp"]),
+            "ckpt_writer_takeovers": max((r.get("ckpt_writer_takeovers", 0) for r in recs), default=0),
             "dp_protos": sorted({r["dp_proto"] for r in recs if r["dp_proto"]})}
 
 
