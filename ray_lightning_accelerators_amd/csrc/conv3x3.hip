@@ -36,6 +36,7 @@
 // Requires Cin % 16 == 0, Cout % 64 == 0, 16-byte aligned bases (checked by the binding).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "common.h"
 #include "kernels.h"
@@ -48,14 +49,14 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kCvThreads = 256;
-constexpr int kTM = 256;        // output pixels per workgroup tile
+constexpr int kTMMax = 512;     // output pixels per workgroup tile: 128 x JB (JB pixel blocks of 32 per wave)
 constexpr int kTN = 64;         // output channels per workgroup tile
 constexpr int kKC = 16;         // reduction channels per chunk (one k-step of 16)
 constexpr int kRow = 24;        // bf16 per halo / weight row: 16 channels + 8 pad (48 B)
 constexpr int kFRow = 96;       // FLIP weight rows: 64 output channels + 32 pad (wgrad's tr-read image)
 constexpr int kWPieces = 9 * kTN * 2;  // 16-byte pieces of a chunk's weights (both layouts)
 constexpr int kNW = (kWPieces + kCvThreads - 1) / kCvThreads;
-constexpr int kMaxNX = 6;       // halo pieces per thread (host checks the shape fits)
+constexpr int kMaxNX = 7;       // halo pieces per thread (host checks the shape fits)
 // LDS buffer: halo rows for kMaxNX pieces per thread, then the weights (kNW pieces
 // per thread in either layout); every thread's stores land in it unconditionally
 // (surplus pieces go to unused rows), so no load is used only under a branch (the
@@ -88,7 +89,7 @@ struct CvSet {
 // block L runs on XCD L % 8) owns a contiguous tile range, its workgroups take every
 // (G / 8)-th tile of it, so tiles running together share halo rows and weights in
 // that XCD's L2.
-template <int NX, bool FLIP, int DEPTH = 4>
+template <int NX, bool FLIP, int JB, int DEPTH>
 __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __restrict__ x,
                                                              const uint16_t* __restrict__ w,
                                                              uint16_t* __restrict__ y, Conv3x3Geom g) {
@@ -97,7 +98,8 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
   const int WP = g.W + 2, HP = g.H + 2;
   const int64_t M = (int64_t)g.N * g.H * g.W;
   const int hw = g.H * g.W;
-  const int tiles_m = (int)((M + kTM - 1) / kTM), tiles_n = g.Cout / kTN;
+  constexpr int TM = 128 * JB;
+  const int tiles_m = (int)((M + TM - 1) / TM), tiles_n = g.Cout / kTN;
   const int total = tiles_m * tiles_n;
   const int per = (total + 7) / 8, gx = (int)(gridDim.x / 8u);
   const int xcd = (int)(blockIdx.x % 8u), slot = (int)(blockIdx.x / 8u);
@@ -118,7 +120,7 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
   auto tile_org = [&](int tile, int64_t* m0, int* co0, int* v0) {
     const int tm = tile / tiles_n;
     *co0 = (tile - tm * tiles_n) * kTN;
-    *m0 = (int64_t)tm * kTM;
+    *m0 = (int64_t)tm * TM;
     const int n0 = (int)(*m0 / hw), oh0 = (int)((*m0 - (int64_t)n0 * hw) / g.W);
     *v0 = n0 * HP + oh0;  // first virtual halo row (the padded layout [n][H + 2][W + 2])
   };
@@ -202,14 +204,14 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
   // transposed-read roles (FLIP A operand): group gq of 16 lanes, lane 4q+p -> row q, channels 4p..4p+3
   const int gq = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
   const int cho = 16 * (gq & 1) + 4 * p4, rwo = 8 * (gq >> 1) + q4;
-  int bpos[2];
+  int bpos[JB];
   auto set_tile = [&](int tile) {  // this lane's two pixels as halo positions of tap (0, 0)
     int64_t m0;
     int co0, v0;
     tile_org(tile, &m0, &co0, &v0);
 #pragma unroll
-    for (int jb = 0; jb < 2; ++jb) {
-      int64_t m = m0 + wave * 64 + jb * 32 + (lane & 31);
+    for (int jb = 0; jb < JB; ++jb) {
+      int64_t m = m0 + wave * (32 * JB) + jb * 32 + (lane & 31);
       if (m >= M) m = M - 1;  // tail pixels compute a duplicate, never stored
       const int n = (int)(m / hw), rem = (int)(m - (int64_t)n * hw);
       const int oh = rem / g.W, ow = rem - oh * g.W;
@@ -217,12 +219,12 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
     }
   };
 
-  f32x16 acc[2][2];
+  f32x16 acc[2][JB];
   auto zero = [&]() {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < JB; ++j)
 #pragma unroll
         for (int k = 0; k < 16; ++k) acc[i][j][k] = 0.f;
   };
@@ -234,7 +236,7 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
     for (int tap = 0; tap < 9; ++tap) {
       const int r = tap / 3, s = tap - (tap / 3) * 3;
       const int toff = r * WP + s;
-      bf16x8 fa[2], fb[2];
+      bf16x8 fa[2], fb[JB];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         if (FLIP) {
@@ -245,12 +247,12 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
         }
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < JB; ++j)
         fb[j] = *reinterpret_cast<const bf16x8*>(X + (bpos[j] + toff) * kRow + kg);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < JB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
   };
 
@@ -261,8 +263,8 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
     int co0, v0;
     tile_org(tile, &m0, &co0, &v0);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t m = m0 + wave * 64 + j * 32 + (lane & 31);
+    for (int j = 0; j < JB; ++j) {
+      const int64_t m = m0 + wave * (32 * JB) + j * 32 + (lane & 31);
       if (m < M) {
         uint16_t* yo = y + m * g.Cout + co0;
 #pragma unroll
@@ -315,12 +317,12 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
 }  // namespace
 
 int conv3x3_vrows(const Conv3x3Geom& g) {
-  // the most virtual halo rows any tile of kTM consecutive pixels touches
+  // the most virtual halo rows any tile of g.tm consecutive pixels touches
   const int64_t M = (int64_t)g.N * g.H * g.W;
-  const int hw = g.H * g.W, HP = g.H + 2;
+  const int hw = g.H * g.W, HP = g.H + 2, TM = g.tm;
   int best = 0;
-  for (int64_t m0 = 0; m0 < M; m0 += kTM) {
-    const int64_t m1 = (m0 + kTM < M ? m0 + kTM : M) - 1;
+  for (int64_t m0 = 0; m0 < M; m0 += TM) {
+    const int64_t m1 = (m0 + TM < M ? m0 + TM : M) - 1;
     const int n0 = (int)(m0 / hw), oh0 = (int)((m0 % hw) / g.W);
     const int n1 = (int)(m1 / hw), oh1 = (int)((m1 % hw) / g.W);
     const int rows = (n1 * HP + oh1 + 2) - (n0 * HP + oh0) + 1;
@@ -331,14 +333,6 @@ int conv3x3_vrows(const Conv3x3Geom& g) {
 
 int conv3x3_pieces_per_thread(const Conv3x3Geom& g) {
   return (g.vrows * (g.W + 2) * 2 + kCvThreads - 1) / kCvThreads;
-}
-
-bool conv3x3_ok(const Conv3x3Geom& g) {
-  // 32-bit element offsets into x, y and w (the kernel's per-tile piece tables)
-  return g.N > 0 && g.H > 0 && g.W > 0 && g.Cin % kKC == 0 && g.Cout % kTN == 0 && g.vrows > 0 &&
-         conv3x3_pieces_per_thread(g) <= kMaxNX && (int64_t)g.N * (g.H + 2) < (1ll << 30) &&
-         (int64_t)g.N * g.H * g.W * (g.Cin > g.Cout ? g.Cin : g.Cout) < (1ll << 31) &&
-         (int64_t)g.Cin * 9 * g.Cout < (1ll << 31);
 }
 
 static int cu_count() {
@@ -352,19 +346,41 @@ static int cu_count() {
   return n;
 }
 
-template <bool FLIP>
+int conv3x3_pick_tm(int N, int H, int W, int Cout) {
+  // 512-pixel tiles halve the weight / halo traffic per MFMA, but only where there
+  // are enough of them to keep every CU busy (ResNet-50: the 56x56 and 28x28 layers)
+  const char* e = getenv("RLA_CONV3X3_TM");  // tests pin either tile size
+  if (e && (e[0] == '2' || e[0] == '5')) return e[0] == '5' ? 512 : 256;
+  const int64_t M = (int64_t)N * H * W;
+  const int64_t tiles512 = (M + 511) / 512 * (Cout / kTN);
+  return tiles512 >= 2 * cu_count() ? 512 : 256;
+}
+
+bool conv3x3_ok(const Conv3x3Geom& g) {
+  // 32-bit element offsets into x, y and w (the kernel's per-tile piece tables)
+  return g.N > 0 && g.H > 0 && g.W > 0 && g.Cin % kKC == 0 && g.Cout % kTN == 0 && g.vrows > 0 &&
+         (g.tm == 256 || g.tm == 512) && conv3x3_pieces_per_thread(g) <= kMaxNX &&
+         (int64_t)g.N * (g.H + 2) < (1ll << 30) &&
+         (int64_t)g.N * g.H * g.W * (g.Cin > g.Cout ? g.Cin : g.Cout) < (1ll << 31) &&
+         (int64_t)g.Cin * 9 * g.Cout < (1ll << 31);
+}
+
+template <bool FLIP, int JB, int DEPTH>
 static void launch_nx(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, hipStream_t st,
                       dim3 grid) {
   const dim3 block(kCvThreads);
   switch (conv3x3_pieces_per_thread(g)) {
     case 1: case 2: case 3: case 4:
-      hipLaunchKernelGGL((conv3x3_kernel<4, FLIP>), grid, block, 0, st, x, w, y, g);
+      hipLaunchKernelGGL((conv3x3_kernel<4, FLIP, JB, DEPTH>), grid, block, 0, st, x, w, y, g);
       break;
     case 5:
-      hipLaunchKernelGGL((conv3x3_kernel<5, FLIP>), grid, block, 0, st, x, w, y, g);
+      hipLaunchKernelGGL((conv3x3_kernel<5, FLIP, JB, DEPTH>), grid, block, 0, st, x, w, y, g);
+      break;
+    case 6:
+      hipLaunchKernelGGL((conv3x3_kernel<6, FLIP, JB, DEPTH>), grid, block, 0, st, x, w, y, g);
       break;
     default:
-      hipLaunchKernelGGL((conv3x3_kernel<6, FLIP>), grid, block, 0, st, x, w, y, g);
+      hipLaunchKernelGGL((conv3x3_kernel<7, FLIP, JB, DEPTH>), grid, block, 0, st, x, w, y, g);
       break;
   }
 }
@@ -373,15 +389,19 @@ bool launch_conv3x3(const uint16_t* x, const uint16_t* w, uint16_t* y, const Con
                     hipStream_t st) {
   if (!conv3x3_ok(g)) return false;
   const int64_t M = (int64_t)g.N * g.H * g.W;
-  const int tiles = (int)((M + kTM - 1) / kTM) * (g.Cout / kTN);
+  const int tiles = (int)((M + g.tm - 1) / g.tm) * (g.Cout / kTN);
   // persistent: one workgroup per CU (the LDS image holds one per CU), or one per tile
   int blocks = cu_count();
   if (blocks > tiles) blocks = tiles;
   const dim3 grid((unsigned)((blocks + 7) / 8 * 8));
-  if (flip)
-    launch_nx<true>(x, w, y, g, st, grid);
-  else
-    launch_nx<false>(x, w, y, g, st, grid);
+  // 512-pixel tiles: twice the accumulators, so two register stages in flight
+  if (g.tm == 512) {
+    if (flip) launch_nx<true, 4, 2>(x, w, y, g, st, grid);
+    else launch_nx<false, 4, 2>(x, w, y, g, st, grid);
+  } else {
+    if (flip) launch_nx<true, 2, 4>(x, w, y, g, st, grid);
+    else launch_nx<false, 2, 4>(x, w, y, g, st, grid);
+  }
   return true;
 }
 

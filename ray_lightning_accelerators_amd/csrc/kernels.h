@@ -289,7 +289,9 @@ void launch_wgrad(const uint16_t* dy, const uint16_t* x, float* out, float* part
 struct Conv3x3Geom {
   int N, H, W, Cin, Cout;
   int vrows;  // halo rows of the largest pixel tile (conv3x3_vrows)
+  int tm;     // pixels per workgroup tile: 256 or 512 (conv3x3_pick_tm)
 };
+int conv3x3_pick_tm(int N, int H, int W, int Cout);
 int conv3x3_vrows(const Conv3x3Geom& g);
 bool conv3x3_ok(const Conv3x3Geom& g);
 // flip: input gradient -- x is dy [N, H, W, Cin], w the FORWARD weight [Cin][3][3][Cout]

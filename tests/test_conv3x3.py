@@ -23,9 +23,16 @@ def _rel(a, b):
     return float((a.float() - b).norm() / b.norm().clamp_min(1e-30))
 
 
+@pytest.fixture(params=["256", "512"])
+def tile_px(request, monkeypatch):
+    """Both workgroup tile sizes (the host picks 512 pixels only for large layers)."""
+    monkeypatch.setenv("RLA_CONV3X3_TM", request.param)
+    return int(request.param)
+
+
 @gpu
 @pytest.mark.parametrize("shape", SHAPES)
-def test_conv3x3_forward_matches_fp32(shape):
+def test_conv3x3_forward_matches_fp32(shape, tile_px):
     from ray_lightning_accelerators_amd import ops
     from ray_lightning_accelerators_amd.ops.conv import conv3x3_hip
 
@@ -46,7 +53,7 @@ def test_conv3x3_forward_matches_fp32(shape):
 
 @gpu
 @pytest.mark.parametrize("shape", SHAPES[:4] + SHAPES[-1:])
-def test_conv3x3_dgrad_matches_fp32(shape):
+def test_conv3x3_dgrad_matches_fp32(shape, tile_px):
     from ray_lightning_accelerators_amd.ops.conv import conv3x3_dgrad_hip
 
     n, h, w, cin, cout = shape
