@@ -39,6 +39,16 @@ for st in "$@"; do
       run dp_phases 300 python -u scripts/dp_phase_probe.py ;;
     recycle)
       run pytest_recycle 300 $PYT tests/test_ddp_gpu.py tests/test_runtime.py -k "recycl" ;;
+    c3pmc)  # counter passes over the 3x3 MFMA convolution, one pass per run
+      cd /tmp
+      for pass in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" \
+                  "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES" "FETCH_SIZE" "WRITE_SIZE"; do
+        tag=$(echo $pass | cut -d' ' -f1)
+        timeout -s KILL 90 rocprofv3 --pmc $pass -d "$R/$O/c3pmc_$tag" -o pmc --output-format csv -- \
+          python "$R/scripts/conv3x3_pmc.py" > "$R/$O/c3pmc_$tag.log" 2>&1 || { echo "[c3pmc $tag] FAILED"; tail -20 "$R/$O/c3pmc_$tag.log"; exit 1; }
+        echo "[c3pmc $tag] ok"
+      done
+      cd "$R" ;;
     tuneaudit)  # config 4 (2 workers sharing the GPU, recycled) with per-fit worker diagnostics audited
       run tune_audit 240 python -u scripts/bench_tune.py --workers 2 --share-gpu 8 --trials 8 --epochs 2 --diag-dir "$R/$O/tune_diag" ;;
     tune)
