@@ -461,8 +461,9 @@ Tensor bn_partial(Tensor x, optional<Tensor> y, optional<Tensor> dy, int64_t C, 
 
 Tensor bn_finalize(Tensor part, double count, optional<Tensor> weight, optional<Tensor> bias,
                    optional<Tensor> running_mean, optional<Tensor> running_var, optional<Tensor> nbt,
-                   double momentum, double eps) {
+                   double momentum, double eps, bool nbt_pending) {
   const bool l2 = part.scalar_type() == at::kDouble;  // second-level rows of bn_partial
+  TORCH_CHECK(!(l2 && nbt_pending), "nbt_pending: conv-epilogue partials are fp32 rows");
   check_dev(part, "partials", l2 ? at::kDouble : at::kFloat);
   TORCH_CHECK(part.dim() == 3 && part.size(1) == 2, "partials must be [blocks, 2, C]");
   const int64_t C = part.size(2);
@@ -481,7 +482,7 @@ Tensor bn_finalize(Tensor part, double count, optional<Tensor> weight, optional<
   else
     rla::launch_bn_finalize(part.data_ptr<float>(), (int)part.size(0), (int)C, count, f32_vec(weight, "weight", C),
                             f32_vec(bias, "bias", C), rm, rv, nbtp, (float)momentum, (float)eps,
-                            stats.data_ptr<float>(), cur_stream(part));
+                            stats.data_ptr<float>(), cur_stream(part), nbt_pending ? 1 : 0);
   return stats;
 }
 
@@ -540,7 +541,8 @@ Tensor maxpool_bwd(Tensor dy, Tensor arg, int64_t H, int64_t W, int64_t k, int64
   return dx;
 }
 
-void bn_apply(Tensor x, Tensor scale, Tensor shift, optional<Tensor> res, bool relu, Tensor y) {
+void bn_apply(Tensor x, Tensor scale, Tensor shift, optional<Tensor> res, bool relu, Tensor y,
+              optional<Tensor> nbt_inc) {
   const int64_t C = scale.numel();
   const int64_t M = bn_rows(x, "x", C);
   bn_same(x, y, "y", C);
@@ -555,7 +557,29 @@ void bn_apply(Tensor x, Tensor scale, Tensor shift, optional<Tensor> res, bool r
   const at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   rla::launch_bn_apply(reinterpret_cast<const uint16_t*>(x.data_ptr()), rp, scale.data_ptr<float>(),
                        shift.data_ptr<float>(), M, (int)C, relu, reinterpret_cast<uint16_t*>(y.data_ptr()),
-                       cur_stream(x));
+                       cur_stream(x), ptr_or_null<int64_t>(nbt_inc, "num_batches_tracked", at::kLong, 1));
+}
+
+// 1x1 conv forward with BatchNorm partial sums: x [M, K] (NHWC rows), w [N, K], both
+// bf16 contiguous; returns (y [M, N] bf16, part [gx, 2, N] fp32 for bn_finalize)
+std::vector<Tensor> conv1x1_stats(Tensor x, Tensor w) {
+  check_dev(x, "x", at::kBFloat16);
+  check_dev(w, "w", at::kBFloat16);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.is_contiguous() && w.is_contiguous(),
+              "conv1x1_stats: x [M, K] and w [N, K] must be contiguous 2-D");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "conv1x1_stats: w must be [N, K]");
+  TORCH_CHECK(rla::conv1x1_stats_ok(M, (int)K, (int)N), "conv1x1_stats: unsupported shape (K % 32, N % 64)");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+              "conv1x1_stats: 16-byte aligned operands");
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const rla::Conv1x1Plan p = rla::conv1x1_stats_plan(M, (int)N);
+  Tensor y = at::empty({M, N}, x.options());
+  Tensor part = at::empty({p.gx, 2, N}, x.options().dtype(at::kFloat));
+  rla::launch_conv1x1_stats(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                            reinterpret_cast<const uint16_t*>(w.data_ptr()), reinterpret_cast<uint16_t*>(y.data_ptr()),
+                            M, (int)K, (int)N, p, part.data_ptr<float>(), cur_stream(x));
+  return {y, part};
 }
 
 void bn_bwd_apply(Tensor x, optional<Tensor> y, Tensor dy, Tensor coef, bool relu, Tensor dx,
@@ -764,9 +788,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_partial", &bn_partial, "fused BN: per-block partial sums (mode 0 fwd stats, 1 bwd dz/dz*x)",
         py::arg("x"), py::arg("y"), py::arg("dy"), py::arg("C"), py::arg("mode"), py::arg("relu"), py::arg("nbt"),
         py::arg("dy2") = py::none(), py::arg("ss") = py::none(), py::arg("dout") = py::none());
-  m.def("bn_finalize", &bn_finalize, "fused BN: mean/invstd/scale/shift + running stats from partials");
+  m.def("bn_finalize", &bn_finalize, "fused BN: mean/invstd/scale/shift + running stats from partials",
+        py::arg("part"), py::arg("count"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"),
+        py::arg("running_var"), py::arg("nbt"), py::arg("momentum"), py::arg("eps"), py::arg("nbt_pending") = false);
   m.def("bn_bwd_finalize", &bn_bwd_finalize, "fused BN backward: dgamma/dbeta + dx coefficients");
-  m.def("bn_apply", &bn_apply, "fused BN apply: y = act(x*scale + shift (+res))");
+  m.def("bn_apply", &bn_apply, "fused BN apply: y = act(x*scale + shift (+res))", py::arg("x"), py::arg("scale"),
+        py::arg("shift"), py::arg("res"), py::arg("relu"), py::arg("y"), py::arg("nbt_inc") = py::none());
+  m.def("conv1x1_stats", &conv1x1_stats, "1x1 conv forward on MFMA + BatchNorm partial sums of its output");
+  m.def("conv1x1_stats_ok", [](int64_t M, int64_t K, int64_t N) { return rla::conv1x1_stats_ok(M, (int)K, (int)N); });
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC bf16 max pool -> (y, one-byte window argmax)");
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max pool backward (gather through the argmax bytes)");
   m.def("bn_bwd_apply", &bn_bwd_apply, "fused BN backward apply: dx (+ dres = relu-masked dy)", py::arg("x"),

@@ -237,7 +237,7 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const P* __restrict__
                                                            float* running_var, const int64_t* nbt, float momentum,
                                                            float eps, const float* __restrict__ mean_in,
                                                            const float* __restrict__ invstd_in,
-                                                           float* __restrict__ out) {
+                                                           float* __restrict__ out, int nbt_pending = 0) {
   __shared__ double sh[2][kFinSlices][kFinCh];
   const int cl = threadIdx.x % kFinCh, sl = threadIdx.x / kFinCh;
   const int c = blockIdx.x * kFinCh + cl;
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const P* __restrict__
     out[3 * C + c] = (beta ? beta[c] : 0.f) - (float)mean * sc;
     if (running_mean) {
       // momentum < 0: cumulative moving average, factor 1 / num_batches_tracked
-      const float mom = momentum >= 0.f ? momentum : 1.f / (float)(nbt ? nbt[0] : 1);
+      const float mom = momentum >= 0.f ? momentum : 1.f / (float)(nbt ? nbt[0] + nbt_pending : 1);
       const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
       running_mean[c] = (1.f - mom) * running_mean[c] + mom * (float)mean;
       running_var[c] = (1.f - mom) * running_var[c] + mom * (float)unbiased;
@@ -316,9 +316,12 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_kernel(const uint16_t* __
                                                               const uint16_t* __restrict__ res,
                                                               const float* __restrict__ scale,
                                                               const float* __restrict__ shift, int64_t M, int C,
-                                                              uint16_t* __restrict__ y) {
+                                                              uint16_t* __restrict__ y, int64_t* nbt_inc) {
   const int G = C >> 3, rpi = kBnThreads / G, tid = threadIdx.x;
   const int g = tid % G, r0 = tid / G;
+  // the statistics came from a conv epilogue (no partial kernel ran): num_batches_tracked
+  // += 1 here, after the finalize that already used the incremented value
+  if (nbt_inc && blockIdx.x == 0 && tid == 0) nbt_inc[0] += 1;
   if (r0 >= rpi) return;
   const f8 sc = ld8f(scale + g * 8), sf = ld8f(shift + g * 8);
   const int64_t col = (int64_t)g * 8, rstride = (int64_t)gridDim.x * rpi;
@@ -473,9 +476,9 @@ void launch_bn_partial(const uint16_t* x, const uint16_t* y, const uint16_t* dy,
 
 void launch_bn_finalize(const float* part, int nparts, int C, double count, const float* gamma,
                         const float* beta, float* running_mean, float* running_var, const int64_t* nbt,
-                        float momentum, float eps, float* stats, hipStream_t s) {
+                        float momentum, float eps, float* stats, hipStream_t s, int nbt_pending) {
   hipLaunchKernelGGL((bn_finalize_kernel<false>), dim3((C + kFinCh - 1) / kFinCh), dim3(1024), 0, s, part, nparts, C, count,
-                     gamma, beta, running_mean, running_var, nbt, momentum, eps, nullptr, nullptr, stats);
+                     gamma, beta, running_mean, running_var, nbt, momentum, eps, nullptr, nullptr, stats, nbt_pending);
 }
 
 void launch_bn_bwd_finalize(const float* part, int nparts, int C, double count, const float* gamma,
@@ -498,16 +501,16 @@ void launch_bn_bwd_finalize64(const double* part, int nparts, int C, double coun
 }
 
 void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* scale, const float* shift, int64_t M,
-                     int C, bool relu, uint16_t* y, hipStream_t s) {
+                     int C, bool relu, uint16_t* y, hipStream_t s, int64_t* nbt_inc) {
   const dim3 grid(apply_grid(M, C)), block(kBnThreads);
   if (relu && res)
-    hipLaunchKernelGGL((bn_apply_kernel<true, true>), grid, block, 0, s, x, res, scale, shift, M, C, y);
+    hipLaunchKernelGGL((bn_apply_kernel<true, true>), grid, block, 0, s, x, res, scale, shift, M, C, y, nbt_inc);
   else if (relu)
-    hipLaunchKernelGGL((bn_apply_kernel<true, false>), grid, block, 0, s, x, res, scale, shift, M, C, y);
+    hipLaunchKernelGGL((bn_apply_kernel<true, false>), grid, block, 0, s, x, res, scale, shift, M, C, y, nbt_inc);
   else if (res)
-    hipLaunchKernelGGL((bn_apply_kernel<false, true>), grid, block, 0, s, x, res, scale, shift, M, C, y);
+    hipLaunchKernelGGL((bn_apply_kernel<false, true>), grid, block, 0, s, x, res, scale, shift, M, C, y, nbt_inc);
   else
-    hipLaunchKernelGGL((bn_apply_kernel<false, false>), grid, block, 0, s, x, res, scale, shift, M, C, y);
+    hipLaunchKernelGGL((bn_apply_kernel<false, false>), grid, block, 0, s, x, res, scale, shift, M, C, y, nbt_inc);
 }
 
 void launch_bn_bwd_apply(const uint16_t* x, const uint16_t* y, const uint16_t* dy, const float* coef, int64_t M,

@@ -81,7 +81,8 @@ void launch_bn_partial(const uint16_t* x, const uint16_t* y, const uint16_t* dy,
 // running stats update (momentum < 0: cumulative average over num_batches_tracked)
 void launch_bn_finalize(const float* part, int nparts, int C, double count, const float* gamma,
                         const float* beta, float* running_mean, float* running_var, const int64_t* nbt,
-                        float momentum, float eps, float* stats, hipStream_t s);
+                        float momentum, float eps, float* stats, hipStream_t s,
+                        int nbt_pending = 0);  // 1: nbt's += 1 is still to come (bn_apply's nbt_inc)
 // the same from the fp64 rows of the second reduction level
 void launch_bn_finalize64(const double* part, int nparts, int C, double count, const float* gamma,
                           const float* beta, float* running_mean, float* running_var, const int64_t* nbt,
@@ -95,13 +96,28 @@ void launch_bn_bwd_finalize64(const double* part, int nparts, int C, double coun
 
 // y = act(x*scale + shift (+ res))
 void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* scale, const float* shift, int64_t M,
-                     int C, bool relu, uint16_t* y, hipStream_t s);
+                     int C, bool relu, uint16_t* y, hipStream_t s,
+                     int64_t* nbt_inc = nullptr);  // block 0 adds 1 (statistics came from a conv epilogue)
 
 // dz = dy * (y > 0 if relu); dx = A*dz + B*x + Cc; dres = dz (if dres)
 void launch_bn_bwd_apply(const uint16_t* x, const uint16_t* y, const uint16_t* dy, const float* coef, int64_t M,
                          int C, bool relu, uint16_t* dx, uint16_t* dres, hipStream_t s,
                          const uint16_t* dy2 = nullptr,  // gradient = dy + dy2
                          const float* ss = nullptr);     // ReLU mask from the fwd stats [4, C], not y
+
+// 1x1 / stride-1 conv forward y[M][N] = x[M][K] . w[N][K]^T with the next BatchNorm's
+// partial sums of bf16(y) in the epilogue: part [gx, 2, N] fp32, bn_finalize's layout
+// (csrc/conv1x1.hip)
+struct Conv1x1Plan {
+  int tnw;            // 32-channel blocks per wave (1 or 2)
+  int gy;             // channel columns of 64 tnw
+  int gx;             // pixel ranges = partial rows (multiple of 8)
+  int tiles_per_blk;  // 128-pixel tiles per range
+};
+bool conv1x1_stats_ok(int64_t M, int K, int N);
+Conv1x1Plan conv1x1_stats_plan(int64_t M, int N);
+void launch_conv1x1_stats(const uint16_t* x, const uint16_t* w, uint16_t* y, int64_t M, int K, int N,
+                          const Conv1x1Plan& p, float* part, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // Fused MNIST-MLP training step (784 -> L1 -> L2 -> 10, ReLU, log_softmax+NLL).

@@ -24,7 +24,7 @@ from torch.utils.data import Dataset
 
 from ..lightning import LightningModule
 from ..ops.bn import BatchNormAct2d
-from ..ops.conv import Conv1x1NHWC, GradFork
+from ..ops.conv import BNStats, Conv1x1NHWC, GradFork
 from ..ops.pool import MaxPool2dNHWC
 from ..ops.shadow import ConvBF16
 
@@ -64,20 +64,32 @@ class Bottleneck(nn.Module):
         self.bn3 = _bn(cout, fused_bn)  # fused: relu(bn3(x) + identity) in one pass
         self.downsample = downsample
 
+    @staticmethod
+    def _conv_bn(conv, bn, x, **kw):
+        """bn(conv(x)) for a 1x1 conv: the conv may compute bn's batch statistics in its
+        epilogue (ops.conv.BNStats; bn then skips its partial pass over the output)."""
+        if isinstance(conv, Conv1x1NHWC) and bn.training:
+            st = BNStats()
+            y = conv(x, fork=kw.pop("fork", None), bn_stats=st)
+            return bn(y, bn_stats=st, **kw)
+        fork = kw.pop("fork", None)
+        return bn(conv(x, fork=fork) if fork is not None else conv(x), **kw)
+
     def forward(self, x):
         if self.fused_bn and self.downsample is not None:
             # conv1 and the downsample conv both read x: their input gradients meet in
             # one tensor (ops.conv.GradFork) instead of an autograd add of two
             fork = GradFork()
-            idt = self.downsample[1](self.downsample[0](x, fork=fork))
-            out = self.bn2(self.conv2(self.bn1(self.conv1(x, fork=fork))))
-            return self.bn3(self.conv3(out), idt, residual_is_ancestor=False)
+            idt = self._conv_bn(self.downsample[0], self.downsample[1], x, fork=fork)
+            out = self.bn2(self.conv2(self._conv_bn(self.conv1, self.bn1, x, fork=fork)))
+            return self._conv_bn(self.conv3, self.bn3, out, residual=idt, residual_is_ancestor=False)
         idt = x if self.downsample is None else self.downsample(x)
         if self.fused_bn:
-            out = self.bn2(self.conv2(self.bn1(self.conv1(x))))
+            out = self.bn2(self.conv2(self._conv_bn(self.conv1, self.bn1, x)))
             # identity shortcut: x is an ancestor of conv3's output, so bn3 may fold
             # its residual gradient into the previous block's bn3 backward (ops/bn.py)
-            return self.bn3(self.conv3(out), idt, residual_is_ancestor=self.downsample is None)
+            return self._conv_bn(self.conv3, self.bn3, out, residual=idt,
+                                 residual_is_ancestor=self.downsample is None)
         out = F.relu(self.bn1(self.conv1(x)), inplace=True)
         out = F.relu(self.bn2(self.conv2(out)), inplace=True)
         out = self.bn3(self.conv3(out))

@@ -81,23 +81,29 @@ fold_stats = {"folded": 0}
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu, group,
-                slot=None, sink=None):
+                slot=None, sink=None, part=None):
         # slot: this layer's own _FoldSlot (a consumer may park dres for our backward);
-        # sink: the producer slot of `residual` (residual is then passed detached)
+        # sink: the producer slot of `residual` (residual is then passed detached);
+        # part: partial sums the producing conv computed in its epilogue (ops.conv.BNStats)
         mod = require()
         C = x.size(1)
         xv = _nhwc(x)
         count = float(xv.numel() // C)
-        part = mod.bn_partial(xv, None, None, C, 0, False, nbt)
+        # num_batches_tracked: += 1 by the partial kernel, or -- with the conv's partials
+        # -- by the apply kernel, after a finalize told to use the incremented value
+        pending = part is not None and nbt is not None
+        if part is None:
+            part = mod.bn_partial(xv, None, None, C, 0, False, nbt)
         if group is not None:
             # SyncBatchNorm: global per-channel sums (equal per-rank batches, as the
             # DistributedSampler shards are)
             part = part.sum(0, keepdim=True)
             dist.all_reduce(part, group=group)
             count *= dist.get_world_size(group)
-        st = mod.bn_finalize(part, count, weight, bias, running_mean, running_var, nbt, momentum, eps)
+        st = mod.bn_finalize(part, count, weight, bias, running_mean, running_var, nbt, momentum, eps, pending)
         y = torch.empty_like(x, memory_format=torch.channels_last)
-        mod.bn_apply(xv, st[2], st[3], _nhwc(residual) if residual is not None else None, relu, _nhwc(y))
+        mod.bn_apply(xv, st[2], st[3], _nhwc(residual) if residual is not None else None, relu, _nhwc(y),
+                     nbt if pending else None)
         ctx.relu, ctx.has_res, ctx.group, ctx.count = relu, residual is not None, group, count
         ctx.slot, ctx.sink = slot, sink
         # ReLU without a residual: the backward recomputes the mask x*scale+shift > 0
@@ -143,7 +149,7 @@ class _BNActFn(torch.autograd.Function):
         # views of the coefficient tensor (no copy kernels): autograd hands them to .grad
         dgamma = wsrc[0] if weight is not None and ctx.needs_input_grad[1] else None
         dbeta = wsrc[1] if ctx.needs_input_grad[2] else None
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None
 
 
 class BatchNormAct2d(nn.BatchNorm2d):
@@ -171,10 +177,15 @@ class BatchNormAct2d(nn.BatchNorm2d):
         return None
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                residual_is_ancestor: bool = False) -> torch.Tensor:
+                residual_is_ancestor: bool = False, bn_stats=None) -> torch.Tensor:
         """``residual_is_ancestor``: the caller guarantees ``x`` is computed from
         ``residual`` (ResNet identity shortcut), so this layer's backward runs before
-        the residual producer's and the residual gradient can be folded into it."""
+        the residual producer's and the residual gradient can be folded into it.
+        ``bn_stats``: an ``ops.conv.BNStats`` the conv producing ``x`` may have filled
+        with x's partial sums (this layer then skips its own partial pass)."""
+        part = None
+        if bn_stats is not None:
+            part, bn_stats.part = bn_stats.part, None
         relu = self.act == "relu"
         use_batch_stats = self.training or not self.track_running_stats
         if fused_ok(x, residual):
@@ -193,7 +204,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
                     x, self.weight, self.bias, residual,
                     self.running_mean if track else None, self.running_var if track else None,
                     self.num_batches_tracked if track else None, momentum, float(self.eps), relu, self._group(),
-                    slot, sink)
+                    slot, sink, part)
                 if slot is not None:
                     y._rla_fold = slot
                 return y

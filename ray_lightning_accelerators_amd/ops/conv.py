@@ -218,23 +218,69 @@ def _acc_dgrad(d: torch.Tensor, dy2: torch.Tensor, wb: torch.Tensor) -> None:
         d.add_(_from2d(torch.mm(dy2, wb), d.size(0), d.size(2), d.size(3)))
 
 
+class BNStats:
+    """Hand-off of a convolution's epilogue BatchNorm statistics to the BatchNorm that
+    consumes its output: the conv fills ``part`` ([rows, 2, C] fp32 partial sums of
+    its bf16 output, ``bn_finalize``'s layout) when its backend computed them, and
+    ``BatchNormAct2d`` then skips its own partial pass over the output."""
+
+    __slots__ = ("part",)
+
+    def __init__(self):
+        self.part: Optional[torch.Tensor] = None
+
+
+def conv1x1_stats_ok(m: int, cin: int, cout: int) -> bool:
+    """Shapes of the 1x1 MFMA forward with BatchNorm statistics (csrc/conv1x1.hip)."""
+    return cin % 32 == 0 and cout % 64 == 0 and cout <= 4096 and os.environ.get("RLA_CONV1X1_STATS", "auto") != "off"
+
+
+def conv1x1_stats_hip(x: torch.Tensor, wb: torch.Tensor):
+    """``conv2d(x, wb)`` for a 1x1 / stride-1 layer on the MFMA kernel, plus the
+    per-channel partial sums of its bf16 output: ``x`` [N, Cin, H, W] channels_last
+    bf16, ``wb`` [Cout, Cin] bf16.  Returns (y channels_last, part [rows, 2, Cout])."""
+    from . import require
+
+    n, _, h, w = x.shape
+    y2, part = require().conv1x1_stats(_nhwc2d(x), wb)
+    return _from2d(y2, n, h, w), part
+
+
+def _bn_partial(y: torch.Tensor) -> torch.Tensor:
+    from . import require
+
+    return require().bn_partial(y.permute(0, 2, 3, 1), None, None, y.size(1), 0, False, None)
+
+
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, shadow=None, fork=None):
+    def forward(ctx, x, weight, shadow=None, fork=None, bn_stats=None):
         n, cin, h, w = x.shape
         cout = weight.size(0)
         # the arena's bf16 shadow (ops/shadow.py) when there is one: no cast kernel
         wb = (shadow if shadow is not None else weight.detach().to(torch.bfloat16)).reshape(cout, cin)
         x2 = _nhwc2d(x)
         key = (x2.size(0), cin, cout)
-        be = _pick("fwd", key, {
-            "gemm": lambda: torch.mm(x2, wb.t()),
-            "miopen": lambda: _conv(x, wb.view(cout, cin, 1, 1), None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1),
-        })
-        if be == "gemm":
+        w4 = wb.view(cout, cin, 1, 1)
+        if bn_stats is not None and conv1x1_stats_ok(x2.size(0), cin, cout):
+            # the next BatchNorm's statistics: in this GEMM's epilogue, or the library
+            # forward + BN's own partial pass -- whichever is faster for the shape
+            be = _pick("fwd_st", key, {
+                "hip": lambda: conv1x1_stats_hip(x, wb),
+                "gemm": lambda: _bn_partial(_from2d(torch.mm(x2, wb.t()), n, h, w)),
+                "miopen": lambda: _bn_partial(_conv(x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)),
+            })
+        else:
+            be = _pick("fwd", key, {
+                "gemm": lambda: torch.mm(x2, wb.t()),
+                "miopen": lambda: _conv(x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1),
+            })
+        if be == "hip":
+            y, bn_stats.part = conv1x1_stats_hip(x, wb)
+        elif be == "gemm":
             y = _from2d(torch.mm(x2, wb.t()), n, h, w)
         else:
-            y = _conv(x, wb.view(cout, cin, 1, 1), None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
+            y = _conv(x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
         ctx.save_for_backward(x, wb)
         ctx.key = key
         ctx.fork = fork
@@ -274,7 +320,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         if be_d == "miopen" and be_w == "miopen" and fork is None:
             # both from MIOpen: one call (its host cost is tens of us per call)
             dx, dw = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, True, False])[:2]
-            return dx, dw.float(), None, None
+            return dx, dw.float(), None, None, None
         if be_d == "gemm":
             dx = _fork_dx(fork, lambda: _from2d(torch.mm(dy2, wb), n, h, w), None)
         elif be_d == "miopen":
@@ -287,7 +333,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         elif be_w == "miopen":
             dw = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
                            [False, True, False])[1].float()
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 def fast_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
@@ -306,14 +352,17 @@ class Conv1x1NHWC(nn.Conv2d):
     def __init__(self, in_channels: int, out_channels: int, device=None, dtype=None):
         super().__init__(in_channels, out_channels, 1, 1, 0, bias=False, device=device, dtype=dtype)
 
-    def forward(self, x: torch.Tensor, fork: Optional[GradFork] = None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, fork: Optional[GradFork] = None,
+                bn_stats: Optional[BNStats] = None) -> torch.Tensor:
+        """``bn_stats``: the BatchNorm reading this output is training on batch
+        statistics -- let this layer compute them where that is faster (BNStats)."""
         if torch.is_autocast_enabled("cuda") and x.is_cuda and x.dtype == torch.float32:
             x = x.to(torch.bfloat16)
         if fast_ok(x, self) and _mode() != "off":
             stats["fast"] += 1
             from .shadow import bf16_weight
 
-            return _Conv1x1Fn.apply(x, self.weight, bf16_weight(self.weight), fork)
+            return _Conv1x1Fn.apply(x, self.weight, bf16_weight(self.weight), fork, bn_stats)
         stats["fallback"] += 1
         return F.conv2d(x, self.weight)
 

@@ -10,6 +10,7 @@
 # bench), share2 (N = 2 rehearsals with both ranks on the one GPU), corners (Tune
 # search-space corners), selftest (native comm self-test, plain + host ASan/UBSan),
 # wgrad (conv weight-gradient kernel tests + probe), rn50b (native ResNet-50 bench),
+# c1stats (1x1 conv + BN statistics kernel),
 # rn50 (ResNet-50 bench, native + stock torch; --deterministic-conv
 # is not run: MIOpen's atomic-free solvers compile for > 3 min without output), rn50prof (its kernel stats)
 set -o pipefail
@@ -71,6 +72,9 @@ for st in "$@"; do
       run rn50_ops 300 python -u scripts/rn50_op_profile.py ;;
     conv1x1)
       run conv1x1 300 python -u scripts/conv1x1_probe.py ;;
+    c1stats)  # 1x1 forward with BN statistics in the epilogue: tests + per-shape timing
+      run pytest_c1stats 300 $PYT tests/test_conv1x1_stats.py tests/test_bn.py -m gpu
+      run c1stats_probe 300 python -u scripts/conv1x1_stats_probe.py ;;
     tunetl)  # cold sweep with the cross-process start-up timeline
       RLA_TIMELINE="$R/$O/tune_timeline.jsonl" run tune_tl 300 python scripts/bench_tune.py --trials 6
       python scripts/timeline_report.py "$O/tune_timeline.jsonl" --merged > "$O/tune_timeline.txt" 2>&1 || true ;;

@@ -1,0 +1,131 @@
+"""1x1 convolution forward with the next BatchNorm's statistics in its epilogue
+(csrc/conv1x1.hip): the output against an fp32 PyTorch reference of the same bf16
+operands, the partial sums against fp64 sums of the kernel's own bf16 output, and
+the BatchNorm that consumes them against the same layer running its own partial
+pass (outputs, running statistics, num_batches_tracked)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+gpu = pytest.mark.gpu
+
+# (M, K, N): ResNet-50 1x1 shapes at small batch, a pixel tail (M % 128 != 0), a
+# column count that is not a multiple of 128 (one 32-channel block per wave), K = 32
+SHAPES = [
+    (2 * 56 * 56, 64, 256),
+    (2 * 56 * 56, 256, 64),
+    (3 * 28 * 28, 512, 128),
+    (5 * 7 * 7, 512, 2048),
+    (4 * 14 * 14, 1024, 256),
+    (1000, 64, 192),
+    (77, 32, 64),
+]
+
+
+def _rel(a, b):
+    return float((a.float() - b).norm() / b.norm().clamp_min(1e-30))
+
+
+@gpu
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv1x1_stats_matches_fp32(shape):
+    from ray_lightning_accelerators_amd import ops
+
+    m, k, n = shape
+    torch.manual_seed(0)
+    dev = torch.device("cuda", 0)
+    x = torch.randn(m, k, device=dev).to(torch.bfloat16)
+    wb = (torch.randn(n, k, device=dev) / k ** 0.5).to(torch.bfloat16)
+    y, part = ops.require().conv1x1_stats(x, wb)
+    ref = x.float() @ wb.float().t()
+    assert y.shape == (m, n) and y.dtype == torch.bfloat16
+    assert _rel(y, ref) < 8e-3, _rel(y, ref)
+    assert part.dim() == 3 and part.size(1) == 2 and part.size(2) == n and part.size(0) % 8 == 0
+    yd = y.double()
+    s = part.double().sum(0)
+    # the sums are of the ROUNDED outputs the kernel stored (what bn_partial would read)
+    assert torch.allclose(s[0], yd.sum(0), rtol=1e-4, atol=1e-3 * m ** 0.5)
+    assert torch.allclose(s[1], (yd * yd).sum(0), rtol=1e-4, atol=1e-3)
+
+
+@gpu
+def test_conv1x1_stats_deterministic():
+    from ray_lightning_accelerators_amd import ops
+
+    torch.manual_seed(1)
+    dev = torch.device("cuda", 0)
+    x = torch.randn(3 * 56 * 56, 64, device=dev).to(torch.bfloat16)
+    wb = torch.randn(256, 64, device=dev).to(torch.bfloat16)
+    y0, p0 = ops.require().conv1x1_stats(x, wb)
+    y1, p1 = ops.require().conv1x1_stats(x, wb)
+    assert torch.equal(y0, y1) and torch.equal(p0, p1)
+
+
+@gpu
+@pytest.mark.parametrize("residual", [False, True])
+def test_bn_consumes_conv_epilogue_stats(residual, monkeypatch):
+    """BatchNormAct2d fed the conv's partial sums == the same layer summing the same
+    conv output itself (both runs take the kernel's y; one drops its partials)."""
+    from ray_lightning_accelerators_amd.ops.bn import BatchNormAct2d
+    from ray_lightning_accelerators_amd.ops.conv import BNStats, Conv1x1NHWC
+
+    torch.manual_seed(2)
+    dev = torch.device("cuda", 0)
+    conv = Conv1x1NHWC(64, 128).to(dev)
+    x0 = torch.randn(4, 64, 20, 20, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = torch.randn(4, 128, 20, 20, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    monkeypatch.setenv("RLA_CONV1X1", "hip")
+    outs = []
+    for use in (False, True):
+        bn = BatchNormAct2d(128).to(dev)
+        bn.momentum = None  # cumulative average: the finalize reads num_batches_tracked
+        x = x0.clone().requires_grad_(True)
+        for _ in range(2):
+            st = BNStats()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = conv(x, bn_stats=st)
+                assert st.part is not None
+                if not use:
+                    st.part = None  # the layer sums y itself
+                z = bn(y, res if residual else None, bn_stats=st)
+        z.float().square().sum().backward()
+        outs.append((z.detach().float(), x.grad.float(), bn.running_mean.clone(), bn.running_var.clone(),
+                     int(bn.num_batches_tracked)))
+    (z0, g0, m0, v0, n0), (z1, g1, m1, v1, n1) = outs
+    assert n0 == n1 == 2
+    assert _rel(z1, z0) < 1e-5
+    assert _rel(g1, g0) < 1e-4
+    assert torch.allclose(m1, m0, rtol=1e-5, atol=1e-6) and torch.allclose(v1, v0, rtol=1e-5, atol=1e-6)
+
+
+@gpu
+def test_resnet_bottleneck_routes_stats(monkeypatch):
+    """A training Bottleneck pinned to the kernel computes its 1x1 layers' BN
+    statistics in the conv epilogue (conv1 / conv3 / stride-1 downsample)."""
+    from ray_lightning_accelerators_amd.models.resnet import Bottleneck
+    from ray_lightning_accelerators_amd.ops import conv as C
+    from torch import nn
+
+    monkeypatch.setenv("RLA_CONV1X1", "hip")
+    calls = {"n": 0}
+    real = C.conv1x1_stats_hip
+
+    def spy(*a, **k):
+        calls["n"] += 1
+        return real(*a, **k)
+
+    monkeypatch.setattr(C, "conv1x1_stats_hip", spy)
+    from ray_lightning_accelerators_amd.ops.bn import BatchNormAct2d
+
+    dev = torch.device("cuda", 0)
+    down = nn.Sequential(C.Conv1x1NHWC(64, 256), BatchNormAct2d(256, act=None))
+    blk = Bottleneck(64, 64, 1, down, fused_bn=True).to(dev).to(memory_format=torch.channels_last)
+    x = torch.randn(2, 64, 16, 16, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = blk(x)
+    y.float().sum().backward()
+    assert calls["n"] == 3
+    assert int(blk.bn1.num_batches_tracked) == int(blk.bn3.num_batches_tracked) == 1
+    assert int(down[1].num_batches_tracked) == 1
+    assert torch.isfinite(x.grad.float()).all()
