@@ -23,7 +23,7 @@
 //     stage is 128 x rows and 64 TNW w rows of 64 B, stored 16-B-unit-major
 //     ([k unit][row]) so the fragment reads -- 32 consecutive rows of one k unit per
 //     half-wave -- are contiguous 512-B ds_read_b128 runs (conflict-free).  A ring of
-//     kStages buffers: the DMA of kStages - 2 stages is in flight behind every stage's
+//     NS buffers: the DMA of NS - 2 stages is in flight behind every stage's
 //     MFMAs, across tile boundaries; each stage is retired by a COUNTED vmcnt (the
 //     DMA is inline asm, invisible to hipcc's wait bookkeeping, and hipcc would
 //     otherwise drain every in-flight load at each epilogue's stores) and one raw
@@ -52,8 +52,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kC1Threads = 256;
-constexpr int kStages = 4;      // LDS ring depth
-constexpr int kC1WRes = 32768;  // resident weight block bytes (K x 64 TNW bf16) at most
+constexpr int kC1LdsBytes = 65536;  // ring (+ resident weights) per workgroup: 2 workgroups per CU
 
 // 16 bytes per lane, global -> LDS, lane-linear from the wave-uniform LDS byte
 // address `lds`; M0 saved and restored in the same statement (LDS-DMA recipe)
@@ -65,7 +64,7 @@ __device__ __forceinline__ void c1_dma16(const void* gsrc, uint32_t lds) {
                : "memory");
 }
 
-template <int TNW, bool WRES>
+template <int TNW, bool WRES, int NS>
 __global__ __launch_bounds__(kC1Threads, 2) void conv1x1_stats_kernel(const uint16_t* __restrict__ x,
                                                                       const uint16_t* __restrict__ w,
                                                                       uint16_t* __restrict__ y, int64_t M, int K,
@@ -78,8 +77,9 @@ __global__ __launch_bounds__(kC1Threads, 2) void conv1x1_stats_kernel(const uint
   constexpr int kDma = kXInst + kWInst;
   // WRES: the workgroup's whole weight block [K / 8 units][BN rows] stays in LDS (DMA'd
   // once, ahead of stage 0) and the ring carries x only
-  constexpr int kWResBytes = WRES ? kC1WRes : 0;
-  __shared__ __attribute__((aligned(16))) uint8_t ring[kStages * kStageBytes + kWResBytes];
+  constexpr int kWResBytes = WRES ? kC1LdsBytes - NS * kStageBytes : 0;
+  static_assert(NS * kStageBytes + kWResBytes <= kC1LdsBytes, "LDS budget (2 workgroups per CU)");
+  __shared__ __attribute__((aligned(16))) uint8_t ring[NS * kStageBytes + kWResBytes];
   __shared__ float red[2][2][BN];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave & 1, wm = wave >> 1, r = lane & 31, h = lane >> 5;
@@ -103,14 +103,14 @@ __global__ __launch_bounds__(kC1Threads, 2) void conv1x1_stats_kernel(const uint
   const int nch = K >> 5;
   const int nst = ntiles * nch;
   const uint32_t ring0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)ring;
-  const uint32_t wres0 = ring0 + kStages * kStageBytes;
+  const uint32_t wres0 = ring0 + NS * kStageBytes;
 
-  // DMA of stage st into ring buffer st % kStages: wave-instruction g of the x part
+  // DMA of stage st into ring buffer st % NS: wave-instruction g of the x part
   // covers k unit g / 2, rows 64 (g & 1) .. +64; of the w part k unit g / (BN / 64)
   auto issue = [&](int st) {
     const int sc = st < nst ? st : nst - 1;
     const int ti = sc / nch, k = (sc - ti * nch) * 32;
-    const uint32_t buf = ring0 + (uint32_t)(st % kStages) * kStageBytes;
+    const uint32_t buf = ring0 + (uint32_t)(st % NS) * kStageBytes;
 #pragma unroll
     for (int u = 0; u < kXInst; ++u) {
       const int g = wave * kXInst + u;
@@ -138,9 +138,9 @@ __global__ __launch_bounds__(kC1Threads, 2) void conv1x1_stats_kernel(const uint
   }
 
   auto compute = [&](int st) {
-    const uint8_t* buf = ring + (st % kStages) * kStageBytes;
+    const uint8_t* buf = ring + (st % NS) * kStageBytes;
     const int ti = st / nch, c = st - ti * nch;
-    const uint8_t* wb = WRES ? ring + kStages * kStageBytes + c * 4 * BN * 16 : buf + kXBytes;
+    const uint8_t* wb = WRES ? ring + NS * kStageBytes + c * 4 * BN * 16 : buf + kXBytes;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ku = 2 * ks + h;
@@ -212,12 +212,12 @@ __global__ __launch_bounds__(kC1Threads, 2) void conv1x1_stats_kernel(const uint
     }
   }
 #pragma unroll
-  for (int d = 0; d < kStages - 1; ++d) issue(d);
+  for (int d = 0; d < NS - 1; ++d) issue(d);
   for (int st = 0; st < nst; ++st) {
-    // stage st landed: the DMA issued after it (kStages - 2 stages) may still fly;
+    // stage st landed: the DMA issued after it (NS - 2 stages) may still fly;
     // then every wave's part is in and every wave has finished reading buffer st - 1
-    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"((kStages - 2) * kDma) : "memory");
-    issue(st + kStages - 1);
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"((NS - 2) * kDma) : "memory");
+    issue(st + NS - 1);
     compute(st);
     const int ti = st / nch;
     if (st - ti * nch == nch - 1) epilogue(ti);
@@ -284,20 +284,26 @@ Conv1x1Plan conv1x1_stats_plan(int64_t M, int N) {
 void launch_conv1x1_stats(const uint16_t* x, const uint16_t* w, uint16_t* y, int64_t M, int K, int N,
                           const Conv1x1Plan& p, float* part, hipStream_t s) {
   const dim3 grid(p.gx * p.gy), block(kC1Threads);
-  const bool wres = (int64_t)K * 64 * p.tnw * 2 <= kC1WRes;
-#define RLA_C1_LAUNCH(T, R)                                                                                  \
-  hipLaunchKernelGGL((conv1x1_stats_kernel<T, R>), grid, block, 0, s, x, w, y, M, K, N, p.gx, p.tiles_per_blk, \
+  // resident weights where they fit beside the x ring: 6 x-only stages (4 in flight)
+  // with a 16 KB weight block, 4 stages with 32 KB; else x + w stream through 4 stages
+  const int64_t wbytes = (int64_t)K * 64 * p.tnw * 2;
+#define RLA_C1_LAUNCH(T, R, NS)                                                                                  \
+  hipLaunchKernelGGL((conv1x1_stats_kernel<T, R, NS>), grid, block, 0, s, x, w, y, M, K, N, p.gx, p.tiles_per_blk, \
                      part)
   if (p.tnw == 2) {
-    if (wres)
-      RLA_C1_LAUNCH(2, true);
+    if (wbytes <= 16384)
+      RLA_C1_LAUNCH(2, true, 6);
+    else if (wbytes <= 32768)
+      RLA_C1_LAUNCH(2, true, 4);
     else
-      RLA_C1_LAUNCH(2, false);
+      RLA_C1_LAUNCH(2, false, 4);
   } else {
-    if (wres)
-      RLA_C1_LAUNCH(1, true);
+    if (wbytes <= 16384)
+      RLA_C1_LAUNCH(1, true, 6);
+    else if (wbytes <= 32768)
+      RLA_C1_LAUNCH(1, true, 4);
     else
-      RLA_C1_LAUNCH(1, false);
+      RLA_C1_LAUNCH(1, false, 4);
   }
 #undef RLA_C1_LAUNCH
 }
