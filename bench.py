@@ -525,9 +525,6 @@ def make_resnet(args, world, rank, dev, x, y, bucket_mb=None):
             info = {"route": "native-reducer", "bucket_mb": bucket_mb or args.bucket_mb}
         opt = fuse_optimizer(torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5), arena,
                              grad_scale_fn=(lambda: sync_.grad_scale) if sync_ is not None else None)
-        from ray_lightning_accelerators_amd.ops.conv import wgrad_stream_enabled
-
-        info["wgrad_stream"] = wgrad_stream_enabled()  # weight gradients on a side stream
 
         def run(n):
             for _ in range(n):

@@ -266,9 +266,11 @@ bool conv1x1_stats_ok(int64_t M, int K, int N) {
   return M > 0 && K >= 32 && K % 32 == 0 && N >= 64 && N % 64 == 0 && N <= 4096;
 }
 
-Conv1x1Plan conv1x1_stats_plan(int64_t M, int N) {
+Conv1x1Plan conv1x1_stats_plan(int64_t M, int K, int N) {
   Conv1x1Plan p;
   p.tnw = N % 128 == 0 ? 2 : 1;
+  // 64-channel columns where that is what keeps the weight block resident (K <= 256)
+  if (p.tnw == 2 && (int64_t)K * 128 * 2 > 32768 && (int64_t)K * 64 * 2 <= 32768) p.tnw = 1;
   p.gy = N / (64 * p.tnw);
   const int mt = (int)((M + 127) / 128);
   // ~2 resident workgroups per CU over the whole grid; gx a multiple of 8 (XCD deal)

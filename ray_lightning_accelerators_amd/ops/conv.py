@@ -167,62 +167,6 @@ def conv3x3_dgrad_hip(dy: torch.Tensor, wb: torch.Tensor) -> torch.Tensor:
     return dx.permute(0, 3, 1, 2)
 
 
-# ---------------------------------------------------------------- side-stream wgrad
-# A layer's weight gradient and its input gradient are independent: with
-# RLA_WGRAD_STREAM=1 the weight gradient runs on a per-device side stream, forked from
-# the backward's stream at that layer, so it overlaps the rest of the backward chain
-# (the BatchNorm passes, the next layers' input gradients and the launch-bound BN
-# finalizes that leave most CUs idle).  Joins: every gradient records a ready event
-# (looked up by data pointer when ParamArena.gather_grads moves it -- a data-parallel
-# bucket closes mid-backward), and the end of each backward joins the side stream
-# into the backward's stream (queue_callback), so anything after backward() sees
-# finished gradients.  Only for autograd's grad steal (ParamArena steal_grads, grads
-# None before backward): an accumulate into an existing .grad would read too early.
-_side_streams: Dict[int, "torch.cuda.Stream"] = {}
-_ready_events: Dict[int, "torch.cuda.Event"] = {}
-_join = {"task": None}
-side_stats = {"wgrad": 0}
-
-
-def wgrad_stream_enabled() -> bool:
-    return os.environ.get("RLA_WGRAD_STREAM", "0") == "1"
-
-
-def ready_event(t: torch.Tensor):
-    """The side-stream ready event of a weight gradient (popped), or None."""
-    return _ready_events.pop(t.data_ptr(), None) if _ready_events else None
-
-
-def _wgrad_async(fn, *inputs: torch.Tensor) -> torch.Tensor:
-    if not (wgrad_stream_enabled() and inputs[0].is_cuda):
-        return fn()
-    dev = inputs[0].device
-    main = torch.cuda.current_stream(dev)
-    side = _side_streams.get(dev.index)
-    if side is None:
-        side = _side_streams[dev.index] = torch.cuda.Stream(device=dev)
-    side.wait_stream(main)
-    with torch.cuda.stream(side):
-        out = fn()
-    for t in inputs:
-        t.record_stream(side)  # the allocator must not hand their blocks out before side is done
-    out.record_stream(main)
-    ev = torch.cuda.Event()
-    ev.record(side)
-    _ready_events[out.data_ptr()] = ev
-    task = torch._C._current_graph_task_id()  # one join per backward pass
-    if _join["task"] != task:
-        _join["task"] = task
-
-        def join():
-            main.wait_stream(side)
-            _ready_events.clear()
-
-        torch.autograd.Variable._execution_engine.queue_callback(join)
-    side_stats["wgrad"] += 1
-    return out
-
-
 def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
     n, c, h, w = t.shape
     return t.permute(0, 2, 3, 1).reshape(n * h * w, c)
@@ -383,13 +327,12 @@ class _Conv1x1Fn(torch.autograd.Function):
             dx = _fork_dx(fork, lambda: _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
                                                   [True, False, False])[0], None)
         if be_w == "hip":
-            dw = _wgrad_async(lambda: wgrad_hip(dy, x, (1, 1), (1, 1), (0, 0)), dy, x)
+            dw = wgrad_hip(dy, x, (1, 1), (1, 1), (0, 0))
         elif be_w == "gemm":
-            dw = _wgrad_async(lambda: torch.ops.aten.mm.dtype(dy2.t(), x2, torch.float32).view(cout, cin, 1, 1),
-                              dy, x)
+            dw = torch.ops.aten.mm.dtype(dy2.t(), x2, torch.float32).view(cout, cin, 1, 1)
         elif be_w == "miopen":
-            dw = _wgrad_async(lambda: _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
-                                                [False, True, False])[1].float(), dy, x)
+            dw = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                           [False, True, False])[1].float()
         return dx, dw, None, None, None
 
 
@@ -507,9 +450,9 @@ class _ConvNHWCFn(torch.autograd.Function):
             dx = _fork_dx(fork, lambda: _conv_bwd(dy, x, wb, None, list(stride), list(padding), [1, 1], False,
                                                   [0, 0], 1, [True, False, False])[0], None)
         if be == "hip":
-            dw = _wgrad_async(lambda: wgrad_hip(dy, x, (kh, kw), stride, padding), dy, x)
+            dw = wgrad_hip(dy, x, (kh, kw), stride, padding)
         elif be == "hip_gen":
-            dw = _wgrad_async(lambda: wgrad_hip(dy, x, (kh, kw), stride, padding, algo=1), dy, x)
+            dw = wgrad_hip(dy, x, (kh, kw), stride, padding, algo=1)
         return dx, dw, None, None, None, None
 
 

@@ -204,16 +204,7 @@ class ParamArena:
         if not pairs:
             return
         if self.device.type == "cuda":
-            from ..ops.conv import ready_event
             from ..ops.optim import build_copy_table, multi_copy
-
-            # weight gradients still being produced on the side stream (ops.conv
-            # RLA_WGRAD_STREAM): the copy waits for them
-            cur = torch.cuda.current_stream(self.device)
-            for i in moved:
-                ev = ready_event(self.params[i].grad)
-                if ev is not None:
-                    cur.wait_event(ev)
 
             key = tuple(moved) + tuple(s.data_ptr() for s, _ in pairs)
             table = self._tables.get(key)
