@@ -525,6 +525,20 @@ std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t s, int64_t pad) {
   return {y, arg};
 }
 
+// dy [N, C] bf16 -> dx [N, HW, C] bf16 (NHWC rows of a channels_last tensor)
+Tensor gap_bwd(Tensor dy, int64_t HW) {
+  check_dev(dy, "dy", at::kBFloat16);
+  TORCH_CHECK(dy.dim() == 2 && dy.is_contiguous() && dy.size(1) % 8 == 0 && HW > 0, "gap_bwd: dy [N, C], C % 8 == 0");
+  const int64_t N = dy.size(0), C = dy.size(1);
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  Tensor dx = at::empty({N, HW, C}, dy.options());
+  TORCH_CHECK(rla::launch_gap_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                                  reinterpret_cast<uint16_t*>(dx.data_ptr()), (int)N, (int)HW, (int)C,
+                                  cur_stream(dy)) == 0,
+              "gap backward launch failed");
+  return dx;
+}
+
 Tensor maxpool_bwd(Tensor dy, Tensor arg, int64_t H, int64_t W, int64_t k, int64_t s, int64_t pad) {
   check_dev(dy, "dy", at::kBFloat16);
   check_dev(arg, "arg", at::kByte);
@@ -797,6 +811,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_stats", &conv1x1_stats, "1x1 conv forward on MFMA + BatchNorm partial sums of its output");
   m.def("conv1x1_stats_ok", [](int64_t M, int64_t K, int64_t N) { return rla::conv1x1_stats_ok(M, (int)K, (int)N); });
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC bf16 max pool -> (y, one-byte window argmax)");
+  m.def("gap_bwd", &gap_bwd, "global average pool backward over NHWC rows (16-byte stores)");
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max pool backward (gather through the argmax bytes)");
   m.def("bn_bwd_apply", &bn_bwd_apply, "fused BN backward apply: dx (+ dres = relu-masked dy)", py::arg("x"),
         py::arg("y"), py::arg("dy"), py::arg("coef"), py::arg("relu"), py::arg("dx"), py::arg("dres"),

@@ -268,9 +268,9 @@ bool conv1x1_stats_ok(int64_t M, int K, int N) {
 
 Conv1x1Plan conv1x1_stats_plan(int64_t M, int K, int N) {
   Conv1x1Plan p;
+  (void)K;  // one 64-channel column per wave pair only where N needs it: the 32-channel
+            // variant's resident weights did not pay for K = 256 / 512 (profiles/r4_c1)
   p.tnw = N % 128 == 0 ? 2 : 1;
-  // 64-channel columns where that is what keeps the weight block resident (K <= 256)
-  if (p.tnw == 2 && (int64_t)K * 128 * 2 > 32768 && (int64_t)K * 64 * 2 <= 32768) p.tnw = 1;
   p.gy = N / (64 * p.tnw);
   const int mt = (int)((M + 127) / 128);
   // ~2 resident workgroups per CU over the whole grid; gx a multiple of 8 (XCD deal)

@@ -52,6 +52,8 @@ int launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int 
                        int k, int s, int pad, hipStream_t stream);
 int launch_maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int H, int W, int C, int OH,
                        int OW, int k, int s, int pad, hipStream_t stream);
+// global average pool backward over NHWC rows: dx[n][p][c] = dy[n][c] / HW
+int launch_gap_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t stream);
 constexpr int kBnMaxC = 2048;  // 8 channels per thread x 256 threads per row
 
 struct BnPlan {

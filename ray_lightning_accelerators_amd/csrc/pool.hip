@@ -110,7 +110,30 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __rest
   *reinterpret_cast<u16x8*>(dx + t * 8) = __builtin_bit_cast(u16x8, __builtin_convertvector(acc, b8));
 }
 
+// Global average pool backward: dx[n][p][c] = dy[n][c] / HW over NHWC rows, one
+// 16-byte store of 8 channels per thread (autograd's expand + channels_last copy
+// ran as an unvectorised broadcast copy, ~44 us per ResNet-50 step).
+__global__ __launch_bounds__(256) void gap_bwd_kernel(const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx,
+                                                      int N, int HW, int C, float scale) {
+  const int G = C >> 3;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)N * HW * G) return;
+  const int g = (int)(t % G);
+  const int n = (int)(t / ((int64_t)HW * G));
+  const f8 d = ld8(dy + (int64_t)n * C + g * 8) * scale;
+  *reinterpret_cast<u16x8*>(dx + t * 8) = __builtin_bit_cast(u16x8, __builtin_convertvector(d, b8));
+}
+
 }  // namespace
+
+int launch_gap_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t stream) {
+  if (C % 8 || HW < 1) return -1;
+  const int64_t total = (int64_t)N * HW * (C / 8);
+  const int64_t blocks = (total + 255) / 256;
+  if (blocks > 0x7fffffff) return -2;
+  hipLaunchKernelGGL(gap_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, dy, dx, N, HW, C, 1.0f / (float)HW);
+  return 0;
+}
 
 int launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int OH, int OW,
                        int k, int s, int pad, hipStream_t stream) {

@@ -25,7 +25,7 @@ from torch.utils.data import Dataset
 from ..lightning import LightningModule
 from ..ops.bn import BatchNormAct2d
 from ..ops.conv import BNStats, Conv1x1NHWC, GradFork
-from ..ops.pool import MaxPool2dNHWC
+from ..ops.pool import MaxPool2dNHWC, global_avg_pool_nhwc
 from ..ops.shadow import ConvBF16
 
 
@@ -137,6 +137,8 @@ class ResNet(nn.Module):
         x = self.bn1(self.conv1(x))
         x = self.maxpool(x if self.fused_bn else F.relu(x, inplace=True))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        if self.fused_bn:
+            return self.fc(global_avg_pool_nhwc(x))  # NHWC backward kernel (ops/pool.py)
         return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
 
 

@@ -57,3 +57,28 @@ class MaxPool2dNHWC(nn.MaxPool2d):
                 and not self.ceil_mode and not self.return_indices):
             return max_pool2d_nhwc(x, k, s, p)
         return super().forward(x)
+
+
+class _GlobalAvgPoolFn(torch.autograd.Function):
+    """[N, C, H, W] channels_last bf16 -> [N, C]: the mean over H*W (torch's reduce
+    kernel), backward one gfx950 broadcast-store kernel straight into channels_last
+    memory (``gap_bwd``)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        n, c, h, w = x.shape
+        ctx.geom = (n, c, h, w)
+        return x.permute(0, 2, 3, 1).reshape(n, h * w, c).mean(1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, c, h, w = ctx.geom
+        dx = require().gap_bwd(dy.to(torch.bfloat16).contiguous(), h * w)
+        return dx.view(n, h, w, c).permute(0, 3, 1, 2)
+
+
+def global_avg_pool_nhwc(x: torch.Tensor) -> torch.Tensor:
+    """``torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)`` with the NHWC backward kernel."""
+    if _nhwc_ok(x):
+        return _GlobalAvgPoolFn.apply(x)
+    return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

@@ -318,6 +318,27 @@ def test_maxpool_nhwc_matches_torch(shape, k, s, p):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(4, 2048, 7, 7), (3, 64, 5, 9)])
+def test_global_avg_pool_nhwc_matches_torch(shape):
+    """NHWC global average pool (torch mean forward, broadcast-store backward kernel)
+    == flatten(adaptive_avg_pool2d): same output, same channels_last gradient."""
+    from ray_lightning_accelerators_amd.ops.pool import global_avg_pool_nhwc
+
+    torch.manual_seed(3)
+    x = torch.randn(*shape, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xa = x.detach().clone().requires_grad_(True)
+    xb = x.detach().clone().requires_grad_(True)
+    ya = global_avg_pool_nhwc(xa)
+    yb = torch.flatten(F.adaptive_avg_pool2d(xb, 1), 1)
+    assert ya.shape == yb.shape and torch.allclose(ya.float(), yb.float(), rtol=1e-2, atol=1e-3)
+    g = torch.randn_like(yb)
+    ya.backward(g)
+    yb.backward(g)
+    assert xa.grad.is_contiguous(memory_format=torch.channels_last)
+    assert torch.allclose(xa.grad.float(), xb.grad.float(), rtol=1e-2, atol=1e-4)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["gemm", "miopen", "auto"])
 def test_conv1x1_backends_match_fp32(mode, monkeypatch):
     """Conv1x1NHWC's GEMM and MIOpen backends: forward, dgrad and the fp32 wgrad

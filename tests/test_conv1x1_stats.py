@@ -10,14 +10,18 @@ import torch.nn.functional as F
 gpu = pytest.mark.gpu
 
 # (M, K, N): ResNet-50 1x1 shapes at small batch, a pixel tail (M % 128 != 0), a
-# column count that is not a multiple of 128 (one 32-channel block per wave), K = 32
+# column count that is not a multiple of 128 (one 32-channel block per wave), K = 32;
+# together they reach every launch variant (resident weights at 2 or 1 workgroups
+# per CU, streamed weights, 32- and 64-channel wave columns)
 SHAPES = [
     (2 * 56 * 56, 64, 256),
     (2 * 56 * 56, 256, 64),
     (3 * 28 * 28, 512, 128),
     (5 * 7 * 7, 512, 2048),
     (4 * 14 * 14, 1024, 256),
+    (3 * 28 * 28, 128, 512),
     (1000, 64, 192),
+    (300, 1024, 192),
     (77, 32, 64),
 ]
 
