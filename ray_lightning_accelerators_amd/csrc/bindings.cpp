@@ -587,7 +587,7 @@ std::vector<Tensor> conv1x1_stats(Tensor x, Tensor w) {
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
               "conv1x1_stats: 16-byte aligned operands");
   const at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  const rla::Conv1x1Plan p = rla::conv1x1_stats_plan(M, (int)K, (int)N);
+  const rla::Conv1x1Plan p = rla::conv1x1_stats_plan(M, (int)N);
   Tensor y = at::empty({M, N}, x.options());
   Tensor part = at::empty({p.gx, 2, N}, x.options().dtype(at::kFloat));
   rla::launch_conv1x1_stats(reinterpret_cast<const uint16_t*>(x.data_ptr()),

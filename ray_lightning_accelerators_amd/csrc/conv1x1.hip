@@ -266,10 +266,10 @@ bool conv1x1_stats_ok(int64_t M, int K, int N) {
   return M > 0 && K >= 32 && K % 32 == 0 && N >= 64 && N % 64 == 0 && N <= 4096;
 }
 
-Conv1x1Plan conv1x1_stats_plan(int64_t M, int K, int N) {
+Conv1x1Plan conv1x1_stats_plan(int64_t M, int N) {
   Conv1x1Plan p;
-  (void)K;  // one 64-channel column per wave pair only where N needs it: the 32-channel
-            // variant's resident weights did not pay for K = 256 / 512 (profiles/r4_c1)
+  // 32-channel wave columns only where N needs them: choosing them to keep a K = 256 /
+  // 512 weight block resident measured slower (profiles/r4_c1/c1stats_probe_v4_wide.log)
   p.tnw = N % 128 == 0 ? 2 : 1;
   p.gy = N / (64 * p.tnw);
   const int mt = (int)((M + 127) / 128);

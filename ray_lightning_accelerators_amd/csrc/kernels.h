@@ -117,7 +117,7 @@ struct Conv1x1Plan {
   int tiles_per_blk;  // 128-pixel tiles per range
 };
 bool conv1x1_stats_ok(int64_t M, int K, int N);
-Conv1x1Plan conv1x1_stats_plan(int64_t M, int K, int N);
+Conv1x1Plan conv1x1_stats_plan(int64_t M, int N);
 void launch_conv1x1_stats(const uint16_t* x, const uint16_t* w, uint16_t* y, int64_t M, int K, int N,
                           const Conv1x1Plan& p, float* part, hipStream_t s);
 
