@@ -28,11 +28,14 @@
 //     DMA is inline asm, invisible to hipcc's wait bookkeeping, and hipcc would
 //     otherwise drain every in-flight load at each epilogue's stores) and one raw
 //     barrier (cdna_hip_programming.md, pipelining across barriers);
+//   * K <= 128 (the ResNet-50 layers this kernel wins): the workgroup's whole weight
+//     block stays in LDS, DMA'd once ahead of stage 0, and the ring carries x only
+//     (6 stages with a 16 KB block, 4 with 32 KB);
 //   * D of 32x32x16 gives a lane one pixel and 4 consecutive channels per 4
-//     accumulators: 8-byte bf16 stores, and the rounded values go straight into the
-//     lane's per-channel sum / sum of squares; one butterfly over the 32 pixel lanes
-//     and a fixed-order LDS add over the two pixel-half waves at the end
-//     (deterministic);
+//     accumulators; the rounded values go straight into the lane's per-channel sum /
+//     sum of squares, and one v_permlane32_swap per dword pair widens the stores to
+//     16 bytes; one butterfly over the 32 pixel lanes and a fixed-order LDS add over
+//     the two pixel-half waves at the end (deterministic);
 //   * grid: workgroups sharing pixel tiles (same x, all channel columns) run on the
 //     same XCD, so x is read from HBM once and re-read from that XCD's L2.
 // Rows past M read a clamped row (never stored, excluded from the sums); stages past
