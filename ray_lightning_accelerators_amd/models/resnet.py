@@ -68,11 +68,10 @@ class Bottleneck(nn.Module):
     def _conv_bn(conv, bn, x, **kw):
         """bn(conv(x)) for a 1x1 conv: the conv may compute bn's batch statistics in its
         epilogue (ops.conv.BNStats; bn then skips its partial pass over the output)."""
+        fork = kw.pop("fork", None)
         if isinstance(conv, Conv1x1NHWC) and bn.training:
             st = BNStats()
-            y = conv(x, fork=kw.pop("fork", None), bn_stats=st)
-            return bn(y, bn_stats=st, **kw)
-        fork = kw.pop("fork", None)
+            return bn(conv(x, fork=fork, bn_stats=st), bn_stats=st, **kw)
         return bn(conv(x, fork=fork) if fork is not None else conv(x), **kw)
 
     def forward(self, x):
