@@ -574,6 +574,32 @@ void bn_apply(Tensor x, Tensor scale, Tensor shift, optional<Tensor> res, bool r
                        cur_stream(x), ptr_or_null<int64_t>(nbt_inc, "num_batches_tracked", at::kLong, 1));
 }
 
+// conv1x1 input gradient + the previous BatchNorm's backward partial (csrc/conv1x1.hip
+// BWD): dy1 [M, K], wt [N, K] (the weight transposed), dy2 / yb / xb [M, N]; returns
+// (d [M, N] bf16, part [rows, 2, N] fp32 for bn_bwd_finalize)
+std::vector<Tensor> conv1x1_bn_bwd(Tensor dy1, Tensor wt, Tensor dy2, Tensor yb, Tensor xb) {
+  for (const Tensor* t : {&dy1, &wt, &dy2, &yb, &xb}) {
+    check_dev(*t, "conv1x1_bn_bwd operand", at::kBFloat16);
+    TORCH_CHECK(t->dim() == 2 && t->is_contiguous() && reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                "conv1x1_bn_bwd: contiguous 16-byte aligned 2-D operands");
+  }
+  const int64_t M = dy1.size(0), K = dy1.size(1), N = wt.size(0);
+  TORCH_CHECK(wt.size(1) == K, "conv1x1_bn_bwd: wt must be [N, K]");
+  for (const Tensor* t : {&dy2, &yb, &xb})
+    TORCH_CHECK(t->size(0) == M && t->size(1) == N, "conv1x1_bn_bwd: dy2 / yb / xb must be [M, N]");
+  TORCH_CHECK(rla::conv1x1_bn_bwd_ok(M, (int)K, (int)N), "conv1x1_bn_bwd: unsupported shape (K <= 128)");
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(dy1.device());
+  int rows = 0;
+  rla::launch_conv1x1_bn_bwd(nullptr, nullptr, nullptr, M, (int)K, (int)N, nullptr, nullptr, nullptr, nullptr, &rows,
+                             cur_stream(dy1));
+  Tensor d = at::empty({M, N}, dy1.options());
+  Tensor part = at::empty({rows, 2, N}, dy1.options().dtype(at::kFloat));
+  auto u = [](const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); };
+  rla::launch_conv1x1_bn_bwd(u(dy1), u(wt), reinterpret_cast<uint16_t*>(d.data_ptr()), M, (int)K, (int)N, u(dy2),
+                             u(yb), u(xb), part.data_ptr<float>(), &rows, cur_stream(dy1));
+  return {d, part};
+}
+
 // 1x1 conv forward with BatchNorm partial sums: x [M, K] (NHWC rows), w [N, K], both
 // bf16 contiguous; returns (y [M, N] bf16, part [gx, 2, N] fp32 for bn_finalize)
 std::vector<Tensor> conv1x1_stats(Tensor x, Tensor w) {
@@ -809,6 +835,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_apply", &bn_apply, "fused BN apply: y = act(x*scale + shift (+res))", py::arg("x"), py::arg("scale"),
         py::arg("shift"), py::arg("res"), py::arg("relu"), py::arg("y"), py::arg("nbt_inc") = py::none());
   m.def("conv1x1_stats", &conv1x1_stats, "1x1 conv forward on MFMA + BatchNorm partial sums of its output");
+  m.def("conv1x1_bn_bwd", &conv1x1_bn_bwd,
+        "1x1 conv input gradient fused with the previous BatchNorm's backward partial -> (d, part)");
+  m.def("conv1x1_bn_bwd_ok", [](int64_t M, int64_t K, int64_t N) { return rla::conv1x1_bn_bwd_ok(M, (int)K, (int)N); });
   m.def("conv1x1_stats_ok", [](int64_t M, int64_t K, int64_t N) { return rla::conv1x1_stats_ok(M, (int)K, (int)N); });
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC bf16 max pool -> (y, one-byte window argmax)");
   m.def("gap_bwd", &gap_bwd, "global average pool backward over NHWC rows (16-byte stores)");

@@ -67,12 +67,24 @@ __device__ __forceinline__ void c1_dma16(const void* gsrc, uint32_t lds) {
                : "memory");
 }
 
-template <int TNW, bool WRES, int NS>
+// BWD: the same GEMM as an input gradient (x = the conv's output gradient dy1 [M][K],
+// w = its weight transposed [N = Cin][K = Cout]) whose epilogue is the PREVIOUS
+// BatchNorm's backward partial pass: with da = bf16(dy1 . W) for block-output pixel m
+// and channel c, d = (da + dy2) * (yb > 0) -- dy2 the folded residual gradient, yb
+// that BatchNorm's (ReLU) output -- is written once (bf16) in place of da, and the
+// partial row sums d and d * xb (xb the BatchNorm's input), bn_partial_kernel<1>'s
+// layout.  da is never written or re-read (ops/conv.py, fuse_bn_dgrad).  dy2 / yb / xb
+// for a tile are loaded at its first stage, two stages ahead of the epilogue.
+template <int TNW, bool WRES, int NS, bool BWD = false>
 __global__ __launch_bounds__(kC1Threads, 2) void conv1x1_stats_kernel(const uint16_t* __restrict__ x,
                                                                       const uint16_t* __restrict__ w,
                                                                       uint16_t* __restrict__ y, int64_t M, int K,
                                                                       int N, int gx, int tiles_per_blk,
-                                                                      float* __restrict__ part) {
+                                                                      float* __restrict__ part,
+                                                                      const uint16_t* __restrict__ dy2 = nullptr,
+                                                                      const uint16_t* __restrict__ yb = nullptr,
+                                                                      const uint16_t* __restrict__ xb = nullptr) {
+  static_assert(!BWD || TNW == 1, "the backward epilogue's prefetch is sized for 32-channel wave columns");
   constexpr int BN = 64 * TNW;                      // workgroup channels
   constexpr int kXBytes = 4 * 128 * 16;             // x part of a stage: [4 k units][128 rows] x 16 B
   constexpr int kStageBytes = kXBytes + (WRES ? 0 : 4 * BN * 16);
@@ -163,6 +175,22 @@ __global__ __launch_bounds__(kC1Threads, 2) void conv1x1_stats_kernel(const uint
   };
 
   const int cw = nb + wn * 32 * TNW;  // wave's first channel
+  // BWD: dy2 / yb / xb of a tile's [2 pixel blocks][2 channel halves] 16-byte chunks
+  u32x4 pre[3][2][2];
+  auto prefetch = [&](int ti) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      int64_t m = (int64_t)(t0 + ti) * 128 + wm * 64 + 32 * j + r;
+      m = m < M ? m : M - 1;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int64_t off = m * N + cw + 16 * p + 8 * h;
+        pre[0][j][p] = *reinterpret_cast<const u32x4*>(dy2 + off);
+        pre[1][j][p] = *reinterpret_cast<const u32x4*>(yb + off);
+        pre[2][j][p] = *reinterpret_cast<const u32x4*>(xb + off);
+      }
+    }
+  };
   // D[n][m]: lane -> pixel r of block j; accumulator 4q + e -> channel 8q + 4h + e.
   // Stores: one v_permlane32_swap per dword of each channel-group pair (q, q + 1)
   // gives lane h channels 16p + 8h .. +8 -- one 16-byte store where the MFMA layout
@@ -182,7 +210,7 @@ __global__ __launch_bounds__(kC1Threads, 2) void conv1x1_stats_kernel(const uint
           bf16x4 b;
 #pragma unroll
           for (int e = 0; e < 4; ++e) b[e] = (__bf16)acc[t][j][4 * q + e];
-          if (ok) {
+          if (!BWD && ok) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               const float f = (float)b[e];
@@ -199,7 +227,26 @@ __global__ __launch_bounds__(kC1Threads, 2) void conv1x1_stats_kernel(const uint
           const auto s0 = __builtin_amdgcn_permlane32_swap(v[2 * p][0], v[2 * p + 1][0], false, false);
           const auto s1 = __builtin_amdgcn_permlane32_swap(v[2 * p][1], v[2 * p + 1][1], false, false);
           const u32x4 o = {s0[0], s1[0], s0[1], s1[1]};
-          if (ok) *reinterpret_cast<u32x4*>(yo + 32 * t + 16 * p) = o;
+          if (BWD) {  // channels cw + 16p + 8h .. +8 of pixel m: the BatchNorm backward partial
+            const bf16x8 da = __builtin_bit_cast(bf16x8, o);
+            const bf16x8 g2 = __builtin_bit_cast(bf16x8, pre[0][j][p]);
+            const bf16x8 ym = __builtin_bit_cast(bf16x8, pre[1][j][p]);
+            const bf16x8 xm = __builtin_bit_cast(bf16x8, pre[2][j][p]);
+            bf16x8 dd;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const float a = (float)ym[k] > 0.f ? (float)da[k] + (float)g2[k] : 0.f;
+              dd[k] = (__bf16)a;
+              if (ok) {
+                const float f = (float)dd[k];
+                ssum[0][8 * p + k] += f;
+                ssq[0][8 * p + k] += f * (float)xm[k];
+              }
+            }
+            if (ok) *reinterpret_cast<bf16x8*>(yo + 16 * p) = dd;
+          } else if (ok) {
+            *reinterpret_cast<u32x4*>(yo + 32 * t + 16 * p) = o;
+          }
         }
       }
 #pragma unroll
@@ -221,8 +268,9 @@ __global__ __launch_bounds__(kC1Threads, 2) void conv1x1_stats_kernel(const uint
     // then every wave's part is in and every wave has finished reading buffer st - 1
     asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"((NS - 2) * kDma) : "memory");
     issue(st + NS - 1);
-    compute(st);
     const int ti = st / nch;
+    if (BWD && st == ti * nch) prefetch(ti);  // the tile's first stage
+    compute(st);
     if (st - ti * nch == nch - 1) epilogue(ti);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup's LDS
@@ -240,7 +288,8 @@ __global__ __launch_bounds__(kC1Threads, 2) void conv1x1_stats_kernel(const uint
         b += __shfl_xor(b, o);
       }
       if (r == 0) {
-        const int c = wn * 32 * TNW + 32 * t + 8 * (e >> 2) + 4 * h + (e & 3);
+        const int c = BWD ? wn * 32 + 16 * (e >> 3) + 8 * h + (e & 7)
+                          : wn * 32 * TNW + 32 * t + 8 * (e >> 2) + 4 * h + (e & 3);
         red[wm][0][c] = a;
         red[wm][1][c] = b;
       }
@@ -311,6 +360,31 @@ void launch_conv1x1_stats(const uint16_t* x, const uint16_t* w, uint16_t* y, int
       RLA_C1_LAUNCH(1, false, 4);
   }
 #undef RLA_C1_LAUNCH
+}
+
+bool conv1x1_bn_bwd_ok(int64_t M, int K, int N) {
+  return M > 0 && K >= 32 && K % 32 == 0 && K <= 128 && N >= 64 && N % 64 == 0 && N <= 4096;
+}
+
+void launch_conv1x1_bn_bwd(const uint16_t* dy1, const uint16_t* wt, uint16_t* d, int64_t M, int K, int N,
+                           const uint16_t* dy2, const uint16_t* yb, const uint16_t* xb, float* part, int* rows,
+                           hipStream_t s) {
+  Conv1x1Plan p = conv1x1_stats_plan(M, N);
+  if (p.tnw != 1) {  // 32-channel wave columns: the epilogue prefetch's register budget
+    p.tnw = 1;
+    p.gy = N / 64;
+    const int mt = (int)((M + 127) / 128);
+    int want = 2 * c1_cu_count() / p.gy;
+    if (want < 8) want = 8;
+    if (want > mt) want = mt;
+    p.tiles_per_blk = (mt + want - 1) / want;
+    const int gx = (mt + p.tiles_per_blk - 1) / p.tiles_per_blk;
+    p.gx = (gx + 7) / 8 * 8;
+  }
+  *rows = p.gx;
+  if (part == nullptr) return;  // size query
+  hipLaunchKernelGGL((conv1x1_stats_kernel<1, true, 6, true>), dim3(p.gx * p.gy), dim3(kC1Threads), 0, s, dy1, wt, d,
+                     M, K, N, p.gx, p.tiles_per_blk, part, dy2, yb, xb);
 }
 
 }  // namespace rla

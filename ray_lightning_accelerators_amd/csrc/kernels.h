@@ -120,6 +120,13 @@ bool conv1x1_stats_ok(int64_t M, int K, int N);
 Conv1x1Plan conv1x1_stats_plan(int64_t M, int N);
 void launch_conv1x1_stats(const uint16_t* x, const uint16_t* w, uint16_t* y, int64_t M, int K, int N,
                           const Conv1x1Plan& p, float* part, hipStream_t s);
+// input gradient of a 1x1 conv (dy1 [M][K] . W, wt = W^T [N][K]) fused with the previous
+// BatchNorm's backward partial: d = (da + dy2) * (yb > 0) written to d, part [rows, 2, N]
+// = sums of d and d * xb.  part == nullptr: only *rows is set (the partial row count).
+bool conv1x1_bn_bwd_ok(int64_t M, int K, int N);
+void launch_conv1x1_bn_bwd(const uint16_t* dy1, const uint16_t* wt, uint16_t* d, int64_t M, int K, int N,
+                           const uint16_t* dy2, const uint16_t* yb, const uint16_t* xb, float* part, int* rows,
+                           hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // Fused MNIST-MLP training step (784 -> L1 -> L2 -> 10, ReLU, log_softmax+NLL).

@@ -63,6 +63,11 @@ class Bottleneck(nn.Module):
         self.conv3 = _conv1x1(width, cout, fused=fused_bn)
         self.bn3 = _bn(cout, fused_bn)  # fused: relu(bn3(x) + identity) in one pass
         self.downsample = downsample
+        if fused_bn and downsample is None and isinstance(self.conv1, Conv1x1NHWC):
+            # identity block: x (the previous bn3's output) reaches autograd only through
+            # conv1 -- the shortcut's gradient is folded into bn3 -- so conv1's input
+            # gradient may compute the previous bn3's backward partial (ops/conv.py)
+            self.conv1.fuse_bn_dgrad = True
 
     @staticmethod
     def _conv_bn(conv, bn, x, **kw):

@@ -68,11 +68,13 @@ def fused_ok(x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> bool:
 class _FoldSlot:
     """Hand-off of a consumer layer's residual gradient to the producer of that residual."""
 
-    __slots__ = ("dres", "claimed")
+    __slots__ = ("dres", "claimed", "x3", "bwd_part")
 
     def __init__(self):
         self.dres = None
         self.claimed = False
+        self.x3 = None        # this layer's input, for a consumer conv fusing our backward partial
+        self.bwd_part = None  # that conv's partial sums of d (ops.conv fuse_bn_dgrad)
 
 
 fold_stats = {"folded": 0}
@@ -106,6 +108,8 @@ class _BNActFn(torch.autograd.Function):
                      nbt if pending else None)
         ctx.relu, ctx.has_res, ctx.group, ctx.count = relu, residual is not None, group, count
         ctx.slot, ctx.sink = slot, sink
+        if slot is not None and relu and residual is not None and group is None:
+            slot.x3 = x  # a 1x1 conv reading y may compute our backward partial (ops/conv.py)
         # ReLU without a residual: the backward recomputes the mask x*scale+shift > 0
         # from the stats (one stream less to read in both backward passes); with a
         # residual the mask needs the sum, so y is kept
@@ -129,9 +133,15 @@ class _BNActFn(torch.autograd.Function):
             fold_stats["folded"] += 1
         # residual layer: dres is the masked incoming gradient d itself -- the partial
         # pass writes it, and the apply pass reads x and d only (csrc/bn_act.hip, WD)
-        dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
-        part = mod.bn_partial(xv, yv, dyv, C, 1, ctx.relu, None, dy2, ss,
-                              _nhwc(dres) if dres is not None else None)
+        fused = ctx.slot.bwd_part if ctx.slot is not None else None
+        if fused is not None:
+            # the consumer 1x1 conv's input-gradient kernel already produced d (= dy here)
+            # and its partial sums (ops/conv.py fuse_bn_dgrad)
+            ctx.slot.bwd_part, part, dres = None, fused, dy
+        else:
+            dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
+            part = mod.bn_partial(xv, yv, dyv, C, 1, ctx.relu, None, dy2, ss,
+                                  _nhwc(dres) if dres is not None else None)
         local = None
         if ctx.group is not None:
             local = mod.bn_bwd_finalize(part, ctx.count, weight, mean, invstd)  # local dgamma / dbeta

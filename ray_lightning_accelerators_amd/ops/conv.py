@@ -31,7 +31,7 @@ from torch import nn
 
 _choice: Dict[Tuple[str, int, int, int], str] = {}
 _timings: Dict[Tuple[str, int, int, int], Dict[str, float]] = {}
-stats = {"fast": 0, "fallback": 0}
+stats = {"fast": 0, "fallback": 0, "bn_dgrad_fused": 0}
 
 _conv = torch.ops.aten.convolution
 _conv_bwd = torch.ops.aten.convolution_backward
@@ -134,6 +134,13 @@ def conv3x3_ok(x: torch.Tensor, wb: torch.Tensor, stride, padding) -> bool:
     cout = wb.size(0)
     return (cin % 64 == 0 and cout % 64 == 0 and wb.is_contiguous(memory_format=torch.channels_last)
             and _conv3x3_shape_ok(n, h, w, cin, cout))
+
+
+@functools.lru_cache(maxsize=256)
+def _bn_bwd_shape_ok(m: int, k: int, n: int) -> bool:
+    from . import require
+
+    return bool(require().conv1x1_bn_bwd_ok(m, k, n))
 
 
 @functools.lru_cache(maxsize=256)
@@ -246,6 +253,16 @@ def conv1x1_stats_hip(x: torch.Tensor, wb: torch.Tensor):
     return _from2d(y2, n, h, w), part
 
 
+def fuse_bn_dgrad_enabled() -> bool:
+    """A 1x1 conv marked ``fuse_bn_dgrad`` (ResNet's identity-block conv1, whose input
+    y is a residual BatchNorm+ReLU's output with no other autograd consumer: the
+    identity shortcut's gradient is folded) computes that BatchNorm's backward partial
+    in its input-gradient kernel (csrc/conv1x1.hip BWD): d = (dx + dy2) * (y > 0) is
+    written once and the plain input gradient is never materialised.
+    ``RLA_FUSE_BN_DGRAD=0`` turns it off (same-box A/B: +0.5 %, profiles/r4_c1)."""
+    return os.environ.get("RLA_FUSE_BN_DGRAD", "1") == "1"
+
+
 def _bn_partial(y: torch.Tensor) -> torch.Tensor:
     from . import require
 
@@ -254,7 +271,7 @@ def _bn_partial(y: torch.Tensor) -> torch.Tensor:
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, shadow=None, fork=None, bn_stats=None):
+    def forward(ctx, x, weight, shadow=None, fork=None, bn_stats=None, fuse_bn=False):
         n, cin, h, w = x.shape
         cout = weight.size(0)
         # the arena's bf16 shadow (ops/shadow.py) when there is one: no cast kernel
@@ -286,6 +303,12 @@ class _Conv1x1Fn(torch.autograd.Function):
         ctx.fork = fork
         if fork is not None:
             fork.users += 1
+        # x is a residual BatchNorm+ReLU's output (its fold slot carries that layer's
+        # input): the input gradient may absorb the BatchNorm's backward partial
+        fold = getattr(x, "_rla_fold", None)
+        ctx.fold = fold if (fuse_bn and fork is None and fold is not None and getattr(fold, "x3", None) is not None
+                            and fuse_bn_dgrad_enabled()
+                            and _bn_bwd_shape_ok(x2.size(0), cout, cin)) else None
         return y
 
     @staticmethod
@@ -299,7 +322,20 @@ class _Conv1x1Fn(torch.autograd.Function):
         dx = dw = None
         be_d = be_w = None
         fork = ctx.fork if ctx.needs_input_grad[0] else None
-        if fork is not None and fork.users >= 2 and fork.dx is not None:
+        fold = ctx.fold
+        if fold is not None and fold.dres is not None and ctx.needs_input_grad[0]:
+            # d = (dy . W + dres_next) * (x > 0) and its BatchNorm partial sums in one
+            # kernel; the producer BatchNorm's backward takes d as its dy
+            from . import require
+            from .bn import fold_stats
+
+            d2, part = require().conv1x1_bn_bwd(dy2, wb.t().contiguous(), _nhwc2d(fold.dres), x2,
+                                                _nhwc2d(fold.x3))
+            fold.dres, fold.bwd_part = None, part
+            fold_stats["folded"] += 1
+            stats["bn_dgrad_fused"] += 1
+            dx = _from2d(d2, n, h, w)
+        elif fork is not None and fork.users >= 2 and fork.dx is not None:
             # second of a forked pair: dx += dy . W in the GEMM itself (beta = 1)
             dx = _fork_dx(fork, None, lambda d: _acc_dgrad(d, dy2, wb))
         elif ctx.needs_input_grad[0]:
@@ -320,7 +356,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         if be_d == "miopen" and be_w == "miopen" and fork is None:
             # both from MIOpen: one call (its host cost is tens of us per call)
             dx, dw = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, True, False])[:2]
-            return dx, dw.float(), None, None, None
+            return dx, dw.float(), None, None, None, None
         if be_d == "gemm":
             dx = _fork_dx(fork, lambda: _from2d(torch.mm(dy2, wb), n, h, w), None)
         elif be_d == "miopen":
@@ -333,7 +369,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         elif be_w == "miopen":
             dw = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
                            [False, True, False])[1].float()
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
 def fast_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
@@ -351,6 +387,9 @@ class Conv1x1NHWC(nn.Conv2d):
 
     def __init__(self, in_channels: int, out_channels: int, device=None, dtype=None):
         super().__init__(in_channels, out_channels, 1, 1, 0, bias=False, device=device, dtype=dtype)
+        # set by a model whose structure makes this layer its input's only autograd
+        # consumer (see fuse_bn_dgrad_enabled)
+        self.fuse_bn_dgrad = False
 
     def forward(self, x: torch.Tensor, fork: Optional[GradFork] = None,
                 bn_stats: Optional[BNStats] = None) -> torch.Tensor:
@@ -362,7 +401,7 @@ class Conv1x1NHWC(nn.Conv2d):
             stats["fast"] += 1
             from .shadow import bf16_weight
 
-            return _Conv1x1Fn.apply(x, self.weight, bf16_weight(self.weight), fork, bn_stats)
+            return _Conv1x1Fn.apply(x, self.weight, bf16_weight(self.weight), fork, bn_stats, self.fuse_bn_dgrad)
         stats["fallback"] += 1
         return F.conv2d(x, self.weight)
 

@@ -133,3 +133,65 @@ def test_resnet_bottleneck_routes_stats(monkeypatch):
     assert int(blk.bn1.num_batches_tracked) == int(blk.bn3.num_batches_tracked) == 1
     assert int(down[1].num_batches_tracked) == 1
     assert torch.isfinite(x.grad.float()).all()
+
+
+@gpu
+@pytest.mark.parametrize("shape", [(2 * 56 * 56, 64, 256), (3 * 28 * 28, 128, 512), (1000, 32, 192), (77, 64, 64)])
+def test_conv1x1_bn_bwd_matches_reference(shape):
+    """Input gradient + previous BatchNorm backward partial in one kernel: d against
+    bf16((bf16(dy1 . W) + dy2) * (yb > 0)) from an fp32 GEMM (one bf16 ulp where the
+    GEMM's fp32 sums round differently), the partial sums against fp64 sums of the
+    kernel's own d."""
+    from ray_lightning_accelerators_amd import ops
+
+    m, k, n = shape
+    torch.manual_seed(3)
+    dev = torch.device("cuda", 0)
+    dy1 = torch.randn(m, k, device=dev).to(torch.bfloat16)
+    w = (torch.randn(k, n, device=dev) / k ** 0.5).to(torch.bfloat16)  # conv weight [Cout = k, Cin = n]
+    dy2 = torch.randn(m, n, device=dev).to(torch.bfloat16)
+    yb = torch.randn(m, n, device=dev).to(torch.bfloat16).clamp_min(0)  # a ReLU output (zeros included)
+    xb = torch.randn(m, n, device=dev).to(torch.bfloat16)
+    d, part = ops.require().conv1x1_bn_bwd(dy1, w.t().contiguous(), dy2, yb, xb)
+    da = (dy1.float() @ w.float()).to(torch.bfloat16)
+    ref = ((da.float() + dy2.float()) * (yb.float() > 0)).to(torch.bfloat16)
+    assert d.shape == (m, n) and d.dtype == torch.bfloat16
+    assert _rel(d, ref.float()) < 8e-3, _rel(d, ref.float())
+    assert torch.equal(d == 0, ref == 0) or bool(((d == 0) != (ref == 0)).float().mean() < 1e-3)
+    s = part.double().sum(0)
+    dd = d.double()
+    assert torch.allclose(s[0], dd.sum(0), rtol=1e-4, atol=1e-3 * m ** 0.5)
+    assert torch.allclose(s[1], (dd * xb.double()).sum(0), rtol=1e-4, atol=1e-3 * m ** 0.5)
+
+
+@gpu
+def test_fused_bn_dgrad_resnet_layer_matches(monkeypatch):
+    """ResNet-50 layer1 (three bottlenecks, two identity shortcuts) with the fused conv1
+    input gradient + bn3 backward partial: the same loss and gradients as the unfused
+    step (the GEMM rounds differently: bf16-level tolerances)."""
+    from ray_lightning_accelerators_amd.models.resnet import resnet50
+    from ray_lightning_accelerators_amd.ops import conv as C
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    full = resnet50(num_classes=10, fused_bn=True).to(dev).to(memory_format=torch.channels_last)
+    layer = full.layer1
+    x0 = torch.randn(4, 64, 32, 32, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("RLA_FUSE_BN_DGRAD", fuse)
+        layer.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        n0 = C.stats["bn_dgrad_fused"]
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = layer(x)
+        y.float().square().mean().backward()
+        assert C.stats["bn_dgrad_fused"] - n0 == (2 if fuse == "1" else 0)  # the two identity blocks' conv1
+        outs.append((y.detach().float(), x.grad.float(),
+                     [p.grad.detach().float().clone() for p in layer.parameters()]))
+    (y0, g0, p0), (y1, g1, p1) = outs
+    assert torch.equal(y0, y1)
+    assert _rel(g1, g0) < 2e-2, _rel(g1, g0)
+    for a, b in zip(p1, p0):
+        assert _rel(a, b) < 3e-2, _rel(a, b)
+
