@@ -63,6 +63,24 @@ def test_resnet_fused_flag_same_parameters():
     assert sum(p.numel() for p in resnet50().parameters()) == RESNET50_PARAMS
 
 
+def test_resnet_marks_only_identity_conv1_for_bn_dgrad_fusion():
+    """Only identity blocks' conv1 may fuse the previous bn3's backward partial (their
+    input has no other autograd consumer); downsample blocks (forked input) and the
+    unfused model never do.  CPU: the training forward still matches with the flags."""
+    from ray_lightning_accelerators_amd.models.resnet import Bottleneck, resnet50
+    from ray_lightning_accelerators_amd.ops.conv import Conv1x1NHWC
+
+    m = resnet50(10, fused_bn=True)
+    flags = [(blk.downsample is None, blk.conv1.fuse_bn_dgrad) for blk in m.modules() if isinstance(blk, Bottleneck)]
+    assert len(flags) == 16 and all(ident == fuse for ident, fuse in flags)
+    assert sum(fuse for _, fuse in flags) == 12
+    assert not any(getattr(c, "fuse_bn_dgrad", False) for c in resnet50(10).modules() if isinstance(c, Conv1x1NHWC))
+    m.train()
+    y = m(torch.randn(2, 3, 32, 32))
+    y.sum().backward()
+    assert all(p.grad is not None for p in m.parameters())
+
+
 # ------------------------------------------------------------------------- GPU
 SHAPES = [(4, 64, 16, 16), (2, 256, 7, 7), (3, 2048, 3, 3), (8, 24, 5, 5), (64, 64, 28, 28)]
 
