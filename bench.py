@@ -538,7 +538,7 @@ def make_resnet(args, world, rank, dev, x, y, bucket_mb=None):
                     sync_.finish()
                 opt.step()
                 opt.zero_grad()
-                state["loss"] = loss
+                state["loss"] = loss.detach()  # (a live autograd graph must not outlive the step)
 
         if args.resnet_graph:
             # the whole training step (forward, backward, gradient gather, fused SGD)
@@ -874,6 +874,14 @@ class _EpochClock(Callback):
     def on_train_end(self, trainer, pl_module):
         self._mark(trainer, "train_end")
         self._resolve()
+        replicas_equal = None
+        arena = getattr(trainer.accelerator_backend, "arena", None)
+        if arena is not None and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            # data-parallel replicas after the fit: bitwise-equal parameters on every rank
+            cs = float(arena.data.double().sum()) + 1e-3 * float(arena.data.double().abs().sum())
+            sums = [None] * dist.get_world_size()
+            dist.all_gather_object(sums, cs)
+            replicas_equal = all(v == sums[0] for v in sums)
         starts = [t for _, n, t in self.marks if n in ("epoch_start", "train_end")]
         secs = torch.tensor([b - a for a, b in zip(starts, starts[1:])], dtype=torch.float64)
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
@@ -901,6 +909,10 @@ class _EpochClock(Callback):
                            "batches": int(trainer.num_training_batches),
                            "val_batches": [int(v) for v in trainer.num_val_batches],
                            "fused": trainer._fused is not None,
+                           "graph_step": (trainer._fused.describe() if hasattr(trainer._fused, "describe") else
+                                          trainer._graph_step_reason),
+                           "replicas_equal": replicas_equal,
+                           "train_loss": float(trainer.callback_metrics.get("train_loss", float("nan"))),
                            "val_loss": float(trainer.callback_metrics.get("ptl/val_loss", float("nan"))),
                            "val_accuracy": float(trainer.callback_metrics.get("ptl/val_accuracy", float("nan"))),
                            "best_model_path": getattr(trainer.checkpoint_callback, "best_model_path", None)}, f)
@@ -915,14 +927,24 @@ def run_trainer(args):
     from ray_lightning_accelerators_amd import runtime as ray
     from ray_lightning_accelerators_amd.models.mnist import MNISTClassifier
 
-    if args.model != "mnist" or args.impl != "native":
-        raise SystemExit("--via trainer runs MNISTClassifier on the framework path")
+    if args.impl != "native":
+        raise SystemExit("--via trainer runs the framework path (--impl native)")
+    rn = args.model == "resnet50"
     gpu = args.device == "cuda"
     env = rank_env()
     out_path = tempfile.mktemp(prefix="rla-bench-", suffix=".json")
     clock = _EpochClock(out_path, trace=os.environ.get("RLA_BENCH_TRACE") == "1")
-    model = MNISTClassifier({"layer_1": args.layer_1, "layer_2": args.layer_2, "lr": args.lr,
-                             "batch_size": args.batch_size})
+    if rn:
+        # BASELINE config 5 through the framework: LightningResNet50 on the resident
+        # synthetic ImageNet set (`--steps` batches per rank and epoch), the whole step
+        # captured by the Trainer (lightning/graph_step.py), a checkpoint every epoch
+        from ray_lightning_accelerators_amd.models.resnet import LightningResNet50
+
+        model = LightningResNet50({"batch_size": args.batch_size, "n_train": args.batch_size * args.steps * args.gpus,
+                                   "lr": 0.1})
+    else:
+        model = MNISTClassifier({"layer_1": args.layer_1, "layer_2": args.layer_2, "lr": args.lr,
+                                 "batch_size": args.batch_size})
     root = tempfile.mkdtemp(prefix="rla-bench-trainer-")
     started = False
     if env is not None:
@@ -944,7 +966,8 @@ def run_trainer(args):
         launch = "ray-actors"
     try:
         trainer = pl.Trainer(default_root_dir=root, max_epochs=args.trainer_epochs, gpus=int(gpu),
-                             progress_bar_refresh_rate=0, callbacks=[clock], accelerator=acc)
+                             progress_bar_refresh_rate=0, callbacks=[clock], accelerator=acc,
+                             benchmark=bool(args.benchmark_algos))
         t0 = time.perf_counter()
         if os.environ.get("RLA_SYNC_DEBUG") == "1" and gpu:
             _sync_debug()  # report every implicit host<->device sync of an in-process fit
@@ -978,21 +1001,23 @@ def run_trainer(args):
     per_epoch = nb * args.batch_size * world
     med = statistics.median(steady)
     value = per_epoch * len(steady) / sum(steady)
+    if rn:
+        base = RESNET_STOCK_BASELINE["torch-graph"] * world
     return {
-        "metric": METRIC + " (Trainer.fit wall-clock incl. validation + checkpointing)",
+        "metric": (RESNET_METRIC if rn else METRIC) + " (Trainer.fit wall-clock incl. validation + checkpointing)",
         "value": round(value, 1),
-        "unit": "samples/s",
+        "unit": "images/s" if rn else "samples/s",
         "n_gpus": world,
         "steps": nb * len(steady),
         "warmup": nb,
         "ms_per_step": round(sum(steady) / (nb * len(steady)) * 1e3, 5),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": None,
+        "vs_baseline": round(value / base, 3) if rn and gpu else None,
         "dtype": "bf16" if gpu else "fp32",
-        "data": "synthetic",
+        "data": "synthetic" + (" (resident on the device)" if rn else ""),
         "config": {
-            "model": f"MNISTClassifier(784-{args.layer_1}-{args.layer_2}-10)",
+            "model": "ResNet-50" if rn else f"MNISTClassifier(784-{args.layer_1}-{args.layer_2}-10)",
             "global_batch": args.batch_size * world,
             "per_gpu_batch": args.batch_size,
             "seq_len": None,
@@ -1004,7 +1029,10 @@ def run_trainer(args):
             "val_batches_per_epoch": rows["val_batches"],
             "checkpointing": True,
             "fused_step": rows["fused"],
+            "graph_step": rows.get("graph_step"),
         },
+        "replicas_equal": rows.get("replicas_equal"),
+        "train_loss": rows.get("train_loss"),
         "epoch_wall_s": [round(v, 5) for v in epochs],
         "epoch_clock": rows.get("clock", "host"),
         "epoch_split": rows["split"],

@@ -33,6 +33,7 @@ _CHOICES = {
     "allreduce_algo": ("auto", "oneshot", "twoshot", "rccl", "torch"),
     "precision": ("32", "bf16"),
     "pg_backend": ("auto", "nccl", "gloo"),
+    "hip_graph_step": ("auto", "on", "off"),
 }
 
 # legacy env names kept working (first release used these spellings)
@@ -66,6 +67,13 @@ class RLAConfig:
     fused_dp: bool = True
     # capture the resident MNIST step into hipGraphs
     use_hip_graph: bool = True
+    # Trainer: capture an autograd LightningModule's whole training step (forward,
+    # backward, gradient all-reduce, fused optimizer) in one hipGraph and replay it
+    # (lightning/graph_step.py).  auto = when the module sets hip_graph_step = True;
+    # on = every module (host-reading steps still fall back); off = never
+    hip_graph_step: str = "auto"
+    # eager warm-up steps before the capture (allocator pools, MIOpen find, autotune)
+    hip_graph_warmup: int = 3
     # ModelCheckpoint writes run in a writer PROCESS (state snapshot taken
     # synchronously into shared memory; pickling, file write and rename off this
     # process; the Trainer drains the writes before fit() returns).  Round 2's

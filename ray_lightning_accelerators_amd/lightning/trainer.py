@@ -159,6 +159,7 @@ class Trainer:
         self.log_every_n_steps = log_every_n_steps
         self.resume_from_checkpoint = resume_from_checkpoint
         self.deterministic = deterministic
+        self.benchmark = bool(benchmark)  # torch.backends.cudnn.benchmark on the workers (MIOpen find)
         self.num_nodes = num_nodes
         self.sync_batchnorm = sync_batchnorm
         self.replace_sampler_ddp = replace_sampler_ddp
@@ -222,6 +223,8 @@ class Trainer:
         self.interrupted = False
         self._has_val_loop = False
         self._fused = None
+        self._graph_step_reason: Optional[str] = None
+        self._log_sink: Optional[list] = None  # GraphedTrainStep records self.log calls here
         self._pending_log = None
         self._staged_logs: List[dict] = []  # deferred log rows whose host copy is in flight
         self._log_dir: Optional[str] = None
@@ -443,6 +446,8 @@ class Trainer:
         """Everything after process-group bring-up and device placement (runs on every worker)."""
         model.trainer = self
         self.model = model
+        if self.benchmark and torch.cuda.is_available():
+            torch.backends.cudnn.benchmark = True  # PL 1.1: Trainer(benchmark=True)
         self.call_setup_hook(model)
         mark("setup_hook_done", rank=self.global_rank)
         self._prepare_dataloaders(model)
@@ -473,10 +478,16 @@ class Trainer:
         return None
 
     def _maybe_fused(self, model: LightningModule):
-        """Model-provided fused training step (e.g. MNISTClassifier's single HIP launch)."""
+        """Model-provided fused training step (e.g. MNISTClassifier's single HIP launch),
+        else the graph-captured autograd step when the module opts in
+        (``lightning/graph_step.py``)."""
         want = self.fused_step
-        if want is False or not hasattr(model, "configure_fused_step"):
+        if want is False:
             return None
+        if not hasattr(model, "configure_fused_step"):
+            from .graph_step import maybe_graph_step
+
+            return maybe_graph_step(self, model)
         if self.accumulate_grad_batches != 1 or self.gradient_clip_val:
             return None
         try:
@@ -563,6 +574,12 @@ class Trainer:
     def _log_metric(self, module, name, value, prog_bar=False, logger=True, on_step=None, on_epoch=None,
                     sync_dist=False, sync_dist_op="mean") -> None:
         fx = self._current_fx or "training_step"
+        if self._log_sink is not None:
+            # graph-captured step: recorded, replayed per step from the device ring
+            self._log_sink.append((name, value, dict(prog_bar=prog_bar, logger=logger, on_step=on_step,
+                                                     on_epoch=on_epoch, sync_dist=sync_dist,
+                                                     sync_dist_op=sync_dist_op), fx))
+            return
         training = fx.startswith("training")
         if on_step is None:
             on_step = training
@@ -882,6 +899,8 @@ class Trainer:
             if prof is not None:
                 prof.disable()
                 self._dump_profile(prof, prof_path)
+        # every rank, before a checkpoint callback may dump on rank 0 only
+        self._consolidate_optimizer_state()
         self.call_hook("on_train_end")
         self.call_hook("on_fit_end")
         if self.logger is not None:
@@ -955,6 +974,13 @@ class Trainer:
             cb.on_train_epoch_end(self, model, epoch_outputs)
         model.on_train_epoch_end(epoch_outputs)
         self._update_lr_schedulers("epoch")
+        if not self._has_val_loop:
+            # PL 1.1 TrainLoop.run_training_epoch: with no validation loop
+            # (should_train_only) the checkpoint callbacks run at every training-epoch
+            # end (check_checkpoint_callback -> ModelCheckpoint.on_validation_end)
+            self._consolidate_optimizer_state()
+            for cb in self.checkpoint_callbacks:
+                cb.on_validation_end(self, model)
         if not validated:
             self._flush_logger()
         self._check_collectives()
@@ -1113,7 +1139,6 @@ class Trainer:
         return False
 
     def _train_batch(self, model: LightningModule, batch, batch_idx: int, is_last: bool):
-        acc = self.accelerator_backend
         self.call_hook("on_batch_start")
         r = model.on_train_batch_start(batch, batch_idx, 0)
         for cb in self.callbacks:
@@ -1124,16 +1149,10 @@ class Trainer:
         self.profiler.start("run_training_batch")
         if self._fused is not None:
             out = self._fused.train_batch(batch, batch_idx)
-            self.global_step += 1
-        else:
-            batch = acc.batch_to_device(batch)
-            out = None
-            for opt_idx, opt in enumerate(self.optimizers or [None]):
-                out = self._optimizer_step_for(model, batch, batch_idx, opt_idx, opt, is_last)
-            accumulate_done = ((batch_idx + 1) % self.accumulate_grad_batches == 0) or is_last
-            if accumulate_done:
+            if not getattr(self._fused, "counts_steps", False):
                 self.global_step += 1
-                self._update_lr_schedulers("step")
+        else:
+            out = self._autograd_step(batch, batch_idx, is_last)
         self.profiler.stop("run_training_batch")
         for cb in self.callbacks:
             cb.on_train_batch_end(self, model, out, batch, batch_idx, 0)
@@ -1141,6 +1160,20 @@ class Trainer:
         self.call_hook("on_batch_end")
         if self.global_step % max(1, self.log_every_n_steps) == 0:
             self._flush_logger()
+        return out
+
+    def _autograd_step(self, batch, batch_idx: int, is_last: bool = False):
+        """The eager autograd step of one batch (every optimizer), step counting and
+        step-interval LR schedulers included."""
+        model = self.get_model()
+        batch = self.accelerator_backend.batch_to_device(batch)
+        out = None
+        for opt_idx, opt in enumerate(self.optimizers or [None]):
+            out = self._optimizer_step_for(model, batch, batch_idx, opt_idx, opt, is_last)
+        accumulate_done = ((batch_idx + 1) % self.accumulate_grad_batches == 0) or is_last
+        if accumulate_done:
+            self.global_step += 1
+            self._update_lr_schedulers("step")
         return out
 
     def _optimizer_step_for(self, model, batch, batch_idx, opt_idx, opt, is_last):
@@ -1209,6 +1242,8 @@ class Trainer:
     def _optimizer_state_dict(self, opt, staged: bool = False):
         if self._fused is not None and hasattr(self._fused, "optimizer_state_dict"):
             return self._fused.optimizer_state_dict()
+        if hasattr(opt, "sync_host_state"):
+            opt.sync_host_state()  # graph replays advance only the host group counters
         if (self._fused is not None and hasattr(self._fused, "sync_optimizer_state")
                 and getattr(self, "_opt_state_synced_step", None) != self.global_step):
             # fused data-parallel step with the owner protocol: every element's Adam
@@ -1226,6 +1261,7 @@ class Trainer:
         every rank reaches), so a checkpoint dump on only some ranks needs none."""
         if (getattr(self, "world_size", 1) > 1 and self._fused is not None
                 and hasattr(self._fused, "sync_optimizer_state") and self.training
+                and getattr(self, "_opt_state_synced_step", None) != self.global_step
                 and any(hasattr(cb, "best_model_path") or "Checkpoint" in type(cb).__name__
                         for cb in self.callbacks)):
             self._fused.sync_optimizer_state()
@@ -1274,6 +1310,7 @@ class Trainer:
     def __getstate__(self):
         d = self.__dict__.copy()
         d["_fused"] = None
+        d["_log_sink"] = None
         d["_pending_log"] = None
         d["_ckpt_writer"] = None
         d["_deferred"] = None

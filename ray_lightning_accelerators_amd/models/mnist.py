@@ -25,11 +25,12 @@ from typing import Any, Dict, Optional
 
 import torch
 import torch.nn.functional as F
-from torch.utils.data import DataLoader, DistributedSampler, RandomSampler, SequentialSampler, Subset, random_split
+from torch.utils.data import DataLoader, DistributedSampler, SequentialSampler, Subset, random_split
 
 from ..config import get_config
 from ..lightning import LightningModule
 from ..lightning.metrics import Accuracy
+from ..lightning.sampling import deterministic_sampler, sampler_order
 from ..ops import fused_mlp
 from .data import SyntheticMNIST
 
@@ -124,52 +125,10 @@ def _u8_source(dataset):
     return None
 
 
-def _deterministic_sampler(sampler) -> bool:
-    """True when every epoch iterates the sampler in the same order."""
-    if isinstance(sampler, DistributedSampler):
-        return not sampler.shuffle
-    return isinstance(sampler, SequentialSampler)
-
-
-def _sampler_order(sampler) -> torch.Tensor:
-    """The sampler's epoch order as an int64 tensor.  DistributedSampler /
-    RandomSampler(no replacement) / SequentialSampler orders are rebuilt with
-    tensor ops (bit-identical to iterating them: same generator draws), not a
-    55K-element Python list per epoch; anything else is iterated."""
-    n = None
-    if isinstance(sampler, DistributedSampler):
-        n = len(sampler.dataset)
-        if sampler.shuffle:
-            g = torch.Generator()
-            g.manual_seed(sampler.seed + sampler.epoch)
-            idx = torch.randperm(n, generator=g)
-        else:
-            idx = torch.arange(n)
-        total = sampler.total_size
-        if not sampler.drop_last:
-            pad = total - n
-            if pad > 0:
-                idx = torch.cat([idx, idx.repeat(-(-pad // n))[:pad]])
-        else:
-            idx = idx[:total]
-        return idx[sampler.rank:total:sampler.num_replicas].contiguous()
-    if isinstance(sampler, SequentialSampler):
-        return torch.arange(len(sampler.data_source))
-    if type(sampler) is RandomSampler and not sampler.replacement:
-        # torch.utils.data.RandomSampler.__iter__ without replacement: the same
-        # global-RNG seed draw (when no generator is set) and the same randperm calls
-        n = len(sampler.data_source)
-        if sampler.generator is None:
-            seed = int(torch.empty((), dtype=torch.int64).random_().item())
-            generator = torch.Generator()
-            generator.manual_seed(seed)
-        else:
-            generator = sampler.generator
-        m = sampler.num_samples
-        parts = [torch.randperm(n, generator=generator) for _ in range(m // n)]
-        parts.append(torch.randperm(n, generator=generator)[: m % n])
-        return torch.cat(parts)
-    return torch.as_tensor(list(iter(sampler)), dtype=torch.int64)
+# the sampler-order helpers live in lightning/sampling.py (shared with the
+# graph-captured autograd step); the old private names stay importable
+_deterministic_sampler = deterministic_sampler
+_sampler_order = sampler_order
 
 
 # rows of the engine's per-step (loss, correct, count, step) ring: two MNIST epochs at

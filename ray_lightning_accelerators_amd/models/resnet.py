@@ -15,6 +15,7 @@ MI355X choices:
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import torch
@@ -155,8 +156,18 @@ def resnet50(num_classes: int = 1000, zero_init_residual: bool = False, fused_bn
 RESNET50_PARAMS = 25_557_032
 
 
+_RESIDENT: dict = {}  # (spec, device) -> device columns, per process (recycled workers reuse them)
+
+
 class SyntheticImageNet(Dataset):
-    """Random images / labels of ImageNet shape, generated per index (deterministic)."""
+    """Random images / labels of ImageNet shape, generated per index (deterministic).
+
+    ``resident_tensors(device)`` is the GPU data path (``lightning/sampling.py``):
+    the whole set generated once -- the SAME per-index values ``__getitem__``
+    returns, on a thread pool -- and held in HBM as a channels_last image tensor
+    plus int64 labels (3,200 images at 224 px = 1.9 GB of 288 GB).  The
+    graph-captured Trainer step then gathers each batch on the device from the
+    DistributedSampler order: no per-image CPU ``randn``, no pageable H2D copy."""
 
     def __init__(self, length: int = 1281, image_size: int = 224, num_classes: int = 1000, seed: int = 0):
         self.length, self.size, self.nc, self.seed = length, image_size, num_classes, seed
@@ -168,17 +179,56 @@ class SyntheticImageNet(Dataset):
         g = torch.Generator().manual_seed(self.seed * 1_000_003 + i)
         return torch.randn(3, self.size, self.size, generator=g), int(torch.randint(0, self.nc, (1,), generator=g))
 
+    def resident_tensors(self, device) -> List[torch.Tensor]:
+        device = torch.device(device)
+        key = (self.length, self.size, self.nc, self.seed, str(device))
+        cols = _RESIDENT.get(key)
+        if cols is not None:
+            return cols
+        from concurrent.futures import ThreadPoolExecutor
+
+        n, s = self.length, self.size
+        host = torch.empty(n, s, s, 3, pin_memory=device.type == "cuda")  # NHWC rows
+        labels = torch.empty(n, dtype=torch.int64)
+
+        def fill(lo_hi):
+            for i in range(*lo_hi):
+                x, y = self[i]
+                host[i].copy_(x.permute(1, 2, 0))
+                labels[i] = y
+
+        workers = max(1, min(8, (os.cpu_count() or 1), n // 64 or 1))
+        step = -(-n // workers)
+        with ThreadPoolExecutor(workers) as ex:
+            list(ex.map(fill, [(a, min(n, a + step)) for a in range(0, n, step)]))
+        x = host.to(device, non_blocking=True).permute(0, 3, 1, 2)  # [N, 3, S, S] channels_last
+        y = labels.to(device, non_blocking=True)
+        if device.type == "cuda":
+            torch.cuda.current_stream(device).synchronize()  # the pinned source is freed below
+        _RESIDENT.clear()  # one resident set per process
+        _RESIDENT[key] = [x, y]
+        return _RESIDENT[key]
+
 
 class LightningResNet50(LightningModule):
-    """ResNet-50 as a LightningModule (SGD momentum, cross-entropy), for RayAccelerator runs."""
+    """ResNet-50 as a LightningModule (SGD momentum, cross-entropy) -- BASELINE.json
+    config 5 through ``RayAccelerator`` + ``Trainer.fit``.
+
+    ``hip_graph_step = True``: the Trainer captures the whole training step
+    (forward, backward, DDP bucket all-reduce, fused SGD) in one hipGraph and
+    replays it (``lightning/graph_step.py``); with the resident synthetic set the
+    batches are gathered on the device inside that graph.  Parameters are
+    channels_last (NHWC convolutions on MFMA, no per-use weight re-layout)."""
+
+    hip_graph_step = True
 
     def __init__(self, config: Optional[dict] = None):
         super().__init__()
         cfg = dict(lr=0.1, momentum=0.9, weight_decay=5e-5, batch_size=64, num_classes=1000,
-                   image_size=224, n_train=512, fused_bn=True)
+                   image_size=224, n_train=512, fused_bn=True, num_workers=0)
         cfg.update(config or {})
         self.cfg = cfg
-        self.model = resnet50(cfg["num_classes"], fused_bn=cfg["fused_bn"])
+        self.model = resnet50(cfg["num_classes"], fused_bn=cfg["fused_bn"]).to(memory_format=torch.channels_last)
 
     def forward(self, x):
         return self.model(x)
@@ -200,4 +250,5 @@ class LightningResNet50(LightningModule):
         from torch.utils.data import DataLoader
 
         ds = SyntheticImageNet(self.cfg["n_train"], self.cfg["image_size"], self.cfg["num_classes"])
-        return DataLoader(ds, batch_size=self.cfg["batch_size"], num_workers=0)
+        return DataLoader(ds, batch_size=self.cfg["batch_size"], num_workers=self.cfg["num_workers"],
+                          drop_last=True)

@@ -47,6 +47,18 @@ class _GroupState:
         else:
             self.buf = torch.zeros(n, device=dev)
         self.step = 0
+        # device scalars (enable_device_scalars): the step counter and learning rate
+        # the kernel reads at run time, so one captured step replays correctly
+        self.step_t: Optional[torch.Tensor] = None
+        self.lr_t: Optional[torch.Tensor] = None
+        self.lr_host: Optional[float] = None
+
+    def sync_lr(self, lr: float) -> None:
+        """Refresh the device learning rate when the host value changed (a scheduler
+        step): one fill kernel, stream-ordered before the next step."""
+        if self.lr_t is not None and lr != self.lr_host:
+            self.lr_t.fill_(lr)
+            self.lr_host = lr
 
 
 def fuse_optimizer(opt: torch.optim.Optimizer, arena: ParamArena,
@@ -82,11 +94,20 @@ def fuse_optimizer(opt: torch.optim.Optimizer, arena: ParamArena,
             p = arena.data[gs.start:gs.end]
             gr = arena.grad[gs.start:gs.end]
             gs.step += 1
+            step, lr_t = gs.step, None
+            if gs.step_t is not None:
+                # device scalars: the counter advances on the stream (inside a captured
+                # step too), the kernel reads it and the learning rate at run time
+                if gs.step_t.device.type != "cuda" or not torch.cuda.is_current_stream_capturing():
+                    gs.sync_lr(float(g["lr"]))
+                gs.step_t.add_(1)
+                # (CPU: never captured -- the host value, in the reference's double precision)
+                step, lr_t = gs.step_t, (gs.lr_t if gs.lr_t.is_cuda else None)
             if gs.kind == "adam":
                 b1, b2 = g["betas"]
                 fused_adam_(p, gr, gs.m, gs.v, lr=float(g["lr"]), betas=(b1, b2), eps=g["eps"],
                             weight_decay=g["weight_decay"], grad_scale=scale, adamw=adamw,
-                            maximize=g.get("maximize", False), step=gs.step)
+                            maximize=g.get("maximize", False), step=step, lr_tensor=lr_t)
                 for q in g["params"]:
                     st = self.state.get(q)
                     if st is not None and "step" in st:
@@ -95,7 +116,7 @@ def fuse_optimizer(opt: torch.optim.Optimizer, arena: ParamArena,
                 fused_sgd_(p, gr, gs.buf if g.get("momentum", 0) != 0 else None, lr=float(g["lr"]),
                            momentum=g.get("momentum", 0.0), dampening=g.get("dampening", 0.0),
                            weight_decay=g.get("weight_decay", 0.0), nesterov=g.get("nesterov", False),
-                           maximize=g.get("maximize", False), grad_scale=scale, step=gs.step,
+                           maximize=g.get("maximize", False), grad_scale=scale, step=step, lr_tensor=lr_t,
                            p_bf16=arena.bf16[gs.start:gs.end] if arena.bf16 is not None else None)
             if gs.kind == "adam" and arena.bf16 is not None:
                 arena.bf16[gs.start:gs.end].copy_(p)  # Adam path: shadow refreshed by one cast
@@ -125,6 +146,29 @@ def fuse_optimizer(opt: torch.optim.Optimizer, arena: ParamArena,
                     b_v.copy_(st["momentum_buffer"].reshape(p.shape))
                     gs.step = max(gs.step, 1)
                     self.state[p] = {"momentum_buffer": b_v}
+        for gs in groups:
+            if gs.step_t is not None:
+                gs.step_t.fill_(gs.step)
+
+    def enable_device_scalars(self):
+        """Step counter and learning rate as device scalars (graph-captured steps:
+        ``lightning/graph_step.py``).  The host ``step`` keeps counting too."""
+        for g, gs in zip(self.param_groups, groups):
+            if gs.step_t is None:
+                gs.step_t = torch.full((1,), gs.step, dtype=torch.int64, device=arena.device)
+                gs.lr_t = torch.full((1,), float(g["lr"]), dtype=torch.float32, device=arena.device)
+                gs.lr_host = float(g["lr"])
+
+    def sync_host_state(self):
+        """Per-parameter ``state[p]["step"]`` (Adam) from the host counters, which a
+        graph replay advances without touching the per-parameter tensors."""
+        for g, gs in zip(self.param_groups, groups):
+            if gs.kind != "adam":
+                continue
+            for q in g["params"]:
+                st = self.state.get(q)
+                if st is not None and "step" in st and float(st["step"]) != float(gs.step):
+                    st["step"].fill_(float(gs.step))
 
     # keep torch's LR-scheduler bookkeeping happy (it wraps optimizer.step)
     step._wrapped_by_lr_sched = True
@@ -138,6 +182,8 @@ def fuse_optimizer(opt: torch.optim.Optimizer, arena: ParamArena,
     opt.step = types.MethodType(counted_step, opt)
     opt.zero_grad = types.MethodType(zero_grad, opt)
     opt.load_state_dict = types.MethodType(load_state_dict, opt)
+    opt.enable_device_scalars = types.MethodType(enable_device_scalars, opt)
+    opt.sync_host_state = types.MethodType(sync_host_state, opt)
     opt._rla_fused = True
     opt._rla_groups = groups
     return opt

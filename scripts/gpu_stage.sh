@@ -128,6 +128,15 @@ for st in "$@"; do
       ASAN_OPTIONS=detect_leaks=1:abort_on_error=0:halt_on_error=1:protect_shadow_gap=0 \
       LSAN_OPTIONS=suppressions=$R/scripts/sanitizers/lsan.supp:print_suppressions=0 \
       UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 run selftest_asan_w2 300 ./build/comm_selftest_asan 2 ;;
+    graphstep)  # Trainer-level graph-captured autograd step: tests + config 5 through Trainer.fit
+      run pytest_graph 600 $PYT tests/test_graph_step.py
+      run rn50_trainer 900 python -u bench.py --via trainer --model resnet50 --steps 20 --trainer-epochs 4
+      run rn50_engine 600 python bench.py --model resnet50 --steps 30 --warmup 10 ;;
+    rn50trainer)
+      run rn50_trainer 900 python -u bench.py --via trainer --model resnet50 --steps 20 --trainer-epochs 4 ;;
+    rn50share2)  # config 5 through Trainer.fit, 2 ranks sharing the GPU (graph-captured DP step)
+      RLA_BENCH_SHARE_GPU=1 run rn50_share2_trainer 900 python -u bench.py --via trainer --model resnet50 --gpus 2 \
+        --steps 10 --trainer-epochs 3 ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac
 done

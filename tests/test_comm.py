@@ -135,10 +135,16 @@ def _gpu_worker(rank, world, port, q, mode):
             # 32 Mi floats = 128 MiB: above the two-shot region -> region-sized launches
             sizes = [1, 2, 7, 64, 1000, 4096 + 3, 65536, 262147, 1 << 20, (1 << 21) + 5, 8 << 20,
                      (20 << 20) + 12, 32 << 20]
+            if world >= 8:  # eight ranks time-slice one device: one region-sized size is enough
+                sizes = sizes[:-1]
             for n in sizes:
                 base = (torch.arange(n, device=dev, dtype=torch.float32) % 31) - 15
                 want = base * (world * (world + 1) / 2)
-                if n > comm.twoshot_capacity:
+                if world == 1:
+                    # world 1: every path is the identity (no peers, no region)
+                    res.setdefault("big_routes", []).append(comm.route(base))
+                    paths = ["router", "bf16_routed"]
+                elif n > comm.twoshot_capacity:
                     res.setdefault("big_routes", []).append(comm.route(base))
                     paths = ["router", "bf16_routed"]
                 else:
@@ -592,13 +598,22 @@ def test_xgmi_twoshot_allreduce(world):
 
 
 @gpu
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
 def test_comm_correctness_matrix(world):
+    """worlds 1 / 2 / 4 / 8 x {one-shot, two-shot fp32, two-shot
+    bf16 wire, router} x 4 B ... 128 MiB, every rank-class (NW) instance of the xGMI
+    kernels; ranks share the one device (IPC of uncached regions, same code path)."""
     out = _run_gpu("matrix", world=world)
+    assert len(out) == world
     for r, res in out.items():
+        assert isinstance(res, dict), (r, res)
+        if world == 1:
+            assert set(res["big_routes"]) == {"none"} and not res["bad"], (r, res)
+            continue
         assert res["xgmi"] and res["twoshot"], (r, res)
         assert not res["bad"], (r, res["bad"][:10])
-        assert res["big_routes"] == ["twoshot", "twoshot"], (r, res["big_routes"])  # no RCCL: chunked two-shot
+        n_big = 1 if world >= 8 else 2
+        assert res["big_routes"] == ["twoshot"] * n_big, (r, res["big_routes"])  # no RCCL: chunked two-shot
 
 
 @gpu
