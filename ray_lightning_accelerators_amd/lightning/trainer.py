@@ -982,7 +982,13 @@ class Trainer:
             for cb in self.checkpoint_callbacks:
                 cb.on_validation_end(self, model)
         if not validated:
-            self._flush_logger()
+            if self.on_gpu and self.logger is not None and self.is_global_zero and torch.cuda.is_available():
+                # rows go out asynchronously (one batched copy, written once it landed):
+                # no host sync at the end of an epoch without validation either
+                self._flush_logger(defer=True)
+                self._stage_pending_log()
+            else:
+                self._flush_logger()
         self._check_collectives()
         mark("epoch_end", epoch=self.current_epoch)
 

@@ -7,6 +7,7 @@ import logging
 import os
 import random
 import sys
+import time
 import tempfile
 from functools import wraps
 from typing import Any, Optional
@@ -160,10 +161,33 @@ def _writer_main(conn) -> None:  # pragma: no cover - runs in the writer process
     import pickle
     from multiprocessing import shared_memory
 
+    import threading
+
     # a forked writer must not enter a parallel region: the parent's OpenMP pool
     # threads do not exist in the child (an intra-op parallel copy would wait on them)
     torch.set_num_threads(1)
-    conn.send(("ready", None))
+    lock = threading.Lock()
+    busy = threading.Event()
+
+    def send(m):
+        with lock:
+            conn.send(m)
+
+    def beat():
+        # while a request is in progress, a "beat" every BEAT_S: a large checkpoint on
+        # a slow filesystem is busy, not stalled (the trainer's stall timer
+        # restarts at every message)
+        while True:
+            busy.wait()
+            time.sleep(ProcessCheckpointWriter.BEAT_S)
+            if busy.is_set():
+                try:
+                    send(("beat", None))
+                except (OSError, EOFError, BrokenPipeError):
+                    return
+
+    threading.Thread(target=beat, daemon=True, name="rla-ckpt-writer-beat").start()
+    send(("ready", None))
     while True:
         try:
             msg = conn.recv()
@@ -171,6 +195,7 @@ def _writer_main(conn) -> None:  # pragma: no cover - runs in the writer process
             return
         op = msg[0]
         err = None
+        busy.set()
         try:
             if op == "save":
                 _, skel, metas, shm_name, filepath = msg
@@ -194,12 +219,16 @@ def _writer_main(conn) -> None:  # pragma: no cover - runs in the writer process
                         os.remove(msg[1])
                     except OSError:
                         pass
+            elif op == "sleep":  # test hook: a long request (heartbeat test)
+                time.sleep(float(msg[1]))
             elif op == "exit":
-                conn.send(("done", None))
+                busy.clear()
+                send(("done", None))
                 return
         except BaseException as e:  # noqa: BLE001 - reported to the trainer
             err = repr(e)
-        conn.send(("done", err))
+        busy.clear()
+        send(("done", err))
 
 
 class ProcessCheckpointWriter:
@@ -214,13 +243,18 @@ class ProcessCheckpointWriter:
     the first save (``spawn``: a fresh interpreter, never a fork of a process that
     holds a GPU context); files are identical to ``atomic_save``'s."""
 
-    def __init__(self):
+    def __init__(self, force_spawn: bool = False):
+        self._start(force_spawn)
+        self._pending = []  # (shared-memory block or None, request) of unacknowledged requests
+        self._err: Optional[str] = None
+
+    def _start(self, force_spawn: bool) -> None:
         import multiprocessing as mp
 
         # fork (instant: torch is already imported) only while this process holds no
         # GPU context; otherwise spawn a fresh interpreter (~1-2 s until ready())
         torch_mod = sys.modules.get("torch")
-        gpu_ctx = torch_mod is not None and torch_mod.cuda.is_initialized()
+        gpu_ctx = force_spawn or (torch_mod is not None and torch_mod.cuda.is_initialized())
         if not gpu_ctx:
             from ..utils import warmup
 
@@ -236,18 +270,17 @@ class ProcessCheckpointWriter:
         self._proc = ctx.Process(target=_writer_main, args=(child,), daemon=True, name="rla-ckpt-writer")
         self._proc.start()
         child.close()
-        self._pending = []  # (shared-memory block or None, request) of unacknowledged requests
-        self._err: Optional[str] = None
         self._ready = False
         self._dead = False
+        self._started_at = time.monotonic()
 
     def ready(self) -> bool:
         """The writer finished starting (interpreter + torch import, ~1-2 s)."""
-        if not self._ready and self._proc.is_alive() and self._conn.poll():
+        while not self._ready and self._proc.is_alive() and self._conn.poll():
             try:
                 self._ready = self._conn.recv()[0] == "ready"
             except EOFError:
-                pass
+                break
         return self._ready
 
     def alive(self) -> bool:
@@ -255,17 +288,29 @@ class ProcessCheckpointWriter:
 
     # a writer silent this long while requests are pending is declared stuck: it is
     # killed and the pending requests are completed in this process (a Tune sweep
-    # once hung here for good, profiles/r4_tune/cfg4_recycle_stalled_run.log)
+    # once hung here for good, profiles/r4_tune/cfg4_recycle_stalled_run.log).  A busy
+    # writer sends a "beat" every BEAT_S, so only true silence counts; its start-up
+    # (a spawned interpreter importing torch on a loaded box) gets STARTUP_S
     STALL_S = 20.0
+    BEAT_S = 1.0
+    STARTUP_S = 180.0
 
     def _recv(self, block: bool):
-        """The writer's next message, or None (non-blocking and nothing there); raises
-        EOFError when the writer died or stayed silent past STALL_S."""
-        if not block:
-            return self._conn.recv() if self._conn.poll() else None
-        if not self._conn.poll(self.STALL_S):
-            raise EOFError("checkpoint writer process stalled")
-        return self._conn.recv()
+        """The writer's next message (heartbeats skipped), or None (non-blocking and
+        nothing there); raises EOFError when the writer died or stayed silent past
+        STALL_S (STARTUP_S before its ready message)."""
+        while True:
+            if not block:
+                if not self._conn.poll():
+                    return None
+            else:
+                limit = self.STALL_S if self._ready else max(
+                    self.STALL_S, self.STARTUP_S - (time.monotonic() - self._started_at))
+                if not self._conn.poll(limit):
+                    raise EOFError("checkpoint writer process stalled")
+            msg = self._conn.recv()
+            if msg[0] != "beat":
+                return msg
 
     def _reap(self, block: bool) -> None:
         try:
@@ -299,10 +344,23 @@ class ProcessCheckpointWriter:
         try:
             self._proc.terminate()
             self._proc.join(timeout=5)
+            if self._proc.is_alive():
+                self._proc.kill()
+                self._proc.join(timeout=5)
         except Exception:  # noqa: BLE001
             pass
         self._dead = True
         pending, self._pending = self._pending, []
+        if self._proc.is_alive():
+            # never replay while the old writer may still finish a rename: a replayed
+            # removal could race its save and resurrect a deleted top-k file
+            for shm, _req in pending:
+                if shm is not None:
+                    shm.close()
+                    shm.unlink()
+            if self._err is None:
+                self._err = f"checkpoint writer process {self._proc.pid} could not be stopped"
+            return
         for shm, req in pending:
             try:
                 if req is not None and req[0] == "save":
@@ -320,6 +378,16 @@ class ProcessCheckpointWriter:
                 if shm is not None:
                     shm.close()
                     shm.unlink()
+        # a fresh writer for the saves to come (spawned: safe from any thread, and
+        # this process may hold a GPU context); until it is ready, saves queue on it
+        try:
+            self._conn.close()
+        except Exception:  # noqa: BLE001
+            pass
+        try:
+            self._start(force_spawn=True)
+        except Exception:  # noqa: BLE001 - no writer: later saves run in-process
+            self._dead = True
 
     def save(self, checkpoint: Any, filepath: str) -> None:
         import pickle

@@ -68,16 +68,17 @@ def fused_ok(x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> bool:
 class _FoldSlot:
     """Hand-off of a consumer layer's residual gradient to the producer of that residual."""
 
-    __slots__ = ("dres", "claimed", "x3", "bwd_part")
+    __slots__ = ("dres", "claimed", "x3", "bwd_part", "bwd_d")
 
     def __init__(self):
         self.dres = None
         self.claimed = False
         self.x3 = None        # this layer's input, for a consumer conv fusing our backward partial
         self.bwd_part = None  # that conv's partial sums of d (ops.conv fuse_bn_dgrad)
+        self.bwd_d = None     # the d those sums are of (the tensor the conv returned as our dy)
 
 
-fold_stats = {"folded": 0}
+fold_stats = {"folded": 0, "fused_rejected": 0}
 
 
 class _BNActFn(torch.autograd.Function):
@@ -134,6 +135,15 @@ class _BNActFn(torch.autograd.Function):
         # residual layer: dres is the masked incoming gradient d itself -- the partial
         # pass writes it, and the apply pass reads x and d only (csrc/bn_act.hip, WD)
         fused = ctx.slot.bwd_part if ctx.slot is not None else None
+        if fused is not None:
+            # the conv's partial sums are of ITS d: valid only when that tensor arrives
+            # here unchanged -- another autograd consumer of our output (a hook, a
+            # feature tap) makes autograd pass d + g instead, and the partial pass then
+            # runs over the sum (dres is already inside d, so no dy2: ADVICE r4)
+            d_ref, ctx.slot.bwd_d = ctx.slot.bwd_d, None
+            if d_ref is None or d_ref.data_ptr() != dy.data_ptr() or d_ref.shape != dy.shape:
+                ctx.slot.bwd_part, fused = None, None
+                fold_stats["fused_rejected"] += 1
         if fused is not None:
             # the consumer 1x1 conv's input-gradient kernel already produced d (= dy here)
             # and its partial sums (ops/conv.py fuse_bn_dgrad)

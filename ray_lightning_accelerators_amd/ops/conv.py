@@ -335,6 +335,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             fold_stats["folded"] += 1
             stats["bn_dgrad_fused"] += 1
             dx = _from2d(d2, n, h, w)
+            fold.bwd_d = dx  # bn backward checks it receives exactly this tensor
         elif fork is not None and fork.users >= 2 and fork.dx is not None:
             # second of a forked pair: dx += dy . W in the GEMM itself (beta = 1)
             dx = _fork_dx(fork, None, lambda d: _acc_dgrad(d, dy2, wb))

@@ -152,13 +152,22 @@ class GradSynchronizer:
                     # no RCCL (ranks sharing a device): a broadcast as the device-side
                     # xGMI allreduce of rank 0's values and everyone else's zeros --
                     # exact, and capturable in the step's hipGraph (a gloo broadcast
-                    # of a device tensor is a host round trip)
-                    f = flat if dtype == torch.float32 else flat.to(torch.float32)  # counters: exact < 2^24
+                    # of a device tensor is a host round trip).  fp32 / bf16 / fp16
+                    # travel as fp32 values (exact); any other dtype (int64 counters,
+                    # fp64) as its raw 16-bit words, each an exact fp32 integer
+                    # 0..65535 -- no value is rounded
+                    if dtype in (torch.float32, torch.bfloat16, torch.float16):
+                        f = flat if dtype == torch.float32 else flat.to(torch.float32)
+                    else:
+                        f = (flat.view(torch.int16).to(torch.int32) & 0xFFFF).to(torch.float32)
                     if dist.get_rank() != 0:
                         f.zero_()
                     comm.allreduce_(f)
-                    if f is not flat:
-                        flat.copy_(f)
+                    if dtype in (torch.float32, torch.bfloat16, torch.float16):
+                        if f is not flat:
+                            flat.copy_(f)
+                    else:
+                        flat.view(torch.int16).copy_(f.to(torch.int32).to(torch.int16))
                 else:
                     dist.broadcast(flat, 0, group=self.pg)
             else:

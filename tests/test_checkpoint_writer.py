@@ -134,7 +134,8 @@ def test_process_checkpoint_writer_matches_atomic_save(tmp_path):
 def test_stalled_writer_process_is_taken_over(tmp_path, monkeypatch):
     """A writer process that stops answering (the Tune config-4 rehearsal once hung on
     it for good) is killed after STALL_S and its queued saves / removals complete in
-    the training process, in order; later saves keep working without it."""
+    the training process, in order, only once the old process is gone; a fresh
+    writer process takes the later saves (respawned, not dead for good)."""
     import os
     import signal
 
@@ -143,7 +144,8 @@ def test_stalled_writer_process_is_taken_over(tmp_path, monkeypatch):
     monkeypatch.setattr(ProcessCheckpointWriter, "STALL_S", 1.0)
     w = ProcessCheckpointWriter()
     assert w._conn.poll(30)  # started
-    os.kill(w._proc.pid, signal.SIGSTOP)  # alive, silent
+    old = w._proc
+    os.kill(old.pid, signal.SIGSTOP)  # alive, silent
 
     def _remove_file(p):
         os.remove(p)
@@ -155,17 +157,37 @@ def test_stalled_writer_process_is_taken_over(tmp_path, monkeypatch):
         w.submit(_remove_file, str(tmp_path / "a.ckpt"))
         w.wait()  # returns after ~STALL_S instead of blocking forever
         assert sorted(os.listdir(tmp_path)) == ["b.ckpt"]
-        assert not w.alive()
-        w.save(ck, str(tmp_path / "c.ckpt"))  # written in-process from now on
+        assert not old.is_alive()  # stopped before anything was replayed
+        assert w.alive() and w._proc.pid != old.pid  # a fresh writer process
+        w.save(ck, str(tmp_path / "c.ckpt"))  # through the new writer
         w.wait()
         atomic_save(ck, str(tmp_path / "ref.ckpt"))
         assert torch.equal(torch.load(tmp_path / "c.ckpt", weights_only=True)["state_dict"]["w"],
                            torch.load(tmp_path / "ref.ckpt", weights_only=True)["state_dict"]["w"])
     finally:
         try:
-            os.kill(w._proc.pid, signal.SIGKILL)
+            os.kill(old.pid, signal.SIGKILL)
         except OSError:
             pass
+        w.close()
+
+
+def test_busy_writer_heartbeats_are_not_a_stall(tmp_path, monkeypatch):
+    """A save that takes longer than STALL_S (large checkpoint, slow filesystem) is
+    busy, not stalled: the writer's heartbeats keep the trainer waiting for it."""
+    from ray_lightning_accelerators_amd.lightning import utilities as u
+
+    monkeypatch.setattr(u.ProcessCheckpointWriter, "STALL_S", 1.0)
+    monkeypatch.setattr(u.ProcessCheckpointWriter, "BEAT_S", 0.2)
+    w = u.ProcessCheckpointWriter()
+    before = u.writer_takeovers
+    try:
+        assert w._conn.poll(30)
+        w._conn.send(("sleep", 3.0))  # a test-only request: busy for 3 s
+        w._pending.append((None, ("sleep", 3.0)))
+        w.wait()
+        assert u.writer_takeovers == before and w.alive()
+    finally:
         w.close()
 
 

@@ -451,6 +451,26 @@ def _gpu_worker(rank, world, port, q, mode):
             e.check()
             res["worst"] = worst
             res["params"] = e.params.cpu().numpy().tobytes()
+        elif mode == "bcast_exact":
+            # DDP buffer broadcast without RCCL (ranks share the device): int64 counters
+            # above 2^24 and fp64 buffers arrive bit-exact, fp32 too
+            from ray_lightning_accelerators_amd.parallel import comm as comm_mod
+            from ray_lightning_accelerators_amd.parallel.arena import ParamArena
+            from ray_lightning_accelerators_amd.parallel.ddp import GradSynchronizer
+
+            comm_mod._default = comm
+            m = torch.nn.Linear(8, 4).to(dev)
+            m.register_buffer("big", torch.tensor([2 ** 40 + 12345 + rank, -7 - rank, 2 ** 24 + 1], device=dev))
+            m.register_buffer("f64", torch.tensor([1.0 + 1e-12 * (rank + 1), -3.5e-300], dtype=torch.float64,
+                                                  device=dev))
+            m.register_buffer("f32", torch.full((5,), 0.1 * (rank + 1), device=dev))
+            sync = GradSynchronizer(m, ParamArena(m), bucket_cap_mb=1.0)
+            sync._broadcast_buffers()
+            torch.cuda.synchronize()
+            res["big"] = m.big.tolist() == [2 ** 40 + 12345, -7, 2 ** 24 + 1]
+            res["f64"] = m.f64.tolist() == [1.0 + 1e-12, -3.5e-300]
+            res["f32"] = bool(torch.all(m.f32 == torch.tensor(0.1, device=dev)))
+            comm.check()
         elif mode == "timeout":
             x = torch.ones(1024, device=dev)
             if rank == 0:
@@ -614,6 +634,13 @@ def test_comm_correctness_matrix(world):
         assert not res["bad"], (r, res["bad"][:10])
         n_big = 1 if world >= 8 else 2
         assert res["big_routes"] == ["twoshot"] * n_big, (r, res["big_routes"])  # no RCCL: chunked two-shot
+
+
+@gpu
+def test_buffer_broadcast_without_rccl_is_exact():
+    out = _run_gpu("bcast_exact")
+    for r, res in out.items():
+        assert isinstance(res, dict) and res["big"] and res["f64"] and res["f32"], (r, res)
 
 
 @gpu

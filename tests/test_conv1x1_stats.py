@@ -195,3 +195,36 @@ def test_fused_bn_dgrad_resnet_layer_matches(monkeypatch):
     for a, b in zip(p1, p0):
         assert _rel(a, b) < 3e-2, _rel(a, b)
 
+
+
+@gpu
+def test_fused_bn_dgrad_guard_with_extra_consumer(monkeypatch):
+    """an extra autograd consumer of an identity block's output (a feature
+    tap) makes autograd hand bn3 the SUM of the conv's d and the tap's gradient; the
+    conv's fused partial sums are of d alone, so bn3 must notice and run its own
+    partial pass -- gradients then match the unfused step."""
+    from ray_lightning_accelerators_amd.models.resnet import resnet50
+    from ray_lightning_accelerators_amd.ops import bn as B
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    layer = resnet50(num_classes=10, fused_bn=True).to(dev).to(memory_format=torch.channels_last).layer1
+    x0 = torch.randn(4, 64, 32, 32, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("RLA_FUSE_BN_DGRAD", fuse)
+        layer.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        r0 = B.fold_stats["fused_rejected"]
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            h = layer[0](x)           # identity-block input: read by layer[1].conv1 ...
+            tap = h.float().mean()    # ... and by a feature tap
+            y = layer[2](layer[1](h))
+        (y.float().square().mean() + 10.0 * tap).backward()
+        if fuse == "1":
+            assert B.fold_stats["fused_rejected"] - r0 >= 1
+        outs.append((x.grad.float(), [p.grad.detach().float().clone() for p in layer.parameters()]))
+    (g0, p0), (g1, p1) = outs
+    assert _rel(g1, g0) < 2e-2, _rel(g1, g0)
+    for a, b in zip(p1, p0):
+        assert _rel(a, b) < 3e-2, _rel(a, b)
