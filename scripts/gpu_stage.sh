@@ -132,6 +132,25 @@ for st in "$@"; do
       run pytest_graph 600 $PYT tests/test_graph_step.py
       run rn50_trainer 900 python -u bench.py --via trainer --model resnet50 --steps 20 --trainer-epochs 4
       run rn50_engine 600 python bench.py --model resnet50 --steps 30 --warmup 10 ;;
+    r5tests)  # round-5 GPU tests: comm matrix worlds 1-8, exact buffer broadcast, fused-dgrad guard, graph step
+      run pytest_r5 900 $PYT tests/test_comm.py tests/test_conv1x1_stats.py tests/test_graph_step.py \
+        -m gpu -k "matrix or bcast_exact or guard or graph or captured" ;;
+    comm5)  # config-5 communication on one GPU (proxies): bucket timings, wire trajectory, overlap trace
+      run comm_buckets2 300 python -u scripts/comm_quantify.py buckets --world 2
+      run comm_buckets8 600 python -u scripts/comm_quantify.py buckets --world 8 --reps 10
+      run comm_traj 900 python -u scripts/comm_quantify.py trajectory --steps 300 ;;
+    comm5trace)  # kernel trace of the captured 2-rank share-GPU ResNet step: one rocprofv3 per rank process
+      cd /tmp
+      for r in 0 1; do
+        RLA_BENCH_SHARE_GPU=1 RANK=$r WORLD_SIZE=2 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29561 \
+          timeout -k 10 900 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/rn50s2trace/r$r" -o run -- \
+          python3 "$R/bench.py" --model resnet50 --gpus 2 --steps 20 --warmup 5 > "$R/$O/rn50s2trace_r$r.log" 2>&1 &
+      done
+      wait -n || { echo "[comm5trace] a rank failed"; tail -30 "$R/$O/rn50s2trace_r0.log"; exit 1; }
+      wait -n || { echo "[comm5trace] a rank failed"; tail -30 "$R/$O/rn50s2trace_r1.log"; exit 1; }
+      cd "$R"
+      python scripts/comm_overlap_report.py "$O/rn50s2trace" --last 10 > "$O/comm_overlap.jsonl" && cat "$O/comm_overlap.jsonl"
+      find "$O/rn50s2trace" -name "*kernel_trace.csv" -size +20M -delete ;;
     rn50trainer)
       run rn50_trainer 900 python -u bench.py --via trainer --model resnet50 --steps 20 --trainer-epochs 4 ;;
     rn50share2)  # config 5 through Trainer.fit, 2 ranks sharing the GPU (graph-captured DP step)

@@ -119,6 +119,19 @@ def test_bench_resnet50_two_ranks_share_gpu_graph_captured():
 
 
 @pytest.mark.gpu
+def test_bench_resnet50_via_trainer_two_ranks_share_gpu():
+    """Config 5 through RayAccelerator + Trainer.fit at world 2 (ranks sharing the
+    GPU): the Trainer captures the autograd step (forward, backward, bucket
+    allreduce, fused SGD) and replays it; replicas end bitwise equal."""
+    out, err = _bench("--via", "trainer", "--model", "resnet50", "--gpus", "2", "--steps", "4", "--batch-size", "16",
+                      "--trainer-epochs", "2", env={"RLA_BENCH_SHARE_GPU": "1"}, timeout=900)
+    g = out["config"]["graph_step"]
+    assert out["n_gpus"] == 2 and g["captured"] and g["resident_data"] and g["fallback"] is None, (out, err[-2000:])
+    assert g["replays"] == g["steps"] - g["warmup_steps"], g
+    assert out["replicas_equal"] is True, out
+
+
+@pytest.mark.gpu
 def test_bench_resnet50_torch_graph_baseline():
     out, _ = _bench("--model", "resnet50", "--impl", "torch-graph", "--steps", "4", "--warmup", "4",
                     "--batch-size", "16", timeout=600)

@@ -178,3 +178,16 @@ def test_bench_resnet50_two_gpus_graph_captured():
     out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert out["config"]["route"] == "native-reducer" and out["config"]["hip_graph"] is True, out
     assert out["dp"]["rccl_world"] == 2 and out["dp"]["comm_error_state"] == 0, out
+
+
+def test_bench_resnet50_via_trainer_two_gpus():
+    """Config 5 through RayAccelerator(num_workers=2) + Trainer.fit on two physical GPUs:
+    graph-captured step over RCCL / xGMI, bitwise-equal replicas, per-epoch checkpoint."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--via", "trainer", "--model", "resnet50",
+                        "--gpus", "2", "--steps", "6", "--batch-size", "32", "--trainer-epochs", "2"],
+                       cwd="/tmp", capture_output=True, text=True, timeout=900)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    g = out["config"]["graph_step"]
+    assert out["n_gpus"] == 2 and g["captured"] and g["fallback"] is None, out
+    assert out["replicas_equal"] is True, out
