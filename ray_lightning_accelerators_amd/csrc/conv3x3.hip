@@ -89,12 +89,21 @@ struct CvSet {
 // block L runs on XCD L % 8) owns a contiguous tile range, its workgroups take every
 // (G / 8)-th tile of it, so tiles running together share halo rows and weights in
 // that XCD's L2.
-template <int NX, bool FLIP, int JB, int DEPTH>
+//
+// WC / CC (round 5): the image width and input channels as compile-time constants
+// (0 = run time) for the shapes that matter (ResNet's 56/64, 28/128, 14/256, 7/512):
+// each tap's halo offset (r (W + 2) + s) rows is then an immediate of the ds_read
+// (one per-lane base per pixel block, set per tile, instead of a multiply-add per
+// tap and block), and a stage's tile / chunk split is a shift.  Global loads take
+// 32-bit byte offsets from the SGPR base (saddr form: no 64-bit address math).
+template <int NX, bool FLIP, int JB, int DEPTH, int WC = 0, int CC = 0>
 __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __restrict__ x,
                                                              const uint16_t* __restrict__ w,
                                                              uint16_t* __restrict__ y, Conv3x3Geom g) {
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * kBufElems];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (WC) g.W = WC;
+  if (CC) g.Cin = CC;
   const int WP = g.W + 2, HP = g.H + 2;
   const int64_t M = (int64_t)g.N * g.H * g.W;
   const int hw = g.H * g.W;
@@ -131,7 +140,7 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
   // chunk cost two runtime integer divisions per piece, ~1K VALU cycles a stage at
   // one wave per SIMD: the MFMAs ran at ~15 % of the step, profiles/r4_rn.)
   int ld_tile = -1;
-  int xoff[NX], woff[kNW];
+  uint32_t xoff[NX], woff[kNW];  // byte offsets from x / w
   uint32_t xok = 0u;
   auto load_geom = [&](int tile) {
     int64_t m0;
@@ -149,7 +158,7 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
       const bool ok = p < xpieces && n < g.N && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
       const int nc = n < g.N ? n : g.N - 1;
       const int ihc = ih < 0 ? 0 : (ih >= g.H ? g.H - 1 : ih), iwc = iw < 0 ? 0 : (iw >= g.W ? g.W - 1 : iw);
-      xoff[i] = ((nc * g.H + ihc) * g.W + iwc) * g.Cin + h * 8;
+      xoff[i] = (uint32_t)(((nc * g.H + ihc) * g.W + iwc) * g.Cin + h * 8) * 2u;
       xok |= ok ? (1u << i) : 0u;
     }
 #pragma unroll
@@ -159,10 +168,10 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
       if (FLIP) {
         // piece = (tap, k, group of 8 co): w[ci0 + k][8 - tap][co0 + 8 grp]
         const int tap = pc >> 7, k = (pc >> 3) & 15, grp = pc & 7;
-        woff[i] = (k * 9 + (8 - tap)) * g.Cout + co0 + grp * 8;
+        woff[i] = (uint32_t)((k * 9 + (8 - tap)) * g.Cout + co0 + grp * 8) * 2u;
       } else {
         const int h = pc & 1, rest = pc >> 1, co = rest % kTN, tap = rest / kTN;
-        woff[i] = ((co0 + co) * 9 + tap) * g.Cin + h * 8;
+        woff[i] = (uint32_t)(((co0 + co) * 9 + tap) * g.Cin + h * 8) * 2u;
       }
     }
   };
@@ -173,13 +182,15 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
       load_geom(tile);
       ld_tile = tile;
     }
-    const int ci0 = cc * kKC;
-    const int wstep = FLIP ? ci0 * 9 * g.Cout : ci0;
+    const uint32_t ci0b = (uint32_t)(cc * kKC) * 2u;
+    const uint32_t wstepb = FLIP ? ci0b * 9u * (uint32_t)g.Cout : ci0b;
     st.ok = xok;
+    const char* xc = reinterpret_cast<const char*>(x);
+    const char* wc = reinterpret_cast<const char*>(w);
 #pragma unroll
-    for (int i = 0; i < NX; ++i) st.x[i] = *reinterpret_cast<const u32x4*>(x + xoff[i] + ci0);
+    for (int i = 0; i < NX; ++i) st.x[i] = *reinterpret_cast<const u32x4*>(xc + (xoff[i] + ci0b));
 #pragma unroll
-    for (int i = 0; i < kNW; ++i) st.w[i] = *reinterpret_cast<const u32x4*>(w + woff[i] + wstep);
+    for (int i = 0; i < kNW; ++i) st.w[i] = *reinterpret_cast<const u32x4*>(wc + (woff[i] + wstepb));
   };
   auto store = [&](const CvSet<NX>& st, int buf) {
     __bf16* X = lds + buf * kBufElems;
@@ -204,8 +215,8 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
   // transposed-read roles (FLIP A operand): group gq of 16 lanes, lane 4q+p -> row q, channels 4p..4p+3
   const int gq = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
   const int cho = 16 * (gq & 1) + 4 * p4, rwo = 8 * (gq >> 1) + q4;
-  int bpos[JB];
-  auto set_tile = [&](int tile) {  // this lane's two pixels as halo positions of tap (0, 0)
+  int bpos[JB];  // this lane's pixel of block j as an LDS element offset of tap (0, 0)
+  auto set_tile = [&](int tile) {
     int64_t m0;
     int co0, v0;
     tile_org(tile, &m0, &co0, &v0);
@@ -215,7 +226,7 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
       if (m >= M) m = M - 1;  // tail pixels compute a duplicate, never stored
       const int n = (int)(m / hw), rem = (int)(m - (int64_t)n * hw);
       const int oh = rem / g.W, ow = rem - oh * g.W;
-      bpos[jb] = (n * HP + oh - v0) * WP + ow;
+      bpos[jb] = ((n * HP + oh - v0) * WP + ow) * kRow + kg;
     }
   };
 
@@ -247,8 +258,8 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
         }
       }
 #pragma unroll
-      for (int j = 0; j < JB; ++j)
-        fb[j] = *reinterpret_cast<const bf16x8*>(X + (bpos[j] + toff) * kRow + kg);
+      for (int j = 0; j < JB; ++j)  // toff * kRow: an immediate offset when WC is set
+        fb[j] = *reinterpret_cast<const bf16x8*>(X + bpos[j] + toff * kRow);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -365,10 +376,32 @@ bool conv3x3_ok(const Conv3x3Geom& g) {
          (int64_t)g.Cin * 9 * g.Cout < (1ll << 31);
 }
 
+// the compile-time-shape instance (WC, CC) when the layer is one of them and its halo
+// needs exactly NX pieces per thread; false: use the run-time-shape kernel
+template <int NX, bool FLIP, int JB, int DEPTH, int WC, int CC>
+static bool launch_fixed(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, hipStream_t st,
+                         dim3 grid) {
+  static const bool generic = getenv("RLA_CONV3X3_GENERIC") != nullptr;  // A/B switch: run-time-shape kernel
+  if (generic || g.W != WC || g.Cin != CC || conv3x3_pieces_per_thread(g) > NX ||
+      conv3x3_pieces_per_thread(g) < NX - 1)
+    return false;
+  hipLaunchKernelGGL((conv3x3_kernel<NX, FLIP, JB, DEPTH, WC, CC>), grid, dim3(kCvThreads), 0, st, x, w, y, g);
+  return true;
+}
+
 template <bool FLIP, int JB, int DEPTH>
 static void launch_nx(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, hipStream_t st,
                       dim3 grid) {
   const dim3 block(kCvThreads);
+  // ResNet-50's stride-1 3x3 shapes (bottleneck conv2 forward; the input gradient of
+  // the same layers reads dy with the same width and channel count)
+  if constexpr (JB == 4) {
+    if (launch_fixed<6, FLIP, JB, DEPTH, 56, 64>(x, w, y, g, st, grid)) return;
+  } else {
+    if (launch_fixed<4, FLIP, JB, DEPTH, 28, 128>(x, w, y, g, st, grid)) return;
+    if (launch_fixed<4, FLIP, JB, DEPTH, 14, 256>(x, w, y, g, st, grid)) return;
+    if (launch_fixed<4, FLIP, JB, DEPTH, 7, 512>(x, w, y, g, st, grid)) return;
+  }
   switch (conv3x3_pieces_per_thread(g)) {
     case 1: case 2: case 3: case 4:
       hipLaunchKernelGGL((conv3x3_kernel<4, FLIP, JB, DEPTH>), grid, block, 0, st, x, w, y, g);

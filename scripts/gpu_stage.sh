@@ -151,6 +151,16 @@ for st in "$@"; do
       cd "$R"
       python scripts/comm_overlap_report.py "$O/rn50s2trace" --last 10 > "$O/comm_overlap.jsonl" && cat "$O/comm_overlap.jsonl"
       find "$O/rn50s2trace" -name "*kernel_trace.csv" -size +20M -delete ;;
+    c3ab)  # 3x3 MFMA convolution: numerics + fixed-shape vs run-time-shape instances, per shape vs MIOpen
+      run pytest_c3 300 $PYT tests/test_conv3x3.py
+      run c3probe_fixed 300 python -u scripts/conv3x3_probe.py
+      RLA_CONV3X3_GENERIC=1 run c3probe_generic 300 python -u scripts/conv3x3_probe.py ;;
+    mnist5)  # one-launch MNIST step after a kernel change: numerics, headline bench, phase stamps, DP cost
+      run pytest_mlp3 600 $PYT tests/test_mlp3.py
+      run bench_default 300 python bench.py
+      run bench_k20 300 python bench.py --gpus 1 --steps 20 --warmup 5
+      run dp_phases 300 python -u scripts/dp_phase_probe.py
+      run dp_probe 300 python -u scripts/dp_overhead_probe.py ;;
     rn50trainer)
       run rn50_trainer 900 python -u bench.py --via trainer --model resnet50 --steps 20 --trainer-epochs 4 ;;
     rn50share2)  # config 5 through Trainer.fit, 2 ranks sharing the GPU (graph-captured DP step)
