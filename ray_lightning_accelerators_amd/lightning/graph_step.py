@@ -123,8 +123,12 @@ def static_reason(trainer, model) -> Optional[str]:
         return "no parameter arena"
     if trainer.accumulate_grad_batches != 1:
         return "accumulate_grad_batches > 1"
-    if getattr(opt, "_hvd_state", None) is not None and trainer.world_size > 1:
-        return "Horovod fusion engine (host-thread negotiation) at world > 1"
+    hst = getattr(opt, "_hvd_state", None)
+    if hst is not None and trainer.world_size > 1:
+        from ..horovod import Average, Compression
+
+        if hst.op != Average or hst.compression is not Compression.none or hst.bpps != 1:
+            return "Horovod DistributedOptimizer with op / compression / backward_passes_per_step other than the default"
     t = type(model)
     for name in ("backward", "optimizer_step", "optimizer_zero_grad", "on_after_backward", "on_before_zero_grad"):
         if getattr(t, name) is not getattr(LightningModule, name) or name in model.__dict__:
@@ -171,6 +175,8 @@ class GraphedTrainStep:
         self._nb = 0
         self._last_rows = None
         self.opt.enable_device_scalars()
+        if getattr(self.opt, "_hvd_state", None) is not None and trainer.world_size > 1:
+            self._adopt_horovod()
         n = max(int(getattr(trainer, "num_training_batches", 0) or 0), 1)
         # two epochs of rows: an epoch's step outputs (ring views) stay valid through
         # its training_epoch_end and the next epoch's blocking log flush
@@ -178,6 +184,29 @@ class GraphedTrainStep:
         self._ring: Optional[torch.Tensor] = None
         self._ring_pos = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self._side = torch.cuda.Stream() if self.cuda else None
+
+    def _adopt_horovod(self) -> None:
+        """Horovod at world > 1: ``hvd.DistributedOptimizer``'s fusion engine negotiates
+        and packs on a host thread, which no graph can record.  The same reduction --
+        the averaged sum of every rank's gradient -- runs instead through the DDP
+        ``GradSynchronizer`` (arena buckets, allreduce on the comm engine's stream,
+        the 1/size average folded into the fused optimizer): the optimizer's fusion
+        hooks are removed, ``synchronize()`` becomes the synchroniser's ``finish()``.
+        Same math as ``op=Average``, capturable."""
+        import types
+
+        from ..parallel.ddp import GradSynchronizer
+
+        st = self.opt._hvd_state
+        for h in st.hooks:
+            h.remove()
+        st.hooks = []
+        st.skip = True  # DistributedOptimizer.step no longer synchronises itself
+        thr = float(os.environ.get("HOROVOD_FUSION_THRESHOLD", str(8 * 1024 * 1024))) / (1 << 20)
+        sync = GradSynchronizer(self.model, self.arena, bucket_cap_mb=max(thr, 0.25), average_in_optimizer=True)
+        self.acc.sync = sync  # before_forward / grad_scale of the accelerator use it
+        self.opt.synchronize = types.MethodType(lambda _self: sync.finish(), self.opt)
+        self.horovod_adopted = True
 
     # ------------------------------------------------------------ describe
     def describe(self) -> Dict[str, Any]:

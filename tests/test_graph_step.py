@@ -226,3 +226,52 @@ def test_gpu_captured_matches_eager(tmpdir, resident):
     torch.testing.assert_close(torch.tensor(r_g.losses), torch.tensor(r_e.losses), rtol=1e-4, atol=1e-5)
     for (k, a), b in zip(t_g.model.state_dict().items(), t_e.model.state_dict().values()):
         torch.testing.assert_close(a.float(), b.float(), rtol=1e-4, atol=1e-5, msg=k)
+
+
+class _Dist(Tiny):
+    """Tiny, picklable across the runtime's actors (module-level class)."""
+
+
+class _AssertGraphStep(pl.Callback):
+    """Worker side: the graph step ran its body (no fallback); Horovod's reduction
+    was adopted by the GradSynchronizer."""
+
+    def __init__(self, want, horovod):
+        self.want, self.horovod = want, horovod
+
+    def on_train_end(self, trainer, pl_module):
+        f = trainer._fused
+        if not self.want:
+            assert f is None
+            return
+        assert isinstance(f, GraphedTrainStep) and not f.failed, getattr(f, "reason", None)
+        assert f.steps_done == trainer.global_step
+        if self.horovod:
+            assert getattr(f, "horovod_adopted", False) and trainer.accelerator_backend.sync is not None
+
+
+@pytest.mark.parametrize("kind", ["ddp", "horovod"])
+def test_graph_body_world2_matches_eager(tmpdir, kind):
+    """World 2 (gloo, runtime actors): the graph-step body -- for Horovod with the
+    DistributedOptimizer's reduction adopted by the DDP GradSynchronizer (the
+    capturable form) -- trains exactly like the eager accelerator path."""
+    from ray_lightning_accelerators_amd import HorovodRayAccelerator, RayAccelerator
+    from ray_lightning_accelerators_amd import runtime as ray
+
+    outs = {}
+    ray.init(num_cpus=2, num_gpus=0)
+    try:
+        for graph in (True, False):
+            m = _Dist()
+            m.hip_graph_step = graph
+            acc = (RayAccelerator(num_workers=2, use_gpu=False) if kind == "ddp"
+                   else HorovodRayAccelerator(num_slots=2, use_gpu=False))
+            t = pl.Trainer(default_root_dir=os.path.join(str(tmpdir), f"{kind}{graph}"), max_epochs=2,
+                           progress_bar_refresh_rate=0, accelerator=acc,
+                           callbacks=[_AssertGraphStep(graph, kind == "horovod")])
+            assert t.fit(m) == 1
+            outs[graph] = {k: v.clone() for k, v in m.state_dict().items()}
+    finally:
+        ray.shutdown()
+    for k in outs[True]:
+        assert torch.equal(outs[True][k], outs[False][k]), k
