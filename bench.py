@@ -421,7 +421,7 @@ def make_torch(args, world, rank, dev, x, y):
             loss = F.nll_loss(F.log_softmax(logits.float(), dim=1), yb)
             loss.backward()
             opt.step()
-            state["loss"] = loss
+            state["loss"] = loss.detach()
 
     return run, (lambda: float(state["loss"].item())), None, {"route": "torch-ddp" if world > 1 else "single"}
 
@@ -591,7 +591,7 @@ def make_resnet(args, world, rank, dev, x, y, bucket_mb=None):
                 loss = F.cross_entropy(out.float(), yb)
                 loss.backward()
                 opt.step()
-                state["loss"] = loss
+                state["loss"] = loss.detach()
 
         if args.impl == "torch-graph" and world == 1:
             # the fair stock baseline: the same stock step (MIOpen convs /
@@ -619,7 +619,7 @@ def make_resnet(args, world, rank, dev, x, y, bucket_mb=None):
                         loss = F.cross_entropy(out.float(), yb)
                         loss.backward()
                         opt.step()
-                        state["loss"] = loss
+                        state["loss"] = loss.detach()
                     tg["g"] = g_
                 for _ in range(n):
                     tg["g"].replay()

@@ -763,12 +763,13 @@ Tensor conv3x3(Tensor x, Tensor w, int64_t N, int64_t H, int64_t W, int64_t Cin,
   TORCH_CHECK(N * (H + 2) * (W + 2) < (int64_t(1) << 30), "conv3x3: too many pixels");
   const at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   rla::Conv3x3Geom g{(int)N, (int)H, (int)W, (int)Cin, (int)Cout, 0,
-                     rla::conv3x3_pick_tm((int)N, (int)H, (int)W, (int)Cout)};
-  static std::map<std::tuple<int64_t, int64_t, int64_t, int>, int> vrows_cache;
+                     rla::conv3x3_pick_tm((int)N, (int)H, (int)W, (int)Cout),
+                     rla::conv3x3_wpb((int)N, (int)H, (int)W, (int)Cout)};
+  static std::map<std::tuple<int64_t, int64_t, int64_t, int, int>, int> vrows_cache;
   static std::mutex mu;
   {
     std::lock_guard<std::mutex> lk(mu);
-    auto key = std::make_tuple(N, H, W, g.tm);
+    auto key = std::make_tuple(N, H, W, g.tm, g.wpb);
     auto it = vrows_cache.find(key);
     if (it == vrows_cache.end()) it = vrows_cache.emplace(key, rla::conv3x3_vrows(g)).first;
     g.vrows = it->second;
@@ -785,7 +786,8 @@ Tensor conv3x3(Tensor x, Tensor w, int64_t N, int64_t H, int64_t W, int64_t Cin,
 bool conv3x3_supported(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout) {
   if (N <= 0 || H <= 0 || W <= 0 || Cout <= 0 || N * (H + 2) * (W + 2) >= (int64_t(1) << 30)) return false;
   rla::Conv3x3Geom g{(int)N, (int)H, (int)W, (int)Cin, (int)Cout, 0,
-                     rla::conv3x3_pick_tm((int)N, (int)H, (int)W, (int)Cout)};
+                     rla::conv3x3_pick_tm((int)N, (int)H, (int)W, (int)Cout),
+                     rla::conv3x3_wpb((int)N, (int)H, (int)W, (int)Cout)};
   g.vrows = rla::conv3x3_vrows(g);
   return rla::conv3x3_ok(g);
 }

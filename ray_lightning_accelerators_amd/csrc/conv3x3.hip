@@ -82,13 +82,15 @@ struct CvSet {
 // kernel: a chunk's pieces are 8 consecutive co of one (k, tap) row, staged as
 // [tap][k][co] and read as A fragments by transposed LDS reads (ds_read_b64_tr_b16).
 //
-// Persistent: gridDim.x workgroups (the CU count), each walks its tiles' chunks as
-// ONE stream -- the next tile's first chunks are in flight while this tile's last
-// ones are multiplied and its results stored -- so the per-tile pipeline fill is paid
-// once per workgroup, not once per tile.  Tiles are dealt XCD by XCD: XCD x (hardware
-// block L runs on XCD L % 8) owns a contiguous tile range, its workgroups take every
-// (G / 8)-th tile of it, so tiles running together share halo rows and weights in
-// that XCD's L2.
+// Persistent: one workgroup per CU, each walks its tiles' chunks as ONE stream -- the
+// next tile's first chunks are in flight while this tile's last ones are multiplied
+// and its results stored -- so the per-tile pipeline fill is paid once per workgroup.
+// Work split (round 5): workgroup g owns output-channel block g % tiles_n and the
+// (g / tiles_n)-th of wpb EQUAL contiguous pixel ranges of it, tiled by TM with a
+// shorter last tile.  Whole tiles dealt over the CUs left the last round mostly idle
+// on every ResNet shape: 784 tiles = 3.06 rounds of 256 at 56x56 and 28x28, 392 =
+// 1.53 at 14x14, 200 tiles on 256 CUs at 7x7 -- a 22-24 % makespan loss.  With
+// tiles_n = 8 (7x7) each XCD (block g runs on XCD g % 8) holds one weight block.
 //
 // WC / CC (round 5): the image width and input channels as compile-time constants
 // (0 = run time) for the shapes that matter (ResNet's 56/64, 28/128, 14/256, 7/512):
@@ -108,28 +110,28 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
   const int64_t M = (int64_t)g.N * g.H * g.W;
   const int hw = g.H * g.W;
   constexpr int TM = 128 * JB;
-  const int tiles_m = (int)((M + TM - 1) / TM), tiles_n = g.Cout / kTN;
-  const int total = tiles_m * tiles_n;
-  const int per = (total + 7) / 8, gx = (int)(gridDim.x / 8u);
-  const int xcd = (int)(blockIdx.x % 8u), slot = (int)(blockIdx.x / 8u);
-  const int t_lo = xcd * per + slot, t_hi = (xcd + 1) * per < total ? (xcd + 1) * per : total;
-  const int ntiles = t_lo < t_hi ? (t_hi - t_lo + gx - 1) / gx : 0;
+  const int tiles_n = g.Cout / kTN;
+  if ((int)blockIdx.x >= g.wpb * tiles_n) return;  // (uniform)
+  const int nblk = (int)blockIdx.x % tiles_n, jr = (int)blockIdx.x / tiles_n;
+  const int64_t p_lo = M * jr / g.wpb, p_hi = M * (jr + 1) / g.wpb;  // this workgroup's pixels
+  const int ntiles = (int)((p_hi - p_lo + TM - 1) / TM);
   if (ntiles == 0) return;
   const int nchunks = g.Cin / kKC;
   const int nst = ntiles * nchunks;
   const int xpieces = g.vrows * WP * 2;  // 16-byte pieces of a chunk's halo image
 
-  // tile of stream stage `st` (clamped: stages past the end re-load the last one)
+  // this workgroup's tile of stream stage `st` (clamped: stages past the end re-load the last one)
   auto tile_of = [&](int st, int* chunk) {
     const int sc = st < nst ? st : nst - 1;
     const int i = sc / nchunks;
     *chunk = sc - i * nchunks;
-    return t_lo + i * gx;
+    return i;
   };
-  auto tile_org = [&](int tile, int64_t* m0, int* co0, int* v0) {
-    const int tm = tile / tiles_n;
-    *co0 = (tile - tm * tiles_n) * kTN;
-    *m0 = (int64_t)tm * TM;
+  // tile i: pixels [m0, m_end) (m_end - m0 <= TM; the last tile of the range is shorter)
+  auto tile_org = [&](int tile, int64_t* m0, int* co0, int* v0, int64_t* m_end = nullptr) {
+    *co0 = nblk * kTN;
+    *m0 = p_lo + (int64_t)tile * TM;
+    if (m_end) *m_end = *m0 + TM < p_hi ? *m0 + TM : p_hi;
     const int n0 = (int)(*m0 / hw), oh0 = (int)((*m0 - (int64_t)n0 * hw) / g.W);
     *v0 = n0 * HP + oh0;  // first virtual halo row (the padded layout [n][H + 2][W + 2])
   };
@@ -217,13 +219,13 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
   const int cho = 16 * (gq & 1) + 4 * p4, rwo = 8 * (gq >> 1) + q4;
   int bpos[JB];  // this lane's pixel of block j as an LDS element offset of tap (0, 0)
   auto set_tile = [&](int tile) {
-    int64_t m0;
+    int64_t m0, m_end;
     int co0, v0;
-    tile_org(tile, &m0, &co0, &v0);
+    tile_org(tile, &m0, &co0, &v0, &m_end);
 #pragma unroll
     for (int jb = 0; jb < JB; ++jb) {
       int64_t m = m0 + wave * (32 * JB) + jb * 32 + (lane & 31);
-      if (m >= M) m = M - 1;  // tail pixels compute a duplicate, never stored
+      if (m >= m_end) m = m_end - 1;  // past the tile: a duplicate, never stored
       const int n = (int)(m / hw), rem = (int)(m - (int64_t)n * hw);
       const int oh = rem / g.W, ow = rem - oh * g.W;
       bpos[jb] = ((n * HP + oh - v0) * WP + ow) * kRow + kg;
@@ -270,13 +272,13 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
   // D[co][m]: lane -> pixel (lane & 31) of block j; accumulator k -> channel
   // (k & 3) + 8 (k >> 2) + 4 (lane >> 5) of block i
   auto epilogue = [&](int tile) {
-    int64_t m0;
+    int64_t m0, m_end;
     int co0, v0;
-    tile_org(tile, &m0, &co0, &v0);
+    tile_org(tile, &m0, &co0, &v0, &m_end);
 #pragma unroll
     for (int j = 0; j < JB; ++j) {
       const int64_t m = m0 + wave * (32 * JB) + j * 32 + (lane & 31);
-      if (m < M) {
+      if (m < m_end) {
         uint16_t* yo = y + m * g.Cout + co0;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -328,16 +330,20 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
 }  // namespace
 
 int conv3x3_vrows(const Conv3x3Geom& g) {
-  // the most virtual halo rows any tile of g.tm consecutive pixels touches
+  // the most virtual halo rows any tile of the partition touches (g.wpb ranges of
+  // M / wpb pixels, each cut into g.tm-pixel tiles from its own start)
   const int64_t M = (int64_t)g.N * g.H * g.W;
   const int hw = g.H * g.W, HP = g.H + 2, TM = g.tm;
   int best = 0;
-  for (int64_t m0 = 0; m0 < M; m0 += TM) {
-    const int64_t m1 = (m0 + TM < M ? m0 + TM : M) - 1;
-    const int n0 = (int)(m0 / hw), oh0 = (int)((m0 % hw) / g.W);
-    const int n1 = (int)(m1 / hw), oh1 = (int)((m1 % hw) / g.W);
-    const int rows = (n1 * HP + oh1 + 2) - (n0 * HP + oh0) + 1;
-    if (rows > best) best = rows;
+  for (int j = 0; j < g.wpb; ++j) {
+    const int64_t lo = M * j / g.wpb, hi = M * (j + 1) / g.wpb;
+    for (int64_t m0 = lo; m0 < hi; m0 += TM) {
+      const int64_t m1 = (m0 + TM < hi ? m0 + TM : hi) - 1;
+      const int n0 = (int)(m0 / hw), oh0 = (int)((m0 % hw) / g.W);
+      const int n1 = (int)(m1 / hw), oh1 = (int)((m1 % hw) / g.W);
+      const int rows = (n1 * HP + oh1 + 2) - (n0 * HP + oh0) + 1;
+      if (rows > best) best = rows;
+    }
   }
   return best;
 }
@@ -357,19 +363,29 @@ static int cu_count() {
   return n;
 }
 
+int conv3x3_wpb(int N, int H, int W, int Cout) {
+  // one workgroup per CU: cu / tiles_n pixel ranges per output-channel block (at least one)
+  const int tiles_n = Cout / kTN, cu = cu_count();
+  const int64_t M = (int64_t)N * H * W;
+  int64_t w = tiles_n > 0 ? cu / tiles_n : 1;
+  if (w < 1) w = 1;
+  if (w > (M + 31) / 32) w = (M + 31) / 32;  // ranges of at least 32 pixels
+  return (int)w;
+}
+
 int conv3x3_pick_tm(int N, int H, int W, int Cout) {
-  // 512-pixel tiles halve the weight / halo traffic per MFMA, but only where there
-  // are enough of them to keep every CU busy (ResNet-50: the 56x56 and 28x28 layers)
+  // 512-pixel tiles halve the weight / halo traffic per MFMA where a workgroup's range
+  // holds at least 1.5 of them (ResNet-50: the 56x56 layers)
   const char* e = getenv("RLA_CONV3X3_TM");  // tests pin either tile size
   if (e && (e[0] == '2' || e[0] == '5')) return e[0] == '5' ? 512 : 256;
   const int64_t M = (int64_t)N * H * W;
-  const int64_t tiles512 = (M + 511) / 512 * (Cout / kTN);
-  return tiles512 >= 2 * cu_count() ? 512 : 256;
+  const int64_t per = M / conv3x3_wpb(N, H, W, Cout);
+  return per >= 768 ? 512 : 256;
 }
 
 bool conv3x3_ok(const Conv3x3Geom& g) {
   // 32-bit element offsets into x, y and w (the kernel's per-tile piece tables)
-  return g.N > 0 && g.H > 0 && g.W > 0 && g.Cin % kKC == 0 && g.Cout % kTN == 0 && g.vrows > 0 &&
+  return g.N > 0 && g.H > 0 && g.W > 0 && g.Cin % kKC == 0 && g.Cout % kTN == 0 && g.vrows > 0 && g.wpb > 0 &&
          (g.tm == 256 || g.tm == 512) && conv3x3_pieces_per_thread(g) <= kMaxNX &&
          (int64_t)g.N * (g.H + 2) < (1ll << 30) &&
          (int64_t)g.N * g.H * g.W * (g.Cin > g.Cout ? g.Cin : g.Cout) < (1ll << 31) &&
@@ -396,7 +412,7 @@ static void launch_nx(const uint16_t* x, const uint16_t* w, uint16_t* y, const C
   // ResNet-50's stride-1 3x3 shapes (bottleneck conv2 forward; the input gradient of
   // the same layers reads dy with the same width and channel count)
   if constexpr (JB == 4) {
-    if (launch_fixed<6, FLIP, JB, DEPTH, 56, 64>(x, w, y, g, st, grid)) return;
+    if (launch_fixed<7, FLIP, JB, DEPTH, 56, 64>(x, w, y, g, st, grid)) return;
   } else {
     if (launch_fixed<4, FLIP, JB, DEPTH, 28, 128>(x, w, y, g, st, grid)) return;
     if (launch_fixed<4, FLIP, JB, DEPTH, 14, 256>(x, w, y, g, st, grid)) return;
@@ -421,12 +437,8 @@ static void launch_nx(const uint16_t* x, const uint16_t* w, uint16_t* y, const C
 bool launch_conv3x3(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, bool flip,
                     hipStream_t st) {
   if (!conv3x3_ok(g)) return false;
-  const int64_t M = (int64_t)g.N * g.H * g.W;
-  const int tiles = (int)((M + g.tm - 1) / g.tm) * (g.Cout / kTN);
-  // persistent: one workgroup per CU (the LDS image holds one per CU), or one per tile
-  int blocks = cu_count();
-  if (blocks > tiles) blocks = tiles;
-  const dim3 grid((unsigned)((blocks + 7) / 8 * 8));
+  // persistent: one workgroup per (pixel range, output-channel block) -- one per CU
+  const dim3 grid((unsigned)(g.wpb * (g.Cout / kTN)));
   // 512-pixel tiles: twice the accumulators, so two register stages in flight
   if (g.tm == 512) {
     if (flip) launch_nx<true, 4, 2>(x, w, y, g, st, grid);

@@ -315,7 +315,9 @@ struct Conv3x3Geom {
   int N, H, W, Cin, Cout;
   int vrows;  // halo rows of the largest pixel tile (conv3x3_vrows)
   int tm;     // pixels per workgroup tile: 256 or 512 (conv3x3_pick_tm)
+  int wpb;    // workgroups per 64-channel output block = contiguous pixel ranges (conv3x3_wpb)
 };
+int conv3x3_wpb(int N, int H, int W, int Cout);
 int conv3x3_pick_tm(int N, int H, int W, int Cout);
 int conv3x3_vrows(const Conv3x3Geom& g);
 bool conv3x3_ok(const Conv3x3Geom& g);
