@@ -751,7 +751,9 @@ void mlp_resident(Tensor x_u8, Tensor labels, Tensor order, Tensor counters, int
 // 3x3 / stride 1 / pad 1 NHWC bf16 convolution (csrc/conv3x3.hip): x [N, H, W, Cin]
 // and w [Cout, 3, 3, Cin] as contiguous memory; returns y as contiguous [N, H, W, Cout].
 // flip: the input gradient -- x = dy, w = the forward weight [Cin][3][3][Cout]
-Tensor conv3x3(Tensor x, Tensor w, int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, bool flip) {
+// stats: also the next BatchNorm's partial sums of bf16(y) -> {y, part [rows, 2, Cout]}
+std::vector<Tensor> conv3x3_impl(Tensor x, Tensor w, int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
+                                 bool flip, bool stats) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda(), "conv3x3: GPU tensors");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "conv3x3: bf16 inputs");
   TORCH_CHECK(x.is_contiguous() && w.is_contiguous(), "conv3x3: contiguous NHWC / [Cout,3,3,Cin] memory");
@@ -775,12 +777,25 @@ Tensor conv3x3(Tensor x, Tensor w, int64_t N, int64_t H, int64_t W, int64_t Cin,
     g.vrows = it->second;
   }
   TORCH_CHECK(rla::conv3x3_ok(g), "conv3x3: unsupported shape (Cin % 16, Cout % 64, halo tile size)");
+  TORCH_CHECK(!(flip && stats), "conv3x3: statistics are a forward epilogue");
   Tensor y = at::empty({N, H, W, Cout}, x.options());
+  Tensor part;
+  if (stats) part = at::empty({g.wpb, 2, Cout}, x.options().dtype(at::kFloat));
   TORCH_CHECK(rla::launch_conv3x3(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                                   reinterpret_cast<const uint16_t*>(w.data_ptr()),
-                                  reinterpret_cast<uint16_t*>(y.data_ptr()), g, flip, cur_stream(x)),
+                                  reinterpret_cast<uint16_t*>(y.data_ptr()), g, flip, cur_stream(x),
+                                  stats ? part.data_ptr<float>() : nullptr),
               "conv3x3: launch refused");
-  return y;
+  if (stats) return {y, part};
+  return {y};
+}
+
+Tensor conv3x3(Tensor x, Tensor w, int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout, bool flip) {
+  return conv3x3_impl(x, w, N, H, W, Cin, Cout, flip, false)[0];
+}
+
+std::vector<Tensor> conv3x3_stats(Tensor x, Tensor w, int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout) {
+  return conv3x3_impl(x, w, N, H, W, Cin, Cout, false, true);
 }
 
 bool conv3x3_supported(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout) {
@@ -864,6 +879,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv3x3", &conv3x3, "3x3 / stride 1 / pad 1 NHWC bf16 convolution on MFMA -> [N, H, W, Cout]",
         py::arg("x"), py::arg("w"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"),
         py::arg("flip") = false);
+  m.def("conv3x3_stats", &conv3x3_stats,
+        "3x3 / stride 1 / pad 1 forward + BatchNorm partial sums of its bf16 output -> (y, part [rows, 2, Cout])");
   m.def("conv3x3_supported", &conv3x3_supported, "shapes the 3x3 MFMA convolution covers");
   m.attr("ARCH") = "gfx950";
 }

@@ -65,6 +65,7 @@ constexpr int kXElems = kMaxNX * kCvThreads / 2 * kRow;
 constexpr int kWElems = (kNW * kCvThreads / 2 * kRow) > (kNW * kCvThreads / 8 * kFRow)
                             ? (kNW * kCvThreads / 2 * kRow) : (kNW * kCvThreads / 8 * kFRow);
 constexpr int kBufElems = kXElems + kWElems;
+static_assert(2 * kBufElems * 2 >= 4 * 32 * 2 * 65 * 4, "ST reduction image fits the halo buffers");
 
 __device__ __forceinline__ bf16x4 tr4(const __bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(p));
@@ -92,16 +93,25 @@ struct CvSet {
 // 1.53 at 14x14, 200 tiles on 256 CUs at 7x7 -- a 22-24 % makespan loss.  With
 // tiles_n = 8 (7x7) each XCD (block g runs on XCD g % 8) holds one weight block.
 //
+// ST (round 5, forward only): the next BatchNorm's batch statistics in the epilogue.
+// A workgroup owns one 64-channel block, so each lane keeps the sums and sums of
+// squares of its 32 channels' bf16-rounded outputs in registers over all its tiles;
+// at the end the 4 waves x 32 pixel lanes are reduced through LDS in a fixed order
+// into row `jr` of part [wpb][2][Cout] (bn_finalize's layout; deterministic), so
+// the BatchNorm skips its own partial pass over y (one full read of the output).
+//
 // WC / CC (round 5): the image width and input channels as compile-time constants
 // (0 = run time) for the shapes that matter (ResNet's 56/64, 28/128, 14/256, 7/512):
 // each tap's halo offset (r (W + 2) + s) rows is then an immediate of the ds_read
 // (one per-lane base per pixel block, set per tile, instead of a multiply-add per
 // tap and block), and a stage's tile / chunk split is a shift.  Global loads take
 // 32-bit byte offsets from the SGPR base (saddr form: no 64-bit address math).
-template <int NX, bool FLIP, int JB, int DEPTH, int WC = 0, int CC = 0>
+template <int NX, bool FLIP, int JB, int DEPTH, int WC = 0, int CC = 0, bool ST = false>
 __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __restrict__ x,
                                                              const uint16_t* __restrict__ w,
-                                                             uint16_t* __restrict__ y, Conv3x3Geom g) {
+                                                             uint16_t* __restrict__ y, Conv3x3Geom g,
+                                                             float* __restrict__ part) {
+  static_assert(!(ST && FLIP), "statistics are a forward epilogue");
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * kBufElems];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (WC) g.W = WC;
@@ -269,6 +279,15 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
     }
   };
 
+  // ST: this lane's channel sums [i][4 q + e] (channel i 32 + 8 q + 4 (lane >> 5) + e)
+  float bs[2][16], bq[2][16];
+  if constexpr (ST) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) bs[i][k] = bq[i][k] = 0.f;
+  }
+
   // D[co][m]: lane -> pixel (lane & 31) of block j; accumulator k -> channel
   // (k & 3) + 8 (k >> 2) + 4 (lane >> 5) of block i
   auto epilogue = [&](int tile) {
@@ -289,6 +308,14 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = (__bf16)acc[i][j][4 * q + e];
             *reinterpret_cast<bf16x4*>(yo + co) = v;
+            if constexpr (ST) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float f = (float)v[e];  // the statistics of what BatchNorm reads
+                bs[i][4 * q + e] += f;
+                bq[i][4 * q + e] = __builtin_fmaf(f, f, bq[i][4 * q + e]);
+              }
+            }
           }
       }
     }
@@ -323,6 +350,29 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
     for (int d = 0; d < DEPTH; ++d) {
       if (it + d >= nst) break;  // uniform
       step(it + d, d & 1, sets[(d + 1) % DEPTH]);
+    }
+  }
+  if constexpr (ST) {
+    // [wave][pixel lane][stat][64 channels], rows padded to 65 floats (lanes of one
+    // write land on distinct banks); the halo buffers are dead after the last stage
+    constexpr int kSR = 65;
+    float* red = reinterpret_cast<float*>(lds);
+    __syncthreads();
+    const int row = (wave * 32 + (lane & 31)) * 2;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int co = i * 32 + 8 * (k >> 2) + 4 * (lane >> 5) + (k & 3);
+        red[row * kSR + co] = bs[i][k];
+        red[(row + 1) * kSR + co] = bq[i][k];
+      }
+    __syncthreads();
+    if (tid < 2 * kTN) {  // (stat, channel): 128 rows in a fixed order
+      const int st = tid >> 6, c = tid & 63;
+      float a = 0.f;
+      for (int r = 0; r < 4 * 32; ++r) a += red[(2 * r + st) * kSR + c];
+      part[((int64_t)jr * 2 + st) * g.Cout + nblk * kTN + c] = a;
     }
   }
 }
@@ -394,58 +444,61 @@ bool conv3x3_ok(const Conv3x3Geom& g) {
 
 // the compile-time-shape instance (WC, CC) when the layer is one of them and its halo
 // needs exactly NX pieces per thread; false: use the run-time-shape kernel
-template <int NX, bool FLIP, int JB, int DEPTH, int WC, int CC>
+template <int NX, bool FLIP, int JB, int DEPTH, int WC, int CC, bool ST>
 static bool launch_fixed(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, hipStream_t st,
-                         dim3 grid) {
+                         dim3 grid, float* part) {
   static const bool generic = getenv("RLA_CONV3X3_GENERIC") != nullptr;  // A/B switch: run-time-shape kernel
   if (generic || g.W != WC || g.Cin != CC || conv3x3_pieces_per_thread(g) > NX ||
       conv3x3_pieces_per_thread(g) < NX - 1)
     return false;
-  hipLaunchKernelGGL((conv3x3_kernel<NX, FLIP, JB, DEPTH, WC, CC>), grid, dim3(kCvThreads), 0, st, x, w, y, g);
+  hipLaunchKernelGGL((conv3x3_kernel<NX, FLIP, JB, DEPTH, WC, CC, ST>), grid, dim3(kCvThreads), 0, st, x, w, y, g,
+                     part);
   return true;
 }
 
-template <bool FLIP, int JB, int DEPTH>
+template <bool FLIP, int JB, int DEPTH, bool ST>
 static void launch_nx(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, hipStream_t st,
-                      dim3 grid) {
+                      dim3 grid, float* part) {
   const dim3 block(kCvThreads);
   // ResNet-50's stride-1 3x3 shapes (bottleneck conv2 forward; the input gradient of
   // the same layers reads dy with the same width and channel count)
   if constexpr (JB == 4) {
-    if (launch_fixed<7, FLIP, JB, DEPTH, 56, 64>(x, w, y, g, st, grid)) return;
+    if (launch_fixed<7, FLIP, JB, DEPTH, 56, 64, ST>(x, w, y, g, st, grid, part)) return;
   } else {
-    if (launch_fixed<4, FLIP, JB, DEPTH, 28, 128>(x, w, y, g, st, grid)) return;
-    if (launch_fixed<4, FLIP, JB, DEPTH, 14, 256>(x, w, y, g, st, grid)) return;
-    if (launch_fixed<4, FLIP, JB, DEPTH, 7, 512>(x, w, y, g, st, grid)) return;
+    if (launch_fixed<4, FLIP, JB, DEPTH, 28, 128, ST>(x, w, y, g, st, grid, part)) return;
+    if (launch_fixed<4, FLIP, JB, DEPTH, 14, 256, ST>(x, w, y, g, st, grid, part)) return;
+    if (launch_fixed<4, FLIP, JB, DEPTH, 7, 512, ST>(x, w, y, g, st, grid, part)) return;
   }
   switch (conv3x3_pieces_per_thread(g)) {
     case 1: case 2: case 3: case 4:
-      hipLaunchKernelGGL((conv3x3_kernel<4, FLIP, JB, DEPTH>), grid, block, 0, st, x, w, y, g);
+      hipLaunchKernelGGL((conv3x3_kernel<4, FLIP, JB, DEPTH, 0, 0, ST>), grid, block, 0, st, x, w, y, g, part);
       break;
     case 5:
-      hipLaunchKernelGGL((conv3x3_kernel<5, FLIP, JB, DEPTH>), grid, block, 0, st, x, w, y, g);
+      hipLaunchKernelGGL((conv3x3_kernel<5, FLIP, JB, DEPTH, 0, 0, ST>), grid, block, 0, st, x, w, y, g, part);
       break;
     case 6:
-      hipLaunchKernelGGL((conv3x3_kernel<6, FLIP, JB, DEPTH>), grid, block, 0, st, x, w, y, g);
+      hipLaunchKernelGGL((conv3x3_kernel<6, FLIP, JB, DEPTH, 0, 0, ST>), grid, block, 0, st, x, w, y, g, part);
       break;
     default:
-      hipLaunchKernelGGL((conv3x3_kernel<7, FLIP, JB, DEPTH>), grid, block, 0, st, x, w, y, g);
+      hipLaunchKernelGGL((conv3x3_kernel<7, FLIP, JB, DEPTH, 0, 0, ST>), grid, block, 0, st, x, w, y, g, part);
       break;
   }
 }
 
 bool launch_conv3x3(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, bool flip,
-                    hipStream_t st) {
-  if (!conv3x3_ok(g)) return false;
+                    hipStream_t st, float* part) {
+  if (!conv3x3_ok(g) || (flip && part)) return false;
   // persistent: one workgroup per (pixel range, output-channel block) -- one per CU
   const dim3 grid((unsigned)(g.wpb * (g.Cout / kTN)));
   // 512-pixel tiles: twice the accumulators, so two register stages in flight
   if (g.tm == 512) {
-    if (flip) launch_nx<true, 4, 2>(x, w, y, g, st, grid);
-    else launch_nx<false, 4, 2>(x, w, y, g, st, grid);
+    if (flip) launch_nx<true, 4, 2, false>(x, w, y, g, st, grid, nullptr);
+    else if (part) launch_nx<false, 4, 2, true>(x, w, y, g, st, grid, part);
+    else launch_nx<false, 4, 2, false>(x, w, y, g, st, grid, nullptr);
   } else {
-    if (flip) launch_nx<true, 2, 4>(x, w, y, g, st, grid);
-    else launch_nx<false, 2, 4>(x, w, y, g, st, grid);
+    if (flip) launch_nx<true, 2, 4, false>(x, w, y, g, st, grid, nullptr);
+    else if (part) launch_nx<false, 2, 4, true>(x, w, y, g, st, grid, part);
+    else launch_nx<false, 2, 4, false>(x, w, y, g, st, grid, nullptr);
   }
   return true;
 }

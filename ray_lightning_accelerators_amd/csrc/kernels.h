@@ -323,6 +323,7 @@ int conv3x3_vrows(const Conv3x3Geom& g);
 bool conv3x3_ok(const Conv3x3Geom& g);
 // flip: input gradient -- x is dy [N, H, W, Cin], w the FORWARD weight [Cin][3][3][Cout]
 // (Cin = the forward's output channels), y is dx [N, H, W, Cout]
+// part (forward only, or null): BatchNorm partial sums of bf16(y), [g.wpb][2][Cout] fp32
 bool launch_conv3x3(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, bool flip,
-                    hipStream_t stream);
+                    hipStream_t stream, float* part = nullptr);
 }  // namespace rla

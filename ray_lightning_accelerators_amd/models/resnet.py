@@ -72,10 +72,10 @@ class Bottleneck(nn.Module):
 
     @staticmethod
     def _conv_bn(conv, bn, x, **kw):
-        """bn(conv(x)) for a 1x1 conv: the conv may compute bn's batch statistics in its
-        epilogue (ops.conv.BNStats; bn then skips its partial pass over the output)."""
+        """bn(conv(x)): a stride-1 1x1 or 3x3 conv may compute bn's batch statistics in
+        its epilogue (ops.conv.BNStats; bn then skips its partial pass over the output)."""
         fork = kw.pop("fork", None)
-        if isinstance(conv, Conv1x1NHWC) and bn.training:
+        if isinstance(conv, (Conv1x1NHWC, ConvBF16)) and bn.training:
             st = BNStats()
             return bn(conv(x, fork=fork, bn_stats=st), bn_stats=st, **kw)
         return bn(conv(x, fork=fork) if fork is not None else conv(x), **kw)
@@ -86,11 +86,11 @@ class Bottleneck(nn.Module):
             # one tensor (ops.conv.GradFork) instead of an autograd add of two
             fork = GradFork()
             idt = self._conv_bn(self.downsample[0], self.downsample[1], x, fork=fork)
-            out = self.bn2(self.conv2(self._conv_bn(self.conv1, self.bn1, x, fork=fork)))
+            out = self._conv_bn(self.conv2, self.bn2, self._conv_bn(self.conv1, self.bn1, x, fork=fork))
             return self._conv_bn(self.conv3, self.bn3, out, residual=idt, residual_is_ancestor=False)
         idt = x if self.downsample is None else self.downsample(x)
         if self.fused_bn:
-            out = self.bn2(self.conv2(self._conv_bn(self.conv1, self.bn1, x)))
+            out = self._conv_bn(self.conv2, self.bn2, self._conv_bn(self.conv1, self.bn1, x))
             # identity shortcut: x is an ancestor of conv3's output, so bn3 may fold
             # its residual gradient into the previous block's bn3 backward (ops/bn.py)
             return self._conv_bn(self.conv3, self.bn3, out, residual=idt,

@@ -162,6 +162,22 @@ def conv3x3_hip(x: torch.Tensor, wb: torch.Tensor) -> torch.Tensor:
     return y.permute(0, 3, 1, 2)
 
 
+def conv3x3_stats_hip(x: torch.Tensor, wb: torch.Tensor):
+    """:func:`conv3x3_hip` plus the per-channel partial sums of its bf16 output from the
+    epilogue (csrc/conv3x3.hip ST): returns (y channels_last, part [rows, 2, Cout])."""
+    from . import require
+
+    n, cin, h, w = x.shape
+    cout = wb.size(0)
+    y, part = require().conv3x3_stats(x.permute(0, 2, 3, 1), wb.permute(0, 2, 3, 1), n, h, w, cin, cout)
+    return y.permute(0, 3, 1, 2), part
+
+
+def conv3x3_stats_enabled() -> bool:
+    """``RLA_CONV3X3_STATS=off`` keeps the 3x3 forward's BatchNorm statistics in BN's own pass."""
+    return os.environ.get("RLA_CONV3X3_STATS", "auto") != "off"
+
+
 def conv3x3_dgrad_hip(dy: torch.Tensor, wb: torch.Tensor) -> torch.Tensor:
     """Input gradient of a 3x3 / stride 1 / pad 1 convolution = the same convolution
     of ``dy`` with the weight flipped in both taps and transposed in channels; the
@@ -413,16 +429,26 @@ class _ConvNHWCFn(torch.autograd.Function):
     device time.  The weight gradient reaches the fp32 master weight in fp32."""
 
     @staticmethod
-    def forward(ctx, x, weight, wb, stride, padding, fork=None):
+    def forward(ctx, x, weight, wb, stride, padding, fork=None, bn_stats=None):
         ctx.c3 = conv3x3_ok(x, wb, stride, padding)
         be = "miopen"
         if ctx.c3:
             key = (x.size(0) * x.size(2) * x.size(3), x.size(1), wb.size(0), 3, 3, 1, 1)
-            be = _pick("fwd_kxk", key, {
-                "miopen": lambda: _conv(x, wb, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1),
-                "hip": lambda: conv3x3_hip(x, wb),
-            })
-        if be == "hip":
+            if bn_stats is not None and conv3x3_stats_enabled():
+                # the next BatchNorm's statistics: in this kernel's epilogue, or the
+                # library forward + BN's own partial pass -- whichever is faster
+                be = _pick("fwd_kxk_st", key, {
+                    "miopen": lambda: _bn_partial(_conv(x, wb, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1)),
+                    "hip_st": lambda: conv3x3_stats_hip(x, wb),
+                })
+            else:
+                be = _pick("fwd_kxk", key, {
+                    "miopen": lambda: _conv(x, wb, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1),
+                    "hip": lambda: conv3x3_hip(x, wb),
+                })
+        if be == "hip_st":
+            y, bn_stats.part = conv3x3_stats_hip(x, wb)
+        elif be == "hip":
             y = conv3x3_hip(x, wb)
         else:
             y = _conv(x, wb, None, list(stride), list(padding), [1, 1], False, [0, 0], 1)
@@ -485,7 +511,7 @@ class _ConvNHWCFn(torch.autograd.Function):
             dxm, dw = _conv_bwd(dy, x, wb, None, list(stride), list(padding), [1, 1], False, [0, 0], 1, mask)[:2]
             if need_dx:
                 dx = _fork_dx(fork, lambda: dxm, None)
-            return dx, dw.float(), None, None, None, None
+            return dx, dw.float(), None, None, None, None, None
         if need_dx:
             dx = _fork_dx(fork, lambda: _conv_bwd(dy, x, wb, None, list(stride), list(padding), [1, 1], False,
                                                   [0, 0], 1, [True, False, False])[0], None)
@@ -493,7 +519,7 @@ class _ConvNHWCFn(torch.autograd.Function):
             dw = wgrad_hip(dy, x, (kh, kw), stride, padding)
         elif be == "hip_gen":
             dw = wgrad_hip(dy, x, (kh, kw), stride, padding, algo=1)
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
 def kxk_fast_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
@@ -504,8 +530,10 @@ def kxk_fast_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
             and wgrad_ok(conv.in_channels, conv.out_channels))
 
 
-def conv_nhwc(x: torch.Tensor, conv: nn.Conv2d, wb: torch.Tensor, fork: Optional[GradFork] = None) -> torch.Tensor:
+def conv_nhwc(x: torch.Tensor, conv: nn.Conv2d, wb: torch.Tensor, fork: Optional[GradFork] = None,
+              bn_stats: Optional[BNStats] = None) -> torch.Tensor:
     """``conv(x)`` with the bf16 weight ``wb`` (the arena shadow), the weight gradient
-    going to ``conv.weight`` in fp32 (``fork``: see :class:`GradFork`)."""
+    going to ``conv.weight`` in fp32 (``fork``: see :class:`GradFork`; ``bn_stats``:
+    see :class:`BNStats`, filled only by the 3x3 stride-1 MFMA forward)."""
     stats["fast"] += 1
-    return _ConvNHWCFn.apply(x, conv.weight, wb, conv.stride, conv.padding, fork)
+    return _ConvNHWCFn.apply(x, conv.weight, wb, conv.stride, conv.padding, fork, bn_stats)

@@ -67,8 +67,10 @@ class ConvBF16(nn.Conv2d):
 
     _rla_reads_bf16_shadow = True
 
-    def forward(self, x: torch.Tensor, fork=None) -> torch.Tensor:
-        """``fork``: an ops.conv.GradFork shared with another consumer of ``x`` (fast path only)."""
+    def forward(self, x: torch.Tensor, fork=None, bn_stats=None) -> torch.Tensor:
+        """``fork``: an ops.conv.GradFork shared with another consumer of ``x`` (fast path only).
+        ``bn_stats``: an ops.conv.BNStats the 3x3 MFMA forward may fill (the next
+        BatchNorm's batch statistics from its epilogue)."""
         if x.is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16 \
                 and self.padding_mode == "zeros":
             wb = bf16_weight(self.weight)
@@ -80,7 +82,7 @@ class ConvBF16(nn.Conv2d):
                     # MIOpen forward / dgrad, weight gradient from the MFMA kernel when
                     # it is the faster one (ops/conv.py)
                     stats["shadow"] += 1
-                    return conv_nhwc(xb, self, wb, fork)
+                    return conv_nhwc(xb, self, wb, fork, bn_stats)
             w = bf16_param(self.weight)
             if w is not None:
                 b = self.bias.to(torch.bfloat16) if self.bias is not None else None

@@ -118,6 +118,10 @@ def _trajectory(rank, world, port, q, steps, wire, bs):
     from ray_lightning_accelerators_amd.parallel.fused_optim import fuse_optimizer
 
     dev = torch.device("cuda", 0)
+    # the same kernels in both runs (no per-shape timing that could pick differently):
+    # the two trajectories then differ by the gradient wire alone
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    torch.backends.cudnn.deterministic = True
     comm_mod._default = NativeCommunicator(use_rccl=False, use_xgmi=True, xgmi_bytes=2 << 20,
                                            twoshot_bytes=64 << 20, spin_limit=1 << 26)
     torch.manual_seed(0)
@@ -126,8 +130,11 @@ def _trajectory(rank, world, port, q, steps, wire, bs):
     arena.enable_bf16_shadow(model)
     sync = GradSynchronizer(model, arena, bucket_cap_mb=8.0, grad_dtype=wire, average_in_optimizer=True)
     sync.broadcast_parameters(0)
-    opt = fuse_optimizer(torch.optim.SGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-5), arena,
-                         grad_scale_fn=lambda: sync.grad_scale)
+    # lr 0.1 x (global batch 2 bs / 256), linear warm-up over the first 30 steps
+    base_lr = 0.1 * 2 * bs / 256
+    sgd = torch.optim.SGD(model.parameters(), lr=base_lr, momentum=0.9, weight_decay=5e-5)
+    opt = fuse_optimizer(sgd, arena, grad_scale_fn=lambda: sync.grad_scale)
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, lambda i: min(1.0, (i + 1) / 30))
     data = _Learnable(4096, 64, seed=100 + rank, device=dev)
     losses = []
     t0 = time.time()
@@ -141,6 +148,7 @@ def _trajectory(rank, world, port, q, steps, wire, bs):
         sync.finish()
         opt.step()
         opt.zero_grad()
+        sched.step()
         losses.append(loss.detach())
     torch.cuda.synchronize()
     comm_mod._default.check()

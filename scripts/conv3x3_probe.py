@@ -1,5 +1,6 @@
 """Device time of ResNet-50's stride-1 3x3 convolutions (batch 128, bf16, NHWC):
-the MFMA kernel (csrc/conv3x3.hip) against MIOpen, forward and input gradient.
+the MFMA kernel (csrc/conv3x3.hip) against MIOpen, forward, forward + BatchNorm
+statistics (the kernel's epilogue vs MIOpen + the partial pass) and input gradient.
 One JSON line per (shape, op).
 
   python scripts/conv3x3_probe.py [--batch 128] [--reps 20]
@@ -11,7 +12,8 @@ import sys
 import torch
 
 sys.path.insert(0, ".")
-from ray_lightning_accelerators_amd.ops.conv import conv3x3_dgrad_hip, conv3x3_hip  # noqa: E402
+from ray_lightning_accelerators_amd import ops  # noqa: E402
+from ray_lightning_accelerators_amd.ops.conv import conv3x3_dgrad_hip, conv3x3_hip, conv3x3_stats_hip  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=128)
@@ -52,6 +54,12 @@ for hw, c in ((56, 64), (28, 128), (14, 256), (7, 512)):
     arms = {
         "fwd_miopen": lambda: conv(x, wb, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1),
         "fwd_hip": lambda: conv3x3_hip(x, wb),
+        # with the next BatchNorm's statistics: the library forward + BN's partial pass
+        # vs the kernel's epilogue (what ops.conv picks between for a bn2-feeding conv2)
+        "fwd_st_miopen": lambda: ops.require().bn_partial(
+            conv(x, wb, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1).permute(0, 2, 3, 1), None, None, c, 0,
+            False, None),
+        "fwd_st_hip": lambda: conv3x3_stats_hip(x, wb),
         "dgrad_miopen": lambda: conv_bwd(dy, x, wb, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
                                          [True, False, False])[0],
         "dgrad_hip": lambda: conv3x3_dgrad_hip(dy, wb),

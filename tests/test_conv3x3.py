@@ -111,3 +111,63 @@ def test_conv_bf16_layer_routes_through_kernel(monkeypatch):
             assert calls["fwd"] >= 1 and calls["dgrad"] >= 1
     assert _rel(outs["hip"][0], outs["miopen"][0]) < 1e-2
     assert _rel(outs["hip"][1], outs["miopen"][1]) < 2e-2
+
+
+@gpu
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv3x3_stats_epilogue(shape, tile_px):
+    """The forward's BatchNorm partial sums (ST epilogue): same y as the plain kernel,
+    and the rows sum to the per-channel sum / sum of squares of the bf16 output."""
+    from ray_lightning_accelerators_amd.ops.conv import conv3x3_hip, conv3x3_stats_hip
+
+    n, h, w, cin, cout = shape
+    torch.manual_seed(2)
+    dev = torch.device("cuda", 0)
+    x = torch.randn(n, cin, h, w, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wb = (torch.randn(cout, cin, 3, 3, device=dev) / (3 * cin ** 0.5)).to(torch.bfloat16)
+    wb = wb.contiguous(memory_format=torch.channels_last)
+    y, part = conv3x3_stats_hip(x, wb)
+    assert torch.equal(y, conv3x3_hip(x, wb))
+    assert part.dim() == 3 and part.size(1) == 2 and part.size(2) == cout and part.dtype == torch.float32
+    yf = y.double().permute(0, 2, 3, 1).reshape(-1, cout)
+    s, q = part.double().sum(0)
+    torch.testing.assert_close(s, yf.sum(0), rtol=1e-4, atol=1e-3 * yf.abs().sum(0).max().item() / yf.size(0) ** 0.5)
+    torch.testing.assert_close(q, yf.square().sum(0), rtol=1e-4, atol=1e-3)
+
+
+@gpu
+def test_resnet_block_bn2_uses_conv3x3_stats(monkeypatch):
+    """A bottleneck's conv2 hands bn2 its epilogue statistics (RLA_CONV3X3_STATS auto,
+    the kernel pinned): the block's output and gradients match the path where bn2 runs
+    its own partial pass."""
+    from ray_lightning_accelerators_amd.models.resnet import Bottleneck
+    from ray_lightning_accelerators_amd.ops import conv as C
+    from ray_lightning_accelerators_amd.parallel.arena import ParamArena
+
+    dev = torch.device("cuda", 0)
+    calls = {"st": 0}
+    real = C.conv3x3_stats_hip
+
+    def st(*a, **k):
+        calls["st"] += 1
+        return real(*a, **k)
+
+    monkeypatch.setattr(C, "conv3x3_stats_hip", st)
+    monkeypatch.setenv("RLA_CONV1X1", "hip_st")  # pins the stats kernel in _pick (other ops: auto)
+    outs = {}
+    for mode in ("auto", "off"):
+        monkeypatch.setenv("RLA_CONV3X3_STATS", mode)
+        torch.manual_seed(0)
+        blk = Bottleneck(256, 64, fused_bn=True).to(dev).to(memory_format=torch.channels_last)
+        arena = ParamArena(blk)
+        arena.enable_bf16_shadow(blk)
+        torch.manual_seed(1)
+        x = torch.randn(4, 256, 14, 14, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        x.requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = blk(x)
+        y.float().square().mean().backward()
+        outs[mode] = (y.detach().float(), x.grad.float(), blk.conv2.weight.grad.clone(), blk.bn2.running_var.clone())
+    assert calls["st"] >= 1
+    for a, b in zip(outs["auto"], outs["off"]):
+        assert _rel(a, b.float()) < 2e-2, _rel(a, b.float())
