@@ -8,7 +8,9 @@ kernel of the same rank was also running (overlapped with backward), and the
 EXPOSED time -- from the end of the last compute kernel before the SGD to the SGD's
 start, which is what the step pays for communication on the critical path.
 
-Usage: python scripts/comm_overlap_report.py TRACE_DIR [--last 10]
+Usage: python scripts/comm_overlap_report.py TRACE_DIR [--last 10] [--timeline OUT_PREFIX]
+(--timeline: per rank, the last step's kernels as CSV -- offset from the step start,
+duration, comm or compute -- small enough to commit next to the summary)
 """
 from __future__ import annotations
 
@@ -59,6 +61,21 @@ def _merge(iv):
     return out
 
 
+def timeline(path, out):
+    rows = _load(path)
+    sgd = [i for i, (_, _, n) in enumerate(rows) if "sgd_kernel" in n]
+    if len(sgd) < 2:
+        return
+    a, b = sgd[-2], sgd[-1]
+    t0 = rows[a][1]
+    with open(out, "w") as f:
+        f.write("start_us,dur_us,kind,kernel\n")
+        for s, e, n in rows[a + 1:b + 1]:
+            short = n.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+            short = short.replace(",", ";")[:120]
+            f.write(f"{(s - t0) / 1e3:.1f},{(e - s) / 1e3:.1f},{'comm' if _is_comm(n) else 'compute'},{short}\n")
+
+
 def report(path, last):
     rows = _load(path)
     sgd = [i for i, (_, _, n) in enumerate(rows) if "sgd_kernel" in n]
@@ -88,8 +105,12 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("trace_dir")
     ap.add_argument("--last", type=int, default=10)
+    ap.add_argument("--timeline", default=None)
     args = ap.parse_args(argv)
     paths = sorted(glob.glob(os.path.join(args.trace_dir, "**", "*kernel_trace.csv"), recursive=True))
+    for i, p in enumerate(paths):
+        if args.timeline:
+            timeline(p, f"{args.timeline}_{i}.csv")
     for p in paths:
         r = report(p, args.last)
         if r is not None:

@@ -284,3 +284,35 @@ def test_owner_state_consolidated_at_validation_end_not_in_dump(tmpdir):
     trainer.global_step = 8
     trainer._optimizer_state_dict(opt)
     assert FakeFused.calls == 2
+
+
+def test_owner_state_consolidated_before_every_save_without_validation(tmpdir, monkeypatch):
+    """with no validation loop the checkpoint callbacks save at every
+    training-epoch end and at train end.  The owner-protocol consolidation (a
+    collective) must run on every rank BEFORE each of those save points, never only
+    inside rank 0's dump."""
+    events = []
+    real = pl.Trainer._consolidate_optimizer_state
+
+    def consolidate(self):
+        events.append(("consolidate", self.global_step))
+        real(self)
+
+    monkeypatch.setattr(pl.Trainer, "_consolidate_optimizer_state", consolidate)
+
+    class Ck(ModelCheckpoint):
+        def on_validation_end(self, trainer, pl_module):
+            events.append(("save", trainer.global_step))
+            super().on_validation_end(trainer, pl_module)
+
+        def on_train_end(self, trainer, pl_module):
+            events.append(("train_end", trainer.global_step))
+            super().on_train_end(trainer, pl_module)
+
+    trainer = pl.Trainer(default_root_dir=str(tmpdir), max_epochs=2, limit_train_batches=2, limit_val_batches=0,
+                         callbacks=[Ck(dirpath=str(tmpdir))])
+    trainer.fit(BoringModel())
+    saves = [i for i, e in enumerate(events) if e[0] in ("save", "train_end")]
+    assert len(saves) == 3, events
+    for i in saves:
+        assert i > 0 and events[i - 1] == ("consolidate", events[i][1]), events
