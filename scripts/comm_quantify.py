@@ -104,7 +104,7 @@ class _Learnable:
         return x, self.y[idx]
 
 
-def _trajectory(rank, world, port, q, steps, wire, bs):
+def _trajectory(rank, world, port, q, steps, wire, bs, seed=0):
     import torch
     import torch.distributed as dist
     import torch.nn.functional as F
@@ -135,7 +135,7 @@ def _trajectory(rank, world, port, q, steps, wire, bs):
     sgd = torch.optim.SGD(model.parameters(), lr=base_lr, momentum=0.9, weight_decay=5e-5)
     opt = fuse_optimizer(sgd, arena, grad_scale_fn=lambda: sync.grad_scale)
     sched = torch.optim.lr_scheduler.LambdaLR(opt, lambda i: min(1.0, (i + 1) / 30))
-    data = _Learnable(4096, 64, seed=100 + rank, device=dev)
+    data = _Learnable(4096, 64, seed=100 + rank + 1000 * seed, device=dev)
     losses = []
     t0 = time.time()
     for i in range(steps):
@@ -193,22 +193,30 @@ def main(argv=None):
         return 0
     import torch
 
+    # two data seeds per wire: the fp32-vs-bf16 gap of one seed is judged against the
+    # seed-to-seed spread of the SAME wire (training from scratch is chaotic: any
+    # difference in the first steps grows into a different trajectory)
     res = {}
-    for wire in ("fp32", "bf16"):
-        out = _spawn(_trajectory, 2, args.steps, wire, args.batch)
-        assert torch.equal(out[0]["params"], out[1]["params"]), "replicas diverged"
-        res[wire] = out
-        print(json.dumps({"wire": wire, "steps": args.steps, "first_loss": out[0]["losses"][0],
-                          "last10_mean_loss": sum(out[0]["losses"][-10:]) / 10, "seconds": round(out[0]["s"], 1),
-                          "replicas_equal": True}), flush=True)
-    a, b = res["fp32"][0], res["bf16"][0]
-    la, lb = torch.tensor(a["losses"]), torch.tensor(b["losses"])
-    dp = (a["params"] - b["params"]).norm() / a["params"].norm()
-    print(json.dumps({"compare": "bf16 wire vs fp32 wire", "max_abs_loss_diff": float((la - lb).abs().max()),
-                      "mean_abs_loss_diff_last50": float((la[-50:] - lb[-50:]).abs().mean()),
-                      "final_param_rel_diff": float(dp),
-                      "losses_every_25": {"fp32": [round(v, 4) for v in a["losses"][::25]],
-                                          "bf16": [round(v, 4) for v in b["losses"][::25]]}}), flush=True)
+    for seed in (0, 1):
+        for wire in ("fp32", "bf16"):
+            out = _spawn(_trajectory, 2, args.steps, wire, args.batch, seed)
+            assert torch.equal(out[0]["params"], out[1]["params"]), "replicas diverged"
+            res[wire, seed] = out[0]
+            ls = out[0]["losses"]
+            print(json.dumps({"wire": wire, "seed": seed, "steps": args.steps, "first_loss": ls[0],
+                              "last50_mean_loss": sum(ls[-50:]) / 50, "seconds": round(out[0]["s"], 1),
+                              "replicas_equal": True,
+                              "losses_every_25": [round(v, 4) for v in ls[::25]]}), flush=True)
+
+    def gap(a, b):
+        la, lb = torch.tensor(a["losses"]), torch.tensor(b["losses"])
+        return {"mean_abs_loss_diff_last50": round(float((la[-50:] - lb[-50:]).abs().mean()), 4),
+                "final_param_rel_diff": round(float((a["params"] - b["params"]).norm() / a["params"].norm()), 4)}
+
+    for seed in (0, 1):
+        print(json.dumps(dict(compare=f"bf16 vs fp32 wire, seed {seed}", **gap(res["fp32", seed], res["bf16", seed]))))
+    print(json.dumps(dict(compare="fp32 seed 0 vs fp32 seed 1 (natural spread)", **gap(res["fp32", 0], res["fp32", 1]))))
+    print(json.dumps(dict(compare="bf16 seed 0 vs bf16 seed 1 (natural spread)", **gap(res["bf16", 0], res["bf16", 1]))))
     return 0
 
 
