@@ -508,8 +508,20 @@ Tensor bn_bwd_finalize(Tensor part, double count, optional<Tensor> weight, Tenso
 }
 
 // x: [N, H, W, C] bf16 (NHWC view of a channels_last tensor); returns (y, argmax bytes)
-std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t s, int64_t pad) {
+std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t s, int64_t pad, c10::optional<Tensor> bn_ss,
+                                c10::optional<Tensor> nbt_inc) {
   check_dev(x, "x", at::kBFloat16);
+  const float* ss = nullptr;
+  int64_t* nbt = nullptr;
+  if (bn_ss.has_value() && bn_ss->defined()) {
+    check_dev(*bn_ss, "bn_ss", at::kFloat);
+    TORCH_CHECK(bn_ss->is_contiguous() && bn_ss->numel() == 4 * x.size(3), "maxpool: bn_ss must be [4, C]");
+    ss = bn_ss->data_ptr<float>();
+  }
+  if (nbt_inc.has_value() && nbt_inc->defined()) {
+    TORCH_CHECK(nbt_inc->is_cuda() && nbt_inc->scalar_type() == at::kLong, "maxpool: nbt_inc int64 on the GPU");
+    nbt = nbt_inc->data_ptr<int64_t>();
+  }
   TORCH_CHECK(x.dim() == 4 && x.is_contiguous(), "maxpool: x must be a contiguous NHWC [N, H, W, C] view");
   const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   TORCH_CHECK(C % 8 == 0 && k >= 1 && s >= 1 && pad >= 0 && 2 * pad <= k, "maxpool: unsupported geometry");
@@ -520,7 +532,8 @@ std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t s, int64_t pad) {
   Tensor arg = at::empty({N, OH, OW, C}, x.options().dtype(at::kByte));
   TORCH_CHECK(rla::launch_maxpool_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                                       reinterpret_cast<uint16_t*>(y.data_ptr()), arg.data_ptr<uint8_t>(), (int)N, (int)H,
-                                      (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)pad, cur_stream(x)) == 0,
+                                      (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)pad, cur_stream(x), ss,
+                                      nbt) == 0,
               "maxpool forward launch failed");
   return {y, arg};
 }
@@ -798,6 +811,55 @@ std::vector<Tensor> conv3x3_stats(Tensor x, Tensor w, int64_t N, int64_t H, int6
   return conv3x3_impl(x, w, N, H, W, Cin, Cout, false, true);
 }
 
+// ResNet stem forward: x [N, H, W, 3] NHWC bf16, w [64, 7, 7, 3] bf16 -> {y [N, OH, OW, 64]} or, with
+// stats, {y, part [rows, 2, 64]} (the next BatchNorm's partial sums of bf16(y))
+std::vector<Tensor> stem_fwd(Tensor x, Tensor w, bool stats) {
+  TORCH_CHECK(x.is_cuda() && w.is_cuda(), "stem: GPU tensors");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "stem: bf16 inputs");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) == 3 && x.is_contiguous(), "stem: x must be contiguous [N, H, W, 3]");
+  TORCH_CHECK(w.numel() == 64 * 147 && w.is_contiguous(), "stem: w must be contiguous [64, 7, 7, 3]");
+  const rla::StemGeom g{(int)x.size(0), (int)x.size(1), (int)x.size(2), (int)((x.size(1) - 1) / 2 + 1),
+                        (int)((x.size(2) - 1) / 2 + 1)};
+  TORCH_CHECK(rla::stem_ok(g), "stem: unsupported shape (W even, W <= 256)");
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor y = at::empty({g.N, g.OH, g.OW, 64}, x.options());
+  Tensor part;
+  if (stats) part = at::empty({rla::stem_grid(g), 2, 64}, x.options().dtype(at::kFloat));
+  TORCH_CHECK(rla::launch_stem_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                   reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                                   reinterpret_cast<uint16_t*>(y.data_ptr()), stats ? part.data_ptr<float>() : nullptr,
+                                   g, cur_stream(x)),
+              "stem: launch refused");
+  if (stats) return {y, part};
+  return {y};
+}
+
+// ResNet stem weight gradient: x [N, H, W, 3], dy [N, OH, OW, 64] (NHWC bf16) -> fp32 [64, 7, 7, 3]
+Tensor stem_wgrad(Tensor x, Tensor dy) {
+  TORCH_CHECK(x.is_cuda() && dy.is_cuda(), "stem_wgrad: GPU tensors");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16, "stem_wgrad: bf16 inputs");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) == 3 && x.is_contiguous(), "stem_wgrad: x must be contiguous [N, H, W, 3]");
+  const rla::StemGeom g{(int)x.size(0), (int)x.size(1), (int)x.size(2), (int)((x.size(1) - 1) / 2 + 1),
+                        (int)((x.size(2) - 1) / 2 + 1)};
+  TORCH_CHECK(rla::stem_ok(g), "stem_wgrad: unsupported shape");
+  TORCH_CHECK(dy.dim() == 4 && dy.size(0) == g.N && dy.size(1) == g.OH && dy.size(2) == g.OW && dy.size(3) == 64 &&
+                  dy.is_contiguous(),
+              "stem_wgrad: dy must be contiguous [N, OH, OW, 64]");
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor part = at::empty({rla::stem_grid(g), 64, 224}, x.options().dtype(at::kFloat));
+  Tensor dw = at::empty({64, 7, 7, 3}, x.options().dtype(at::kFloat));
+  TORCH_CHECK(rla::launch_stem_wgrad(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                     reinterpret_cast<const uint16_t*>(dy.data_ptr()), part.data_ptr<float>(),
+                                     dw.data_ptr<float>(), g, cur_stream(x)),
+              "stem_wgrad: launch refused");
+  return dw;
+}
+
+bool stem_supported(int64_t N, int64_t H, int64_t W) {
+  const rla::StemGeom g{(int)N, (int)H, (int)W, (int)((H - 1) / 2 + 1), (int)((W - 1) / 2 + 1)};
+  return rla::stem_ok(g);
+}
+
 bool conv3x3_supported(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout) {
   if (N <= 0 || H <= 0 || W <= 0 || Cout <= 0 || N * (H + 2) * (W + 2) >= (int64_t(1) << 30)) return false;
   rla::Conv3x3Geom g{(int)N, (int)H, (int)W, (int)Cin, (int)Cout, 0,
@@ -856,7 +918,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "1x1 conv input gradient fused with the previous BatchNorm's backward partial -> (d, part)");
   m.def("conv1x1_bn_bwd_ok", [](int64_t M, int64_t K, int64_t N) { return rla::conv1x1_bn_bwd_ok(M, (int)K, (int)N); });
   m.def("conv1x1_stats_ok", [](int64_t M, int64_t K, int64_t N) { return rla::conv1x1_stats_ok(M, (int)K, (int)N); });
-  m.def("maxpool_fwd", &maxpool_fwd, "NHWC bf16 max pool -> (y, one-byte window argmax)");
+  m.def("maxpool_fwd", &maxpool_fwd,
+        "NHWC bf16 max pool -> (y, one-byte window argmax); bn_ss: pool bf16(relu(x * scale + shift)) instead",
+        py::arg("x"), py::arg("k"), py::arg("s"), py::arg("pad"), py::arg("bn_ss") = py::none(),
+        py::arg("nbt_inc") = py::none());
   m.def("gap_bwd", &gap_bwd, "global average pool backward over NHWC rows (16-byte stores)");
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max pool backward (gather through the argmax bytes)");
   m.def("bn_bwd_apply", &bn_bwd_apply, "fused BN backward apply: dx (+ dres = relu-masked dy)", py::arg("x"),
@@ -882,5 +947,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv3x3_stats", &conv3x3_stats,
         "3x3 / stride 1 / pad 1 forward + BatchNorm partial sums of its bf16 output -> (y, part [rows, 2, Cout])");
   m.def("conv3x3_supported", &conv3x3_supported, "shapes the 3x3 MFMA convolution covers");
+  m.def("stem_fwd", &stem_fwd, "ResNet stem 7x7/s2 conv (3 -> 64) on MFMA [+ BatchNorm partial sums]");
+  m.def("stem_supported", &stem_supported, "input shapes the stem kernel covers");
+  m.def("stem_wgrad", &stem_wgrad, "ResNet stem weight gradient on MFMA -> fp32 [64, 7, 7, 3] (channels_last order)");
   m.attr("ARCH") = "gfx950";
 }

@@ -48,8 +48,11 @@ void launch_sumsq(const float* x, int64_t n, float* out, hipStream_t stream);
 constexpr int kBnThreads = 256;
 
 // NHWC bf16 max pooling with a one-byte window argmax (csrc/pool.hip)
+// bn_ss (or null): x is a BatchNorm's input, pooled as bf16(relu(x * ss[2] + ss[3])) (the stem's
+// BatchNorm + ReLU folded into the pool); nbt_inc as launch_bn_apply's
 int launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int OH, int OW,
-                       int k, int s, int pad, hipStream_t stream);
+                       int k, int s, int pad, hipStream_t stream, const float* bn_ss = nullptr,
+                       int64_t* nbt_inc = nullptr);
 int launch_maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int H, int W, int C, int OH,
                        int OW, int k, int s, int pad, hipStream_t stream);
 // global average pool backward over NHWC rows: dx[n][p][c] = dy[n][c] / HW
@@ -326,4 +329,17 @@ bool conv3x3_ok(const Conv3x3Geom& g);
 // part (forward only, or null): BatchNorm partial sums of bf16(y), [g.wpb][2][Cout] fp32
 bool launch_conv3x3(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, bool flip,
                     hipStream_t stream, float* part = nullptr);
+
+// ResNet stem: 7x7 / stride 2 / pad 3 convolution, 3 -> 64 channels, NHWC bf16 (csrc/stem.hip);
+// part (or null): BatchNorm partial sums of bf16(y), [stem_grid(g)][2][64] fp32
+struct StemGeom {
+  int N, H, W, OH, OW;
+};
+bool stem_ok(const StemGeom& g);
+int stem_grid(const StemGeom& g);
+bool launch_stem_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, const StemGeom& g,
+                     hipStream_t stream);
+// weight gradient: dy [N, OH, OW, 64] bf16 -> dw [64][7][7][3] fp32; part: [stem_grid(g)][64][224] fp32 workspace
+bool launch_stem_wgrad(const uint16_t* x, const uint16_t* dy, float* part, float* dw, const StemGeom& g,
+                       hipStream_t stream);
 }  // namespace rla

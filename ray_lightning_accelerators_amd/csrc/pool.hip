@@ -27,15 +27,32 @@ __device__ __forceinline__ f8 ld8(const uint16_t* p) {
   return __builtin_convertvector(__builtin_bit_cast(b8, *reinterpret_cast<const u16x8*>(p)), f8);
 }
 
-// one thread: 8 channels of one output pixel
+// one thread: 8 channels of one output pixel.
+// BN (the stem's BatchNorm + ReLU folded in, round 5): the input is the BatchNorm's
+// INPUT and each window element is first mapped exactly as bn_apply_kernel<relu>
+// would store it -- bf16(max(x * scale + shift, 0)) with one fused multiply-add --
+// so the pooled values and argmax equal the unfused pair's, and the 205 MB
+// activation between them is never written or re-read.  ss = the finalize's
+// [4, C] stats (rows 2, 3: scale, shift); nbt_inc as bn_apply's.
+template <bool BN>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                           uint8_t* __restrict__ arg, int N, int H, int W, int C,
-                                                          int OH, int OW, int k, int s, int pad) {
+                                                          int OH, int OW, int k, int s, int pad,
+                                                          const float* __restrict__ ss, int64_t* nbt_inc) {
   const int G = C >> 3;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (BN && nbt_inc && t == 0) nbt_inc[0] += 1;
   const int64_t total = (int64_t)N * OH * OW * G;
   if (t >= total) return;
   const int g = (int)(t % G);
+  f8 sc, sf;
+  if (BN) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      sc[c] = ss[2 * C + g * 8 + c];
+      sf[c] = ss[3 * C + g * 8 + c];
+    }
+  }
   int64_t p = t / G;
   const int ow = (int)(p % OW);
   p /= OW;
@@ -55,7 +72,13 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __rest
     for (int kw = 0; kw < k; ++kw) {
       const int w = w0 + kw;
       if (w < 0 || w >= W) continue;
-      const f8 v = ld8(x + (((int64_t)n * H + h) * W + w) * C + g * 8);
+      f8 v = ld8(x + (((int64_t)n * H + h) * W + w) * C + g * 8);
+      if (BN) {
+        v = __builtin_elementwise_fma(v, sc, sf);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = v[c] > 0.f ? v[c] : 0.f;
+        v = __builtin_convertvector(__builtin_convertvector(v, b8), f8);  // the bf16 bn_apply stores
+      }
       const uint8_t pos = (uint8_t)(kh * k + kw);
 #pragma unroll
       for (int c = 0; c < 8; ++c)
@@ -136,13 +159,17 @@ int launch_gap_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipSt
 }
 
 int launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int OH, int OW,
-                       int k, int s, int pad, hipStream_t stream) {
+                       int k, int s, int pad, hipStream_t stream, const float* bn_ss, int64_t* nbt_inc) {
   if (C % 8 || k < 1 || k > 15 || s < 1) return -1;
   const int64_t total = (int64_t)N * OH * OW * (C / 8);
   const int64_t blocks = (total + 255) / 256;
   if (blocks > 0x7fffffff) return -2;
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, y, arg, N, H, W, C, OH,
-                     OW, k, s, pad);
+  if (bn_ss)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, x, y, arg, N, H, W, C,
+                       OH, OW, k, s, pad, bn_ss, nbt_inc);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, x, y, arg, N, H, W,
+                       C, OH, OW, k, s, pad, nullptr, nullptr);
   return 0;
 }
 

@@ -139,8 +139,14 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.bn1(self.conv1(x))
-        x = self.maxpool(x if self.fused_bn else F.relu(x, inplace=True))
+        if self.fused_bn and self.bn1.training:
+            # the stem kernel may compute bn1's batch statistics in its epilogue, and
+            # bn1 + ReLU run inside the max pool's pass (ops/bn.py ``pool``)
+            st = BNStats()
+            x = self.bn1(self.conv1(x, bn_stats=st), bn_stats=st, pool=self.maxpool)
+        else:
+            x = self.bn1(self.conv1(x))
+            x = self.maxpool(x if self.fused_bn else F.relu(x, inplace=True))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         if self.fused_bn:
             return self.fc(global_avg_pool_nhwc(x))  # NHWC backward kernel (ops/pool.py)

@@ -84,10 +84,12 @@ fold_stats = {"folded": 0, "fused_rejected": 0}
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu, group,
-                slot=None, sink=None, part=None):
+                slot=None, sink=None, part=None, pool=None):
         # slot: this layer's own _FoldSlot (a consumer may park dres for our backward);
         # sink: the producer slot of `residual` (residual is then passed detached);
-        # part: partial sums the producing conv computed in its epilogue (ops.conv.BNStats)
+        # part: partial sums the producing conv computed in its epilogue (ops.conv.BNStats);
+        # pool: (k, s, pad) of a max pool applied to relu(bn(x)) in the same pass (the
+        # ResNet stem): the normalised activation is never written, the output is pooled
         mod = require()
         C = x.size(1)
         xv = _nhwc(x)
@@ -104,6 +106,17 @@ class _BNActFn(torch.autograd.Function):
             dist.all_reduce(part, group=group)
             count *= dist.get_world_size(group)
         st = mod.bn_finalize(part, count, weight, bias, running_mean, running_var, nbt, momentum, eps, pending)
+        if pool is not None:
+            # pooled bf16(relu(x * scale + shift)) + one-byte argmax (csrc/pool.hip BN); the
+            # backward scatters through the argmax, then runs the usual recomputed-mask pass
+            k, s_, pad = pool
+            yp, arg = mod.maxpool_fwd(xv, k, s_, pad, st, nbt if pending else None)
+            ctx.relu, ctx.has_res, ctx.group, ctx.count = True, False, group, count
+            ctx.slot, ctx.sink, ctx.recomp = slot, sink, True
+            ctx.pool = (x.size(2), x.size(3), k, s_, pad)
+            ctx.save_for_backward(x, None, weight, st, arg)
+            return yp.permute(0, 3, 1, 2)
+        ctx.pool = None
         y = torch.empty_like(x, memory_format=torch.channels_last)
         mod.bn_apply(xv, st[2], st[3], _nhwc(residual) if residual is not None else None, relu, _nhwc(y),
                      nbt if pending else None)
@@ -115,16 +128,19 @@ class _BNActFn(torch.autograd.Function):
         # from the stats (one stream less to read in both backward passes); with a
         # residual the mask needs the sum, so y is kept
         ctx.recomp = relu and residual is None
-        ctx.save_for_backward(x, y if relu and not ctx.recomp else None, weight, st)
+        ctx.save_for_backward(x, y if relu and not ctx.recomp else None, weight, st, None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         mod = require()
-        x, y, weight, st = ctx.saved_tensors
+        x, y, weight, st, arg = ctx.saved_tensors
         mean, invstd = st[0], st[1]
         ss = st if ctx.recomp else None
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        if ctx.pool is not None:  # gradient of the pooled output -> of relu(bn(x)), through the argmax
+            H, W, k, s_, pad = ctx.pool
+            dy = mod.maxpool_bwd(dy.permute(0, 2, 3, 1), arg, H, W, k, s_, pad).permute(0, 3, 1, 2)
         C = x.size(1)
         xv, dyv = _nhwc(x), _nhwc(dy)
         yv = _nhwc(y) if y is not None else None
@@ -169,7 +185,7 @@ class _BNActFn(torch.autograd.Function):
         # views of the coefficient tensor (no copy kernels): autograd hands them to .grad
         dgamma = wsrc[0] if weight is not None and ctx.needs_input_grad[1] else None
         dbeta = wsrc[1] if ctx.needs_input_grad[2] else None
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None, None
 
 
 class BatchNormAct2d(nn.BatchNorm2d):
@@ -187,6 +203,14 @@ class BatchNormAct2d(nn.BatchNorm2d):
         self._warned = False
         self.fold_residual_grad = True  # see the module docstring
 
+    def _pool_geometry(self, pool, residual):
+        k, s, p = getattr(pool, "kernel_size", None), getattr(pool, "stride", None), getattr(pool, "padding", None)
+        if (self.act == "relu" and residual is None and isinstance(pool, nn.MaxPool2d) and isinstance(k, int)
+                and isinstance(s, int) and isinstance(p, int) and pool.dilation == 1 and not pool.ceil_mode
+                and not pool.return_indices and 2 * p <= k and 1 <= k <= 15 and s >= 1):
+            return (k, s, p)
+        return None
+
     def extra_repr(self) -> str:
         return super().extra_repr() + f", act={self.act}, sync={self.sync}"
 
@@ -197,12 +221,19 @@ class BatchNormAct2d(nn.BatchNorm2d):
         return None
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                residual_is_ancestor: bool = False, bn_stats=None) -> torch.Tensor:
+                residual_is_ancestor: bool = False, bn_stats=None, pool: Optional[nn.Module] = None) -> torch.Tensor:
         """``residual_is_ancestor``: the caller guarantees ``x`` is computed from
         ``residual`` (ResNet identity shortcut), so this layer's backward runs before
         the residual producer's and the residual gradient can be folded into it.
         ``bn_stats``: an ``ops.conv.BNStats`` the conv producing ``x`` may have filled
-        with x's partial sums (this layer then skips its own partial pass)."""
+        with x's partial sums (this layer then skips its own partial pass).
+        ``pool``: a max-pool module applied to this layer's output -- returns
+        ``pool(self(x))``, on the training path as ONE pass (BatchNorm + ReLU folded
+        into the pool kernel; the normalised activation is never materialised)."""
+        geo = self._pool_geometry(pool, residual) if pool is not None else None
+        if pool is not None and (geo is None or not fused_ok(x, residual)
+                                 or not (self.training or not self.track_running_stats)):
+            return pool(self.forward(x, residual, residual_is_ancestor, bn_stats))
         part = None
         if bn_stats is not None:
             part, bn_stats.part = bn_stats.part, None
@@ -224,7 +255,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
                     x, self.weight, self.bias, residual,
                     self.running_mean if track else None, self.running_var if track else None,
                     self.num_batches_tracked if track else None, momentum, float(self.eps), relu, self._group(),
-                    slot, sink, part)
+                    slot, sink, part, geo)
                 if slot is not None:
                     y._rla_fold = slot
                 return y

@@ -31,7 +31,7 @@ from torch import nn
 
 _choice: Dict[Tuple[str, int, int, int], str] = {}
 _timings: Dict[Tuple[str, int, int, int], Dict[str, float]] = {}
-stats = {"fast": 0, "fallback": 0, "bn_dgrad_fused": 0}
+stats = {"fast": 0, "fallback": 0, "bn_dgrad_fused": 0, "stem": 0}
 
 _conv = torch.ops.aten.convolution
 _conv_bwd = torch.ops.aten.convolution_backward
@@ -520,6 +520,75 @@ class _ConvNHWCFn(torch.autograd.Function):
         elif be == "hip_gen":
             dw = wgrad_hip(dy, x, (kh, kw), stride, padding, algo=1)
         return dx, dw, None, None, None, None, None
+
+
+@functools.lru_cache(maxsize=64)
+def _stem_shape_ok(n: int, h: int, w: int) -> bool:
+    from . import require
+
+    return bool(require().stem_supported(n, h, w))
+
+
+def stem_fast_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    """The ResNet stem (7x7 / stride 2 / pad 3, 3 -> 64, no bias) on an NHWC bf16 input
+    the MFMA stem kernel covers (csrc/stem.hip); ``RLA_STEM=off`` keeps MIOpen."""
+    return (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and x.size(1) == 3
+            and conv.in_channels == 3 and conv.out_channels == 64 and conv.kernel_size == (7, 7)
+            and conv.stride == (2, 2) and conv.padding == (3, 3) and conv.dilation == (1, 1)
+            and conv.groups == 1 and conv.bias is None and conv.padding_mode == "zeros"
+            and os.environ.get("RLA_STEM", "auto") != "off" and _stem_shape_ok(x.size(0), x.size(2), x.size(3)))
+
+
+def stem_hip(x: torch.Tensor, wb: torch.Tensor, stats: bool = False):
+    """``conv2d(x, wb, stride=2, padding=3)`` for the stem on the MFMA kernel: ``x`` [N, 3,
+    H, W] bf16 (any layout; made NHWC-contiguous), ``wb`` [64, 3, 7, 7] bf16 channels_last.
+    Returns y [N, 64, OH, OW] channels_last, or (y, part [rows, 2, 64]) with ``stats``."""
+    from . import require
+
+    xn = x.permute(0, 2, 3, 1).contiguous()
+    out = require().stem_fwd(xn, wb.permute(0, 2, 3, 1).contiguous(), stats)
+    y = out[0].permute(0, 3, 1, 2)
+    return (y, out[1]) if stats else y
+
+
+def stem_wgrad_hip(x: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
+    """Weight gradient of the stem on the MFMA kernel (csrc/stem.hip): fp32 [64, 3, 7, 7]
+    with channels_last strides (the master weight's layout)."""
+    from . import require
+
+    dw = require().stem_wgrad(x.permute(0, 2, 3, 1).contiguous(), dy.permute(0, 2, 3, 1).contiguous())
+    return dw.permute(0, 3, 1, 2)
+
+
+class _StemFn(torch.autograd.Function):
+    """Stem forward (with the next BatchNorm's statistics when asked) and weight gradient
+    on the MFMA kernels; the input gradient, if one is wanted, from MIOpen."""
+
+    @staticmethod
+    def forward(ctx, x, weight, wb, bn_stats=None):
+        if bn_stats is not None:
+            y, bn_stats.part = stem_hip(x, wb, stats=True)
+        else:
+            y = stem_hip(x, wb)
+        ctx.save_for_backward(x, wb)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wb = ctx.saved_tensors
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = _conv_bwd(dy, x, wb, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1, [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            dw = stem_wgrad_hip(x, dy)
+        return dx, dw, None, None
+
+
+def stem_conv(x: torch.Tensor, conv: nn.Conv2d, wb: torch.Tensor, bn_stats: Optional[BNStats] = None) -> torch.Tensor:
+    """``conv(x)`` for the ResNet stem (:func:`stem_fast_ok`) with the bf16 shadow ``wb``."""
+    stats["stem"] += 1
+    return _StemFn.apply(x, conv.weight, wb, bn_stats)
 
 
 def kxk_fast_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:

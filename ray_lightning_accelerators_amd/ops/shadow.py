@@ -75,9 +75,13 @@ class ConvBF16(nn.Conv2d):
                 and self.padding_mode == "zeros":
             wb = bf16_weight(self.weight)
             if wb is not None and torch.is_grad_enabled() and self.weight.requires_grad:
-                from .conv import conv_nhwc, kxk_fast_ok
+                from .conv import conv_nhwc, kxk_fast_ok, stem_conv, stem_fast_ok
 
                 xb = x.to(torch.bfloat16)
+                if stem_fast_ok(xb, self):
+                    # ResNet stem: MFMA kernel (+ the next BatchNorm's statistics)
+                    stats["shadow"] += 1
+                    return stem_conv(xb, self, wb, bn_stats)
                 if kxk_fast_ok(xb, self):
                     # MIOpen forward / dgrad, weight gradient from the MFMA kernel when
                     # it is the faster one (ops/conv.py)

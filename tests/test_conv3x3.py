@@ -171,3 +171,110 @@ def test_resnet_block_bn2_uses_conv3x3_stats(monkeypatch):
     assert calls["st"] >= 1
     for a, b in zip(outs["auto"], outs["off"]):
         assert _rel(a, b.float()) < 2e-2, _rel(a, b.float())
+
+
+STEM_SHAPES = [(2, 224, 224), (3, 32, 32), (2, 30, 46), (1, 17, 20)]
+
+
+@gpu
+@pytest.mark.parametrize("shape", STEM_SHAPES)
+def test_stem_forward_and_stats_match_fp32(shape):
+    """ResNet stem on the MFMA kernel (csrc/stem.hip): 7x7 / stride 2 / pad 3, 3 -> 64,
+    against an fp32 conv of the same bf16 operands; the statistics rows sum to the
+    per-channel sums of the bf16 output."""
+    from ray_lightning_accelerators_amd.ops.conv import stem_hip
+
+    n, h, w = shape
+    torch.manual_seed(3)
+    dev = torch.device("cuda", 0)
+    x = torch.randn(n, 3, h, w, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wb = (torch.randn(64, 3, 7, 7, device=dev) / 12).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = stem_hip(x, wb)
+    ref = F.conv2d(x.float(), wb.float(), stride=2, padding=3)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(y, ref) < 8e-3, _rel(y, ref)
+    y2, part = stem_hip(x, wb, stats=True)
+    assert torch.equal(y, y2)
+    yf = y.double().permute(0, 2, 3, 1).reshape(-1, 64)
+    s, q = part.double().sum(0)
+    torch.testing.assert_close(s, yf.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(q, yf.square().sum(0), rtol=1e-4, atol=1e-2)
+
+
+@gpu
+def test_resnet_stem_routes_through_kernel(monkeypatch):
+    """The fused ResNet's stem runs the MFMA kernel with bn1's statistics; output and
+    the stem weight's gradient match RLA_STEM=off (MIOpen forward + bn1's own pass)."""
+    from ray_lightning_accelerators_amd.models.resnet import resnet50
+    from ray_lightning_accelerators_amd.ops import conv as C
+    from ray_lightning_accelerators_amd.parallel.arena import ParamArena
+
+    dev = torch.device("cuda", 0)
+    outs = {}
+    for mode in ("auto", "off"):
+        monkeypatch.setenv("RLA_STEM", mode)
+        C._stem_shape_ok.cache_clear()
+        torch.manual_seed(0)
+        m = resnet50(num_classes=10, fused_bn=True).to(dev).to(memory_format=torch.channels_last)
+        arena = ParamArena(m)
+        arena.enable_bf16_shadow(m)
+        torch.manual_seed(1)
+        x = torch.randn(2, 3, 64, 64, device=dev).contiguous(memory_format=torch.channels_last)
+        before = C.stats["stem"]
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            st = C.BNStats()
+            y = m.bn1(m.conv1(x, bn_stats=st), bn_stats=st)
+        y.float().square().mean().backward()
+        used = C.stats["stem"] - before
+        assert (used >= 1) == (mode == "auto"), (mode, used)
+        outs[mode] = (y.detach().float(), m.conv1.weight.grad.clone(), m.bn1.running_var.clone())
+    for a, b in zip(outs["auto"], outs["off"]):
+        assert _rel(a, b.float()) < 2e-2, _rel(a, b.float())
+
+
+@gpu
+def test_bn_relu_folded_into_maxpool_matches_unfused():
+    """bn1 + ReLU inside the max pool's pass (ops/bn.py ``pool``): pooled output,
+    running statistics and every gradient equal the unfused bn -> pool pair."""
+    from ray_lightning_accelerators_amd.ops.bn import BatchNormAct2d
+    from ray_lightning_accelerators_amd.ops.pool import MaxPool2dNHWC
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(4)
+    x0 = torch.randn(3, 64, 22, 18, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g0 = torch.randn(3, 64, 11, 9, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for fold in (True, False):
+        torch.manual_seed(5)
+        bn = BatchNormAct2d(64).to(dev)
+        with torch.no_grad():
+            bn.weight.uniform_(-1, 1)  # negative scales too: the affine map is not monotone
+            bn.bias.uniform_(-0.5, 0.5)
+        pool = MaxPool2dNHWC(3, 2, 1)
+        x = x0.clone().requires_grad_(True)
+        y = bn(x, pool=pool) if fold else pool(bn(x))
+        y.backward(g0)
+        outs.append((y.detach(), x.grad, bn.weight.grad, bn.bias.grad, bn.running_mean, bn.running_var,
+                     bn.num_batches_tracked))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b), (a - b).abs().max() if a.is_floating_point() else (a, b)
+
+
+@gpu
+@pytest.mark.parametrize("shape", STEM_SHAPES)
+def test_stem_wgrad_matches_fp32(shape):
+    """Stem weight gradient on the MFMA kernel against fp32 autograd of the same bf16 operands."""
+    from ray_lightning_accelerators_amd.ops.conv import stem_wgrad_hip
+
+    n, h, w = shape
+    torch.manual_seed(6)
+    dev = torch.device("cuda", 0)
+    x = torch.randn(n, 3, h, w, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    oh, ow = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    dy = torch.randn(n, 64, oh, ow, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w32 = torch.zeros(64, 3, 7, 7, device=dev, requires_grad=True)
+    F.conv2d(x.float(), w32, stride=2, padding=3).backward(dy.float())
+    dw = stem_wgrad_hip(x, dy)
+    assert dw.shape == (64, 3, 7, 7) and dw.dtype == torch.float32
+    assert dw.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(dw, w32.grad) < 1e-4, _rel(dw, w32.grad)
