@@ -416,8 +416,35 @@ int* bn_tickets(int device, hipStream_t stream) {
   return p;
 }
 
+// the stem's pooled BatchNorm (ops/bn.py `pool`): dy is the POOLED output's gradient
+// [N, OH, OW, C] and arg its window argmax; geometry (H, W, k, s, pad) of the pool
+static bool pool_grad(const Tensor& x, const optional<Tensor>& pool_arg, const Tensor& dy,
+                      const std::vector<int64_t>& geo, int64_t C, rla::PoolGrad* pg) {
+  if (!(pool_arg.has_value() && pool_arg->defined())) return false;
+  TORCH_CHECK(geo.size() == 5, "pool geometry (H, W, k, s, pad)");
+  const int64_t H = geo[0], W = geo[1], k = geo[2], s = geo[3], pad = geo[4];
+  TORCH_CHECK(k >= 1 && k <= 15 && s >= 1 && pad >= 0 && 2 * pad <= k, "pool: bad geometry");
+  const int64_t OH = (H + 2 * pad - k) / s + 1, OW = (W + 2 * pad - k) / s + 1;
+  TORCH_CHECK(x.numel() % (H * W * C) == 0, "pool: x is not [N, H, W, C]");
+  const int64_t N = x.numel() / (H * W * C);
+  check_dev(dy, "dy", at::kBFloat16);
+  TORCH_CHECK(dy.is_contiguous() && dy.numel() == N * OH * OW * C, "pool: dy must be the pooled [N, OH, OW, C]");
+  TORCH_CHECK(pool_arg->is_cuda() && pool_arg->scalar_type() == at::kByte && pool_arg->is_contiguous() &&
+                  pool_arg->numel() == dy.numel(),
+              "pool: arg must be the forward's argmax bytes");
+  *pg = rla::PoolGrad{reinterpret_cast<const uint16_t*>(dy.data_ptr()), pool_arg->data_ptr<uint8_t>(), (int)H,
+                      (int)W, (int)OH, (int)OW, (int)k, (int)s, (int)pad};
+  return true;
+}
+
 Tensor bn_partial(Tensor x, optional<Tensor> y, optional<Tensor> dy, int64_t C, int64_t mode, bool relu,
-                  optional<Tensor> nbt, optional<Tensor> dy2, optional<Tensor> ss, optional<Tensor> dout) {
+                  optional<Tensor> nbt, optional<Tensor> dy2, optional<Tensor> ss, optional<Tensor> dout,
+                  optional<Tensor> pool_arg, std::vector<int64_t> pool_geo) {
+  rla::PoolGrad pg{};
+  const bool pooled = mode == 1 && dy.has_value() && pool_grad(x, pool_arg, *dy, pool_geo, C, &pg);
+  TORCH_CHECK(!pooled || (relu && ss.has_value() && ss->defined() && !(dout.has_value() && dout->defined()) &&
+                          !(dy2.has_value() && dy2->defined())),
+              "pooled BN backward: ReLU with the forward stats only");
   const int64_t M = bn_rows(x, "x", C);
   TORCH_CHECK(M > 0, "fused BN: empty input");
   TORCH_CHECK(mode == 0 || mode == 1, "fused BN: mode 0 (forward) or 1 (backward)");
@@ -425,7 +452,7 @@ Tensor bn_partial(Tensor x, optional<Tensor> y, optional<Tensor> dy, int64_t C, 
   const uint16_t* dyp = nullptr;
   if (mode == 1) {
     TORCH_CHECK(dy.has_value(), "backward partial needs dy");
-    bn_same(x, *dy, "dy", C);
+    if (!pooled) bn_same(x, *dy, "dy", C);
     dyp = reinterpret_cast<const uint16_t*>(dy->data_ptr());
     if (relu && !(ss.has_value() && ss->defined())) {
       TORCH_CHECK(y.has_value(), "ReLU backward needs the saved output y (or the forward stats)");
@@ -455,7 +482,7 @@ Tensor bn_partial(Tensor x, optional<Tensor> y, optional<Tensor> dy, int64_t C, 
   }
   rla::launch_bn_partial(reinterpret_cast<const uint16_t*>(x.data_ptr()), yp, dyp, M, (int)C, (int)mode, relu,
                          plan, part.data_ptr<float>(), nbtp, cur_stream(x), mode == 1 ? bn_dy2(x, dy2, C) : nullptr,
-                         mode == 1 && relu ? bn_ss(ss, C) : nullptr, lv, doutp);
+                         mode == 1 && relu ? bn_ss(ss, C) : nullptr, lv, doutp, pooled ? &pg : nullptr);
   return tickets ? rows : part;
 }
 
@@ -636,12 +663,18 @@ std::vector<Tensor> conv1x1_stats(Tensor x, Tensor w) {
 }
 
 void bn_bwd_apply(Tensor x, optional<Tensor> y, Tensor dy, Tensor coef, bool relu, Tensor dx,
-                  optional<Tensor> dres, optional<Tensor> dy2, optional<Tensor> ss) {
+                  optional<Tensor> dres, optional<Tensor> dy2, optional<Tensor> ss, optional<Tensor> pool_arg,
+                  std::vector<int64_t> pool_geo) {
   check_dev(coef, "coef", at::kFloat);
   TORCH_CHECK(coef.dim() == 2 && coef.size(0) == 5, "coef must be [5, C]");
   const int64_t C = coef.size(1);
   const int64_t M = bn_rows(x, "x", C);
-  bn_same(x, dy, "dy", C);
+  rla::PoolGrad pg{};
+  const bool pooled = pool_grad(x, pool_arg, dy, pool_geo, C, &pg);
+  TORCH_CHECK(!pooled || (relu && ss.has_value() && ss->defined() && !(dres.has_value() && dres->defined()) &&
+                          !(dy2.has_value() && dy2->defined())),
+              "pooled BN backward: ReLU with the forward stats only");
+  if (!pooled) bn_same(x, dy, "dy", C);
   bn_same(x, dx, "dx", C);
   const uint16_t* yp = nullptr;
   const float* ssp = relu ? bn_ss(ss, C) : nullptr;
@@ -659,7 +692,7 @@ void bn_bwd_apply(Tensor x, optional<Tensor> y, Tensor dy, Tensor coef, bool rel
   rla::launch_bn_bwd_apply(reinterpret_cast<const uint16_t*>(x.data_ptr()), yp,
                            reinterpret_cast<const uint16_t*>(dy.data_ptr()), coef.data_ptr<float>(), M, (int)C,
                            relu, reinterpret_cast<uint16_t*>(dx.data_ptr()), drp, cur_stream(x), bn_dy2(x, dy2, C),
-                           ssp);
+                           ssp, pooled ? &pg : nullptr);
 }
 
 // dW of an NHWC bf16 convolution (csrc/conv_wgrad.hip): dy [N, OH, OW, Cout] and
@@ -906,7 +939,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp_param_count", &mlp_param_count);
   m.def("bn_partial", &bn_partial, "fused BN: per-block partial sums (mode 0 fwd stats, 1 bwd dz/dz*x)",
         py::arg("x"), py::arg("y"), py::arg("dy"), py::arg("C"), py::arg("mode"), py::arg("relu"), py::arg("nbt"),
-        py::arg("dy2") = py::none(), py::arg("ss") = py::none(), py::arg("dout") = py::none());
+        py::arg("dy2") = py::none(), py::arg("ss") = py::none(), py::arg("dout") = py::none(),
+        py::arg("pool_arg") = py::none(), py::arg("pool_geo") = std::vector<int64_t>{});
   m.def("bn_finalize", &bn_finalize, "fused BN: mean/invstd/scale/shift + running stats from partials",
         py::arg("part"), py::arg("count"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("nbt"), py::arg("momentum"), py::arg("eps"), py::arg("nbt_pending") = false);
@@ -926,7 +960,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max pool backward (gather through the argmax bytes)");
   m.def("bn_bwd_apply", &bn_bwd_apply, "fused BN backward apply: dx (+ dres = relu-masked dy)", py::arg("x"),
         py::arg("y"), py::arg("dy"), py::arg("coef"), py::arg("relu"), py::arg("dx"), py::arg("dres"),
-        py::arg("dy2") = py::none(), py::arg("ss") = py::none());
+        py::arg("dy2") = py::none(), py::arg("ss") = py::none(), py::arg("pool_arg") = py::none(),
+        py::arg("pool_geo") = std::vector<int64_t>{});
   m.def("conv_wgrad", &conv_wgrad, "NHWC bf16 conv weight gradient on MFMA -> fp32 [Cout, KH, KW, Cin]",
         py::arg("dy"), py::arg("x"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("OH"),
         py::arg("OW"), py::arg("Cout"), py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"), py::arg("ph"),

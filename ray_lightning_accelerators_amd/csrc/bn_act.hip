@@ -22,6 +22,7 @@
 #include <stdlib.h>
 
 #include "kernels.h"
+#include "pool_gather.h"
 
 namespace rla {
 namespace {
@@ -96,7 +97,10 @@ struct BnL2 {
   int group;      // blocks per group (1: no second level)
 };
 
-template <int MODE, bool RELU, bool DY2 = false, bool RECOMP = false, bool WD = false>
+// POOL (backward of the ResNet stem's BatchNorm, whose output was max-pooled in the
+// same pass, ops/bn.py `pool`): dy is gathered from the pooled gradient through the
+// argmax bytes (pool_gather.h) instead of read from a materialised maxpool_bwd output.
+template <int MODE, bool RELU, bool DY2 = false, bool RECOMP = false, bool WD = false, bool POOL = false>
 __global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(const uint16_t* __restrict__ x,
                                                                 const uint16_t* __restrict__ y,
                                                                 const uint16_t* __restrict__ dy, int64_t M, int C,
@@ -104,7 +108,8 @@ __global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(const uint16_t* 
                                                                 int64_t* nbt, const uint16_t* __restrict__ dy2 = nullptr,
                                                                 const float* __restrict__ ss = nullptr,
                                                                 BnL2 l2 = BnL2{nullptr, nullptr, 1},
-                                                                uint16_t* __restrict__ dout = nullptr) {
+                                                                uint16_t* __restrict__ dout = nullptr,
+                                                                PoolGrad pg = PoolGrad{}) {
   // forward: one input stream, so twice the rows in flight per thread
   constexpr int U = MODE == 0 ? 8 : 4;
   __shared__ float sh[2][kBnThreads * 8];
@@ -131,7 +136,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(const uint16_t* 
         xv[u] = ld8(px + u * step);
         if (MODE == 1) {
           const int64_t off = (px - x) + u * step;
-          dv[u] = ld8(dy + off);
+          dv[u] = POOL ? pool_grad8<f8, b8, u8x16>(pg, C, r + u * rpi, (int)col) : ld8(dy + off);
           if (DY2) dv[u] += ld8(dy2 + off);
           if (RELU && !RECOMP) dv[u] = relu_mask(dv[u], ld8(y + off));
         }
@@ -156,7 +161,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_partial_kernel(const uint16_t* 
         q += xv * xv;
       } else {
         const int64_t off = px - x;
-        f8 d = ld8(dy + off);
+        f8 d = POOL ? pool_grad8<f8, b8, u8x16>(pg, C, r, (int)col) : ld8(dy + off);
         if (DY2) d += ld8(dy2 + off);
         if (RELU) d = relu_mask(d, RECOMP ? bn_affine(xv, sc, sf) : ld8(y + off));
         if (WD) d = st8r(dout + off, d);
@@ -356,7 +361,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_kernel(const uint16_t* __
   }
 }
 
-template <bool RELU, bool DRES, bool DY2 = false, bool RECOMP = false>
+template <bool RELU, bool DRES, bool DY2 = false, bool RECOMP = false, bool POOL = false>
 __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_kernel(const uint16_t* __restrict__ x,
                                                                   const uint16_t* __restrict__ y,
                                                                   const uint16_t* __restrict__ dy,
@@ -364,7 +369,8 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_kernel(const uint16_t
                                                                   uint16_t* __restrict__ dx,
                                                                   uint16_t* __restrict__ dres,
                                                                   const uint16_t* __restrict__ dy2 = nullptr,
-                                                                  const float* __restrict__ ss = nullptr) {
+                                                                  const float* __restrict__ ss = nullptr,
+                                                                  PoolGrad pg = PoolGrad{}) {
   const int G = C >> 3, rpi = kBnThreads / G, tid = threadIdx.x;
   const int g = tid % G, r0 = tid / G;
   if (r0 >= rpi) return;
@@ -377,7 +383,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_kernel(const uint16_t
   const int64_t col = (int64_t)g * 8, rstride = (int64_t)gridDim.x * rpi;
   for (int64_t r = (int64_t)blockIdx.x * rpi + r0; r < M; r += rstride) {
     const int64_t o = r * C + col;
-    f8 d = ld8(dy + o);
+    f8 d = POOL ? pool_grad8<f8, b8, u8x16>(pg, C, r, (int)col) : ld8(dy + o);
     if (DY2) d += ld8(dy2 + o);
     const f8 xv = ld8(x + o);
     if (RELU) d = relu_mask(d, RECOMP ? bn_affine(xv, sc, sf) : ld8(y + o));
@@ -427,9 +433,14 @@ BnPlan bn_plan(int64_t M, int C) {
 
 void launch_bn_partial(const uint16_t* x, const uint16_t* y, const uint16_t* dy, int64_t M, int C, int mode,
                        bool relu, const BnPlan& plan, float* part, int64_t* nbt, hipStream_t s, const uint16_t* dy2,
-                       const float* ss, BnLevel2 lv, uint16_t* dout) {
+                       const float* ss, BnLevel2 lv, uint16_t* dout, const PoolGrad* pool) {
   const dim3 grid(plan.blocks), block(kBnThreads);
   const BnL2 L{lv.rows, lv.tickets, lv.rows ? plan.group : 1};
+  if (pool) {  // the stem: ReLU mask recomputed from the forward stats, dy gathered through the pool
+    hipLaunchKernelGGL((bn_partial_kernel<1, true, false, true, false, true>), grid, block, 0, s, x, y, dy, M, C,
+                       plan.rows_per_blk, part, nullptr, nullptr, ss, L, nullptr, *pool);
+    return;
+  }
   if (mode == 1 && dout) {  // residual layer: d written here (y-mask or none)
     if (relu && dy2)
       hipLaunchKernelGGL((bn_partial_kernel<1, true, true, false, true>), grid, block, 0, s, x, y, dy, M, C,
@@ -515,8 +526,13 @@ void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* scale,
 
 void launch_bn_bwd_apply(const uint16_t* x, const uint16_t* y, const uint16_t* dy, const float* coef, int64_t M,
                          int C, bool relu, uint16_t* dx, uint16_t* dres, hipStream_t s, const uint16_t* dy2,
-                         const float* ss) {
+                         const float* ss, const PoolGrad* pool) {
   const dim3 grid(apply_grid(M, C)), block(kBnThreads);
+  if (pool) {
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false, false, true, true>), grid, block, 0, s, x, y, dy, coef, M, C,
+                       dx, dres, nullptr, ss, *pool);
+    return;
+  }
   if (relu && ss && !dres) {  // no residual: the mask is recomputed from x and the forward stats
     if (dy2)
       hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false, true, true>), grid, block, 0, s, x, y, dy, coef, M, C, dx,

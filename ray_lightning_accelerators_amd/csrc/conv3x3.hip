@@ -32,7 +32,8 @@
 //     neighbouring pixel tiles run on the same XCD, so the halo / weight re-reads hit
 //     that XCD's L2.
 // Epilogue: D of 32x32x16 gives a lane one pixel and 4 consecutive output channels
-// per 4 accumulator values: 8-byte bf16 stores.
+// per 4 accumulator values; a v_permlane32_swap between the two half-waves (same
+// pixel) turns two 8-byte stores into one 16-byte store (round 5).
 // Requires Cin % 16 == 0, Cout % 64 == 0, 16-byte aligned bases (checked by the binding).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -297,26 +298,40 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
 #pragma unroll
     for (int j = 0; j < JB; ++j) {
       const int64_t m = m0 + wave * (32 * JB) + j * 32 + (lane & 31);
-      if (m < m_end) {
-        uint16_t* yo = y + m * g.Cout + co0;
+      // lanes l and l ^ 32 hold the same pixel (the swap stays in-pixel); one
+      // v_permlane32_swap per dword of each channel-group pair (q, q + 1) gives lane
+      // half (lane >> 5) channels 16 p + 8 (lane >> 5) .. + 8: 16-byte stores
+      const bool ok = m < m_end;
+      uint16_t* yo = y + (ok ? m : 0) * g.Cout + co0 + 8 * (lane >> 5);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i) {
+        uint32_t v[4][2];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int co = i * 32 + 8 * q + 4 * (lane >> 5);
-            bf16x4 v;
+        for (int q = 0; q < 4; ++q) {
+          bf16x4 b;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = (__bf16)acc[i][j][4 * q + e];
-            *reinterpret_cast<bf16x4*>(yo + co) = v;
-            if constexpr (ST) {
+          for (int e = 0; e < 4; ++e) b[e] = (__bf16)acc[i][j][4 * q + e];
+          if constexpr (ST) {
+            if (ok) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
-                const float f = (float)v[e];  // the statistics of what BatchNorm reads
+                const float f = (float)b[e];  // the statistics of what BatchNorm reads
                 bs[i][4 * q + e] += f;
                 bq[i][4 * q + e] = __builtin_fmaf(f, f, bq[i][4 * q + e]);
               }
             }
           }
+          const u32x2 pk = __builtin_bit_cast(u32x2, b);
+          v[q][0] = pk[0];
+          v[q][1] = pk[1];
+        }
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const auto s0 = __builtin_amdgcn_permlane32_swap(v[2 * p][0], v[2 * p + 1][0], false, false);
+          const auto s1 = __builtin_amdgcn_permlane32_swap(v[2 * p][1], v[2 * p + 1][1], false, false);
+          const u32x4 o = {s0[0], s1[0], s0[1], s1[1]};
+          if (ok) *reinterpret_cast<u32x4*>(yo + 32 * i + 16 * p) = o;
+        }
       }
     }
   };

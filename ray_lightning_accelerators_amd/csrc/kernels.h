@@ -57,6 +57,12 @@ int launch_maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int
                        int OW, int k, int s, int pad, hipStream_t stream);
 // global average pool backward over NHWC rows: dx[n][p][c] = dy[n][c] / HW
 int launch_gap_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t stream);
+// a max pool's backward seen from the layer before it (csrc/pool_gather.h)
+struct PoolGrad {
+  const uint16_t* g;   // gradient of the pooled output [N, OH, OW, C] bf16
+  const uint8_t* arg;  // window argmax bytes [N, OH, OW, C]
+  int H, W, OH, OW, k, s, pad;
+};
 constexpr int kBnMaxC = 2048;  // 8 channels per thread x 256 threads per row
 
 struct BnPlan {
@@ -80,7 +86,8 @@ void launch_bn_partial(const uint16_t* x, const uint16_t* y, const uint16_t* dy,
                        const uint16_t* dy2 = nullptr,   // backward: gradient = dy + dy2
                        const float* ss = nullptr,       // backward ReLU mask from the fwd stats, not y
                        BnLevel2 l2 = BnLevel2{nullptr, nullptr},
-                       uint16_t* dout = nullptr);       // backward: also write d = masked dy (+dy2), bf16
+                       uint16_t* dout = nullptr,        // backward: also write d = masked dy (+dy2), bf16
+                       const PoolGrad* pool = nullptr);  // backward: dy gathered through a max pool (relu, ss)
 
 // forward finalize of `nparts` partial rows: stats[0]=mean [1]=invstd [2]=scale [3]=shift ([4, C]);
 // running stats update (momentum < 0: cumulative average over num_batches_tracked)
@@ -108,7 +115,8 @@ void launch_bn_apply(const uint16_t* x, const uint16_t* res, const float* scale,
 void launch_bn_bwd_apply(const uint16_t* x, const uint16_t* y, const uint16_t* dy, const float* coef, int64_t M,
                          int C, bool relu, uint16_t* dx, uint16_t* dres, hipStream_t s,
                          const uint16_t* dy2 = nullptr,  // gradient = dy + dy2
-                         const float* ss = nullptr);     // ReLU mask from the fwd stats [4, C], not y
+                         const float* ss = nullptr,      // ReLU mask from the fwd stats [4, C], not y
+                         const PoolGrad* pool = nullptr);  // dy gathered through a max pool (relu, ss)
 
 // 1x1 / stride-1 conv forward y[M][N] = x[M][K] . w[N][K]^T with the next BatchNorm's
 // partial sums of bf16(y) in the epilogue: part [gx, 2, N] fp32, bn_finalize's layout

@@ -95,6 +95,8 @@ __global__ __launch_bounds__(kStThreads) void stem_fwd_kernel(const uint16_t* __
 
   const int pp = g.W >> 1;  // pixel pairs per input row
   const int npieces = kRowsIn * pp;
+  uint8_t* scratch = lds + 2 * bufb;  // the weight staging area, dead after the prologue
+  __syncthreads();                    // (every wave built its fragments from it)
   Piece pc[kNP];
   // the tile's 9 input rows, 12 bytes (a pixel pair) per piece; rows outside the image read row 0 (zeroed at store)
   auto load = [&](int t) {
@@ -118,19 +120,19 @@ __global__ __launch_bounds__(kStThreads) void stem_fwd_kernel(const uint16_t* __
     uint8_t* B = lds + buf * bufb;
 #pragma unroll
     for (int u = 0; u < kNP; ++u) {
+      // unconditional (surplus pieces go to a dead scratch slot): a store under a branch
+      // lets hipcc sink the piece's global load into it and wait for it right there
       const int p = tid + u * kStThreads;
-      if (p < npieces) {
-        const int q = p / pp, c2 = p - q * pp;
-        const int ih = 2 * oh0 - 3 + q;
-        const bool ok = ih >= 0 && ih < g.H;
-        const uint32_t a0 = ok ? pc[u].v[0] : 0u, a1 = ok ? pc[u].v[1] : 0u, a2 = ok ? pc[u].v[2] : 0u;
-        // bf16 elements e0..e5 = (a0.lo a0.hi a1.lo a1.hi a2.lo a2.hi)
-        const u32x2 lo = {a0, a1 & 0xFFFFu};                          // e0 e1 | e2 0
-        const u32x2 hi = {(a1 >> 16) | (a2 << 16), a2 >> 16};         // e3 e4 | e5 0
-        uint8_t* dst = B + q * rowb + (3 + 2 * c2) * 8;
-        *reinterpret_cast<u32x2*>(dst) = lo;
-        *reinterpret_cast<u32x2*>(dst + 8) = hi;
-      }
+      const int q = p / pp, c2 = p - q * pp;
+      const int ih = 2 * oh0 - 3 + q;
+      const bool ok = ih >= 0 && ih < g.H;
+      const uint32_t a0 = ok ? pc[u].v[0] : 0u, a1 = ok ? pc[u].v[1] : 0u, a2 = ok ? pc[u].v[2] : 0u;
+      // bf16 elements e0..e5 = (a0.lo a0.hi a1.lo a1.hi a2.lo a2.hi)
+      const u32x2 lo = {a0, a1 & 0xFFFFu};                          // e0 e1 | e2 0
+      const u32x2 hi = {(a1 >> 16) | (a2 << 16), a2 >> 16};         // e3 e4 | e5 0
+      uint8_t* dst = p < npieces ? B + q * rowb + (3 + 2 * c2) * 8 : scratch;
+      *reinterpret_cast<u32x2*>(dst) = lo;
+      *reinterpret_cast<u32x2*>(dst + 8) = hi;
     }
   };
 
@@ -169,25 +171,40 @@ __global__ __launch_bounds__(kStThreads) void stem_fwd_kernel(const uint16_t* __
 #pragma unroll
     for (int h = 0; h < kT; ++h) {
       const int oh = oh0 + h;
-      if (oh < g.OH && ow < g.OW) {
-        uint16_t* yo = y + (((int64_t)n * g.OH + oh) * g.OW + ow) * 64;
+      // lanes l and l ^ 32 hold the same pixel (the swap stays in-pixel); one
+      // v_permlane32_swap per dword of each channel-group pair (q, q + 1) gives lane
+      // half hl channels 16 p + 8 hl .. + 8: 16-byte stores instead of 8-byte ones
+      const bool ok = oh < g.OH && ow < g.OW;
+      uint16_t* yo = y + (((int64_t)n * g.OH + (ok ? oh : 0)) * g.OW + (ok ? ow : 0)) * 64 + 8 * (lane >> 5);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i) {
+        uint32_t v[4][2];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            bf16x4 v;
+        for (int q = 0; q < 4; ++q) {
+          bf16x4 b;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = (__bf16)acc[h][i][4 * q + e];
-            *reinterpret_cast<bf16x4*>(yo + i * 32 + 8 * q + 4 * (lane >> 5)) = v;
-            if constexpr (ST) {
+          for (int e = 0; e < 4; ++e) b[e] = (__bf16)acc[h][i][4 * q + e];
+          if constexpr (ST) {
+            if (ok) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
-                const float f = (float)v[e];
+                const float f = (float)b[e];
                 bs[i][4 * q + e] += f;
                 bq[i][4 * q + e] = __builtin_fmaf(f, f, bq[i][4 * q + e]);
               }
             }
           }
+          const u32x2 pk = __builtin_bit_cast(u32x2, b);
+          v[q][0] = pk[0];
+          v[q][1] = pk[1];
+        }
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const auto s0 = __builtin_amdgcn_permlane32_swap(v[2 * p][0], v[2 * p + 1][0], false, false);
+          const auto s1 = __builtin_amdgcn_permlane32_swap(v[2 * p][1], v[2 * p + 1][1], false, false);
+          const u32x4 o = {s0[0], s1[0], s0[1], s1[1]};
+          if (ok) *reinterpret_cast<u32x4*>(yo + 32 * i + 16 * p) = o;
+        }
       }
     }
   };
@@ -198,9 +215,12 @@ __global__ __launch_bounds__(kStThreads) void stem_fwd_kernel(const uint16_t* __
     __syncthreads();
     for (int t = t_lo; t < t_hi; ++t) {
       const int buf = (t - t_lo) & 1;
-      if (t + 1 < t_hi) load(t + 1);  // in flight behind this tile's MFMAs
+      // in flight behind this tile's MFMAs; unconditional (the last tile re-loads itself):
+      // a load under a branch makes the loaded registers a join value, and hipcc then
+      // waits for each load right after issuing it to copy the registers
+      load(t + 1 < t_hi ? t + 1 : t);
       compute(buf);
-      if (t + 1 < t_hi) store(t + 1, buf ^ 1);
+      store(t + 1 < t_hi ? t + 1 : t, buf ^ 1);  // (the last tile: a dead copy of itself)
       epilogue(t);
       __syncthreads();
     }
@@ -260,7 +280,7 @@ __device__ __forceinline__ bf16x8 scat8(bf16x4 lo, bf16x4 hi) {
 __global__ __launch_bounds__(kStThreads) void stem_wgrad_kernel(const uint16_t* __restrict__ x,
                                                                 const uint16_t* __restrict__ dy,
                                                                 float* __restrict__ part, StemGeom g) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kWgLds];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kWgLds + 16];  // + a scratch slot for surplus pieces
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rowb = (g.W + 8) * 8;
   const int ohp = (g.OH + kT - 1) / kT;
@@ -301,19 +321,17 @@ __global__ __launch_bounds__(kStThreads) void stem_wgrad_kernel(const uint16_t* 
     const int n = t / ohp, oh0 = (t - n * ohp) * kT;
     uint8_t* B = lds + buf * kWgBuf;
 #pragma unroll
-    for (int u = 0; u < kNP; ++u) {
+    for (int u = 0; u < kNP; ++u) {  // unconditional: see stem_fwd_kernel's store
       const int p = tid + u * kStThreads;
-      if (p < npieces) {
-        const int q = p / pp, c2 = p - q * pp;
-        const int ih = 2 * oh0 - 3 + q;
-        const bool ok = ih >= 0 && ih < g.H;
-        const uint32_t a0 = ok ? pc[u].v[0] : 0u, a1 = ok ? pc[u].v[1] : 0u, a2 = ok ? pc[u].v[2] : 0u;
-        const u32x2 lo = {a0, a1 & 0xFFFFu};
-        const u32x2 hi = {(a1 >> 16) | (a2 << 16), a2 >> 16};
-        uint8_t* dst = B + q * rowb + (3 + 2 * c2) * 8;
-        *reinterpret_cast<u32x2*>(dst) = lo;
-        *reinterpret_cast<u32x2*>(dst + 8) = hi;
-      }
+      const int q = p / pp, c2 = p - q * pp;
+      const int ih = 2 * oh0 - 3 + q;
+      const bool ok = ih >= 0 && ih < g.H;
+      const uint32_t a0 = ok ? pc[u].v[0] : 0u, a1 = ok ? pc[u].v[1] : 0u, a2 = ok ? pc[u].v[2] : 0u;
+      const u32x2 lo = {a0, a1 & 0xFFFFu};
+      const u32x2 hi = {(a1 >> 16) | (a2 << 16), a2 >> 16};
+      uint8_t* dst = p < npieces ? B + q * rowb + (3 + 2 * c2) * 8 : lds + kWgLds;
+      *reinterpret_cast<u32x2*>(dst) = lo;
+      *reinterpret_cast<u32x2*>(dst + 8) = hi;
     }
     uint8_t* D = B + kBufBytes;
 #pragma unroll
@@ -366,9 +384,10 @@ __global__ __launch_bounds__(kStThreads) void stem_wgrad_kernel(const uint16_t* 
     __syncthreads();
     for (int t = t_lo; t < t_hi; ++t) {
       const int buf = (t - t_lo) & 1;
-      if (t + 1 < t_hi) load(t + 1);
+      load(t + 1 < t_hi ? t + 1 : t);  // unconditional: see stem_fwd_kernel
+      asm volatile("" ::: "memory");    // keep the loads ahead of the tile's LDS reads / MFMAs
       compute(buf);
-      if (t + 1 < t_hi) store(t + 1, buf ^ 1);
+      store(t + 1 < t_hi ? t + 1 : t, buf ^ 1);
       __syncthreads();
     }
   }

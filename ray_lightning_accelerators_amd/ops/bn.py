@@ -138,9 +138,26 @@ class _BNActFn(torch.autograd.Function):
         mean, invstd = st[0], st[1]
         ss = st if ctx.recomp else None
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        if ctx.pool is not None:  # gradient of the pooled output -> of relu(bn(x)), through the argmax
-            H, W, k, s_, pad = ctx.pool
-            dy = mod.maxpool_bwd(dy.permute(0, 2, 3, 1), arg, H, W, k, s_, pad).permute(0, 3, 1, 2)
+        if ctx.pool is not None:
+            # dy is the POOLED output's gradient: both backward passes gather relu(bn(x))'s
+            # gradient through the argmax bytes themselves (csrc/pool_gather.h) -- the
+            # 205 MB maxpool_bwd output is never written or read
+            geo = list(ctx.pool)
+            dyp = dy.permute(0, 2, 3, 1)
+            part = mod.bn_partial(_nhwc(x), None, dyp, x.size(1), 1, True, None, None, st, None, arg, geo)
+            if ctx.group is not None:
+                local = mod.bn_bwd_finalize(part, ctx.count, weight, mean, invstd)
+                part = part.sum(0, keepdim=True)
+                dist.all_reduce(part, group=ctx.group)
+            else:
+                local = None
+            coef = mod.bn_bwd_finalize(part, ctx.count, weight, mean, invstd)
+            dx = torch.empty_like(x, memory_format=torch.channels_last)
+            mod.bn_bwd_apply(_nhwc(x), None, dyp, coef, True, _nhwc(dx), None, None, st, arg, geo)
+            wsrc = local if local is not None else coef
+            dgamma = wsrc[0] if weight is not None and ctx.needs_input_grad[1] else None
+            dbeta = wsrc[1] if ctx.needs_input_grad[2] else None
+            return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None, None
         C = x.size(1)
         xv, dyv = _nhwc(x), _nhwc(dy)
         yv = _nhwc(y) if y is not None else None

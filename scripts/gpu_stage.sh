@@ -156,7 +156,7 @@ for st in "$@"; do
       run c3probe_fixed 300 python -u scripts/conv3x3_probe.py
       RLA_CONV3X3_GENERIC=1 run c3probe_generic 300 python -u scripts/conv3x3_probe.py ;;
     stem)  # ResNet stem kernel: numerics + device time vs MIOpen (+ BN statistics)
-      run pytest_stem 300 $PYT tests/test_conv3x3.py -k stem
+      run pytest_stem 300 $PYT tests/test_conv3x3.py -k "stem or maxpool"
       run stem_probe 300 python -u scripts/stem_probe.py ;;
     mnist5)  # one-launch MNIST step after a kernel change: numerics, headline bench, phase stamps, DP cost
       run pytest_mlp3 600 $PYT tests/test_mlp3.py
