@@ -479,6 +479,8 @@ static void launch_nx(const uint16_t* x, const uint16_t* w, uint16_t* y, const C
   // the same layers reads dy with the same width and channel count)
   if constexpr (JB == 4) {
     if (launch_fixed<7, FLIP, JB, DEPTH, 56, 64, ST>(x, w, y, g, st, grid, part)) return;
+    // 28x28: a workgroup's range is one whole image (784 pixels = a 512 + a 272 tile)
+    if (launch_fixed<5, FLIP, JB, DEPTH, 28, 128, ST>(x, w, y, g, st, grid, part)) return;
   } else {
     if (launch_fixed<4, FLIP, JB, DEPTH, 28, 128, ST>(x, w, y, g, st, grid, part)) return;
     if (launch_fixed<4, FLIP, JB, DEPTH, 14, 256, ST>(x, w, y, g, st, grid, part)) return;
