@@ -471,6 +471,10 @@ class Trainer:
             self.run_train()
         finally:
             self.wait_checkpoints()  # every checkpoint file is on disk when fit returns
+            q = getattr(self, "_deferred", None)
+            if q is not None:  # its thread ends with the fit (a later save starts a new one)
+                self._deferred = None
+                q.close()
         f = self._fused
         if f is not None and hasattr(f, "check"):
             f.check(blocking=True)  # the epoch-end checks trail by one epoch: the last one here
@@ -1517,4 +1521,10 @@ class _DeferredCheckpoints:
         with self._cv:
             while self._pending:
                 self._cv.wait()
+        self._raise()
+
+    def close(self) -> None:
+        """Finish the queued saves and end the thread."""
+        self._q.put(None)
+        self._t.join()
         self._raise()

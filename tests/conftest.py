@@ -29,3 +29,13 @@ def gpu_count() -> int:
 
 requires_gpu = pytest.mark.skipif(
     "os.environ.get('RLA_FORCE_NO_GPU') == '1'", reason="GPU disabled by env")
+
+
+def pytest_runtest_setup(item):
+    # debug census (RLA_DBG_THREADS=1): threads alive before the MNIST one-launch fidelity test
+    import os
+    if os.environ.get("RLA_DBG_THREADS") == "1" and "one_launch_grads" in item.nodeid:
+        import sys
+        import threading
+        names = [(t.name, type(t).__name__, t.daemon) for t in threading.enumerate()]
+        print(f"\n[threads before {item.nodeid}] {len(names)}: {names}", file=sys.stderr, flush=True)
