@@ -888,6 +888,13 @@ Tensor stem_wgrad(Tensor x, Tensor dy) {
   return dw;
 }
 
+// debug: every CU's LDS filled with `pattern` (blocks x 160 KB workgroups)
+void lds_poison(int64_t pattern, int64_t blocks) {
+  Tensor sink = at::empty({1}, at::TensorOptions().device(at::kCUDA).dtype(at::kInt));
+  TORCH_CHECK(rla::launch_lds_poison((uint32_t)pattern, sink.data_ptr<int>(), (int)blocks,
+                                     cur_stream(sink)) == 0, "lds_poison: launch refused");
+}
+
 bool stem_supported(int64_t N, int64_t H, int64_t W) {
   const rla::StemGeom g{(int)N, (int)H, (int)W, (int)((H - 1) / 2 + 1), (int)((W - 1) / 2 + 1)};
   return rla::stem_ok(g);
@@ -984,6 +991,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv3x3_supported", &conv3x3_supported, "shapes the 3x3 MFMA convolution covers");
   m.def("stem_fwd", &stem_fwd, "ResNet stem 7x7/s2 conv (3 -> 64) on MFMA [+ BatchNorm partial sums]");
   m.def("stem_supported", &stem_supported, "input shapes the stem kernel covers");
+  m.def("lds_poison", &lds_poison, "debug: fill every CU's LDS with a 32-bit pattern", py::arg("pattern"),
+        py::arg("blocks") = 2048);
   m.def("stem_wgrad", &stem_wgrad, "ResNet stem weight gradient on MFMA -> fp32 [64, 7, 7, 3] (channels_last order)");
   m.attr("ARCH") = "gfx950";
 }

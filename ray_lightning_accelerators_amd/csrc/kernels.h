@@ -350,4 +350,7 @@ bool launch_stem_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p
 // weight gradient: dy [N, OH, OW, 64] bf16 -> dw [64][7][7][3] fp32; part: [stem_grid(g)][64][224] fp32 workspace
 bool launch_stem_wgrad(const uint16_t* x, const uint16_t* dy, float* part, float* dw, const StemGeom& g,
                        hipStream_t stream);
+
+// debug tooling (csrc/debug_tools.hip): fill the whole LDS of `blocks` workgroups with `pattern`
+int launch_lds_poison(uint32_t pattern, int* sink, int blocks, hipStream_t stream);
 }  // namespace rla

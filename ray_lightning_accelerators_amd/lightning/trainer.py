@@ -473,7 +473,6 @@ class Trainer:
             self.wait_checkpoints()  # every checkpoint file is on disk when fit returns
             q = getattr(self, "_deferred", None)
             if q is not None:  # its thread ends with the fit (a later save starts a new one)
-                self._deferred = None
                 q.close()
         f = self._fused
         if f is not None and hasattr(f, "check"):
@@ -1302,7 +1301,7 @@ class Trainer:
         arrive as floats.  The training loop keeps dispatching meanwhile."""
         mark("ckpt_stage_begin")
         q = getattr(self, "_deferred", None)
-        if q is None:
+        if q is None or q.closed:
             q = self._deferred = _DeferredCheckpoints()
         q.drain_done()  # earlier decisions (best model path / score) are in place
         # ranks > 0 never write a file: no device snapshot, no host copy
@@ -1478,6 +1477,7 @@ class _DeferredCheckpoints:
         self._pending = 0
         self._cv = threading.Condition()
         self._stream = torch.cuda.Stream()
+        self.closed = False
         self._t = threading.Thread(target=self._loop, name="rla-deferred-ckpt", daemon=True)
         self._t.start()
 
@@ -1524,7 +1524,9 @@ class _DeferredCheckpoints:
         self._raise()
 
     def close(self) -> None:
-        """Finish the queued saves and end the thread."""
-        self._q.put(None)
-        self._t.join()
+        """Finish the queued saves and end the thread (idempotent)."""
+        if not self.closed:
+            self.closed = True
+            self._q.put(None)
+            self._t.join()
         self._raise()

@@ -1,7 +1,6 @@
 """Debug probe: does the MNIST one-launch step read LDS it never wrote?
 
-Fills the LDS of every CU with Inf by running the 3x3 MFMA convolution over an
-all-Inf input (its halo / weight images cover ~120 KB of each CU's LDS), then runs
+Fills the whole LDS of every CU with bf16 +Inf (csrc/debug_tools.hip), then runs
 the one-launch fidelity check (tests/test_mlp3.py::test_mlp3_one_launch_grads_vs_fp32_autograd).
 A pass right after a plain run and a failure after the poison means a
 read-before-write of LDS in the step kernel.
@@ -18,16 +17,11 @@ sys.path.insert(0, ".")
 sys.path.insert(0, "tests")
 
 
-def poison():
-    from ray_lightning_accelerators_amd.ops.conv import conv3x3_hip
+def poison(pattern=0x7F807F80):
+    """Every CU's whole LDS (160 KB) set to `pattern` (default: bf16 +Inf pairs)."""
+    from ray_lightning_accelerators_amd import ops
 
-    dev = torch.device("cuda", 0)
-    x = torch.full((64, 64, 56, 56), float("inf"), device=dev).to(torch.bfloat16)
-    x = x.contiguous(memory_format=torch.channels_last)
-    w = torch.full((64, 64, 3, 3), float("inf"), device=dev).to(torch.bfloat16).contiguous(
-        memory_format=torch.channels_last)
-    for _ in range(3):
-        conv3x3_hip(x, w)
+    ops.require().lds_poison(pattern, 4096)
     torch.cuda.synchronize()
 
 
