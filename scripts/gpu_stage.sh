@@ -32,6 +32,8 @@ for st in "$@"; do
       tail -3 "$O/pytest_gpu.log"
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
       run bench_default 300 python bench.py ;;
+    k20)  # the driver's bench window
+      run bench_k20 300 python bench.py --steps 20 --warmup 5 ;;
     dp)
       RLA_FIDELITY_LOG="$R/$O/fidelity.jsonl" run pytest_dp 600 $PYT tests/test_mlp3.py tests/test_comm.py -k "loopback or fused_dp or fp32"
       run dp_probe 300 python -u scripts/dp_overhead_probe.py
