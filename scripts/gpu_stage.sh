@@ -114,6 +114,17 @@ for st in "$@"; do
           || { echo "pmc pass $n failed"; tail -20 "$O/pmc_$n.log"; exit 1; }
       done
       find "$O" -name "*counter_collection.csv" ;;
+    pmc5)  # counter passes over the round-5 convolution kernels only (scripts/kernel_pmc_driver.py)
+      cd /tmp
+      for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS" \
+                  "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_WAIT_INST_LDS" "FETCH_SIZE" "WRITE_SIZE"; do
+        n=$(echo $pass | cut -d' ' -f1)
+        timeout -s KILL 120 rocprofv3 --pmc $pass --output-format csv -d "$R/$O/pmc5_$n" -o run -- \
+          python3 "$R/scripts/kernel_pmc_driver.py" > "$R/$O/pmc5_$n.log" 2>&1 \
+          || { echo "pmc pass $n failed"; tail -20 "$R/$O/pmc5_$n.log"; exit 1; }
+      done
+      cd "$R"
+      python scripts/pmc_summary.py $O/pmc5_* > "$O/pmc5_summary.md" && cat "$O/pmc5_summary.md" ;;
     share2)
       RLA_BENCH_SHARE_GPU=1 run share2_ray 300 python bench.py --gpus 2 --steps 500 --warmup 50
       RLA_BENCH_SHARE_GPU=1 run share2_hvd 300 python bench.py --gpus 2 --steps 500 --warmup 50 --accelerator horovod
