@@ -253,30 +253,61 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
         for (int k = 0; k < 16; ++k) acc[i][j][k] = 0.f;
   };
 
+  // One wave per SIMD: nothing else hides an LDS read's latency, so tap t + 1's
+  // fragments are read into the second register set while tap t's MFMAs run (round 5:
+  // the straight form waited lgkmcnt(0) before every tap's MFMAs).  Not in the 512-pixel
+  // statistics instances: their second fragment set spilled (172 B of scratch per lane
+  // at 56x56, forward + statistics 65.6 -> 94.4 us).
+  constexpr bool kPipe = !(ST && JB == 4);
+  auto fetch = [&](const __bf16* X, const __bf16* Wt, int tap, bf16x8 (&fa)[2], bf16x8 (&fb)[JB]) {
+    const int r = tap / 3, s = tap - (tap / 3) * 3;
+    const int toff = r * WP + s;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (FLIP) {
+        const __bf16* pa = Wt + (tap * 16 + rwo) * kFRow + i * 32 + cho;
+        fa[i] = __builtin_shufflevector(tr4(pa), tr4(pa + 4 * kFRow), 0, 1, 2, 3, 4, 5, 6, 7);
+      } else {
+        fa[i] = *reinterpret_cast<const bf16x8*>(Wt + (tap * kTN + i * 32 + (lane & 31)) * kRow + kg);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < JB; ++j)  // toff * kRow: an immediate offset when WC is set
+      fb[j] = *reinterpret_cast<const bf16x8*>(X + bpos[j] + toff * kRow);
+  };
   auto compute = [&](int buf) {
     const __bf16* X = lds + buf * kBufElems;
     const __bf16* Wt = X + kXElems;
+    if constexpr (!kPipe) {
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int r = tap / 3, s = tap - (tap / 3) * 3;
+        const int toff = r * WP + s;
+        bf16x8 a[2], b[JB];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          a[i] = *reinterpret_cast<const bf16x8*>(Wt + (tap * kTN + i * 32 + (lane & 31)) * kRow + kg);
+#pragma unroll
+        for (int j = 0; j < JB; ++j) b[j] = *reinterpret_cast<const bf16x8*>(X + bpos[j] + toff * kRow);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < JB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+      return;
+    }
+    bf16x8 fa[2][2], fb[2][JB];
+    fetch(X, Wt, 0, fa[0], fb[0]);
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
-      const int r = tap / 3, s = tap - (tap / 3) * 3;
-      const int toff = r * WP + s;
-      bf16x8 fa[2], fb[JB];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        if (FLIP) {
-          const __bf16* pa = Wt + (tap * 16 + rwo) * kFRow + i * 32 + cho;
-          fa[i] = __builtin_shufflevector(tr4(pa), tr4(pa + 4 * kFRow), 0, 1, 2, 3, 4, 5, 6, 7);
-        } else {
-          fa[i] = *reinterpret_cast<const bf16x8*>(Wt + (tap * kTN + i * 32 + (lane & 31)) * kRow + kg);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < JB; ++j)  // toff * kRow: an immediate offset when WC is set
-        fb[j] = *reinterpret_cast<const bf16x8*>(X + bpos[j] + toff * kRow);
+      const int cur = tap & 1;
+      if (tap + 1 < 9) fetch(X, Wt, tap + 1, fa[cur ^ 1], fb[cur ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of this tap's MFMAs
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < JB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < JB; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][i], fb[cur][j], acc[i][j], 0, 0, 0);
     }
   };
 

@@ -509,10 +509,12 @@ WgradPlan wgrad_plan(const WgradGeom& g, int splits, int algo) {
       // waves, the second round on 40% of the chip)
       S = 256 / tiles;
       if (S > T / 4) S = T / 4;       // >= 4 stages per split
-      // fp32 partials (9 taps) at most ~2x the dy + x bytes (the generic kernel
-      // re-reads those 9x; the autotuner picks between the two)
+      // fp32 partials (9 taps) at most ~4x the dy + x bytes (the generic kernel
+      // re-reads those 9x; the autotuner picks between the two).  Round 5 split sweep
+      // (profiles/r5_wsplit): at 7x7x512 the old 2x cap left S = 2 and 64 of 256 CUs
+      // busy, 205 us; S = 4 (3x the input bytes in partials) runs 123 us
       const double in_bytes = 2.0 * (double)g.N * g.OH * g.OW * (g.Cout + (double)g.Cin);
-      const int64_t max_part = (int64_t)(2.0 * in_bytes / (4.0 * 9.0 * g.Cout * g.Cin));
+      const int64_t max_part = (int64_t)(4.0 * in_bytes / (4.0 * 9.0 * g.Cout * g.Cin));
       if (S > max_part) S = max_part;
     }
     if (S < 1) S = 1;
@@ -539,12 +541,15 @@ WgradPlan wgrad_plan(const WgradGeom& g, int splits, int algo) {
     // ~512 workgroups (2 per CU, the loads of 8 waves in flight per CU) ...
     S = (512 + tiles - 1) / tiles;
     // ... at least 4 stages per split, and fp32 partials (written, then re-read by
-    // the reduce) of at most half the bytes the tiles read
+    // the reduce) of at most the bytes the tiles read.  (Half, before the round-5
+    // split sweep, profiles/r5_wsplit: that cap left the small-M layers under-filled
+    // -- 7x7 512 <-> 2048 at S = 3, 41 us vs 34 at S = 8; 14x14 1024 -> 2048 / 2 at
+    // S = 2, 92 us vs 71 at S = 4.)
     const int64_t max_rows = M / (4 * kb);
     if (S > max_rows) S = max_rows;
     const double in_bytes = 2.0 * (double)M * (g.Cout + (double)g.Cin) * g.KH * g.KW;  // per-tap tiles
     const double part_bytes = 4.0 * (double)g.Cout * g.Cin * g.KH * g.KW;
-    const int64_t max_part = (int64_t)(0.5 * in_bytes / part_bytes);
+    const int64_t max_part = (int64_t)(in_bytes / part_bytes);
     if (S > max_part) S = max_part;
   }
   if (S < 1) S = 1;

@@ -63,6 +63,8 @@ for st in "$@"; do
     wgrad)  # MFMA conv weight-gradient kernel: numerics + per-shape timing vs MIOpen / hipBLASLt
       run pytest_wgrad 300 $PYT tests/test_conv_wgrad.py tests/test_bn.py
       run wgrad_probe 300 python -u scripts/wgrad_probe.py ;;
+    wsplit)  # weight-gradient split-count sweep (planner's S vs fixed S per shape)
+      run wgrad_split 600 python -u scripts/wgrad_split_sweep.py ;;
     rn50b)  # native ResNet-50 bench: eager and whole-step hipGraph
       run rn50_base 600 python bench.py --model resnet50 --steps 30 --warmup 10
       run rn50_graph 600 python bench.py --model resnet50 --steps 30 --warmup 10 --resnet-graph 1 ;;
@@ -168,6 +170,11 @@ for st in "$@"; do
       run pytest_c3 300 $PYT tests/test_conv3x3.py
       run c3probe_fixed 300 python -u scripts/conv3x3_probe.py
       RLA_CONV3X3_GENERIC=1 run c3probe_generic 300 python -u scripts/conv3x3_probe.py ;;
+    c3pipe)  # 3x3 MFMA convolution after a schedule change: numerics + per-shape time vs MIOpen
+      run pytest_c3 300 $PYT tests/test_conv3x3.py
+      run c3probe 300 python -u scripts/conv3x3_probe.py ;;
+    wtests)  # weight-gradient + 3x3 kernels numerics
+      run pytest_w 300 $PYT tests/test_conv_wgrad.py tests/test_conv3x3.py ;;
     stem)  # ResNet stem kernel: numerics + device time vs MIOpen (+ BN statistics)
       run pytest_stem 300 $PYT tests/test_conv3x3.py -k "stem or maxpool"
       run stem_probe 300 python -u scripts/stem_probe.py ;;
