@@ -407,32 +407,44 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_kernel(const uint16_t* __
 #pragma unroll
         for (int k = 0; k < 16; ++k) acc[t][i][j][k] = 0.f;
 
+  // The 12 (k-step, tap) products of a stage as one stream: the next product's
+  // fragments are read while this one's MFMAs run (one wave per SIMD: nothing else
+  // hides the transposed reads' latency; round 5, as in conv3x3.hip).
+  auto rd_a = [&](int kk, bf16x8 (&fa)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const __bf16* pa = A + (kk * 16 + rwo) * SA + 32 * i + cho;
+      fa[i] = cat8(tr4(pa), tr4(pa + 4 * SA));
+    }
+  };
+  auto rd_b = [&](int kk, int t, bf16x8 (&fb)[2]) {
+    const int j = kk * 16 / OWP, p0 = kk * 16 - j * OWP;
+    const int xb = (j + r) * XP + p0 + t + rwo;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const __bf16* pb = B + xb * SB + 32 * jj + cho;
+      fb[jj] = cat8(tr4(pb), tr4(pb + 4 * SB));
+    }
+  };
   auto compute = [&]() {
     if (r >= 3) return;  // wave-uniform
+    bf16x8 fa[2][2], fb[2][2];
+    rd_a(0, fa[0]);
+    rd_b(0, 0, fb[0]);
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int j = kk * 16 / OWP, p0 = kk * 16 - j * OWP;
-      bf16x8 fa[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const __bf16* pa = A + (kk * 16 + rwo) * SA + 32 * i + cho;
-        fa[i] = cat8(tr4(pa), tr4(pa + 4 * SA));
+    for (int q = 0; q < 12; ++q) {
+      const int kk = q / 3, t = q - (q / 3) * 3;
+      if (q + 1 < 12) {
+        const int kn = (q + 1) / 3, tn = (q + 1) - ((q + 1) / 3) * 3;
+        if (tn == 0) rd_a(kn, fa[kn & 1]);
+        rd_b(kn, tn, fb[(q + 1) & 1]);
       }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int t = 0; t < 3; ++t) {
-        const int xb = (j + r) * XP + p0 + t + rwo;
-        bf16x8 fb[2];
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-          const __bf16* pb = B + xb * SB + 32 * jj + cho;
-          fb[jj] = cat8(tr4(pb), tr4(pb + 4 * SB));
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj)
-            acc[t][i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[jj], acc[t][i][jj], 0, 0, 0);
-      }
+        for (int jj = 0; jj < 2; ++jj)
+          acc[t][i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[kk & 1][i], fb[q & 1][jj], acc[t][i][jj], 0, 0, 0);
     }
   };
   // one LDS image, two register sets: stage `it` goes to LDS while stage it + 1 is
