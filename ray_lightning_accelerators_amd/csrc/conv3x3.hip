@@ -67,6 +67,19 @@ constexpr int kWElems = (kNW * kCvThreads / 2 * kRow) > (kNW * kCvThreads / 8 * 
                             ? (kNW * kCvThreads / 2 * kRow) : (kNW * kCvThreads / 8 * kFRow);
 constexpr int kBufElems = kXElems + kWElems;
 static_assert(2 * kBufElems * 2 >= 4 * 32 * 2 * 65 * 4, "ST reduction image fits the halo buffers");
+// Compile-time-shape instances pad every halo row by kHPad elements (160 B = 40 banks):
+// the row stride is then 12 W dwords mod 64, so 32 consecutive output pixels that
+// wrap into the next image row keep the bank sequence of one row (in the plain
+// [W + 2] layout the wrap shifts it by 24 dwords and a ds_read_b128 lane group
+// collides: modelled 1.3-1.9x the conflict-free LDS cycles of the pixel reads,
+// profiles/r5_pmc).  Run-time-shape instances keep the unpadded layout.
+constexpr int kHPad = 80;
+__host__ __device__ constexpr int halo_rows_max(int nx, int wc) { return nx * kCvThreads / 2 / (wc + 2) + 1; }
+__host__ __device__ constexpr int x_elems(int nx, int wc) {
+  return wc == 0 ? kXElems
+                 : (nx * kCvThreads / 2 * kRow + kHPad * halo_rows_max(nx, wc) > kXElems
+                        ? nx * kCvThreads / 2 * kRow + kHPad * halo_rows_max(nx, wc) : kXElems);
+}
 
 __device__ __forceinline__ bf16x4 tr4(const __bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(p));
@@ -113,11 +126,23 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
                                                              uint16_t* __restrict__ y, Conv3x3Geom g,
                                                              float* __restrict__ part) {
   static_assert(!(ST && FLIP), "statistics are a forward epilogue");
-  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * kBufElems];
+  constexpr int XE = x_elems(NX, WC), BE = XE + kWElems;  // halo / whole buffer elements
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * BE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (WC) g.W = WC;
   if (CC) g.Cin = CC;
   const int WP = g.W + 2, HP = g.H + 2;
+  const int RS = WC ? (WC + 2) * kRow + kHPad : WP * kRow;  // halo row stride (elements)
+  // padded layout: LDS element offset of this thread's halo piece i (the same every chunk)
+  uint32_t xlds[WC ? NX : 1];
+  if constexpr (WC != 0) {
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int p = tid + i * kCvThreads, pix = p >> 1;
+      const int vr = pix / WP, q = pix - vr * WP;
+      xlds[i] = (uint32_t)(vr * RS + q * kRow + (p & 1) * 8);
+    }
+  }
   const int64_t M = (int64_t)g.N * g.H * g.W;
   const int hw = g.H * g.W;
   constexpr int TM = 128 * JB;
@@ -206,13 +231,14 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
     for (int i = 0; i < kNW; ++i) st.w[i] = *reinterpret_cast<const u32x4*>(wc + (woff[i] + wstepb));
   };
   auto store = [&](const CvSet<NX>& st, int buf) {
-    __bf16* X = lds + buf * kBufElems;
-    __bf16* Wt = X + kXElems;
+    __bf16* X = lds + buf * BE;
+    __bf16* Wt = X + XE;
     const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int i = 0; i < NX; ++i) {
-      const int p = tid + i * kCvThreads;  // p >= xpieces: a row past the image, never read
-      *reinterpret_cast<u32x4*>(X + (p >> 1) * kRow + (p & 1) * 8) = (st.ok >> i) & 1u ? st.x[i] : z;
+    for (int i = 0; i < NX; ++i) {  // p >= xpieces: a row past the image, never read
+      const int p = tid + i * kCvThreads;
+      const uint32_t off = WC ? xlds[WC ? i : 0] : (uint32_t)((p >> 1) * kRow + (p & 1) * 8);
+      *reinterpret_cast<u32x4*>(X + off) = (st.ok >> i) & 1u ? st.x[i] : z;
     }
 #pragma unroll
     for (int i = 0; i < kNW; ++i) {
@@ -239,7 +265,7 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
       if (m >= m_end) m = m_end - 1;  // past the tile: a duplicate, never stored
       const int n = (int)(m / hw), rem = (int)(m - (int64_t)n * hw);
       const int oh = rem / g.W, ow = rem - oh * g.W;
-      bpos[jb] = ((n * HP + oh - v0) * WP + ow) * kRow + kg;
+      bpos[jb] = (n * HP + oh - v0) * RS + ow * kRow + kg;
     }
   };
 
@@ -261,7 +287,7 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
   constexpr bool kPipe = !(ST && JB == 4);
   auto fetch = [&](const __bf16* X, const __bf16* Wt, int tap, bf16x8 (&fa)[2], bf16x8 (&fb)[JB]) {
     const int r = tap / 3, s = tap - (tap / 3) * 3;
-    const int toff = r * WP + s;
+    const int toff = r * RS + s * kRow;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       if (FLIP) {
@@ -272,23 +298,23 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
       }
     }
 #pragma unroll
-    for (int j = 0; j < JB; ++j)  // toff * kRow: an immediate offset when WC is set
-      fb[j] = *reinterpret_cast<const bf16x8*>(X + bpos[j] + toff * kRow);
+    for (int j = 0; j < JB; ++j)  // toff: an immediate offset when WC is set
+      fb[j] = *reinterpret_cast<const bf16x8*>(X + bpos[j] + toff);
   };
   auto compute = [&](int buf) {
-    const __bf16* X = lds + buf * kBufElems;
-    const __bf16* Wt = X + kXElems;
+    const __bf16* X = lds + buf * BE;
+    const __bf16* Wt = X + XE;
     if constexpr (!kPipe) {
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int r = tap / 3, s = tap - (tap / 3) * 3;
-        const int toff = r * WP + s;
+        const int toff = r * RS + s * kRow;
         bf16x8 a[2], b[JB];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
           a[i] = *reinterpret_cast<const bf16x8*>(Wt + (tap * kTN + i * 32 + (lane & 31)) * kRow + kg);
 #pragma unroll
-        for (int j = 0; j < JB; ++j) b[j] = *reinterpret_cast<const bf16x8*>(X + bpos[j] + toff * kRow);
+        for (int j = 0; j < JB; ++j) b[j] = *reinterpret_cast<const bf16x8*>(X + bpos[j] + toff);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
