@@ -127,6 +127,7 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
                                                              float* __restrict__ part) {
   static_assert(!(ST && FLIP), "statistics are a forward epilogue");
   constexpr int XE = x_elems(NX, WC), BE = XE + kWElems;  // halo / whole buffer elements
+  static_assert(2 * BE * 2 <= 160 * 1024, "two LDS buffers fit the CU's 160 KiB");
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * BE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (WC) g.W = WC;
