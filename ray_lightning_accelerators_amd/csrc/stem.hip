@@ -414,25 +414,35 @@ __global__ __launch_bounds__(kStThreads) void stem_wgrad_kernel(const uint16_t* 
     *reinterpret_cast<float4*>(dst + i) = *reinterpret_cast<const float4*>(red + i);
 }
 
-// out[co][r][s][c] (fp32, [64][7][7][3]) = sum over rows g in order of part[g][co][32 r + 4 s + c]
+// out[co][r][s][c] (fp32, [64][7][7][3]) = sum over the G partial rows of
+// part[g][co][32 r + 4 s + c].  A block owns 32 consecutive part columns; its 8 row
+// groups each sum rows rg, rg + 8, ... (8 loads in flight), then the groups are added
+// in order 0..7 through LDS (fixed order: deterministic).  The one-thread-per-output
+// form walked all G = 256 rows 4 loads at a time: 64 dependent round trips, 23 us a
+// step (profiles/r5_final/kernel_stats_rn50.csv).
+constexpr int kRedCols = 32, kRedGroups = 256 / kRedCols;
 __global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
                                                                int G) {
-  const int o = blockIdx.x * 256 + threadIdx.x;
-  if (o >= 64 * 147) return;
-  const int co = o / 147, rem = o - co * 147, r = rem / 21, j = rem - r * 21, s = j / 3, c = j - s * 3;
-  const float* p = part + co * 224 + 32 * r + 4 * s + c;
+  __shared__ float sh[kRedGroups][kRedCols];
+  const int cl = threadIdx.x % kRedCols, rg = threadIdx.x / kRedCols;
+  const int col = blockIdx.x * kRedCols + cl;  // < 64 * 224 (grid = 14336 / 32)
+  const float* p = part + col;
   float a = 0.f;
-  int k = 0;
-  for (; k + 4 <= G; k += 4) {  // 4 loads in flight, summed in row order
-    const float v0 = p[(int64_t)k * 14336], v1 = p[(int64_t)(k + 1) * 14336], v2 = p[(int64_t)(k + 2) * 14336],
-                v3 = p[(int64_t)(k + 3) * 14336];
-    a += v0;
-    a += v1;
-    a += v2;
-    a += v3;
+  int k = rg;
+  for (; k + 7 * kRedGroups < G; k += 8 * kRedGroups) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(k + u * kRedGroups) * 14336];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a += v[u];
   }
-  for (; k < G; ++k) a += p[(int64_t)k * 14336];
-  out[o] = a;
+  for (; k < G; k += kRedGroups) a += p[(int64_t)k * 14336];
+  sh[rg][cl] = a;
+  __syncthreads();
+  if (rg != 0) return;
+  for (int q = 1; q < kRedGroups; ++q) a += sh[q][cl];
+  const int co = col / 224, j = col - co * 224, r = j >> 5, s = (j >> 2) & 7, c = j & 3;
+  if (r < 7 && s < 7 && c < 3) out[co * 147 + r * 21 + s * 3 + c] = a;
 }
 
 int st_cu_count() {
@@ -465,7 +475,7 @@ bool launch_stem_wgrad(const uint16_t* x, const uint16_t* dy, float* part, float
   if (!stem_ok(g)) return false;
   const int G = stem_grid(g);
   hipLaunchKernelGGL(stem_wgrad_kernel, dim3(G), dim3(kStThreads), 0, s, x, dy, part, g);
-  hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3((64 * 147 + 255) / 256), dim3(256), 0, s, part, dw, G);
+  hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(64 * 224 / kRedCols), dim3(256), 0, s, part, dw, G);
   return true;
 }
 

@@ -23,6 +23,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--splits", default="2,4,8,16,32,64")
+    ap.add_argument("--algo", type=int, default=0, help="1: the generic tap-GEMM kernel for every shape")
+    ap.add_argument("--kernel", type=int, default=0, help="only shapes with this kernel size (0: all)")
     args = ap.parse_args()
     from ray_lightning_accelerators_amd import ops
 
@@ -31,18 +33,18 @@ def main():
     svals = [int(s) for s in args.splits.split(",")]
     tot_auto = tot_best = 0.0
     for (h, cin, cout, k, st, count) in SHAPES:
-        if count == 0:
+        if count == 0 or (args.kernel and k != args.kernel):
             continue
         pad = k // 2
         n = args.batch
         oh = (h + 2 * pad - k) // st + 1
         x = torch.randn(n, cin, h, h, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dy = torch.randn(n, cout, oh, oh, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        auto_plan = list(mod.conv_wgrad_plan(n, h, h, cin, oh, oh, cout, k, k, st, st, pad, pad, 0))
+        auto_plan = list(mod.conv_wgrad_plan(n, h, h, cin, oh, oh, cout, k, k, st, st, pad, pad, 0, args.algo))
         R = 10
-        t = {"auto": _time(lambda: wgrad_hip(dy, x, (k, k), (st, st), (pad, pad), 0), R) * 1e3 / R}
+        t = {"auto": _time(lambda: wgrad_hip(dy, x, (k, k), (st, st), (pad, pad), 0, args.algo), R) * 1e3 / R}
         for s in svals:
-            t[str(s)] = _time(lambda: wgrad_hip(dy, x, (k, k), (st, st), (pad, pad), s), R) * 1e3 / R
+            t[str(s)] = _time(lambda: wgrad_hip(dy, x, (k, k), (st, st), (pad, pad), s, args.algo), R) * 1e3 / R
         best = min(t, key=t.get)
         tot_auto += count * t["auto"]
         tot_best += count * t[best]
