@@ -20,7 +20,16 @@ from ray_lightning_accelerators_amd.parallel.mlp_engine import FusedMLPEngine  #
 ap = argparse.ArgumentParser()
 ap.add_argument("--k", type=int, default=20)
 ap.add_argument("--windows", type=int, default=50)
+ap.add_argument("--sched", choices=["default", "spin", "yield", "blocking"], default="default",
+                help="hipSetDeviceFlags scheduling mode, set before the first HIP call")
+ap.add_argument("--graphs", default="0,1,2,4,5,10,20")
 args = ap.parse_args()
+if args.sched != "default":
+    import ctypes
+
+    flag = {"spin": 1, "yield": 2, "blocking": 4}[args.sched]
+    rc = ctypes.CDLL("libamdhip64.so").hipSetDeviceFlags(ctypes.c_uint(flag))
+    print(json.dumps({"hipSetDeviceFlags": args.sched, "rc": rc}), flush=True)
 dev = torch.device("cuda", 0)
 x, y = synthetic_mnist(55000, seed=0)
 
@@ -51,7 +60,7 @@ for _ in range(200):
 print(json.dumps({"idle_sync_us": round(statistics.median(ts) * 1e6, 2),
                   "one_kernel_window_us": round(statistics.median(tk) * 1e6, 2)}), flush=True)
 
-for G in [0, 1, 2, 4, 5, 10, 20]:
+for G in [int(v) for v in args.graphs.split(",")]:
     if G and args.k % G:
         continue
     eng = FusedMLPEngine(32, 64, 32, lr=1e-1, device=dev, seed=0)
