@@ -579,6 +579,22 @@ Tensor gap_bwd(Tensor dy, int64_t HW) {
   return dx;
 }
 
+// d [N, C, H, W] channels_last bf16 (in place) += g [N*OH*OW, C] bf16 at every s-th pixel
+void strided_add_(Tensor d, Tensor g, int64_t s) {
+  TORCH_CHECK(d.is_cuda() && d.scalar_type() == at::kBFloat16, "strided_add_: d must be a bf16 GPU tensor");
+  check_dev(g, "g", at::kBFloat16);
+  TORCH_CHECK(d.dim() == 4 && d.is_contiguous(at::MemoryFormat::ChannelsLast), "strided_add_: d channels_last [N, C, H, W]");
+  const int64_t N = d.size(0), C = d.size(1), H = d.size(2), W = d.size(3);
+  TORCH_CHECK(s >= 1 && C % 8 == 0, "strided_add_: C % 8 == 0, s >= 1");
+  const int64_t OH = (H - 1) / s + 1, OW = (W - 1) / s + 1;
+  TORCH_CHECK(g.is_contiguous() && g.numel() == N * OH * OW * C && g.size(-1) == C, "strided_add_: g [N*OH*OW, C]");
+  const at::hip::HIPGuardMasqueradingAsCUDA guard(d.device());
+  TORCH_CHECK(rla::launch_strided_add(reinterpret_cast<uint16_t*>(d.data_ptr()),
+                                      reinterpret_cast<const uint16_t*>(g.data_ptr()), (int)N, (int)H, (int)W, (int)C,
+                                      (int)OH, (int)OW, (int)s, cur_stream(d)) == 0,
+              "strided add launch failed");
+}
+
 Tensor maxpool_bwd(Tensor dy, Tensor arg, int64_t H, int64_t W, int64_t k, int64_t s, int64_t pad) {
   check_dev(dy, "dy", at::kBFloat16);
   check_dev(arg, "arg", at::kByte);
@@ -963,6 +979,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "NHWC bf16 max pool -> (y, one-byte window argmax); bn_ss: pool bf16(relu(x * scale + shift)) instead",
         py::arg("x"), py::arg("k"), py::arg("s"), py::arg("pad"), py::arg("bn_ss") = py::none(),
         py::arg("nbt_inc") = py::none());
+  m.def("strided_add_", &strided_add_, "d[:, :, ::s, ::s] += g in place over NHWC bf16 rows (fp32 add)");
   m.def("gap_bwd", &gap_bwd, "global average pool backward over NHWC rows (16-byte stores)");
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max pool backward (gather through the argmax bytes)");
   m.def("bn_bwd_apply", &bn_bwd_apply, "fused BN backward apply: dx (+ dres = relu-masked dy)", py::arg("x"),

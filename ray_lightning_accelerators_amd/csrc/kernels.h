@@ -57,6 +57,9 @@ int launch_maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int
                        int OW, int k, int s, int pad, hipStream_t stream);
 // global average pool backward over NHWC rows: dx[n][p][c] = dy[n][c] / HW
 int launch_gap_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t stream);
+// d [N, H, W, C] += g [N, OH, OW, C] at every s-th pixel (NHWC bf16, fp32 add)
+int launch_strided_add(uint16_t* d, const uint16_t* g, int N, int H, int W, int C, int OH, int OW, int s,
+                       hipStream_t stream);
 // a max pool's backward seen from the layer before it (csrc/pool_gather.h)
 struct PoolGrad {
   const uint16_t* g;   // gradient of the pooled output [N, OH, OW, C] bf16

@@ -147,7 +147,38 @@ __global__ __launch_bounds__(256) void gap_bwd_kernel(const uint16_t* __restrict
   *reinterpret_cast<u16x8*>(dx + t * 8) = __builtin_bit_cast(u16x8, __builtin_convertvector(d, b8));
 }
 
+// d[n][oh s][ow s][:] += g[(n OH + oh) OW + ow][:] over NHWC bf16 rows: the strided
+// downsample branch's input gradient added into every s-th pixel of the parked one
+// (ops/conv.py GradFork).  One thread = 8 channels: fp32 add, one bf16 rounding --
+// exactly ATen's bf16 add_, which ran this strided view through its non-vectorised
+// elementwise path (~22 us a call, profiles/r5_final3/kernel_stats_rn50.csv).
+__global__ __launch_bounds__(256) void strided_add_kernel(uint16_t* __restrict__ d, const uint16_t* __restrict__ g,
+                                                          int N, int H, int W, int C, int OH, int OW, int s) {
+  const int G = C >> 3;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)N * OH * OW * G) return;
+  const int gi = (int)(t % G);
+  const int64_t p = t / G;
+  const int ow = (int)(p % OW);
+  const int64_t q = p / OW;
+  const int oh = (int)(q % OH), n = (int)(q / OH);
+  uint16_t* dp = d + (((int64_t)n * H + (int64_t)oh * s) * W + (int64_t)ow * s) * C + gi * 8;
+  const f8 a = ld8(dp) + ld8(g + t * 8);
+  *reinterpret_cast<u16x8*>(dp) = __builtin_bit_cast(u16x8, __builtin_convertvector(a, b8));
+}
+
 }  // namespace
+
+int launch_strided_add(uint16_t* d, const uint16_t* g, int N, int H, int W, int C, int OH, int OW, int s,
+                       hipStream_t stream) {
+  if (C % 8 || s < 1 || (OH - 1) * s >= H || (OW - 1) * s >= W) return -1;
+  const int64_t total = (int64_t)N * OH * OW * (C / 8);
+  const int64_t blocks = (total + 255) / 256;
+  if (blocks > 0x7fffffff) return -2;
+  if (blocks == 0) return 0;
+  hipLaunchKernelGGL(strided_add_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, d, g, N, H, W, C, OH, OW, s);
+  return 0;
+}
 
 int launch_gap_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t stream) {
   if (C % 8 || HW < 1) return -1;

@@ -481,6 +481,17 @@ class _ConvNHWCFn(torch.autograd.Function):
                 # (measured and reverted, round 5: the same sum as ONE strided batched
                 # GEMM with beta = 1 into every stride-th pixel -- hipBLASLt ran it as
                 # MT256x16x64 at ~205 us a call vs ~21 us for this GEMM + strided add)
+                s_ = stride[0]
+                if (s_ == stride[1] and d.dtype == torch.bfloat16 and g2.dtype == torch.bfloat16
+                        and d.is_contiguous(memory_format=torch.channels_last) and g2.is_contiguous()
+                        and d.size(1) % 8 == 0 and (d.size(2) - 1) // s_ + 1 == oh_
+                        and (d.size(3) - 1) // s_ + 1 == ow_):
+                    # 16-byte vectors over the NHWC rows, same fp32 add + one rounding
+                    # as ATen's add_ (which took its non-vectorised strided path)
+                    from . import require
+
+                    require().strided_add_(d, g2, s_)
+                    return
                 view = d[:, :, ::stride[0], ::stride[1]]
                 view.add_(_from2d(g2, n_, oh_, ow_))
 

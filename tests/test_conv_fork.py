@@ -67,3 +67,26 @@ def test_forked_convs_match_autograd_sum(stride):
         err = (got[0] - ref[0]).norm() / ref[0].norm()
         assert err < 2e-2, err  # bf16 dgrad outputs, different rounding points
         assert torch.allclose(got[1], ref[1]) and torch.allclose(got[2], ref[2])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,c,h,w,s", [(2, 256, 56, 56, 2), (3, 64, 15, 9, 2), (1, 32, 7, 7, 3), (2, 16, 8, 8, 1)])
+def test_strided_add_matches_aten_bitwise(n, c, h, w, s):
+    """The fork's strided add (csrc/pool.hip strided_add_kernel) against ATen's bf16
+    add_ on the strided view: fp32 add and one rounding in both, so bitwise equal."""
+    import torch
+
+    from ray_lightning_accelerators_amd.ops import require
+
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cpu").manual_seed(n * 100 + c)
+    d = torch.randn(n, c, h, w, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    oh, ow = (h - 1) // s + 1, (w - 1) // s + 1
+    g2 = torch.randn(n * oh * ow, c, generator=g).to(dev, torch.bfloat16)
+    ref = d.clone()
+    ref[:, :, ::s, ::s].add_(g2.view(n, oh, ow, c).permute(0, 3, 1, 2))
+    require().strided_add_(d, g2, s)
+    torch.cuda.synchronize()
+    assert torch.equal(d.view(torch.int16), ref.view(torch.int16))
