@@ -42,6 +42,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import statistics
 import subprocess
@@ -109,9 +110,6 @@ def parse(argv=None):
     ap.add_argument("--lr", type=float, default=1e-1)
     ap.add_argument("--graph-steps", type=int, default=8,
                     help="optimizer steps per captured hipGraph (native, torch-graph); 0 = eager launches")
-    ap.add_argument("--launch", choices=["graph", "loop"], default="graph",
-                    help="mnist native one-launch step: 'graph' replays hipGraphs of --graph-steps steps; "
-                         "'loop' issues the timed window's launches back to back from one C++ call")
     ap.add_argument("--n-data", type=int, default=55000)
     ap.add_argument("--trainer-epochs", type=int, default=4, help="--via trainer: epochs (the first is warm-up)")
     ap.add_argument("--bucket-mb", type=float, default=8.0, help="resnet50 DDP bucket cap (MiB)")
@@ -265,9 +263,6 @@ def make_native(args, world, rank, dev, x, y, force_split=False):
         route = f"split-{get_native_comm(create=False).route(eng.comm_buffer)}"  # oneshot / rccl / torch
     graphed = False
     gsteps = graph_steps_for(args.graph_steps, args.steps)
-    if args.launch == "loop" and eng._loop_ok():
-        eng.launch_loop = True
-        gsteps = 0  # no capture: run() issues each window from one C++ launch loop
     tuned = None
     if eng.one_launch_dp and args.dp_proto == "auto" and gsteps > 0:
         tuned = tune_dp_proto(eng, world, rank, dev, gsteps)
@@ -286,7 +281,7 @@ def make_native(args, world, rank, dev, x, y, force_split=False):
     one = eng.native and (eng.one_launch_dp if world > 1 else eng.one_launch)
     info = {"route": route, "hip_graph_steps": gsteps if graphed else 0,
             "step_kernel": ("one-launch" if one else "head+tail") if eng.native else "torch-cpu",
-            "step_launch": "cpp-loop" if eng.launch_loop else ("hip-graph" if graphed else "eager")}
+            "step_launch": "hip-graph" if graphed else "eager"}
     if eng.dp_ctx is not None:
         info["dp_proto"] = eng.dp_proto
         if tuned is not None:
@@ -724,6 +719,12 @@ def run_rank(args):
     n_ranks = dist.get_world_size() if world > 1 else 1
     value = args.steps * args.batch_size * n_ranks / elapsed
     loss = last_loss()
+    # fail fast on a diverged / corrupted run: a throughput measured on
+    # non-finite training state is not a result
+    csum = checksum() if checksum is not None else 0.0
+    if not (math.isfinite(loss) and math.isfinite(csum)):
+        raise SystemExit(f"bench: non-finite training state after the timed steps "
+                         f"(final_train_loss={loss}, parameter checksum={csum})")
     stock = None
     if args.compare_stock and not rn and args.impl == "native" and dev.type == "cuda":
         # the stock stack in the same job, same ranks / data / batch / step count
@@ -912,9 +913,12 @@ class _EpochClock(Callback):
                            "graph_step": (trainer._fused.describe() if hasattr(trainer._fused, "describe") else
                                           trainer._graph_step_reason),
                            "replicas_equal": replicas_equal,
-                           "train_loss": float(trainer.callback_metrics.get("train_loss", float("nan"))),
-                           "val_loss": float(trainer.callback_metrics.get("ptl/val_loss", float("nan"))),
-                           "val_accuracy": float(trainer.callback_metrics.get("ptl/val_accuracy", float("nan"))),
+                           "train_loss": float(trainer.callback_metrics.get(
+                               "train_loss", trainer.callback_metrics.get("ptl/train_loss", float("nan")))),
+                           "val_loss": float(trainer.callback_metrics.get(
+                               "ptl/val_loss", trainer.callback_metrics.get("val_loss", float("nan")))),
+                           "val_accuracy": float(trainer.callback_metrics.get(
+                               "ptl/val_accuracy", trainer.callback_metrics.get("val_acc", float("nan")))),
                            "best_model_path": getattr(trainer.checkpoint_callback, "best_model_path", None)}, f)
 
 
@@ -940,8 +944,10 @@ def run_trainer(args):
         # captured by the Trainer (lightning/graph_step.py), a checkpoint every epoch
         from ray_lightning_accelerators_amd.models.resnet import LightningResNet50
 
+        # validation every epoch on a held-out resident set: 2 batches per rank (~10 % of
+        # the 20 training steps, the reference MNIST example's 5,000 / 55,000 ratio)
         model = LightningResNet50({"batch_size": args.batch_size, "n_train": args.batch_size * args.steps * args.gpus,
-                                   "lr": 0.1})
+                                   "n_val": args.batch_size * 2 * args.gpus, "lr": 0.1})
     else:
         model = MNISTClassifier({"layer_1": args.layer_1, "layer_2": args.layer_2, "lr": args.lr,
                                  "batch_size": args.batch_size})
@@ -994,6 +1000,9 @@ def run_trainer(args):
     with open(out_path) as f:
         rows = json.load(f)
     os.unlink(out_path)
+    tl = rows.get("train_loss")
+    if tl is None or not math.isfinite(tl):
+        raise SystemExit(f"bench: non-finite training loss after Trainer.fit (train_loss={tl})")
     world = rows["world"]
     nb = rows["batches"]
     epochs = rows["epoch_s"]
@@ -1001,6 +1010,10 @@ def run_trainer(args):
     per_epoch = nb * args.batch_size * world
     med = statistics.median(steady)
     value = per_epoch * len(steady) / sum(steady)
+    # the same epochs without their validation passes (training + checkpoint only)
+    split_steady = rows["split"][1:] or rows["split"]
+    no_val_s = sum(max(e - r["val_s"], 1e-9) for e, r in zip(steady, split_steady))
+    value_no_val = per_epoch * len(steady) / no_val_s
     if rn:
         base = RESNET_STOCK_BASELINE["torch-graph"] * world
     return {
@@ -1027,7 +1040,8 @@ def run_trainer(args):
             "launch": launch,
             "epochs": args.trainer_epochs,
             "val_batches_per_epoch": rows["val_batches"],
-            "checkpointing": True,
+            "train_steps_per_epoch": nb,
+            "checkpointing": f"every epoch ({nb} steps)",
             "fused_step": rows["fused"],
             "graph_step": rows.get("graph_step"),
         },
@@ -1041,6 +1055,7 @@ def run_trainer(args):
         "fit_wall_s": round(fit_s, 2),
         "val_loss": rows["val_loss"],
         "val_accuracy": rows["val_accuracy"],
+        "value_without_validation": round(value_no_val, 1),
     }
 
 

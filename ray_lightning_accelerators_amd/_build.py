@@ -45,7 +45,7 @@ def _torch_paths() -> Dict[str, object]:
 
 EXTENSIONS = {
     "_C": {
-        "hip": ["optim_kernels.hip", "mlp_kernels.hip", "mlp_adam.hip", "mlp_step3.hip", "bn_act.hip", "pool.hip", "conv_wgrad.hip", "conv3x3.hip", "conv1x1.hip", "stem.hip", "mlp_resident.hip", "debug_tools.hip"],
+        "hip": ["optim_kernels.hip", "mlp_kernels.hip", "mlp_adam.hip", "mlp_step3.hip", "bn_act.hip", "pool.hip", "conv_wgrad.hip", "conv3x3.hip", "conv1x1.hip", "stem.hip"],
         "cpp": ["bindings.cpp"],
         "torch": True,
         "libs": [],

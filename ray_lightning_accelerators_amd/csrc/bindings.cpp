@@ -751,65 +751,6 @@ std::vector<int64_t> conv_wgrad_plan(int64_t N, int64_t H, int64_t W, int64_t Ci
   return {p.kind, p.wa, p.wb, p.splits, p.rows_per_split};
 }
 
-// Resident training loop (csrc/mlp_resident.hip): K steps in one workgroup.  The
-// device state follows the mlp3 convention; the engine re-primes its pipelined
-// kernels' buffers (H1pre, bf16 shadows) before it runs them again.
-void mlp_resident(Tensor x_u8, Tensor labels, Tensor order, Tensor counters, int64_t n_batches, int64_t B,
-                  int64_t L1, int64_t L2, int64_t K, Tensor params, Tensor exp_avg, Tensor exp_avg_sq,
-                  optional<Tensor> stats, double lr, double beta1, double beta2, double eps, double weight_decay,
-                  optional<Tensor> lr_t, bool adamw) {
-  TORCH_CHECK(rla::resident_supported((int)L1, (int)L2, (int)B), "no resident MLP kernel for ", L1, "/", L2,
-              " batch ", B);
-  TORCH_CHECK(K >= 0, "mlp_resident: K must be >= 0");
-  const int64_t np = mlp_param_count(L1, L2);
-  check_dev(params, "params", at::kFloat);
-  check_dev(exp_avg, "exp_avg", at::kFloat);
-  check_dev(exp_avg_sq, "exp_avg_sq", at::kFloat);
-  TORCH_CHECK(params.numel() == np && exp_avg.numel() == np && exp_avg_sq.numel() == np,
-              "param / Adam arenas must hold ", np, " floats");
-  check_dev(counters, "counters", at::kLong);
-  TORCH_CHECK(counters.numel() >= 10, "counters must hold 10 int64");
-  check_dev(x_u8, "x_u8", at::kByte);
-  TORCH_CHECK(x_u8.dim() == 2 && x_u8.size(1) == 784, "x_u8 must be [N, 784]");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(x_u8.data_ptr()) % 16 == 0, "x_u8 must be 16-byte aligned");
-  check_dev(labels, "labels", at::kLong);
-  TORCH_CHECK(labels.numel() == x_u8.size(0), "labels must match the dataset");
-  check_dev(order, "order", at::kLong);
-  TORCH_CHECK(n_batches >= 1 && order.numel() >= 2 * n_batches * B, "order must be [2, n_batches * B]");
-  const at::hip::HIPGuardMasqueradingAsCUDA guard(params.device());
-  rla::ResidentArgs a{};
-  a.x_u8 = x_u8.data_ptr<uint8_t>();
-  a.labels = labels.data_ptr<int64_t>();
-  a.order = order.data_ptr<int64_t>();
-  a.order_stride = order.numel() / 2;
-  a.n_data = x_u8.size(0);
-  a.counters = counters.data_ptr<int64_t>();
-  a.n_batches = n_batches;
-  a.B = (int)B;
-  a.L1 = (int)L1;
-  a.L2 = (int)L2;
-  a.K = (int)K;
-  a.params = params.data_ptr<float>();
-  a.exp_avg = exp_avg.data_ptr<float>();
-  a.exp_avg_sq = exp_avg_sq.data_ptr<float>();
-  a.stats = nullptr;
-  a.stats_ring = 0;
-  if (stats.has_value() && stats->defined()) {
-    check_dev(*stats, "stats", at::kFloat);
-    TORCH_CHECK(stats->dim() == 2 && stats->size(1) == 4, "stats must be [ring, 4]");
-    a.stats = stats->data_ptr<float>();
-    a.stats_ring = (int)stats->size(0);
-  }
-  a.lr = (float)lr;
-  a.beta1 = (float)beta1;
-  a.beta2 = (float)beta2;
-  a.eps = (float)eps;
-  a.weight_decay = (float)weight_decay;
-  a.lr_ptr = ptr_or_null<const float>(lr_t, "lr_tensor", at::kFloat, 1);
-  a.adamw = adamw ? 1 : 0;
-  TORCH_CHECK(rla::launch_mlp_resident(a, cur_stream(params)) == 0, "resident MLP launch failed");
-}
-
 // 3x3 / stride 1 / pad 1 NHWC bf16 convolution (csrc/conv3x3.hip): x [N, H, W, Cin]
 // and w [Cout, 3, 3, Cin] as contiguous memory; returns y as contiguous [N, H, W, Cout].
 // flip: the input gradient -- x = dy, w = the forward weight [Cin][3][3][Cout]
@@ -904,13 +845,6 @@ Tensor stem_wgrad(Tensor x, Tensor dy) {
   return dw;
 }
 
-// debug: every CU's LDS filled with `pattern` (blocks x 160 KB workgroups)
-void lds_poison(int64_t pattern, int64_t blocks) {
-  Tensor sink = at::empty({1}, at::TensorOptions().device(at::kCUDA).dtype(at::kInt));
-  TORCH_CHECK(rla::launch_lds_poison((uint32_t)pattern, sink.data_ptr<int>(), (int)blocks,
-                                     cur_stream(sink)) == 0, "lds_poison: launch refused");
-}
-
 bool stem_supported(int64_t N, int64_t H, int64_t W) {
   const rla::StemGeom g{(int)N, (int)H, (int)W, (int)((H - 1) / 2 + 1), (int)((W - 1) / 2 + 1)};
   return rla::stem_ok(g);
@@ -994,12 +928,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("OH"), py::arg("OW"), py::arg("Cout"),
         py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
         py::arg("splits") = 0, py::arg("algo") = 0);
-  m.def("mlp_resident", &mlp_resident, "K MNIST-MLP training steps in one resident workgroup",
-        py::arg("x_u8"), py::arg("labels"), py::arg("order"), py::arg("counters"), py::arg("n_batches"),
-        py::arg("B"), py::arg("L1"), py::arg("L2"), py::arg("K"), py::arg("params"), py::arg("exp_avg"),
-        py::arg("exp_avg_sq"), py::arg("stats"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"),
-        py::arg("weight_decay"), py::arg("lr_tensor"), py::arg("adamw") = false);
-  m.def("resident_supported", &rla::resident_supported, "layer sizes / batch the resident kernel covers");
   m.def("conv3x3", &conv3x3, "3x3 / stride 1 / pad 1 NHWC bf16 convolution on MFMA -> [N, H, W, Cout]",
         py::arg("x"), py::arg("w"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"),
         py::arg("flip") = false);
@@ -1008,8 +936,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv3x3_supported", &conv3x3_supported, "shapes the 3x3 MFMA convolution covers");
   m.def("stem_fwd", &stem_fwd, "ResNet stem 7x7/s2 conv (3 -> 64) on MFMA [+ BatchNorm partial sums]");
   m.def("stem_supported", &stem_supported, "input shapes the stem kernel covers");
-  m.def("lds_poison", &lds_poison, "debug: fill every CU's LDS with a 32-bit pattern", py::arg("pattern"),
-        py::arg("blocks") = 2048);
   m.def("stem_wgrad", &stem_wgrad, "ResNet stem weight gradient on MFMA -> fp32 [64, 7, 7, 3] (channels_last order)");
   m.attr("ARCH") = "gfx950";
 }

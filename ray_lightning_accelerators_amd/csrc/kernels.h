@@ -263,28 +263,6 @@ enum MLP3Kind { kMLP3Step = 0, kMLP3Head = 1, kMLP3TailGrad = 2, kMLP3TailAdam =
 int64_t mlp3_hand_words(int L1, int L2);  // int64 words of the one-launch step's hand-off buffer
 int launch_mlp3(const MLP3Args& a, int kind, hipStream_t stream);
 
-// Resident training loop (csrc/mlp_resident.hip): K steps of the 784-32-64-10 MLP,
-// batch 32, Adam, in ONE workgroup with the model held in registers / LDS.
-struct ResidentArgs {
-  const uint8_t* x_u8;    // [N_data, 784]
-  const int64_t* labels;  // [N_data]
-  const int64_t* order;   // [2][order_stride]
-  int64_t order_stride;
-  int64_t n_data;         // rows of x_u8 (sample indices are clamped into it)
-  int64_t* counters;      // engine device state (mlp_step3.hip convention)
-  int64_t n_batches;
-  int B, L1, L2, K;
-  float* params;
-  float* exp_avg;
-  float* exp_avg_sq;
-  float* stats;
-  int stats_ring;
-  float lr, beta1, beta2, eps, weight_decay;
-  const float* lr_ptr;
-  int adamw;
-};
-bool resident_supported(int L1, int L2, int B);
-int launch_mlp_resident(const ResidentArgs& a, hipStream_t stream);
 int mlp3_act_rows(int L1, int L2);
 // the packed DP exchange's wire form of fp32 pairs, encoded and decoded (tests)
 int dp_pack_roundtrip(const float* x, float* y, int64_t n, int tag, hipStream_t stream);
@@ -354,6 +332,4 @@ bool launch_stem_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p
 bool launch_stem_wgrad(const uint16_t* x, const uint16_t* dy, float* part, float* dw, const StemGeom& g,
                        hipStream_t stream);
 
-// debug tooling (csrc/debug_tools.hip): fill the whole LDS of `blocks` workgroups with `pattern`
-int launch_lds_poison(uint32_t pattern, int* sink, int blocks, hipStream_t stream);
 }  // namespace rla

@@ -174,6 +174,8 @@ class GraphedTrainStep:
         self._B = 0
         self._nb = 0
         self._last_rows = None
+        self._last_batch = None
+        self._eval_resident: Dict[int, Any] = {}
         self.opt.enable_device_scalars()
         if getattr(self.opt, "_hvd_state", None) is not None and trainer.world_size > 1:
             self._adopt_horovod()
@@ -225,6 +227,23 @@ class GraphedTrainStep:
         t, model, acc, opt = self.trainer, self.model, self.acc, self.opt
         calls: List[tuple] = []
         batch = batch_fn()
+        self._last_batch = batch  # a rejected resident step re-runs THIS batch eagerly
+        # eager (not captured) step: the forward's buffer updates (BatchNorm running
+        # statistics, num_batches_tracked) are undone if the step is rejected below,
+        # so the eager re-run applies them once
+        saved = None
+        if not torch.cuda.is_available() or not torch.cuda.is_current_stream_capturing():
+            saved = [(b, b.detach().clone()) for b in model.buffers()]
+        try:
+            return self._body_checked(t, model, acc, opt, calls, batch, batch_idx, probe)
+        except _Unsupported:
+            if saved is not None:
+                with torch.no_grad():
+                    for b, c in saved:
+                        b.copy_(c)
+            raise
+
+    def _body_checked(self, t, model, acc, opt, calls, batch, batch_idx: int, probe: bool):
         acc.before_forward(sync=True)
         t._log_sink = calls
         mode = HostReadProbe() if probe else None
@@ -281,7 +300,13 @@ class GraphedTrainStep:
     def _after_step(self, replayed: bool, direct=None) -> Dict[str, torch.Tensor]:
         """Python side of one executed step: host counters, the replayed ``self.log``
         calls (ring views; ``direct``: the step's own tensors when its layout did not
-        match the ring's), the step output."""
+        match the ring's), the step output.
+
+        Validity window: replayed steps' outputs and logged values are VIEWS of the
+        device ring (``ring_rows`` >= 2 epochs of steps), so a consumer that keeps one
+        longer than two epochs sees a later step's value -- clone what must outlive
+        that (the Trainer's own consumers do: ModelCheckpoint / EarlyStopping convert
+        to host floats, ``defer_checkpoint`` clones its values)."""
         t = self.trainer
         if replayed:
             for gs in self.opt._rla_groups:
@@ -315,9 +340,12 @@ class GraphedTrainStep:
         on this path: ``failed``)."""
         if self._side is not None:
             self._side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(self._side):
-                layout, vals = self._body(batch_fn, batch_idx, probe)
-            torch.cuda.current_stream().wait_stream(self._side)
+            try:
+                with torch.cuda.stream(self._side):
+                    layout, vals = self._body(batch_fn, batch_idx, probe)
+            finally:
+                # also on a rejection: the eager re-run reads the side stream's gather
+                torch.cuda.current_stream().wait_stream(self._side)
         else:
             layout, vals = self._body(batch_fn, batch_idx, probe)
         if self._log_meta is None:
@@ -397,7 +425,15 @@ class GraphedTrainStep:
     def train_batch(self, batch, batch_idx: int):
         t = self.trainer
         if isinstance(batch, tuple) and len(batch) == 2 and batch[0] == "__rla_resident__":
-            out = self._step(self._resident_batch, batch_idx, resident=True)
+            if self.failed:  # rejected earlier this epoch: gather on the device, eager step
+                return self._eager(self._resident_batch(), batch_idx, count_step=True)
+            try:
+                out = self._step(self._resident_batch, batch_idx, resident=True)
+            except _Unsupported as e:
+                # the batch was gathered (the cursor advanced): the eager path re-runs it
+                self.reason = str(e)
+                self._give_up()
+                return self._eager(self._last_batch, batch_idx, count_step=True)
             t.global_step += 1
             t._update_lr_schedulers("step")
             return out
@@ -424,6 +460,19 @@ class GraphedTrainStep:
             return t._autograd_step(batch, batch_idx)
         t.global_step += 1
         t._update_lr_schedulers("step")
+        return out
+
+    def _eager(self, batch, batch_idx: int, count_step: bool):
+        """The Trainer's eager autograd step of an already gathered batch.
+        ``count_step``: advance global_step / step schedulers (per-batch dispatch);
+        a chunk's steps are counted by the Trainer after the chunk."""
+        t = self.trainer
+        if count_step:
+            return t._autograd_step(batch, batch_idx)
+        model = t.get_model()
+        out = None
+        for opt_idx, opt in enumerate(t.optimizers or [None]):
+            out = t._optimizer_step_for(model, batch, batch_idx, opt_idx, opt, False)
         return out
 
     # ------------------------------------------------------- resident data
@@ -477,7 +526,15 @@ class GraphedTrainStep:
         outs = []
         first = self.steps_done
         for _ in range(n_steps):
-            outs.append(self._step(self._resident_batch, 0, resident=True))
+            if self.failed:
+                outs.append(self._eager(self._resident_batch(), 0, count_step=False))
+                continue
+            try:
+                outs.append(self._step(self._resident_batch, 0, resident=True))
+            except _Unsupported as e:
+                self.reason = str(e)
+                self._give_up()
+                outs.append(self._eager(self._last_batch, 0, count_step=False))
         k = min(n_steps, self.ring_rows)
         done = self.steps_done - first
         if self._ring is not None and done == n_steps:
@@ -518,7 +575,53 @@ class GraphedTrainStep:
         pass  # read from param_groups before every replay (sync_lr)
 
     def eval_compatible(self, model) -> bool:
-        return False
+        """Validation gathers its batches on the device when the val set is resident
+        (eval_epoch decides per loader; other loaders iterate as usual)."""
+        return self.cuda
+
+    def eval_epoch(self, dl, limit: int):
+        """A validation pass over a RESIDENT dataset (``SyntheticImageNet``,
+        ``TensorDataset``): the loader's sampler order rebuilt as a tensor (the same
+        global-RNG draw as iterating it), every batch gathered on the device and run
+        through ``validation_step`` / ``validation_step_end`` exactly as the loader
+        path does -- no per-item CPU work, no pageable H2D copy.  Returns the step
+        outputs, or None (then the Trainer iterates the loader)."""
+        from torch.utils.data._utils.collate import default_collate
+
+        if dl is None or dl.batch_size is None or dl.collate_fn is not default_collate:
+            return None
+        key = id(dl.dataset)
+        got = self._eval_resident.get(key)
+        if got is None:
+            got = resident_tensors(dl.dataset, self.dev)
+            if got is None:
+                return None
+            self._eval_resident[key] = got
+        cols, idx_map = got
+        order = loader_order(dl)
+        if idx_map is not None:
+            order = idx_map[order]
+        B = int(dl.batch_size)
+        n = order.numel()
+        nb = n // B if dl.drop_last else -(-n // B)
+        nb = min(nb, int(limit))
+        if nb <= 0:
+            return []
+        assert int(order.max()) < cols[0].size(0) and int(order.min()) >= 0  # the gather trusts indices
+        order = order[: nb * B].to(self.dev, non_blocking=False)
+        t, model = self.trainer, self.model
+        outs = []
+        for i in range(nb):
+            batch = [gather_rows(c, order[i * B:(i + 1) * B]) for c in cols]
+            t._current_fx = "validation_step"
+            with self.acc.autocast():
+                out = model.validation_step(batch, i)
+            t._current_fx = "validation_step_end"
+            out = model.validation_step_end(out)
+            t._current_fx = None
+            if out is not None:
+                outs.append(out)
+        return outs
 
     def check(self, blocking: bool = True) -> None:
         pass

@@ -777,9 +777,10 @@ class Trainer:
                 outputs = []
                 res = self._fused.eval_epoch(dl, limit) if fused_eval else None
                 if res is not None:
-                    # the whole pass in one launch over the resident data: one output
-                    # standing for `limit` equal-size batches (same epoch-end mean)
-                    all_outputs.append([res])
+                    # the pass over the resident data: either one output standing for
+                    # `limit` equal-size batches (the fused MNIST pass, same epoch-end
+                    # mean) or the per-batch outputs (device-gathered batches)
+                    all_outputs.append(res if isinstance(res, list) else [res])
                     continue
                 for batch_idx, batch in enumerate(dl):
                     if batch_idx >= limit:

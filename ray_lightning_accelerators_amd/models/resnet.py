@@ -211,7 +211,8 @@ class SyntheticImageNet(Dataset):
         y = labels.to(device, non_blocking=True)
         if device.type == "cuda":
             torch.cuda.current_stream(device).synchronize()  # the pinned source is freed below
-        _RESIDENT.clear()  # one resident set per process
+        while len(_RESIDENT) >= 2:  # a train and a validation set per process (recycled workers)
+            _RESIDENT.pop(next(iter(_RESIDENT)))
         _RESIDENT[key] = [x, y]
         return _RESIDENT[key]
 
@@ -231,7 +232,7 @@ class LightningResNet50(LightningModule):
     def __init__(self, config: Optional[dict] = None):
         super().__init__()
         cfg = dict(lr=0.1, momentum=0.9, weight_decay=5e-5, batch_size=64, num_classes=1000,
-                   image_size=224, n_train=512, fused_bn=True, num_workers=0)
+                   image_size=224, n_train=512, n_val=0, fused_bn=True, num_workers=0)
         cfg.update(config or {})
         self.cfg = cfg
         self.model = resnet50(cfg["num_classes"], fused_bn=cfg["fused_bn"]).to(memory_format=torch.channels_last)
@@ -248,9 +249,33 @@ class LightningResNet50(LightningModule):
         self.log("train_loss", loss)
         return loss
 
+    def validation_step(self, batch, batch_idx):
+        """Loss and top-1 of one held-out batch (BatchNorm in eval mode: running stats)."""
+        x, y = batch
+        x = x.contiguous(memory_format=torch.channels_last)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=x.is_cuda):
+            logits = self(x)
+        loss = F.cross_entropy(logits.float(), y)
+        return {"val_loss": loss, "val_acc": (logits.argmax(1) == y).float().mean()}
+
+    def validation_epoch_end(self, outputs):
+        if outputs:
+            self.log("val_loss", torch.stack([o["val_loss"] for o in outputs]).mean())
+            self.log("val_acc", torch.stack([o["val_acc"] for o in outputs]).mean())
+
     def configure_optimizers(self):
         return torch.optim.SGD(self.parameters(), lr=self.cfg["lr"], momentum=self.cfg["momentum"],
                                weight_decay=self.cfg["weight_decay"])
+
+    def val_dataloader(self):
+        """``n_val`` held-out synthetic images (seed 1: disjoint from the training
+        draws); none when ``n_val`` is 0."""
+        if not self.cfg["n_val"]:
+            return None
+        from torch.utils.data import DataLoader
+
+        ds = SyntheticImageNet(self.cfg["n_val"], self.cfg["image_size"], self.cfg["num_classes"], seed=1)
+        return DataLoader(ds, batch_size=self.cfg["batch_size"], num_workers=self.cfg["num_workers"])
 
     def train_dataloader(self):
         from torch.utils.data import DataLoader

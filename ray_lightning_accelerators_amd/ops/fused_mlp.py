@@ -273,25 +273,6 @@ def mlp3_launch(
     )
 
 
-RESIDENT_SHAPES = {(32, 64, 32)}  # (L1, L2, batch) of the resident kernel (csrc/mlp_resident.hip)
-
-
-def resident_supported(L1: int, L2: int, B: int) -> bool:
-    return (int(L1), int(L2), int(B)) in RESIDENT_SHAPES
-
-
-def mlp_resident(*, x_u8, labels, order, counters, n_batches: int, B: int, L1: int, L2: int, K: int, params,
-                 exp_avg, exp_avg_sq, stats=None, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0, lr_tensor=None, adamw: bool = False) -> None:
-    """K training steps of the MNIST MLP in ONE resident workgroup (csrc/mlp_resident.hip):
-    weights, Adam state and operand images stay on one CU for the whole window."""
-    from . import require
-
-    require().mlp_resident(x_u8, labels, order, counters, int(n_batches), int(B), int(L1), int(L2), int(K), params,
-                           exp_avg, exp_avg_sq, stats, float(lr), float(betas[0]), float(betas[1]), float(eps),
-                           float(weight_decay), lr_tensor, bool(adamw))
-
-
 def mlp_adam_(params, grads, exp_avg, exp_avg_sq, shadow, *, L1: int, L2: int, lr: float, step: torch.Tensor,
               betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, grad_scale: float = 1.0,
               adamw: bool = False, lr_tensor: Optional[torch.Tensor] = None) -> None:

@@ -161,6 +161,10 @@ class GradSynchronizer:
                     # 0..65535 -- no value is rounded
                     if dtype in (torch.float32, torch.bfloat16, torch.float16):
                         f = flat if dtype == torch.float32 else flat.to(torch.float32)
+                    elif flat.element_size() == 1:
+                        # bool / uint8 / int8: each byte as an exact fp32 integer (an odd
+                        # byte count has no 16-bit view -- ADVICE r5)
+                        f = flat.view(torch.uint8).to(torch.float32)
                     else:
                         f = (flat.view(torch.int16).to(torch.int32) & 0xFFFF).to(torch.float32)
                     if dist.get_rank() != 0:
@@ -169,6 +173,8 @@ class GradSynchronizer:
                     if dtype in (torch.float32, torch.bfloat16, torch.float16):
                         if f is not flat:
                             flat.copy_(f)
+                    elif flat.element_size() == 1:
+                        flat.view(torch.uint8).copy_(f.to(torch.uint8))
                     else:
                         flat.view(torch.int16).copy_(f.to(torch.int32).to(torch.int16))
                 else:

@@ -77,7 +77,6 @@ class FusedMLPEngine:
         dp_proto: Optional[str] = None,
         dp_rearm: Optional[Callable[[], None]] = None,
         dp_loop: bool = False,
-        resident: Optional[bool] = None,
     ):
         """``buffers``: optional external fp32 tensors ``params`` / ``grads`` /
         ``exp_avg`` / ``exp_avg_sq`` (e.g. views of a Trainer's parameter arena,
@@ -159,14 +158,6 @@ class FusedMLPEngine:
         self._graph = None
         self._graph_steps = 0
         self._tail_graphs: Dict[int, "torch.cuda.CUDAGraph"] = {}  # remainder sizes (powers of two)
-        # run(): a window of one-launch steps as back-to-back launches from ONE C++
-        # call instead of hipGraph replays (see _run_loop; RLA_MLP_LAUNCH_LOOP=1)
-        self.launch_loop = os.environ.get("RLA_MLP_LAUNCH_LOOP", "0") == "1"
-        # run(): at world 1, a window of steps as ONE launch of the resident kernel
-        # (csrc/mlp_resident.hip: the model lives on one CU for the whole window, no
-        # hand-off between steps); RLA_MLP_RESIDENT=0 / resident=False keeps the
-        # pipelined one-launch steps (hipGraph replays)
-        self.resident = (os.environ.get("RLA_MLP_RESIDENT", "0") == "1") if resident is None else bool(resident)
         self._shadow_stale = False
         self._primed = False
         self._host_epochs = False
@@ -394,9 +385,8 @@ class FusedMLPEngine:
             fused_mlp.mlp3_launch(fused_mlp.MLP3_PRIME, **self._kw3())
         self._primed = True
 
-    def _device_step(self, repeat: int = 1) -> None:
-        """One step (``repeat``: that many back-to-back launches; one-launch kinds only)."""
-        assert repeat == 1 or self._loop_ok()
+    def _device_step(self) -> None:
+        """One optimizer step on the device (or the fp32 reference step on the CPU)."""
         if self.x_u8 is None:
             raise RuntimeError("set_data() first")
         if not self._primed:
@@ -407,12 +397,12 @@ class FusedMLPEngine:
             kw = self._kw3()
             if self.world_size == 1 and not self.dp_loop:
                 kind = fused_mlp.MLP3_STEP1 if self.one_launch else fused_mlp.MLP3_STEP
-                fused_mlp.mlp3_launch(kind, stats=self.stats, repeat=repeat, **kw)
+                fused_mlp.mlp3_launch(kind, stats=self.stats, **kw)
             elif self.dp_ctx is not None:
                 kind = fused_mlp.MLP3_STEP1_DP if self.one_launch_dp else fused_mlp.MLP3_STEP_DP
                 fused_mlp.mlp3_launch(kind, stats=self.stats, grad_scale=1.0 / self.dp_ctx[0],
                                       dp_ctx=self.dp_ctx, dp_proto=fused_mlp.DP_PROTOS.get(self.dp_proto, -1),
-                                      dp_loop=self.dp_loop, repeat=repeat, **kw)
+                                      dp_loop=self.dp_loop, **kw)
                 self._stepped_owner = self._stepped_owner or (self.one_launch_dp and self.dp_proto == "owner")
             else:
                 fused_mlp.mlp3_launch(fused_mlp.MLP3_HEAD, stats=self.stats, **kw)
@@ -529,44 +519,7 @@ class FusedMLPEngine:
         self._device_step()
         self._advance_host(1)
 
-    def _loop_ok(self) -> bool:
-        """A step is ONE launch (world 1 one-launch, or the one-launch DP step)."""
-        if not self.native:
-            return False
-        if self.world_size == 1 and not self.dp_loop:
-            return self.one_launch
-        return self.dp_ctx is not None and self.one_launch_dp
-
-    def resident_ok(self) -> bool:
-        """run() takes the resident kernel: world 1, the (L1, L2, B) it is built for."""
-        return (self.resident and self.native and self.world_size == 1 and not self.dp_loop
-                and self.x_u8 is not None and fused_mlp.resident_supported(self.L1, self.L2, self.B))
-
-    def _run_resident(self, n_steps: int) -> None:
-        """The window as resident launches, one per stretch up to the epoch end (where
-        the host refills the next epoch's order buffer, as the graph path does)."""
-        done = 0
-        while done < n_steps:
-            k = min(n_steps - done, self.n_batches - self.step_in_epoch)
-            fused_mlp.mlp_resident(x_u8=self.x_u8, labels=self.labels, order=self.order, counters=self.counters,
-                                   n_batches=self.n_batches, B=self.B, L1=self.L1, L2=self.L2, K=k,
-                                   params=self.params, exp_avg=self.exp_avg, exp_avg_sq=self.exp_avg_sq,
-                                   stats=self.stats, lr=self.lr, betas=self.betas, eps=self.eps,
-                                   weight_decay=self.wd, lr_tensor=self.lr_tensor)
-            self._advance_host(k)
-            done += k
-        # the pipelined kernels' state (bf16 shadows, pending H1pre) is rebuilt before
-        # they run again
-        self._shadow_stale = True
-        self._primed = False
-
     def run(self, n_steps: int) -> None:
-        if n_steps > 0 and self.resident_ok():
-            self._run_resident(n_steps)
-            return
-        if self.launch_loop and self._loop_ok():
-            self._run_loop(n_steps)
-            return
         done = 0
         while done < n_steps:
             g, k = self._pick_graph(n_steps - done)
@@ -574,23 +527,6 @@ class FusedMLPEngine:
                 g.replay()
             else:
                 self._device_step()
-            self._advance_host(k)
-            done += k
-
-    def _run_loop(self, n_steps: int) -> None:
-        """``launch_loop``: the window's one-launch steps issued by ONE C++ call that
-        launches the kernel back to back (no hipGraph).  A graph replay costs ~10-16 us
-        of fixed host + dispatch time per replay (MI355X_MICROARCH.md
-        'graph-replay-floor'); back-to-back launches from an idle stream start in
-        ~3-5 us and then stay ahead of the ~8 us GPU step (host launch ~3.5 us each),
-        so a short timed window pays less fixed cost.  Chunks stop at epoch ends, where
-        the host refills the next epoch's order buffer (as the graph path does)."""
-        if not self._primed:
-            self.prime()
-        done = 0
-        while done < n_steps:
-            k = min(n_steps - done, self.n_batches - self.step_in_epoch)
-            self._device_step(repeat=k)
             self._advance_host(k)
             done += k
 

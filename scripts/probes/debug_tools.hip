@@ -1,3 +1,6 @@
+// ARCHIVED DEBUG KERNEL (not built; removed from the _C extension in round 6).
+// LDS poison fill used for the round-5 one-launch investigation
+// (profiles/r5_mnist/poison_full_128.log); build it standalone if needed again.
 // Debug tooling: fill every CU's LDS with a bit pattern (e.g. bf16 +Inf pairs), so a
 // kernel that reads LDS it never wrote shows it deterministically instead of only
 // after some earlier kernel happened to leave such bytes there (tests / probes only).

@@ -1,3 +1,7 @@
+// ARCHIVED NEGATIVE RESULT (not built; removed from the _C extension in round 6).
+// The resident one-workgroup training loop measured 14.1 vs 8.4 us/step for the
+// pipelined one-launch step (profiles/r4_resident/); kept for reference only.  It
+// needs the ResidentArgs declaration that kernels.h carried until round 5.
 // Resident MNIST training loop: K optimizer steps of the 784-32-64-10 MLP (batch
 // 32, bf16 MFMA compute, fp32 master weights, Adam) in ONE workgroup of ONE launch.
 //

@@ -44,3 +44,14 @@ def predict_test(trainer: Trainer, model: LightningModule, dm: LightningDataModu
         acc.update(y_hat.cpu(), y)
     average_acc = acc.compute()
     assert average_acc >= 0.5, f"expected > 0.5 test accuracy, got {average_acc}"
+
+
+def update_worst(worst: dict, errs: dict) -> None:
+    """Fold one step's per-tensor errors into running maxima WITHOUT losing a NaN:
+    Python's max(0.0, nan) is 0.0, so a non-finite error is recorded as +inf (which
+    no bound accepts) instead of being silently dropped."""
+    import math
+
+    for k, e in errs.items():
+        e = float(e)
+        worst[k] = math.inf if not math.isfinite(e) else max(worst[k], e)

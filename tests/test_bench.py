@@ -66,6 +66,17 @@ def test_bench_single_rank_cpu():
     assert out["n_gpus"] == 1 and out["vs_baseline"] is None and out["dtype"] == "fp32"
 
 
+def test_bench_refuses_non_finite_training():
+    """a run whose training state goes non-finite (an injected NaN
+    learning rate) is not a result -- bench.py exits non-zero and prints no JSON line."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--steps", "3",
+                        "--warmup", "1", "--n-data", "512", "--lr", "nan"], cwd="/tmp", capture_output=True,
+                       text=True, timeout=300)
+    assert p.returncode != 0
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")], p.stdout
+    assert "non-finite" in p.stderr, p.stderr[-2000:]
+
+
 def test_bench_via_trainer_cpu():
     out, _ = _bench("--device", "cpu", "--gpus", "2", "--via", "trainer", "--trainer-epochs", "2", timeout=600)
     assert out["n_gpus"] == 2 and out["config"]["accelerator"] == "RayAccelerator"

@@ -7,6 +7,7 @@ GPUs do over xGMI (same protocol, same kernels; only the physical link
 differs).  RCCL itself refuses two ranks on one device, so its path is tested
 at world size 1 plus the routing fallback.
 """
+import math
 import os
 import socket
 
@@ -445,7 +446,9 @@ def _gpu_worker(rank, world, port, q, mode):
                           for r in range(world)) / world
                 for k, a, b in zip(names, fused_mlp.mlp_unpack(g.cpu(), L1, L2).values(),
                                    fused_mlp.mlp_unpack(ref, L1, L2).values()):
-                    worst[k] = max(worst[k], (a - b).norm().item() / max(b.norm().item(), 1e-12))
+                    e_k = (a - b).norm().item() / max(b.norm().item(), 1e-12)
+                    # NaN-proof: max(0.0, nan) is 0.0, so a non-finite error is recorded as inf
+                    worst[k] = max(worst[k], e_k) if math.isfinite(e_k) else math.inf
             torch.cuda.synchronize()
             comm.check()
             e.check()
@@ -464,12 +467,17 @@ def _gpu_worker(rank, world, port, q, mode):
             m.register_buffer("f64", torch.tensor([1.0 + 1e-12 * (rank + 1), -3.5e-300], dtype=torch.float64,
                                                   device=dev))
             m.register_buffer("f32", torch.full((5,), 0.1 * (rank + 1), device=dev))
+            # 1-byte dtypes with an odd element count (no 16-bit view)
+            m.register_buffer("u8", torch.tensor([255, rank, 7], dtype=torch.uint8, device=dev))
+            m.register_buffer("flag", torch.tensor([rank == 0, rank != 0, True], device=dev))
             sync = GradSynchronizer(m, ParamArena(m), bucket_cap_mb=1.0)
             sync._broadcast_buffers()
             torch.cuda.synchronize()
             res["big"] = m.big.tolist() == [2 ** 40 + 12345, -7, 2 ** 24 + 1]
             res["f64"] = m.f64.tolist() == [1.0 + 1e-12, -3.5e-300]
             res["f32"] = bool(torch.all(m.f32 == torch.tensor(0.1, device=dev)))
+            res["u8"] = m.u8.tolist() == [255, 0, 7]
+            res["bool"] = m.flag.tolist() == [True, False, True]
             comm.check()
         elif mode == "timeout":
             x = torch.ones(1024, device=dev)
@@ -641,6 +649,7 @@ def test_buffer_broadcast_without_rccl_is_exact():
     out = _run_gpu("bcast_exact")
     for r, res in out.items():
         assert isinstance(res, dict) and res["big"] and res["f64"] and res["f32"], (r, res)
+        assert res["u8"] and res["bool"], (r, res)
 
 
 @gpu

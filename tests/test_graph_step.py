@@ -130,6 +130,33 @@ def test_host_read_falls_back(tmpdir):
     assert r_h.losses == r_e.losses  # the fallback trains exactly like eager
 
 
+class LogsFloat(Tiny):
+    """self.log of a Python float: rejected by the step body (after the forward) --
+    on the RESIDENT path too, where the batch is a device-gathered sentinel."""
+
+    def training_step(self, batch, batch_idx):
+        loss = super().training_step(batch, batch_idx)
+        self.log("lr_host", 0.05)
+        return loss
+
+
+def test_resident_rejection_falls_back_like_eager(tmpdir):
+    """a step rejected on the resident-data path must not crash the fit:
+    the gathered batch is re-run by the eager path, every later step too, and the
+    forward of the rejected attempt leaves no trace (BN running statistics and
+    num_batches_tracked updated once) -- bit-identical to the plain eager Trainer."""
+    t_f, r_f = _fit(LogsFloat(), tmpdir, "f", epochs=2)
+    f = t_f._fused
+    assert f.failed and "lr_host" in f.reason
+    m_e = LogsFloat()
+    m_e.hip_graph_step = False
+    t_e, r_e = _fit(m_e, tmpdir, "e", epochs=2)
+    assert r_f.losses == r_e.losses and len(r_f.losses) == 24
+    assert t_f.global_step == t_e.global_step == 24
+    for (k, a), b in zip(t_f.model.state_dict().items(), t_e.model.state_dict().values()):
+        assert torch.equal(a, b), k
+
+
 def test_static_rejections(tmpdir):
     class Hooked(Tiny):
         def on_after_backward(self):

@@ -13,15 +13,9 @@ import torch.nn.functional as F
 
 from ray_lightning_accelerators_amd.ops import fused_mlp
 from ray_lightning_accelerators_amd.parallel.mlp_engine import FusedMLPEngine, shard_indices
+from helpers import update_worst
 
 gpu = pytest.mark.gpu
-
-
-@pytest.fixture(autouse=True)
-def _pipelined_kernels(monkeypatch):
-    """These tests pin the pipelined / one-launch step kernels (mlp_step3.hip): run()
-    would otherwise take the resident kernel at world 1 (tests/test_mlp_resident.py)."""
-    monkeypatch.setenv("RLA_MLP_RESIDENT", "0")
 
 
 def _rel(a, b):
@@ -436,6 +430,69 @@ def _per_tensor_rel(g, ref, L1, L2):
     return {k: _rel(x, y) for k, x, y in zip(_NAMES, a.values(), b.values())}
 
 
+_STATE = ("params", "exp_avg", "exp_avg_sq", "shadow", "h1pre", "xring", "yring", "counters", "hand", "order")
+
+
+def _snapshot(eng):
+    """Clone of every device buffer a one-launch step reads (pre-step state)."""
+    return {k: getattr(eng, k).clone() for k in _STATE}
+
+
+def _h1pre_dense(h1pre_slot, L1, Bp=32):
+    """[Bp, L1] fp64 view of one H1pre ring slot (32.32 fixed point, MFMA-fragment order)."""
+    b = torch.arange(Bp).view(-1, 1)
+    m = torch.arange(L1).view(1, -1)
+    pos = (((b // 16) * (L1 // 16) + m // 16) * 4 + b % 4) * 64 + ((b % 16) // 4) * 16 + m % 16
+    return h1pre_slot.cpu()[pos].double() / 2.0 ** 32
+
+
+def _pre_step_check(snap, x, y, idx, L1, L2, B, cur, epoch):
+    """Which input of the coming step is inconsistent?  Every word the step reads is
+    checked against what the engine's invariants say it must hold."""
+    Bp = 32
+    out = {}
+    c = snap["counters"].cpu()
+    slot = int(c[3])
+    out["counters"] = c[:11].tolist()
+    out["counters_ok"] = bool(torch.equal(c[0:5], c[5:10]) and int(c[1]) == cur and int(c[4]) == epoch % 2)
+    yr = snap["yring"].view(2, Bp).cpu()[slot]
+    out["yring_ok"] = bool(torch.equal(yr[:B].long(), y[idx]) and bool((yr[B:] == -1).all()))
+    xr = snap["xring"].view(2, 49, Bp, 16).cpu()[slot].float().permute(1, 0, 2).reshape(Bp, 784)
+    xe = (x[idx].float() * (1.0 / 255.0)).to(torch.bfloat16).float()
+    out["xring_ok"] = bool(torch.equal(xr[:B], xe) and bool((xr[B:] == 0).all()))
+    h1 = snap["h1pre"].view(2, Bp * L1)
+    cur_h = _h1pre_dense(h1[slot], L1)
+    w1 = snap["shadow"][: L1 * 784].view(L1, 784).cpu().double()
+    ref_h = xe.double() @ w1.T
+    out["h1pre_rel_err"] = float((cur_h[:B] - ref_h).norm() / max(ref_h.norm(), 1e-30))
+    out["h1pre_pad_rows_zero"] = bool((cur_h[B:] == 0).all())
+    out["h1pre_next_slot_zero"] = bool((h1[slot ^ 1] == 0).all())
+    np_ = fused_mlp.mlp_param_count(L1, L2)
+    out["shadow_ok"] = bool(torch.equal(snap["shadow"][:np_].cpu(), snap["params"].cpu().to(torch.bfloat16)))
+    out["params_finite"] = bool(torch.isfinite(snap["params"]).all())
+    out["adam_state_finite"] = bool(torch.isfinite(snap["exp_avg"]).all() and torch.isfinite(snap["exp_avg_sq"]).all())
+    return out
+
+
+def _session_facts(eng):
+    """Process-level facts at a failing step: buffer addresses, allocator state,
+    threads and child processes alive (a long GPU session differs from a short one
+    in exactly these)."""
+    import threading
+
+    facts = {"ptrs": {k: hex(getattr(eng, k).data_ptr()) for k in _STATE},
+             "mem_alloc_mb": torch.cuda.memory_allocated() >> 20, "mem_reserved_mb": torch.cuda.memory_reserved() >> 20,
+             "threads": sorted(t.name for t in threading.enumerate()),
+             "stream": hex(torch.cuda.current_stream().cuda_stream)}
+    try:
+        import psutil
+
+        facts["children"] = [(c.pid, " ".join(c.cmdline())[:120]) for c in psutil.Process().children(recursive=True)]
+    except Exception as e:  # noqa: BLE001 - diagnostics only
+        facts["children"] = repr(e)
+    return facts
+
+
 def _fidelity_log(name, rows):
     import json
     import os
@@ -446,64 +503,104 @@ def _fidelity_log(name, rows):
             f.write(json.dumps({"test": name, **rows}) + "\n")
 
 
+def _diff_summary(a, b):
+    """Elements that differ between two engines' buffers (count, first indices)."""
+    out = {}
+    for k in _STATE:
+        ta, tb = getattr(a, k), getattr(b, k)
+        ne = (ta != tb) if ta.dtype != torch.bfloat16 else (ta.view(torch.int16) != tb.view(torch.int16))
+        n = int(ne.sum())
+        if n:
+            out[k] = {"n": n, "first": ne.nonzero().flatten()[:6].tolist()}
+    return out
+
+
+def _fidelity_run(eng, x, y, L1, L2, B, n_steps, world=1, autocast=False, make=None):
+    """Step ``eng`` n_steps times; every step, the gradient it applied (recovered from
+    Adam's first moment: m_t = b1 m_{t-1} + (1 - b1) g_t) against fp32 autograd on the
+    same batch at the same parameters, per tensor, normwise.  Non-finite errors count
+    as +inf (helpers.update_worst).  Between steps the test reads only what the error
+    needs (params, exp_avg), as a production run would.
+
+    The first step that breaks a bound is documented post mortem: ``make()`` builds a
+    FRESH engine with the same init and data, stepped to the same point (one-launch,
+    and two-launch), and every buffer is compared with the failing engine's --
+    equal means the result is a deterministic function of the inputs (then the
+    inputs, or the oracle, are what to look at); different names the buffers and
+    first elements the failing run got wrong.  The failing engine's post-step state is
+    checked against the engine's invariants for the NEXT step (_pre_step_check)."""
+    b1 = eng.betas[0]
+    worst = {k: 0.0 for k in _NAMES}
+    worst_ac = {k: 0.0 for k in _NAMES}
+    first_bad = None
+    for step in range(n_steps):
+        epoch, cur = eng.epoch, eng.step_in_epoch
+        idx = shard_indices(x.size(0), world, 0, epoch, eng.seed, True)[cur * B:(cur + 1) * B]
+        p0, m0 = eng.params.clone(), eng.exp_avg.clone()
+        eng.step()
+        g = (eng.exp_avg - b1 * m0) / (1 - b1)
+        ref = _fp32_ref_grads(p0, x[idx], y[idx], L1, L2)
+        errs = _per_tensor_rel(g, ref, L1, L2)
+        update_worst(worst, errs)
+        if step < 3:
+            print(f"STEP {step} errs " + " ".join(f"{k}={v:.4g}" for k, v in errs.items()), flush=True)
+        if autocast:
+            update_worst(worst_ac, _per_tensor_rel(_autocast_grads(p0, x[idx], y[idx], L1, L2, _dev()), ref, L1, L2))
+        if first_bad is None and not all(errs[k] < GRAD_BOUND[k] for k in _NAMES):
+            torch.cuda.synchronize()
+            first_bad = {"step": step, "epoch": epoch, "cur": cur, "errs": errs,
+                         "g_finite": bool(torch.isfinite(g).all()), "p0_finite": bool(torch.isfinite(p0).all()),
+                         "g_nonfinite_idx": (~torch.isfinite(g)).nonzero().flatten()[:8].tolist(),
+                         "hand": eng.hand[:20].tolist(), "counters_after": eng.counters[:11].tolist(),
+                         "session": _session_facts(eng)}
+            ne, nc = eng.epoch, eng.step_in_epoch
+            nidx = shard_indices(x.size(0), world, 0, ne, eng.seed, True)[nc * B:(nc + 1) * B]
+            first_bad["post_state_for_next_step"] = _pre_step_check(_snapshot(eng), x, y, nidx, L1, L2, B, nc, ne)
+            if make is not None:
+                for label, one in (("fresh_one_launch", True), ("fresh_two_launch", False)):
+                    f = make()
+                    if not one and f.dp_ctx is not None:
+                        continue  # the loopback exchange exists only in the one-launch step
+                    f.one_launch = f.one_launch and one
+                    fb1 = f.betas[0]
+                    for _ in range(step):
+                        f.step()
+                    fp0, fm0 = f.params.clone(), f.exp_avg.clone()
+                    f.step()
+                    torch.cuda.synchronize()
+                    first_bad[label] = {
+                        "errs": _per_tensor_rel((f.exp_avg - fb1 * fm0) / (1 - fb1),
+                                                _fp32_ref_grads(fp0, x[idx], y[idx], L1, L2), L1, L2),
+                        "pre_step_params_equal": bool(torch.equal(fp0, p0)),
+                        "diff_vs_failing": _diff_summary(f, eng)}
+    return worst, worst_ac, first_bad
+
+
 @gpu
-@pytest.mark.parametrize("L1,L2", [(32, 64), pytest.param(128, 256, marks=pytest.mark.xfail(
-    strict=False, reason="known intermittent wrong first step in long GPU sessions only "
-                         "(profiles/r5_mnist/one_launch_128_256.md); off by default for L1 > 64"))])
+@pytest.mark.parametrize("L1,L2", [(32, 64), (128, 256)])
 def test_mlp3_one_launch_grads_vs_fp32_autograd(L1, L2, monkeypatch):
     """The production kernel (one-launch Step1) against fp32 PyTorch autograd, every
-    step of 2+ epochs on the (non-trivial) synthetic task: the gradient the kernel
-    applied is recovered exactly from its Adam first moment (m_t = b1 m_{t-1} +
-    (1 - b1) g_t) and compared per tensor, normwise, with the fp32 gradient of the
-    same batch at the same parameters."""
+    step of 2+ epochs on the (non-trivial) synthetic task, held to the absolute bounds
+    and to 1.5x stock bf16 autocast's own error on the same batches (+0.01)."""
+    import json
+
     from ray_lightning_accelerators_amd.models.data import synthetic_mnist
 
     B, nb = 32, 24
     x, y = synthetic_mnist(B * nb + 7, seed=11)
     monkeypatch.setenv("RLA_MLP_ONE_LAUNCH", "1")  # the one-launch kernel at every width
-    eng = FusedMLPEngine(L1, L2, B, lr=1e-3, device=_dev(), seed=1)
+    def make():
+        e = FusedMLPEngine(L1, L2, B, lr=1e-3, device=_dev(), seed=1)
+        e.set_data(x, y)
+        return e
+
+    eng = make()
     assert eng.one_launch
-    eng.set_data(x, y)
-    b1 = eng.betas[0]
-    worst = {k: 0.0 for k in _NAMES}
-    worst_ac = {k: 0.0 for k in _NAMES}
-    first_bad = None  # diagnostics: the first step whose error breaks a bound
-    for step in range(2 * nb + 5):  # two epoch switches
-        epoch, cur = eng.epoch, eng.step_in_epoch
-        idx = shard_indices(x.size(0), 1, 0, epoch, eng.seed, True)[cur * B:(cur + 1) * B]
-        p0, m0 = eng.params.clone(), eng.exp_avg.clone()
-        eng.step()
-        g = (eng.exp_avg - b1 * m0) / (1 - b1)
-        ref = _fp32_ref_grads(p0, x[idx], y[idx], L1, L2)
-        ac = _autocast_grads(p0, x[idx], y[idx], L1, L2, _dev())
-        errs = _per_tensor_rel(g, ref, L1, L2)
-        for k, e in errs.items():
-            worst[k] = max(worst[k], e)
-        for k, e in _per_tensor_rel(ac, ref, L1, L2).items():
-            worst_ac[k] = max(worst_ac[k], e)
-        if first_bad is None and any(errs[k] >= GRAD_BOUND[k] for k in _NAMES):
-            def fin(t):
-                t = t.float()
-                return {"finite": bool(torch.isfinite(t).all()), "nonfinite": int((~torch.isfinite(t)).sum()),
-                        "absmax": float(t[torch.isfinite(t)].abs().max()) if bool(torch.isfinite(t).any()) else None}
-            nf = (~torch.isfinite(g)).nonzero().flatten()[:8].tolist()
-            first_bad = {"state": {"counters": eng.counters.tolist(), "hand": eng.hand[:20].tolist(),
-                                   "stats": eng.stats[:4].tolist(), "params": fin(eng.params),
-                                   "exp_avg": fin(eng.exp_avg), "exp_avg_sq": fin(eng.exp_avg_sq),
-                                   "shadow": fin(eng.shadow), "xring": fin(eng.xring),
-                                   "h1pre_absmax": int(eng.h1pre.abs().max()), "yring": eng.yring.tolist()[:8],
-                                   "g_nonfinite_idx": nf}}
-            first_bad.update({"step": step, "epoch": epoch, "cur": cur, "errs": errs,
-                         "g_finite": bool(torch.isfinite(g).all()), "p0_finite": bool(torch.isfinite(p0).all()),
-                         "ref_norm": float(ref.norm()), "g_norm": float(g.double().norm()),
-                         "mem_alloc_mb": torch.cuda.memory_allocated() >> 20,
-                         "mem_reserved_mb": torch.cuda.memory_reserved() >> 20})
+    worst, worst_ac, first_bad = _fidelity_run(eng, x, y, L1, L2, B, 2 * nb + 5, autocast=True, make=make)
     eng.check()
     _fidelity_log(f"one_launch_grads_{L1}_{L2}", {"steps": 2 * nb + 5, "max_rel_err": worst,
                                                   "stock_bf16_autocast_max_rel_err": worst_ac})
     if first_bad is not None:
-        import json
-
         print("FIRST_BAD " + json.dumps(first_bad, default=str), flush=True)
     for k in _NAMES:
         assert worst[k] < GRAD_BOUND[k], (k, worst, first_bad)
@@ -517,29 +614,32 @@ def test_mlp3_dp_loopback_grads_vs_fp32_autograd(proto):
     fp32 autograd, every step over 2+ epochs: the exchanged-and-averaged gradient
     (4 identical contributions) is the rank's own fp32 gradient up to bf16 compute and
     the protocol's wire rounding."""
+    import json
+
     from ray_lightning_accelerators_amd.models.data import synthetic_mnist
 
     L1, L2, B, nb = 32, 64, 32, 20
     x, y = synthetic_mnist(B * nb + 3, seed=12)
-    c, ctx = _loopback_ctx(4)
-    eng = FusedMLPEngine(L1, L2, B, lr=1e-3, device=_dev(), seed=2, dp_context=ctx, dp_proto=proto, dp_loop=True)
+    comms = []
+
+    def make():
+        cc, cx = _loopback_ctx(4)
+        comms.append(cc)  # alive as long as its engine
+        e = FusedMLPEngine(L1, L2, B, lr=1e-3, device=_dev(), seed=2, dp_context=cx, dp_proto=proto, dp_loop=True)
+        e.set_data(x, y)
+        return e
+
+    eng = make()
+    c = comms[0]
     assert eng.one_launch_dp
-    eng.set_data(x, y)
-    b1 = eng.betas[0]
-    worst = {k: 0.0 for k in _NAMES}
-    for _ in range(2 * nb + 3):
-        epoch, cur = eng.epoch, eng.step_in_epoch
-        idx = shard_indices(x.size(0), 1, 0, epoch, eng.seed, True)[cur * B:(cur + 1) * B]
-        p0, m0 = eng.params.clone(), eng.exp_avg.clone()
-        eng.step()
-        g = (eng.exp_avg - b1 * m0) / (1 - b1)
-        ref = _fp32_ref_grads(p0, x[idx], y[idx], L1, L2)
-        for k, e in _per_tensor_rel(g, ref, L1, L2).items():
-            worst[k] = max(worst[k], e)
+    worst, _, first_bad = _fidelity_run(eng, x, y, L1, L2, B, 2 * nb + 3, make=make)
     assert c.error_state() == 0
+    eng.check()
     _fidelity_log(f"dp_loopback4_{proto}_grads", {"steps": 2 * nb + 3, "max_rel_err": worst})
+    if first_bad is not None:
+        print("FIRST_BAD " + json.dumps(first_bad, default=str), flush=True)
     for k in _NAMES:
-        assert worst[k] < GRAD_BOUND[k], (k, worst)
+        assert worst[k] < GRAD_BOUND[k], (k, worst, first_bad)
 
 
 @gpu

@@ -34,6 +34,47 @@ def test_resnet50_trainer_cpu(tmpdir):
     assert torch.isfinite(torch.as_tensor(float(trainer.callback_metrics["train_loss"])))
 
 
+def test_resnet50_trainer_validation_cpu(tmpdir):
+    """the config-5 module validates every epoch -- held-out loss
+    and top-1 in callback_metrics, finite."""
+    model = LightningResNet50({"image_size": 32, "num_classes": 10, "batch_size": 4, "n_train": 8, "n_val": 8,
+                               "lr": 0.01})
+    trainer = pl.Trainer(default_root_dir=str(tmpdir), max_epochs=2, checkpoint_callback=False,
+                         num_sanity_val_steps=0)
+    assert trainer.fit(model) == 1
+    assert trainer.num_val_batches == [2]
+    for k in ("val_loss", "val_acc"):
+        v = float(trainer.callback_metrics[k])
+        assert v == v and abs(v) != float("inf"), (k, v)
+    assert 0.0 <= float(trainer.callback_metrics["val_acc"]) <= 1.0
+
+
+@pytest.mark.gpu
+def test_resnet50_resident_validation_matches_loader(tmpdir):
+    """On the GPU the captured Trainer step gathers validation batches from the
+    resident set (no per-image CPU work); the metrics equal iterating the loader."""
+    from ray_lightning_accelerators_amd.lightning.graph_step import GraphedTrainStep
+
+    cfg = {"image_size": 32, "num_classes": 10, "batch_size": 8, "n_train": 32, "n_val": 20, "lr": 0.01}
+    model = LightningResNet50(cfg)
+    trainer = pl.Trainer(default_root_dir=str(tmpdir), gpus=1, max_epochs=1, checkpoint_callback=False,
+                         num_sanity_val_steps=0)
+    assert trainer.fit(model) == 1
+    assert isinstance(trainer._fused, GraphedTrainStep) and trainer._fused._eval_resident
+    got = (float(trainer.callback_metrics["val_loss"]), float(trainer.callback_metrics["val_acc"]))
+    # the same weights through the loader path (3 batches, the last one partial)
+    model.eval()
+    dl = model.val_dataloader()
+    losses, accs = [], []
+    with torch.no_grad():
+        for i, (x, y) in enumerate(dl):
+            out = model.validation_step((x.cuda(), y.cuda()), i)
+            losses.append(out["val_loss"])
+            accs.append(out["val_acc"])
+    want = (float(torch.stack(losses).mean()), float(torch.stack(accs).mean()))
+    assert abs(got[0] - want[0]) < 1e-3 * max(1.0, abs(want[0])) and abs(got[1] - want[1]) < 1e-6, (got, want)
+
+
 @pytest.mark.gpu
 def test_resnet50_gpu_step_bf16():
     """One fused-optimizer training step on the GPU (NHWC, bf16 autocast)."""
