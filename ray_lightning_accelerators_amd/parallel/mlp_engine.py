@@ -136,14 +136,12 @@ class FusedMLPEngine:
         self.yring = bufs["yring"]
         self.head_part = bufs["head_part"]
         self.hand = bufs["hand"]
-        # world size 1, B <= 32: the whole step as ONE launch (RLA_MLP_ONE_LAUNCH=0: head + tail).
-        # Default for hidden widths <= 64 only (the headline 32-64 model and Tune's small
-        # corners): the 128-256 instance gave a wrong first step in 3 of 5 full GPU test
-        # sessions and never in isolation (profiles/r5_mnist/one_launch_128_256.md), so
-        # wider models take the two-launch step unless RLA_MLP_ONE_LAUNCH=1 forces it.
-        ol = os.environ.get("RLA_MLP_ONE_LAUNCH", "auto")
-        self.one_launch = (self.B <= fused_mlp.ONE_LAUNCH_MAX_B and ol != "0"
-                           and (ol == "1" or self.L1 <= 64))
+        # world size 1, B <= 32: the whole step as ONE launch at every width
+        # (RLA_MLP_ONE_LAUNCH=0: head + tail).  Round 5 gated widths > 64 off after
+        # intermittent fidelity failures in long GPU sessions; round 6's post-mortem
+        # showed the step bitwise equal to the two-launch step from a fresh engine in
+        # the failing session (docs/one_launch_investigation.md), so the gate is gone.
+        self.one_launch = self.B <= fused_mlp.ONE_LAUNCH_MAX_B and os.environ.get("RLA_MLP_ONE_LAUNCH") != "0"
         # world size > 1 with the xGMI context: the same one launch, each block
         # exchanging its values with the peers (protocol: self.dp_proto)
         self.dp_proto = "packed"

@@ -81,6 +81,7 @@ int main(int argc, char** argv) {
         CK(hipStreamSynchronize(side));
       }
     } else if (method == 1) {
+      CK(hipDeviceSynchronize());  // the previous trial's async copy has read `pinned`
       for (long i = 0; i < n; ++i) pinned[i] = B;
       CK(hipMemcpyAsync(buf, pinned, bytes, hipMemcpyHostToDevice, 0));
     } else if (method == 2) {
