@@ -174,15 +174,61 @@ constexpr int kHandAck = 0, kHandErr = 16, kHandWords = 32;
 // vmcnt(0) has resolved the sample index; the rest of the head pass reads LDS
 // only) by the one wave that uses them, so the round trip hides under the head pass.
 struct RepPre {
-  bool active;  // wave-uniform: wave 0 of a W1 tile block
+  bool active;  // wave-uniform: the PreWave of a W1 tile block
   int64_t si;
   int kt;
   uint4 xn;
   int64_t yn;
+  uint32_t raw;  // LDS byte address of the DMA landing area (kPreRawBytes), PreWave::hidden
 };
 
-template <int BC, int L1, int L2, bool MULTI, bool REP>
-__device__ __forceinline__ void head_body(const MLP3Args& a, char* smem, RepPre* pre = nullptr) {
+struct NoHook {
+  __device__ void operator()() const {}
+};
+
+// The next batch's pixels / labels, fetched during the head pass by LDS-DMA
+// (global_load_lds: no destination VGPR) from a tile wave that has no W1 column
+// (PreWave): the compiler does not see these loads, so none of the counted waits it
+// places for its own loads -- and no register it reuses next to a pending load's
+// destination -- can wait for their HBM round trip inside the head pass.  With
+// plain loads (rounds 2-4, wave 0) the softmax waited vmcnt(0) for the label load (a
+// register-pair hazard on its destination) and with it for every prologue load.
+// The consumer, the same wave, waits vmcnt(0) itself (it has no stores in flight).
+// M0 is saved and restored in the same statement (LDS-DMA recipe, as conv1x1.hip).
+__device__ __forceinline__ void dma_lds16(const void* gsrc, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds)
+               : "memory");
+}
+__device__ __forceinline__ void dma_lds4(const void* gsrc, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds)
+               : "memory");
+}
+constexpr int kPreRawBytes = 64 * 16 + 64 * 4;  // pixels (16 B per lane) + labels (4 B per lane)
+template <int L1>
+struct PreWave {
+  // a tile wave without a W1 column (no Adam stores before the consumer), when there is one
+  static constexpr bool hidden = L1 / 16 < kWaves;
+  static constexpr int wave = hidden ? kWaves - 1 : 0;
+};
+
+// REP: `hook` issues the block's PRIVATE prologue loads (Adam state of its W1 tile,
+// the parked X tile, the next sample index) right after the head's loads of SHARED
+// state, so they are the youngest kRepHookLoads vector loads of every wave and the
+// acknowledgement waits for the shared ones only (vmcnt(kRepHookLoads)).  Issued in
+// the kernel prologue instead (rounds 2-4), they were older than the head's loads,
+// and the ack's vmcnt(0) waited for their HBM round trips: every tile block's head
+// pass ended ~1.2 us after block 0's (profiles/r4_dp/dp_phases_wire16.log).
+constexpr int kRepHookLoads = 6;
+
+template <int BC, int L1, int L2, bool MULTI, bool REP, class Hook = NoHook>
+__device__ __forceinline__ void head_body(const MLP3Args& a, char* smem, RepPre* pre = nullptr,
+                                          const Hook& hook = Hook{}) {
   using C = Cfg3<BC, L1, L2>;
   using O = Off<L1, L2>;
   using A = Act<L1, L2>;
@@ -326,6 +372,11 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem, RepPre*
 #pragma unroll
     for (int i = 0; i < KPG1; ++i)
       w2tf[i] = ld8z(kg1 < KG1, O::W2T + (int64_t)(ct1 * 16 + r16) * L2 + (kg1 * KPG1 + i) * 32 + 8 * g);
+    if constexpr (REP) {
+      asm volatile("" ::: "memory");  // the hook's loads stay younger than every load above
+      hook();
+      asm volatile("" ::: "memory");
+    }
     // LDS writes last: their waits cover only the earliest loads (in-order vmcnt)
     if (tid < NBIAS) sBias[tid] = bias_v;
     if (tid < BC) sY[tid] = yok ? (slot ? y1 : y0) : -1;
@@ -427,14 +478,28 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem, RepPre*
       // the consumed H1pre slot) then wait for every block's LOADS instead of every
       // block's whole head pass.  (The weight fragments of dH2 / dH1 were issued
       // in the prologue ~1.5 us earlier: this wait costs little.)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // The wait as the BUILTIN (not inline asm), so the compiler's own wait bookkeeping
+      // sees it; it waits for every load older than the hook's (all shared state).
+      // gfx9 encoding: vmcnt in bits 3:0, expcnt 7 (bits 6:4), lgkmcnt 15 (bits 11:8).
+      asm volatile("" ::: "memory");
+      static_assert(kRepHookLoads < 16, "vmcnt immediate");
+      __builtin_amdgcn_s_waitcnt(0x0F70 | kRepHookLoads);  // vmcnt(kRepHookLoads): the hook's loads may fly on
+      asm volatile("" ::: "memory");
       __syncthreads();
       if (tid == 0)
         __hip_atomic_fetch_add(reinterpret_cast<long long*>(a.hand + kHandAck), 1ll, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
       if (pre->active) {
-        pre->xn = *reinterpret_cast<const uint4*>(a.x_u8 + pre->si * kD + pre->kt * 16);
-        pre->yn = a.labels[pre->si];
+        if constexpr (PreWave<L1>::hidden) {
+          // lane l: the 16 pixels of row (l & 31) -> raw + 16 l; dword (l & 1) of the
+          // label of row (l >> 1) -> raw + 1024 + 4 l (row r's int64 at raw + 1024 + 8 r)
+          const int64_t sr = __shfl(pre->si, lane >> 1, 64);
+          dma_lds16(a.x_u8 + pre->si * kD + pre->kt * 16, pre->raw);
+          dma_lds4(reinterpret_cast<const char*>(a.labels + sr) + 4 * (lane & 1), pre->raw + 1024u);
+        } else {
+          pre->xn = *reinterpret_cast<const uint4*>(a.x_u8 + pre->si * kD + pre->kt * 16);
+          pre->yn = a.labels[pre->si];
+        }
       }
     }
 
@@ -1531,7 +1596,8 @@ struct One {
   // after the head's region: H2^T, dH2^T, dH1^T images, then the tile's X / W1 slices + Adam scalars
   static constexpr size_t oImg = C::total;
   static constexpr size_t oTile = oImg + (size_t)(2 * L2 + L1) * C::TS * 2;
-  static constexpr size_t lds = oTile + (size_t)(2 * 32 + L1) * kXSS * 2 + 64;
+  static constexpr size_t oRaw = oTile + (size_t)(2 * 32 + L1) * kXSS * 2 + 64;  // PreWave DMA area
+  static constexpr size_t lds = oRaw + kPreRawBytes;
 };
 static_assert(One<128, 256>::lds <= 160 * 1024, "one-launch LDS budget");
 
@@ -1608,9 +1674,7 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
   const int m = w * 16 + r16, pix = kt * 16 + 4 * g;
   const bool mw = tile && w < TN1;  // tile waves owning a 16-neuron column
   const int64_t gidx = mw ? (int64_t)m * kD + pix : 0;
-  F4 p4 = *reinterpret_cast<const F4*>(a.params + gidx);
-  F4 m4 = *reinterpret_cast<const F4*>(a.exp_avg + gidx);
-  F4 v4 = *reinterpret_cast<const F4*>(a.exp_avg_sq + gidx);
+  F4 p4, m4, v4;  // loaded by the head's hook (below)
   SmallRes r;
   r.kind = -1;
   const int task = (blk - 1 - kTiles) * kWaves + w;
@@ -1620,39 +1684,43 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
   // prefetch -- before wave 0 issued a single head-pass load (profiles/r4_dp)
   const float lr_now = a.lr_ptr ? ((const __attribute__((address_space(4))) float*)(a.lr_ptr))[0] : a.lr;
   // wave 0 of a tile: row (lane & 31) of X[t] (parked by the previous step) and the
-  // sample index of row (lane & 31) of the NEXT batch (its pixels load after the head pass)
+  // sample index of row (lane & 31) of the NEXT batch (its pixels load after the ack)
   __bf16* XR = reinterpret_cast<__bf16*>(a.xring);
   constexpr int64_t tile_elems = (int64_t)Bp * 16;
   const int xb = lane & 31;
-  bf16x8 xc0 = zero8(), xc1 = zero8();
-  int64_t si = 0;
+  bf16x8 xc0, xc1;
+  RepPre pre;
+  pre.active = tile && w == PreWave<L1>::wave;
+  pre.raw = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)(smem + One<L1, L2>::oRaw);
+  pre.kt = tile ? kt : 0;
+  pre.xn = make_uint4(0u, 0u, 0u, 0u);
+  pre.yn = -1;
   int64_t nc = cursor + 1, nob = ob;
   if (nc >= a.n_batches) { nc = 0; nob ^= 1; }
-  if (tile && w == 0) {  // wave-uniform
-    const __bf16* cur = XR + (slot * kTiles + kt) * tile_elems + xb * 16;
+  // the private prologue loads, exactly kRepHookLoads per wave on every block (clamped
+  // addresses where the wave does not need them): the next sample index first (its
+  // value is needed right after the ack, so it is waited for before the others)
+  const int kt_c = tile ? kt : 0;
+  auto hook = [&]() {
+    pre.si = a.order[nob * a.order_stride + nc * B + (xb < B ? xb : 0)];
+    const __bf16* cur = XR + (slot * kTiles + kt_c) * tile_elems + xb * 16;
     xc0 = ld8(cur);
     xc1 = ld8(cur + 8);
-    si = a.order[nob * a.order_stride + nc * B + (xb < B ? xb : 0)];
-  }
+    p4 = *reinterpret_cast<const F4*>(a.params + gidx);
+    m4 = *reinterpret_cast<const F4*>(a.exp_avg + gidx);
+    v4 = *reinterpret_cast<const F4*>(a.exp_avg_sq + gidx);
+  };
   if (tid == 0 && blk > 0)
     adam_scalars(*sh_o, a.advance_step ? c0 + 1 : c0, lr_now, a.beta1, a.beta2, a.eps, a.weight_decay, a.adamw);
 
   // ---- the serial chain, on this CU (tile wave 0 also issues the next batch's loads) ----
-  RepPre pre;
-  pre.active = tile && w == 0;
-  pre.si = si;
-  pre.kt = tile ? kt : 0;
-  pre.xn = make_uint4(0u, 0u, 0u, 0u);
-  pre.yn = -1;
-  head_body<32, L1, L2, false, true>(a, smem, &pre);
+  head_body<32, L1, L2, false, true>(a, smem, &pre, hook);
 
   // (the block's acknowledgement went out inside head_body, once its loads had landed)
   if (a.stamps && blk == 1 && tid == 0) a.stamps[9] = __builtin_amdgcn_s_memrealtime();
 
   if (tile) {
     // the next batch's pixels (+ label, tile 0) were issued inside the head pass
-    const uint4 xn = pre.xn;
-    const int yn = (int)pre.yn;
     if (w == 0 && lane < 32) {
       *reinterpret_cast<bf16x8*>(sX + xb * kXSS) = xc0;
       *reinterpret_cast<bf16x8*>(sX + xb * kXSS + 8) = xc1;
@@ -1718,8 +1786,16 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
       *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.shadow) + gidx) = w4;
       *reinterpret_cast<bf16x4*>(sW + m * kXSS + 4 * g) = w4;
     }
-    if (w == 0 && lane >= 32) {
+    if (w == PreWave<L1>::wave && lane >= 32) {
       // X[t+1] row xb -> sXn, parked in xring[slot ^ 1] for the next step (+ its labels, tile 0)
+      uint4 xn = pre.xn;
+      int yn = (int)pre.yn;
+      if constexpr (PreWave<L1>::hidden) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA (this wave's only vector-memory ops in flight)
+        const char* raw = smem + One<L1, L2>::oRaw;
+        xn = *reinterpret_cast<const uint4*>(raw + 16 * lane);
+        yn = (int)*reinterpret_cast<const int64_t*>(raw + 1024 + 8 * xb);
+      }
       bf16x8 lo = zero8(), hi = zero8();
       if (xb < B) u8x16_to_bf16(xn, lo, hi);
       *reinterpret_cast<bf16x8*>(sXn + xb * kXSS) = lo;

@@ -515,6 +515,21 @@ def _diff_summary(a, b):
     return out
 
 
+def _word_diff(a, b, k=12):
+    """The raw 32-bit words where two same-shaped buffers differ: index and both values
+    (hex and as fp32) -- a stray writer's values name it (a counter, a flag, a float)."""
+    wa, wb = a.contiguous().view(torch.int32).flatten(), b.contiguous().view(torch.int32).flatten()
+    ne = (wa != wb).nonzero().flatten()
+    out = {"n": int(ne.numel())}
+    idx = ne[:k]
+    if idx.numel():
+        va, vb = wa[idx].cpu(), wb[idx].cpu()
+        out["words"] = [(int(i), f"{int(p) & 0xFFFFFFFF:08x}", f"{int(q) & 0xFFFFFFFF:08x}",
+                         float(p.view(torch.float32)), float(q.view(torch.float32)))
+                        for i, p, q in zip(idx.tolist(), va, vb)]
+    return out
+
+
 def _fidelity_run(eng, x, y, L1, L2, B, n_steps, world=1, autocast=False, make=None):
     """Step ``eng`` n_steps times; every step, the gradient it applied (recovered from
     Adam's first moment: m_t = b1 m_{t-1} + (1 - b1) g_t) against fp32 autograd on the
@@ -584,6 +599,10 @@ def _fidelity_run(eng, x, y, L1, L2, B, n_steps, world=1, autocast=False, make=N
                         "errs": _per_tensor_rel((f.exp_avg - fb1 * fm0) / (1 - fb1),
                                                 _fp32_ref_grads(fp0, x[idx], y[idx], L1, L2), L1, L2),
                         "pre_step_params_equal": bool(torch.equal(fp0, p0)),
+                        "pre_step_params_words": _word_diff(p0, fp0),
+                        "pre_step_exp_avg_words": _word_diff(m0, fm0),
+                        "order_words": _word_diff(eng.order, f.order),
+                        "x_u8_equal": bool(torch.equal(eng.x_u8, f.x_u8)),
                         "diff_vs_failing": _diff_summary(f, eng)}
     return worst, worst_ac, first_bad
 
