@@ -199,7 +199,8 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
   check_dev(xring, "xring", at::kBFloat16);
   TORCH_CHECK(xring.numel() >= 2 * 49 * Bp * 16, "xring must hold 2 * 49 * round_up(B, 32) * 16");
   check_dev(h1pre, "h1pre", at::kLong);
-  TORCH_CHECK(h1pre.numel() >= 2 * Bp * L1, "h1pre must hold 2 * round_up(B, 32) * L1");
+  TORCH_CHECK(h1pre.numel() >= 2 * rla::mlp3_h1_copies((int)L1) * Bp * L1,
+              "h1pre must hold 2 * mlp3_h1_copies(L1) * round_up(B, 32) * L1");
   check_dev(act, "act", at::kBFloat16);
   TORCH_CHECK(act.numel() >= rla::mlp3_act_rows((int)L1, (int)L2) * Bp, "act must hold (L1 + 2 L2 + 16) * Bp");
   check_dev(counters, "counters", at::kLong);
@@ -888,6 +889,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "3 tail-adam, 4 prime, 5 step with the in-kernel xGMI exchange, 6 one-launch step (B <= 32)");
   m.def("dp_pack_roundtrip", &dp_pack_roundtrip, "packed DP exchange wire form of fp32 pairs, encoded + decoded");
   m.def("mlp3_hand_words", [](int64_t l1, int64_t l2) { return rla::mlp3_hand_words((int)l1, (int)l2); });
+  m.def("mlp3_h1_copies", [](int64_t l1) { return rla::mlp3_h1_copies((int)l1); },
+        "H1pre copies per ring slot of the v3 step (the layer-1 partials' atomic fan-in is split over them)");
   m.def("mlp3_dp_area_floats", []() { return rla::comm::kDpUnitAreaFloats; },
         "aux receive-area stride (floats) of the one-launch step's packed / owner protocols");
   m.def("mlp_adam", &mlp_adam, "MLP arena Adam + bf16 shadow refresh (update=False: refresh only)");

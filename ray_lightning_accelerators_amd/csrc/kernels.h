@@ -226,7 +226,7 @@ struct MLP3Args {
   uint16_t* shadow;         // bf16 weight shadows (mlp_shadow_layout)
   uint16_t* dh1t;           // [L1][Bp] bf16
   uint16_t* xring;          // [2][49][Bp][16] bf16 X tiles
-  int64_t* h1pre;           // [2][Bp * L1] layer-1 pre-activations, 32.32 fixed point (fragment order)
+  int64_t* h1pre;           // [2][copies][Bp * L1] layer-1 pre-activations, 32.32 fixed point (fragment order)
   uint16_t* act;            // [L1 + 2*L2 + 16][Bp] bf16 head -> tail: H1^T, H2^T, dH2^T, dZ^T
   int* yring;               // [2][Bp] int32 staged labels (-1 past B), slot-indexed like xring
   float* stats;
@@ -264,6 +264,7 @@ int64_t mlp3_hand_words(int L1, int L2);  // int64 words of the one-launch step'
 int launch_mlp3(const MLP3Args& a, int kind, hipStream_t stream);
 
 int mlp3_act_rows(int L1, int L2);
+int mlp3_h1_copies(int L1);  // H1pre copies per ring slot (mlp_step3.hip H1Copies)
 // the packed DP exchange's wire form of fp32 pairs, encoded and decoded (tests)
 int dp_pack_roundtrip(const float* x, float* y, int64_t n, int tag, hipStream_t stream);
 

@@ -111,6 +111,18 @@ __device__ __forceinline__ unsigned long long f32_to_fixed(float x) {
 }
 __device__ __forceinline__ float fixed_to_f32(int64_t q) { return (float)((double)q * (1.0 / 4294967296.0)); }
 
+// H1pre copies per ring slot: the 49 W1 tiles' layer-1 partials are spread over G
+// copies (tile kt adds into copy kt % G) and the head sums the copies as it loads
+// them (integer adds: exact, order-free).  Device-scope atomics to ONE address
+// serialise at ~12 ns each (MI355X_MICROARCH.md "fanin"), so 49 tiles adding into the
+// same 8-byte word drained ~0.6 us after the tiles were done (measured: plain stores
+// in place of the atomics cut the step 8.38 -> 7.87 us, profiles/r6_h1copies); two
+// copies halve every chain.  One copy at L1 = 128 (the head's loads would double).
+template <int L1>
+struct H1Copies {
+  static constexpr int G = L1 <= 64 ? 2 : 1;
+};
+
 // Gather one 16-pixel tile of batch (ob, cursor) as bf16 rows into xring slot
 // `dst_slot` (rows >= B zero); block kt == 0 also stages that batch's labels
 // into yring (-1 for padded rows), so no kernel chases the sample index on
@@ -283,8 +295,12 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem, RepPre*
   // the tail of this step accumulates the next step's H1pre into the other slot;
   // in fragment order this block's rows are one contiguous BC * L1 range
   if constexpr (!REP) {
-    uint4* z = reinterpret_cast<uint4*>(a.h1pre + (slot ^ 1) * (int64_t)Bp * L1 + (int64_t)c * BC * L1);
-    for (int i = tid; i < BC * L1 / 2; i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int cp = 0; cp < H1Copies<L1>::G; ++cp) {
+      uint4* z = reinterpret_cast<uint4*>(a.h1pre + ((slot ^ 1) * H1Copies<L1>::G + cp) * (int64_t)Bp * L1 +
+                                          (int64_t)c * BC * L1);
+      for (int i = tid; i < BC * L1 / 2; i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
   }
   const float invB = 1.f / (float)a.B;
   constexpr int KS2 = L1 / 32, KS3 = C::KS3, KSH = C::KSH;
@@ -323,7 +339,8 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem, RepPre*
     // Labels and H1pre of BOTH ring slots are loaded before the barrier and
     // selected after it: none of these loads waits for the counters read.
     constexpr int NQ = (BC * L1 / 4 + kThreads - 1) / kThreads;
-    longlong2 qs[NQ][2][2];  // [item][slot][half]
+    constexpr int G = H1Copies<L1>::G;
+    longlong2 qs[NQ][2][G][2];  // [item][slot][copy][half]
     bool qok[NQ];
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
@@ -332,11 +349,14 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem, RepPre*
       // rows past round_up(B, 32) exist only in the last chunk's LDS image
       qok[k] = f4 < BC * L1 / 4 && row0 + mtl * 16 < Bp;
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int64_t* src = a.h1pre + (qok[k] ? s * (int64_t)Bp * L1 + (int64_t)row0 * L1 + f4 * 4 : 0);
-        qs[k][s][0] = *reinterpret_cast<const longlong2*>(src);
-        qs[k][s][1] = *reinterpret_cast<const longlong2*>(src + 2);
-      }
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int cp = 0; cp < G; ++cp) {
+          const int64_t* src =
+              a.h1pre + (qok[k] ? (s * G + cp) * (int64_t)Bp * L1 + (int64_t)row0 * L1 + f4 * 4 : 0);
+          qs[k][s][cp][0] = *reinterpret_cast<const longlong2*>(src);
+          qs[k][s][cp][1] = *reinterpret_cast<const longlong2*>(src + 2);
+        }
     }
     // labels of both ring slots (staged by the previous step; -1 past B)
     const bool yok = tid < BC && row0 + tid < Bp;
@@ -388,7 +408,11 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem, RepPre*
       for (int k = 0; k < NQ; ++k) {
         const int f4 = tid + k * kThreads;
         if (f4 >= BC * L1 / 4) continue;
-        if (!qok[k]) qs[k][0][0] = qs[k][0][1] = qs[k][1][0] = qs[k][1][1] = make_longlong2(0, 0);
+        if (!qok[k])
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int cp = 0; cp < G; ++cp) qs[k][s][cp][0] = qs[k][s][cp][1] = make_longlong2(0, 0);
         const int f = f4 * 4;
         const int ln = f & 63, i = (f >> 6) & 3, blk = f >> 8;
         const int ct = blk % C::TN1, mtl = blk / C::TN1;
@@ -399,7 +423,14 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem, RepPre*
         bf16x4 hs[2];
 #pragma unroll
         for (int sl = 0; sl < 2; ++sl) {
-          const int64_t q[4] = {qs[k][sl][0].x, qs[k][sl][0].y, qs[k][sl][1].x, qs[k][sl][1].y};
+          int64_t q[4] = {qs[k][sl][0][0].x, qs[k][sl][0][0].y, qs[k][sl][0][1].x, qs[k][sl][0][1].y};
+#pragma unroll
+          for (int cp = 1; cp < G; ++cp) {
+            q[0] += qs[k][sl][cp][0].x;
+            q[1] += qs[k][sl][cp][0].y;
+            q[2] += qs[k][sl][cp][1].x;
+            q[3] += qs[k][sl][cp][1].y;
+          }
 #pragma unroll
           for (int k = 0; k < 4; ++k) hs[sl][k] = relu_bf(fixed_to_f32(q[k]) + sBias[m + k]);
         }
@@ -1384,8 +1415,9 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
       // the H1pre slot the head consumed (cn[3] ^ 1) is zero for the step after
       // this one to accumulate into (the one-launch step relies on it)
       const int Bp = (a.B + 31) / 32 * 32;
-      uint4* z = reinterpret_cast<uint4*>(a.h1pre + (cn[3] ^ 1) * (int64_t)Bp * a.L1);
-      const int nz = Bp * a.L1 / 2, nsb = (int)gridDim.x - kTiles;
+      constexpr int G = H1Copies<L1>::G;
+      uint4* z = reinterpret_cast<uint4*>(a.h1pre + (cn[3] ^ 1) * G * (int64_t)Bp * L1);
+      const int nz = G * Bp * L1 / 2, nsb = (int)gridDim.x - kTiles;
       for (int i = sblk * NT + tid; i < nz; i += nsb * NT) z[i] = make_uint4(0u, 0u, 0u, 0u);
     }
     if (mode == kAdam) {
@@ -1551,7 +1583,9 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
   *reinterpret_cast<bf16x4*>(sW + m * kXSS + 4 * g) = w4;
   __syncthreads();
   if (do_fwd) {
-    unsigned long long* h1 = reinterpret_cast<unsigned long long*>(a.h1pre + slot * (int64_t)Bp * L1);
+    constexpr int G = H1Copies<L1>::G;
+    unsigned long long* h1 =
+        reinterpret_cast<unsigned long long*>(a.h1pre + (slot * G + kt % G) * (int64_t)Bp * L1);
     const bf16x8 bfrag = (g < 2) ? ld8(sW + (ct * 16 + r16) * kXSS + 8 * g) : zero8();
     for (int mt = 0; mt < Bp / 16; ++mt) {
       const bf16x8 afrag = (g < 2) ? ld8(sXn + (mt * 16 + r16) * kXSS + 8 * g) : zero8();
@@ -1661,6 +1695,7 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
   const bool tile = blk >= 1 && blk <= kTiles, small = blk > kTiles;
   const int kt = blk - 1;
   if (a.stamps && blk == 1 && tid == 0) a.stamps[8] = __builtin_amdgcn_s_memrealtime();
+  stamp_max(a, 13);  // probe builds: the latest block start (dispatch skew)
 
   // the state of this step: nobody overwrites it before every block's ack
   const int64_t c0 = ld_state(a.counters, 0), cursor = ld_state(a.counters, 1);
@@ -1718,6 +1753,7 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
 
   // (the block's acknowledgement went out inside head_body, once its loads had landed)
   if (a.stamps && blk == 1 && tid == 0) a.stamps[9] = __builtin_amdgcn_s_memrealtime();
+  stamp_max(a, 12);  // probe builds: the latest head-pass end over all blocks
 
   if (tile) {
     // the next batch's pixels (+ label, tile 0) were issued inside the head pass
@@ -1726,6 +1762,7 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
       *reinterpret_cast<bf16x8*>(sX + xb * kXSS + 8) = xc1;
     }
     __syncthreads();
+    if (a.stamps && blk == 1 && tid == 0) a.stamps[7] = __builtin_amdgcn_s_memrealtime();
     bf16x4 w4;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     if (mw) {
@@ -1806,9 +1843,13 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
       if (kt == 0) a.yring[(slot ^ 1) * Bp + xb] = xb < B ? yn : -1;
     }
     __syncthreads();
+    if (a.stamps && blk == 1 && tid == 0) a.stamps[14] = __builtin_amdgcn_s_memrealtime();
+    stamp_max(a, 15);  // probe builds: the latest tile block past its staging barrier
     if (mw) {
       // next step's layer-1 partial: H1pre[b][m] += sum_{16 px} X'[b][px] W1[m][px]
-      unsigned long long* h1 = reinterpret_cast<unsigned long long*>(a.h1pre + (slot ^ 1) * (int64_t)Bp * L1);
+      constexpr int G = H1Copies<L1>::G;
+      unsigned long long* h1 =
+          reinterpret_cast<unsigned long long*>(a.h1pre + ((slot ^ 1) * G + kt % G) * (int64_t)Bp * L1);
       const bf16x8 bfrag = (g < 2) ? ld8(sW + (w * 16 + r16) * kXSS + 8 * g) : zero8();
 #pragma unroll
       for (int mt = 0; mt < Bp / 16; ++mt) {
@@ -1820,6 +1861,7 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
       }
     }
     if (a.stamps && blk == 1 && tid == 0) a.stamps[10] = __builtin_amdgcn_s_memrealtime();
+    stamp_max(a, 5);  // probe builds: the latest W1-tile block end
   } else if (small) {
     const RepLds L{(const __bf16*)(smem + C::oH1T), sH2T, sDH2T, (const __bf16*)(smem + C::odZT), sDH1T, C::TS};
     small_compute<L1, L2, true>(a, true, task, r, &L);
@@ -1860,11 +1902,12 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
     one_wait_acks(a, seq, &sh_fail);  // every block has read the weights / biases this overwrites
     if (adam_done) small_store<L1, L2>(a, r, store_mv);  // r.v: the new weights
     else small_finalize<L1, L2>(a, true, r, *sh_o);
+    stamp_max(a, 6);  // probe builds: the latest small-parameter block end
   } else {
     // block 0: stats, the consumed H1pre slot zeroed (the invariant), then the advanced state
     one_wait_acks(a, seq, &sh_fail);
-    uint4* z = reinterpret_cast<uint4*>(a.h1pre + slot * (int64_t)Bp * L1);
-    for (int i = tid; i < Bp * L1 / 2; i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
+    uint4* z = reinterpret_cast<uint4*>(a.h1pre + slot * H1Copies<L1>::G * (int64_t)Bp * L1);
+    for (int i = tid; i < H1Copies<L1>::G * Bp * L1 / 2; i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
     if (tid == 0) {
       const float* misc = (const float*)(smem + C::oMisc);
       const int64_t t = c0 + 1;
@@ -1964,6 +2007,7 @@ int dp_pack_roundtrip(const float* x, float* y, int64_t n, int tag, hipStream_t 
 }
 
 int mlp3_act_rows(int L1, int L2) { return L1 + 2 * L2 + 16; }
+int mlp3_h1_copies(int L1) { return L1 <= 64 ? H1Copies<64>::G : H1Copies<128>::G; }
 int64_t mlp3_hand_words(int, int) { return kHandWords; }
 
 int launch_mlp3(const MLP3Args& a, int kind, hipStream_t stream) {

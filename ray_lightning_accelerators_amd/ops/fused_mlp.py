@@ -189,14 +189,22 @@ def mlp3_hand_words(L1: int, L2: int) -> int:
 W1_TILES = IN_FEATURES // 16
 
 
+def mlp3_h1_copies(L1: int) -> int:
+    """H1pre copies per ring slot (csrc/mlp_step3.hip ``H1Copies``): the 49 W1 tiles'
+    layer-1 partials are atomically added into ``copies`` separate buffers (tile kt
+    into copy kt % copies), which the head sums as it loads them."""
+    return 2 if int(L1) <= 64 else 1
+
+
 def mlp3_buffers(L1: int, L2: int, B: int, device) -> Dict[str, torch.Tensor]:
     """Device scratch of the v3 pipelined step (see csrc/mlp_step3.hip)."""
     bp = (B + 31) // 32 * 32
     return {
         "dh1t": torch.zeros(L1 * bp, dtype=torch.bfloat16, device=device),
         "xring": torch.zeros(2 * W1_TILES * bp * 16, dtype=torch.bfloat16, device=device),
-        # 32.32 fixed point: integer atomics make the 49-way split-K sum order-independent
-        "h1pre": torch.zeros(2 * bp * L1, dtype=torch.int64, device=device),
+        # 32.32 fixed point: integer atomics make the 49-way split-K sum order-independent;
+        # [slot][copy][Bp * L1] (see mlp3_h1_copies)
+        "h1pre": torch.zeros(2 * mlp3_h1_copies(L1) * bp * L1, dtype=torch.int64, device=device),
         "act": torch.zeros((L1 + 2 * L2 + 16) * bp, dtype=torch.bfloat16, device=device),
         "yring": torch.full((2 * bp,), -1, dtype=torch.int32, device=device),
         # [0, 5) current state, [5, 10) the head's advanced copy (published by the tail),

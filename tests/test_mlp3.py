@@ -41,6 +41,15 @@ def _emulate_bf16_grads(params, x, y, L1, L2, B):
     return torch.cat([t.reshape(-1) for t in g])
 
 
+@gpu
+def test_mlp3_h1_copies_mirror():
+    """The Python buffer sizing mirrors the kernels' H1pre copy count."""
+    from ray_lightning_accelerators_amd import ops
+
+    for L1 in (32, 64, 128):
+        assert ops.require().mlp3_h1_copies(L1) == fused_mlp.mlp3_h1_copies(L1)
+
+
 def _data(n, seed=0):
     g = torch.Generator().manual_seed(seed)
     x = torch.randint(0, 256, (n, 784), generator=g, dtype=torch.uint8)
@@ -460,7 +469,7 @@ def _pre_step_check(snap, x, y, idx, L1, L2, B, cur, epoch):
     xr = snap["xring"].view(2, 49, Bp, 16).cpu()[slot].float().permute(1, 0, 2).reshape(Bp, 784)
     xe = (x[idx].float() * (1.0 / 255.0)).to(torch.bfloat16).float()
     out["xring_ok"] = bool(torch.equal(xr[:B], xe) and bool((xr[B:] == 0).all()))
-    h1 = snap["h1pre"].view(2, Bp * L1)
+    h1 = snap["h1pre"].view(2, fused_mlp.mlp3_h1_copies(L1), Bp * L1).sum(1)  # the copies add up
     cur_h = _h1pre_dense(h1[slot], L1)
     w1 = snap["shadow"][: L1 * 784].view(L1, 784).cpu().double()
     ref_h = xe.double() @ w1.T
