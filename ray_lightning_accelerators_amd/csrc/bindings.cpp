@@ -198,7 +198,7 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
   TORCH_CHECK(dh1t.numel() >= L1 * Bp, "dh1t must hold L1 * round_up(B, 32)");
   check_dev(xring, "xring", at::kBFloat16);
   TORCH_CHECK(xring.numel() >= 2 * 49 * Bp * 16, "xring must hold 2 * 49 * round_up(B, 32) * 16");
-  check_dev(h1pre, "h1pre", at::kLong);
+  check_dev(h1pre, "h1pre", at::kInt);
   TORCH_CHECK(h1pre.numel() >= 2 * rla::mlp3_h1_copies((int)L1) * Bp * L1,
               "h1pre must hold 2 * mlp3_h1_copies(L1) * round_up(B, 32) * L1");
   check_dev(act, "act", at::kBFloat16);
@@ -229,7 +229,7 @@ void mlp3(int64_t kind, Tensor x_u8, Tensor labels, Tensor order, Tensor counter
   a.shadow = reinterpret_cast<uint16_t*>(shadow.data_ptr());
   a.dh1t = reinterpret_cast<uint16_t*>(dh1t.data_ptr());
   a.xring = reinterpret_cast<uint16_t*>(xring.data_ptr());
-  a.h1pre = h1pre.data_ptr<int64_t>();
+  a.h1pre = h1pre.data_ptr<int>();
   a.act = reinterpret_cast<uint16_t*>(act.data_ptr());
   a.yring = yring.data_ptr<int>();
   a.stats = ptr_or_null<float>(stats, "stats", at::kFloat, 4);
@@ -659,7 +659,7 @@ std::vector<Tensor> conv1x1_bn_bwd(Tensor dy1, Tensor wt, Tensor dy2, Tensor yb,
 
 // 1x1 conv forward with BatchNorm partial sums: x [M, K] (NHWC rows), w [N, K], both
 // bf16 contiguous; returns (y [M, N] bf16, part [gx, 2, N] fp32 for bn_finalize)
-std::vector<Tensor> conv1x1_stats(Tensor x, Tensor w) {
+std::vector<Tensor> conv1x1_stats(Tensor x, Tensor w, optional<Tensor> pre_ss, optional<Tensor> nbt_inc) {
   check_dev(x, "x", at::kBFloat16);
   check_dev(w, "w", at::kBFloat16);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.is_contiguous() && w.is_contiguous(),
@@ -669,13 +669,27 @@ std::vector<Tensor> conv1x1_stats(Tensor x, Tensor w) {
   TORCH_CHECK(rla::conv1x1_stats_ok(M, (int)K, (int)N), "conv1x1_stats: unsupported shape (K % 32, N % 64)");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
               "conv1x1_stats: 16-byte aligned operands");
+  const float* pre = nullptr;
+  int64_t* nbt = nullptr;
+  if (pre_ss.has_value() && pre_ss->defined()) {
+    // a deferred BatchNorm + ReLU on x: bn_finalize's [4, K] stats (rows 2 / 3 = scale / shift)
+    check_dev(*pre_ss, "pre_ss", at::kFloat);
+    TORCH_CHECK(pre_ss->is_contiguous() && pre_ss->dim() == 2 && pre_ss->size(0) == 4 && pre_ss->size(1) == K,
+                "conv1x1_stats: pre_ss must be [4, K] contiguous fp32");
+    TORCH_CHECK(rla::conv1x1_pre_ok(M, (int)K, (int)N), "conv1x1_stats: pre_ss needs K <= 512");
+    pre = pre_ss->data_ptr<float>();
+    if (nbt_inc.has_value() && nbt_inc->defined()) {
+      check_dev(*nbt_inc, "nbt_inc", at::kLong);
+      nbt = nbt_inc->data_ptr<int64_t>();
+    }
+  }
   const at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const rla::Conv1x1Plan p = rla::conv1x1_stats_plan(M, (int)N);
   Tensor y = at::empty({M, N}, x.options());
   Tensor part = at::empty({p.gx, 2, N}, x.options().dtype(at::kFloat));
   rla::launch_conv1x1_stats(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                             reinterpret_cast<const uint16_t*>(w.data_ptr()), reinterpret_cast<uint16_t*>(y.data_ptr()),
-                            M, (int)K, (int)N, p, part.data_ptr<float>(), cur_stream(x));
+                            M, (int)K, (int)N, p, part.data_ptr<float>(), cur_stream(x), pre, nbt);
   return {y, part};
 }
 
@@ -717,7 +731,7 @@ void bn_bwd_apply(Tensor x, optional<Tensor> y, Tensor dy, Tensor coef, bool rel
 // (the channels_last weight's memory order).
 Tensor conv_wgrad(Tensor dy, Tensor x, int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t OH, int64_t OW,
                   int64_t Cout, int64_t KH, int64_t KW, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
-                  int64_t splits, int64_t algo) {
+                  int64_t splits, int64_t algo, optional<Tensor> pre_ss) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda(), "conv_wgrad: GPU tensors");
   TORCH_CHECK(algo == 0 || algo == 1, "conv_wgrad: algo 0 (auto) or 1 (generic)");
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "conv_wgrad: bf16 inputs");
@@ -735,11 +749,22 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int64_t N, int64_t H, int64_t W, int64_t 
   rla::WgradGeom g{(int)N, (int)H, (int)W, (int)Cin, (int)OH, (int)OW, (int)Cout, (int)KH, (int)KW,
                    (int)sh, (int)sw, (int)ph, (int)pw};
   const rla::WgradPlan plan = rla::wgrad_plan(g, (int)splits, (int)algo);
+  const float* pre = nullptr;
+  if (pre_ss.has_value() && pre_ss->defined()) {
+    // x is a deferred BatchNorm + ReLU's input: the generic kernel stages the activation
+    check_dev(*pre_ss, "pre_ss", at::kFloat);
+    TORCH_CHECK(pre_ss->is_contiguous() && pre_ss->dim() == 2 && pre_ss->size(0) == 4 && pre_ss->size(1) == Cin,
+                "conv_wgrad: pre_ss must be [4, Cin] contiguous fp32");
+    TORCH_CHECK(KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && plan.kind == 0,
+                "conv_wgrad: pre_ss on 1x1 / stride-1 geometry only");
+    pre = pre_ss->data_ptr<float>();
+  }
   Tensor out = at::empty({Cout, KH, KW, Cin}, x.options().dtype(at::kFloat));
   Tensor part;
   if (plan.splits > 1) part = at::empty({(int64_t)plan.splits * Cout * KH * KW * Cin}, out.options());
   rla::launch_wgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
-                    out.data_ptr<float>(), plan.splits > 1 ? part.data_ptr<float>() : nullptr, g, plan, cur_stream(x));
+                    out.data_ptr<float>(), plan.splits > 1 ? part.data_ptr<float>() : nullptr, g, plan, cur_stream(x),
+                    pre);
   return out;
 }
 
@@ -907,7 +932,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd_finalize", &bn_bwd_finalize, "fused BN backward: dgamma/dbeta + dx coefficients");
   m.def("bn_apply", &bn_apply, "fused BN apply: y = act(x*scale + shift (+res))", py::arg("x"), py::arg("scale"),
         py::arg("shift"), py::arg("res"), py::arg("relu"), py::arg("y"), py::arg("nbt_inc") = py::none());
-  m.def("conv1x1_stats", &conv1x1_stats, "1x1 conv forward on MFMA + BatchNorm partial sums of its output");
+  m.def("conv1x1_stats", &conv1x1_stats, "1x1 conv forward on MFMA + BatchNorm partial sums of its output",
+        py::arg("x"), py::arg("w"), py::arg("pre_ss") = py::none(), py::arg("nbt_inc") = py::none());
+  m.def("conv1x1_pre_ok", [](int64_t M, int64_t K, int64_t N) { return rla::conv1x1_pre_ok(M, (int)K, (int)N); });
   m.def("conv1x1_bn_bwd", &conv1x1_bn_bwd,
         "1x1 conv input gradient fused with the previous BatchNorm's backward partial -> (d, part)");
   m.def("conv1x1_bn_bwd_ok", [](int64_t M, int64_t K, int64_t N) { return rla::conv1x1_bn_bwd_ok(M, (int)K, (int)N); });
@@ -926,7 +953,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad", &conv_wgrad, "NHWC bf16 conv weight gradient on MFMA -> fp32 [Cout, KH, KW, Cin]",
         py::arg("dy"), py::arg("x"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("OH"),
         py::arg("OW"), py::arg("Cout"), py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"), py::arg("ph"),
-        py::arg("pw"), py::arg("splits") = 0, py::arg("algo") = 0);
+        py::arg("pw"), py::arg("splits") = 0, py::arg("algo") = 0, py::arg("pre_ss") = py::none());
   m.def("conv_wgrad_plan", &conv_wgrad_plan, "the wgrad kernel's (kind, wa, wb, splits, rows_per_split)",
         py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("OH"), py::arg("OW"), py::arg("Cout"),
         py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),

@@ -75,7 +75,17 @@ __device__ __forceinline__ void c1_dma16(const void* gsrc, uint32_t lds) {
 // partial row sums d and d * xb (xb the BatchNorm's input), bn_partial_kernel<1>'s
 // layout.  da is never written or re-read (ops/conv.py, fuse_bn_dgrad).  dy2 / yb / xb
 // for a tile are loaded at its first stage, two stages ahead of the epilogue.
-template <int TNW, bool WRES, int NS, bool BWD = false>
+//
+// PRE: x is the raw input of a BatchNorm + ReLU whose apply pass was deferred to this
+// conv (ResNet's bn2 -> conv3, ops/bn.py ``defer``): every x fragment becomes
+// bf16(relu(x * scale + shift)) after its LDS read -- the exact expression of
+// bn_apply_kernel, so y is bitwise the unfused conv of the applied activation -- and
+// the activation is never written (one read + one write of [M, K] less per layer).
+// pre_ss is bn_finalize's [4, K] (rows 2 / 3: scale / shift), staged once into LDS;
+// nbt_inc: num_batches_tracked += 1 (the apply kernel's job when the BatchNorm's
+// statistics came from a conv epilogue).
+constexpr int kPreMaxK = 512;
+template <int TNW, bool WRES, int NS, bool BWD = false, bool PRE = false>
 __global__ __launch_bounds__(kC1Threads, 2) void conv1x1_stats_kernel(const uint16_t* __restrict__ x,
                                                                       const uint16_t* __restrict__ w,
                                                                       uint16_t* __restrict__ y, int64_t M, int K,
@@ -83,8 +93,11 @@ __global__ __launch_bounds__(kC1Threads, 2) void conv1x1_stats_kernel(const uint
                                                                       float* __restrict__ part,
                                                                       const uint16_t* __restrict__ dy2 = nullptr,
                                                                       const uint16_t* __restrict__ yb = nullptr,
-                                                                      const uint16_t* __restrict__ xb = nullptr) {
+                                                                      const uint16_t* __restrict__ xb = nullptr,
+                                                                      const float* __restrict__ pre_ss = nullptr,
+                                                                      int64_t* __restrict__ nbt_inc = nullptr) {
   static_assert(!BWD || TNW == 1, "the backward epilogue's prefetch is sized for 32-channel wave columns");
+  static_assert(!(BWD && PRE), "PRE is a forward variant");
   constexpr int BN = 64 * TNW;                      // workgroup channels
   constexpr int kXBytes = 4 * 128 * 16;             // x part of a stage: [4 k units][128 rows] x 16 B
   constexpr int kStageBytes = kXBytes + (WRES ? 0 : 4 * BN * 16);
@@ -96,7 +109,16 @@ __global__ __launch_bounds__(kC1Threads, 2) void conv1x1_stats_kernel(const uint
   static_assert(NS * kStageBytes + kWResBytes <= kC1LdsBytes, "LDS budget (2 workgroups per CU)");
   __shared__ __attribute__((aligned(16))) uint8_t ring[NS * kStageBytes + kWResBytes];
   __shared__ float red[2][2][BN];
+  __shared__ __attribute__((aligned(16))) float pre_tab[PRE ? 2 * kPreMaxK : 4];  // [scale | shift]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if constexpr (PRE) {
+    if (nbt_inc && blockIdx.x == 0 && tid == 0) nbt_inc[0] += 1;
+    for (int i = tid; i < K; i += kC1Threads) {
+      pre_tab[i] = pre_ss[2 * K + i];
+      pre_tab[kPreMaxK + i] = pre_ss[3 * K + i];
+    }
+    __syncthreads();  // ahead of every DMA: the loop's counted waits see DMA only
+  }
   const int wn = wave & 1, wm = wave >> 1, r = lane & 31, h = lane >> 5;
   // XCD-aware (x, y): hardware block b runs on XCD b % 8; the gy column blocks of a
   // pixel range x all sit on XCD x % 8 (gx is a multiple of 8)
@@ -166,6 +188,21 @@ __global__ __launch_bounds__(kC1Threads, 2) void conv1x1_stats_kernel(const uint
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         fb[j] = *reinterpret_cast<const bf16x8*>(buf + (ku * 128 + wm * 64 + 32 * j + r) * 16);
+      if constexpr (PRE) {  // channels 32 c + 8 ku .. +8 of both pixel fragments
+        const float* sc = pre_tab + c * 32 + ku * 8;
+        const float4 s0 = *reinterpret_cast<const float4*>(sc), s1 = *reinterpret_cast<const float4*>(sc + 4);
+        const float4 h0 = *reinterpret_cast<const float4*>(sc + kPreMaxK);
+        const float4 h1 = *reinterpret_cast<const float4*>(sc + kPreMaxK + 4);
+        const float scl[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const float sft[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float v = __builtin_fmaf((float)fb[j][e], scl[e], sft[e]);
+            fb[j][e] = (__bf16)(v > 0.f ? v : 0.f);
+          }
+      }
 #pragma unroll
       for (int t = 0; t < TNW; ++t)
 #pragma unroll
@@ -318,6 +355,8 @@ bool conv1x1_stats_ok(int64_t M, int K, int N) {
   return M > 0 && K >= 32 && K % 32 == 0 && N >= 64 && N % 64 == 0 && N <= 4096;
 }
 
+bool conv1x1_pre_ok(int64_t M, int K, int N) { return conv1x1_stats_ok(M, K, N) && K <= kPreMaxK; }
+
 Conv1x1Plan conv1x1_stats_plan(int64_t M, int N) {
   Conv1x1Plan p;
   // 32-channel wave columns only where N needs them: choosing them to keep a K = 256 /
@@ -336,14 +375,20 @@ Conv1x1Plan conv1x1_stats_plan(int64_t M, int N) {
 }
 
 void launch_conv1x1_stats(const uint16_t* x, const uint16_t* w, uint16_t* y, int64_t M, int K, int N,
-                          const Conv1x1Plan& p, float* part, hipStream_t s) {
+                          const Conv1x1Plan& p, float* part, hipStream_t s, const float* pre_ss, int64_t* nbt_inc) {
   const dim3 grid(p.gx * p.gy), block(kC1Threads);
   // resident weights where they fit beside the x ring: 6 x-only stages (4 in flight)
   // with a 16 KB weight block, 4 stages with 32 KB; else x + w stream through 4 stages
   const int64_t wbytes = (int64_t)K * 64 * p.tnw * 2;
-#define RLA_C1_LAUNCH(T, R, NS)                                                                                  \
-  hipLaunchKernelGGL((conv1x1_stats_kernel<T, R, NS>), grid, block, 0, s, x, w, y, M, K, N, p.gx, p.tiles_per_blk, \
-                     part)
+#define RLA_C1_LAUNCH(T, R, NS)                                                                                   \
+  do {                                                                                                            \
+    if (pre_ss)                                                                                                   \
+      hipLaunchKernelGGL((conv1x1_stats_kernel<T, R, NS, false, true>), grid, block, 0, s, x, w, y, M, K, N, p.gx, \
+                         p.tiles_per_blk, part, nullptr, nullptr, nullptr, pre_ss, nbt_inc);                     \
+    else                                                                                                          \
+      hipLaunchKernelGGL((conv1x1_stats_kernel<T, R, NS>), grid, block, 0, s, x, w, y, M, K, N, p.gx,             \
+                         p.tiles_per_blk, part);                                                                  \
+  } while (0)
   if (p.tnw == 2) {
     if (wbytes <= 16384)
       RLA_C1_LAUNCH(2, true, 6);

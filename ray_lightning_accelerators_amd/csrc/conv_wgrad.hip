@@ -75,11 +75,19 @@ __device__ __forceinline__ int64_t x_row(int64_t m, const WgradGeom& g, int r, i
   return (int64_t)((n * g.H + ih) * g.W + iw);
 }
 
-template <int WA, int WB, bool GEN, int DEPTH = 2>
+// PRE (1x1 / stride 1 only): x is the raw input of a deferred BatchNorm + ReLU
+// (ops/bn.py ``defer``; the forward conv applied it in its fragments, conv1x1.hip PRE):
+// each x chunk is staged as bf16(relu(x * scale + shift)) -- bn_apply_kernel's exact
+// expression -- so the gradient is bitwise the one of the materialised activation.
+// A thread's x chunks keep their channel columns across stages: 16 coefficients per
+// chunk in registers, loaded once.
+template <int WA, int WB, bool GEN, int DEPTH = 2, bool PRE = false>
 __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t* __restrict__ dy,
                                                            const uint16_t* __restrict__ x, float* __restrict__ out,
                                                            WgradGeom g, int64_t M, int64_t rows_per_split,
-                                                           int tiles_co, int tiles_ci, int splits) {
+                                                           int tiles_co, int tiles_ci, int splits,
+                                                           const float* __restrict__ pre_ss = nullptr) {
+  static_assert(!(PRE && GEN), "PRE: 1x1 / stride-1 geometry");
   constexpr int NWT = WA * WB;          // wave tiles per workgroup tile
   constexpr int KS = 4 / NWT;           // waves sharing one wave tile (reduction split)
   constexpr int KB = KS == 4 ? 64 : 32;  // rows per stage: every wave gets >= 1 k-step of 16
@@ -147,6 +155,18 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t* __res
       st.ok |= ok ? (1u << (NA + i)) : 0u;
     }
   };
+  float pre_sc[PRE ? NB : 1][8], pre_sf[PRE ? NB : 1][8];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int c = tid + i * kWgThreads, col = (c % (TCI / 8)) * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        pre_sc[i][e] = pre_ss[2 * g.Cin + ci0 + col + e];
+        pre_sf[i][e] = pre_ss[3 * g.Cin + ci0 + col + e];
+      }
+    }
+  }
   auto store = [&](const Set& st, int buf) {
     __bf16* A = lds + buf * STAGE;
     __bf16* B = A + KB * SA;
@@ -159,7 +179,17 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t* __res
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int c = tid + i * kWgThreads, row = c / (TCI / 8), col = (c % (TCI / 8)) * 8;
-      *reinterpret_cast<u32x4*>(B + row * SB + col) = (st.ok >> (NA + i)) & 1u ? st.b[i] : z;
+      u32x4 v = st.b[i];
+      if constexpr (PRE) {
+        bf16x8 h = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float a = __builtin_fmaf((float)h[e], pre_sc[i][e], pre_sf[i][e]);
+          h[e] = (__bf16)(a > 0.f ? a : 0.f);
+        }
+        v = __builtin_bit_cast(u32x4, h);
+      }
+      *reinterpret_cast<u32x4*>(B + row * SB + col) = (st.ok >> (NA + i)) & 1u ? v : z;
     }
   };
 
@@ -486,11 +516,14 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_kernel(const uint16_t* __
 
 template <int WA, int WB>
 void launch_tile(const uint16_t* dy, const uint16_t* x, float* out, const WgradGeom& g, int64_t M, int64_t rps,
-                 int S, bool gen, hipStream_t st) {
+                 int S, bool gen, hipStream_t st, const float* pre_ss) {
   const int tco = g.Cout / (64 * WA), tci = g.Cin / (64 * WB);
   const int total = tco * tci * g.KH * g.KW * S;
   const dim3 grid((unsigned)((total + 7) / 8 * 8)), block(kWgThreads);
-  if (gen)
+  if (pre_ss)  // the binding admits PRE on 1x1 / stride-1 geometry only (gen == false)
+    hipLaunchKernelGGL((wgrad_kernel<WA, WB, false, 2, true>), grid, block, 0, st, dy, x, out, g, M, rps, tco, tci, S,
+                       pre_ss);
+  else if (gen)
     hipLaunchKernelGGL((wgrad_kernel<WA, WB, true>), grid, block, 0, st, dy, x, out, g, M, rps, tco, tci, S);
   else
     hipLaunchKernelGGL((wgrad_kernel<WA, WB, false>), grid, block, 0, st, dy, x, out, g, M, rps, tco, tci, S);
@@ -574,7 +607,7 @@ WgradPlan wgrad_plan(const WgradGeom& g, int splits, int algo) {
 }
 
 void launch_wgrad(const uint16_t* dy, const uint16_t* x, float* out, float* part, const WgradGeom& g,
-                  const WgradPlan& p, hipStream_t st) {
+                  const WgradPlan& p, hipStream_t st, const float* pre_ss) {
   const int64_t M = (int64_t)g.N * g.OH * g.OW;
   if (p.kind == 1) {
     float* dst = p.splits > 1 ? part : out;
@@ -593,12 +626,12 @@ void launch_wgrad(const uint16_t* dy, const uint16_t* x, float* out, float* part
   float* dst = p.splits > 1 ? part : out;
   const int key = p.wa * 10 + p.wb;
   switch (key) {
-    case 22: launch_tile<2, 2>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st); break;
-    case 41: launch_tile<4, 1>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st); break;
-    case 14: launch_tile<1, 4>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st); break;
-    case 21: launch_tile<2, 1>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st); break;
-    case 12: launch_tile<1, 2>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st); break;
-    default: launch_tile<1, 1>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st); break;
+    case 22: launch_tile<2, 2>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st, pre_ss); break;
+    case 41: launch_tile<4, 1>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st, pre_ss); break;
+    case 14: launch_tile<1, 4>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st, pre_ss); break;
+    case 21: launch_tile<2, 1>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st, pre_ss); break;
+    case 12: launch_tile<1, 2>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st, pre_ss); break;
+    default: launch_tile<1, 1>(dy, x, dst, g, M, p.rows_per_split, p.splits, gen, st, pre_ss); break;
   }
   }
   if (p.splits > 1) {

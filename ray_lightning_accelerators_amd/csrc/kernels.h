@@ -131,9 +131,13 @@ struct Conv1x1Plan {
   int tiles_per_blk;  // 128-pixel tiles per range
 };
 bool conv1x1_stats_ok(int64_t M, int K, int N);
+// pre_ss ([4, K] BatchNorm stats, K <= 512): x is a deferred BatchNorm + ReLU's input,
+// each x fragment becomes bf16(relu(x * scale + shift)) in the kernel (nbt_inc += 1)
+bool conv1x1_pre_ok(int64_t M, int K, int N);
 Conv1x1Plan conv1x1_stats_plan(int64_t M, int N);
 void launch_conv1x1_stats(const uint16_t* x, const uint16_t* w, uint16_t* y, int64_t M, int K, int N,
-                          const Conv1x1Plan& p, float* part, hipStream_t s);
+                          const Conv1x1Plan& p, float* part, hipStream_t s, const float* pre_ss = nullptr,
+                          int64_t* nbt_inc = nullptr);
 // input gradient of a 1x1 conv (dy1 [M][K] . W, wt = W^T [N][K]) fused with the previous
 // BatchNorm's backward partial: d = (da + dy2) * (yb > 0) written to d, part [rows, 2, N]
 // = sums of d and d * xb.  part == nullptr: only *rows is set (the partial row count).
@@ -226,7 +230,7 @@ struct MLP3Args {
   uint16_t* shadow;         // bf16 weight shadows (mlp_shadow_layout)
   uint16_t* dh1t;           // [L1][Bp] bf16
   uint16_t* xring;          // [2][49][Bp][16] bf16 X tiles
-  int64_t* h1pre;           // [2][copies][Bp * L1] layer-1 pre-activations, 32.32 fixed point (fragment order)
+  int* h1pre;               // [2][copies][Bp * L1] layer-1 pre-activations, 12.20 fixed point (fragment order)
   uint16_t* act;            // [L1 + 2*L2 + 16][Bp] bf16 head -> tail: H1^T, H2^T, dH2^T, dZ^T
   int* yring;               // [2][Bp] int32 staged labels (-1 past B), slot-indexed like xring
   float* stats;
@@ -296,8 +300,10 @@ struct WgradPlan {
 // splits <= 0: automatic; algo 0: the halo kernel when the geometry allows, 1: generic
 WgradPlan wgrad_plan(const WgradGeom& g, int splits, int algo = 0);
 // part: splits * Cout * KH * KW * Cin floats when plan.splits > 1 (else unused)
+// pre_ss ([4, Cin] BatchNorm stats; generic 1x1 / stride-1 plans only): x is a deferred
+// BatchNorm + ReLU's input, staged as bf16(relu(x * scale + shift))
 void launch_wgrad(const uint16_t* dy, const uint16_t* x, float* out, float* part, const WgradGeom& g,
-                  const WgradPlan& p, hipStream_t stream);
+                  const WgradPlan& p, hipStream_t stream, const float* pre_ss = nullptr);
 
 // ---------------------------------------------------------------------------
 // 3x3 / stride 1 / pad 1 NHWC bf16 convolution on MFMA (csrc/conv3x3.hip):

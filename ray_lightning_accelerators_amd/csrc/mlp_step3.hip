@@ -19,7 +19,7 @@
 //   tail(t)   blocks [0, 49): one 16-pixel W1 column tile each: dW1 tile =
 //             X[t]_tile^T dH1 (MFMA; X^T by ds_read_b64_tr_b16), Adam on the
 //             tile, then gather X[t+1]'s tile (u8 -> bf16) and add
-//             X[t+1]_tile . W1_tile^T into H1pre[t+1] (32.32 fixed-point integer atomics,
+//             X[t+1]_tile . W1_tile^T into H1pre[t+1] (17.15 fixed-point int32 atomics,
 //             49 adders per element) -- layer 1 is linear in W1 and this block
 //             holds the freshly updated tile in registers.  The X tile is parked
 //             in `xring` for tail(t+1)'s dW1.
@@ -101,15 +101,22 @@ constexpr bool fits3() {
 
 __device__ __forceinline__ __bf16 relu_bf(float x) { return (__bf16)fmaxf(x, 0.f); }
 
-// H1pre partial sums travel as 32.32 fixed point: the 49 tile contributions are
-// added with integer atomics, which are associative, so the sum (and the whole
-// step) is bitwise reproducible whatever order the atomics land in.  Scaling by
-// 2^32 is exact in fp32; |partial| < 2^31 holds for any sane weights.
-constexpr float kFix = 4294967296.0f;  // 2^32
-__device__ __forceinline__ unsigned long long f32_to_fixed(float x) {
-  return (unsigned long long)__float2ll_rn(x * kFix);
+// H1pre partial sums travel as 12.20 fixed point in int32: the 49 tile
+// contributions are added with integer atomics, which are associative, so the sum
+// (and the whole step) is bitwise reproducible whatever order the atomics land in.
+// Resolution 2^-20 (9.5e-7; H1's bf16 rounding right after is 4.9e-4 at 0.1).  Each
+// tile's 16-pixel partial saturates at +-32 (an average |w| of 2 over pixels in
+// [0, 1]), so the 49-term sum stays inside +-1568 and can never wrap.  32-bit words
+// halve the bytes every head pass loads and every atomic moves against round 5's
+// 32.32 int64 (same box: 7.81 vs 8.08 us/step steady, profiles/r6_h1copies).
+// Cost: a pre-activation within ~1e-6 of zero can take the other side of the ReLU
+// than an fp32 sum would (tests/test_mlp3.py models the rounding in its emulation).
+constexpr float kFix = 1048576.0f;  // 2^20
+constexpr float kFixSat = 33554432.0f;  // 2^25 = 32.0 in fixed point
+__device__ __forceinline__ unsigned f32_to_fixed(float x) {
+  return (unsigned)__float2int_rn(fminf(fmaxf(x * kFix, -kFixSat), kFixSat));
 }
-__device__ __forceinline__ float fixed_to_f32(int64_t q) { return (float)((double)q * (1.0 / 4294967296.0)); }
+__device__ __forceinline__ float fixed_to_f32(int q) { return (float)q * (1.0f / 1048576.0f); }
 
 // H1pre copies per ring slot: the 49 W1 tiles' layer-1 partials are spread over G
 // copies (tile kt adds into copy kt % G) and the head sums the copies as it loads
@@ -299,7 +306,7 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem, RepPre*
     for (int cp = 0; cp < H1Copies<L1>::G; ++cp) {
       uint4* z = reinterpret_cast<uint4*>(a.h1pre + ((slot ^ 1) * H1Copies<L1>::G + cp) * (int64_t)Bp * L1 +
                                           (int64_t)c * BC * L1);
-      for (int i = tid; i < BC * L1 / 2; i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
+      for (int i = tid; i < BC * L1 / 4; i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
     }
   }
   const float invB = 1.f / (float)a.B;
@@ -340,7 +347,7 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem, RepPre*
     // selected after it: none of these loads waits for the counters read.
     constexpr int NQ = (BC * L1 / 4 + kThreads - 1) / kThreads;
     constexpr int G = H1Copies<L1>::G;
-    longlong2 qs[NQ][2][G][2];  // [item][slot][copy][half]
+    int4 qs[NQ][2][G];  // [item][slot][copy]: 4 consecutive int32 words
     bool qok[NQ];
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
@@ -352,10 +359,8 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem, RepPre*
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int cp = 0; cp < G; ++cp) {
-          const int64_t* src =
-              a.h1pre + (qok[k] ? (s * G + cp) * (int64_t)Bp * L1 + (int64_t)row0 * L1 + f4 * 4 : 0);
-          qs[k][s][cp][0] = *reinterpret_cast<const longlong2*>(src);
-          qs[k][s][cp][1] = *reinterpret_cast<const longlong2*>(src + 2);
+          const int* src = a.h1pre + (qok[k] ? (s * G + cp) * (int64_t)Bp * L1 + (int64_t)row0 * L1 + f4 * 4 : 0);
+          qs[k][s][cp] = *reinterpret_cast<const int4*>(src);
         }
     }
     // labels of both ring slots (staged by the previous step; -1 past B)
@@ -412,7 +417,7 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem, RepPre*
 #pragma unroll
           for (int s = 0; s < 2; ++s)
 #pragma unroll
-            for (int cp = 0; cp < G; ++cp) qs[k][s][cp][0] = qs[k][s][cp][1] = make_longlong2(0, 0);
+            for (int cp = 0; cp < G; ++cp) qs[k][s][cp] = make_int4(0, 0, 0, 0);
         const int f = f4 * 4;
         const int ln = f & 63, i = (f >> 6) & 3, blk = f >> 8;
         const int ct = blk % C::TN1, mtl = blk / C::TN1;
@@ -423,13 +428,13 @@ __device__ __forceinline__ void head_body(const MLP3Args& a, char* smem, RepPre*
         bf16x4 hs[2];
 #pragma unroll
         for (int sl = 0; sl < 2; ++sl) {
-          int64_t q[4] = {qs[k][sl][0][0].x, qs[k][sl][0][0].y, qs[k][sl][0][1].x, qs[k][sl][0][1].y};
+          int q[4] = {qs[k][sl][0].x, qs[k][sl][0].y, qs[k][sl][0].z, qs[k][sl][0].w};
 #pragma unroll
-          for (int cp = 1; cp < G; ++cp) {
-            q[0] += qs[k][sl][cp][0].x;
-            q[1] += qs[k][sl][cp][0].y;
-            q[2] += qs[k][sl][cp][1].x;
-            q[3] += qs[k][sl][cp][1].y;
+          for (int cp = 1; cp < G; ++cp) {  // two's-complement adds: exact while the true sum fits
+            q[0] += qs[k][sl][cp].x;
+            q[1] += qs[k][sl][cp].y;
+            q[2] += qs[k][sl][cp].z;
+            q[3] += qs[k][sl][cp].w;
           }
 #pragma unroll
           for (int k = 0; k < 4; ++k) hs[sl][k] = relu_bf(fixed_to_f32(q[k]) + sBias[m + k]);
@@ -1417,7 +1422,7 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
       const int Bp = (a.B + 31) / 32 * 32;
       constexpr int G = H1Copies<L1>::G;
       uint4* z = reinterpret_cast<uint4*>(a.h1pre + (cn[3] ^ 1) * G * (int64_t)Bp * L1);
-      const int nz = G * Bp * L1 / 2, nsb = (int)gridDim.x - kTiles;
+      const int nz = G * Bp * L1 / 4, nsb = (int)gridDim.x - kTiles;
       for (int i = sblk * NT + tid; i < nz; i += nsb * NT) z[i] = make_uint4(0u, 0u, 0u, 0u);
     }
     if (mode == kAdam) {
@@ -1584,13 +1589,13 @@ __global__ __launch_bounds__(64 * (L1 / 16)) void mlp3_tail_kernel(MLP3Args a, i
   __syncthreads();
   if (do_fwd) {
     constexpr int G = H1Copies<L1>::G;
-    unsigned long long* h1 =
-        reinterpret_cast<unsigned long long*>(a.h1pre + (slot * G + kt % G) * (int64_t)Bp * L1);
+    unsigned* h1 =
+        reinterpret_cast<unsigned*>(a.h1pre + (slot * G + kt % G) * (int64_t)Bp * L1);
     const bf16x8 bfrag = (g < 2) ? ld8(sW + (ct * 16 + r16) * kXSS + 8 * g) : zero8();
     for (int mt = 0; mt < Bp / 16; ++mt) {
       const bf16x8 afrag = (g < 2) ? ld8(sXn + (mt * 16 + r16) * kXSS + 8 * g) : zero8();
       const f32x4 d = mfma16(afrag, bfrag, f32x4{0.f, 0.f, 0.f, 0.f});
-      unsigned long long* dst = h1 + (int64_t)((mt * TN1 + ct) * 4) * 64 + lane;
+      unsigned* dst = h1 + (int64_t)((mt * TN1 + ct) * 4) * 64 + lane;
 #pragma unroll
       for (int i = 0; i < 4; ++i) atomicAdd(dst + i * 64, f32_to_fixed(d[i]));
     }
@@ -1848,14 +1853,13 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
     if (mw) {
       // next step's layer-1 partial: H1pre[b][m] += sum_{16 px} X'[b][px] W1[m][px]
       constexpr int G = H1Copies<L1>::G;
-      unsigned long long* h1 =
-          reinterpret_cast<unsigned long long*>(a.h1pre + ((slot ^ 1) * G + kt % G) * (int64_t)Bp * L1);
+      unsigned* h1 = reinterpret_cast<unsigned*>(a.h1pre + ((slot ^ 1) * G + kt % G) * (int64_t)Bp * L1);
       const bf16x8 bfrag = (g < 2) ? ld8(sW + (w * 16 + r16) * kXSS + 8 * g) : zero8();
 #pragma unroll
       for (int mt = 0; mt < Bp / 16; ++mt) {
         const bf16x8 afrag = (g < 2) ? ld8(sXn + (mt * 16 + r16) * kXSS + 8 * g) : zero8();
         const f32x4 d = mfma16(afrag, bfrag, f32x4{0.f, 0.f, 0.f, 0.f});
-        unsigned long long* dst = h1 + (int64_t)((mt * TN1 + w) * 4) * 64 + lane;
+        unsigned* dst = h1 + (int64_t)((mt * TN1 + w) * 4) * 64 + lane;
 #pragma unroll
         for (int i = 0; i < 4; ++i) atomicAdd(dst + i * 64, f32_to_fixed(d[i]));
       }
@@ -1907,7 +1911,7 @@ __global__ __launch_bounds__(kThreads) void mlp3_one_kernel(MLP3Args a) {
     // block 0: stats, the consumed H1pre slot zeroed (the invariant), then the advanced state
     one_wait_acks(a, seq, &sh_fail);
     uint4* z = reinterpret_cast<uint4*>(a.h1pre + slot * H1Copies<L1>::G * (int64_t)Bp * L1);
-    for (int i = tid; i < H1Copies<L1>::G * Bp * L1 / 2; i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (int i = tid; i < H1Copies<L1>::G * Bp * L1 / 4; i += kThreads) z[i] = make_uint4(0u, 0u, 0u, 0u);
     if (tid == 0) {
       const float* misc = (const float*)(smem + C::oMisc);
       const int64_t t = c0 + 1;

@@ -34,6 +34,7 @@ C > 2048, eval with autograd) runs the plain PyTorch composition.
 """
 from __future__ import annotations
 
+import os
 import warnings
 from typing import Optional
 
@@ -78,13 +79,65 @@ class _FoldSlot:
         self.bwd_d = None     # the d those sums are of (the tensor the conv returned as our dy)
 
 
-fold_stats = {"folded": 0, "fused_rejected": 0}
+fold_stats = {"folded": 0, "fused_rejected": 0, "deferred": 0, "materialized": 0}
+
+
+def defer_enabled() -> bool:
+    """``RLA_BN_DEFER=0`` keeps every BatchNorm's apply pass (see :class:`DeferredApply`)."""
+    return os.environ.get("RLA_BN_DEFER", "1") != "0"
+
+
+class DeferredApply:
+    """A BatchNorm + ReLU whose apply pass was left to its consumer (ResNet's bn2, read
+    only by conv3): the layer returns its INPUT x (an autograd alias standing for
+    relu(x * scale + shift)) tagged ``_rla_pre`` with this record, and a 1x1 conv that
+    understands it applies the map to its operand fragments (csrc/conv1x1.hip PRE,
+    csrc/conv_wgrad.hip PRE) -- the [M, C] activation is never written or re-read.
+    Any other consumer must call :func:`materialize` first.  ``nbt``: the
+    num_batches_tracked increment the skipped apply kernel would have made (when the
+    statistics came from a conv epilogue), taken by whichever kernel applies the map."""
+
+    __slots__ = ("st", "nbt", "used")
+
+    def __init__(self):
+        self.st = None
+        self.nbt = None
+        self.used = False
+
+    def take_nbt(self):
+        n, self.nbt = self.nbt, None
+        return n
+
+
+class _MaterializeFn(torch.autograd.Function):
+    """relu(x * scale + shift) of a deferred BatchNorm output, for a consumer that cannot
+    apply it itself; the gradient passes through unchanged (the deferred tensor already
+    stands for the activation in the autograd graph)."""
+
+    @staticmethod
+    def forward(ctx, x, pre):
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+        require().bn_apply(_nhwc(x), pre.st[2], pre.st[3], None, True, _nhwc(y), pre.take_nbt())
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy, None
+
+
+def materialize(x: torch.Tensor) -> torch.Tensor:
+    """The real activation of a possibly deferred BatchNorm output (no-op otherwise)."""
+    pre = getattr(x, "_rla_pre", None)
+    if pre is None:
+        return x
+    fold_stats["materialized"] += 1
+    return _MaterializeFn.apply(x, pre)
 
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu, group,
-                slot=None, sink=None, part=None, pool=None):
+                slot=None, sink=None, part=None, pool=None, defer=None):
         # slot: this layer's own _FoldSlot (a consumer may park dres for our backward);
         # sink: the producer slot of `residual` (residual is then passed detached);
         # part: partial sums the producing conv computed in its epilogue (ops.conv.BNStats);
@@ -117,6 +170,14 @@ class _BNActFn(torch.autograd.Function):
             ctx.save_for_backward(x, None, weight, st, arg)
             return yp.permute(0, 3, 1, 2)
         ctx.pool = None
+        if defer is not None:
+            # the consumer applies relu(x * scale + shift) itself (DeferredApply): x stands
+            # for the activation; the backward is the usual recomputed-mask one
+            defer.st, defer.nbt = st, (nbt if pending else None)
+            ctx.relu, ctx.has_res, ctx.group, ctx.count = True, False, group, count
+            ctx.slot, ctx.sink, ctx.recomp = slot, sink, True
+            ctx.save_for_backward(x, None, weight, st, None)
+            return x
         y = torch.empty_like(x, memory_format=torch.channels_last)
         mod.bn_apply(xv, st[2], st[3], _nhwc(residual) if residual is not None else None, relu, _nhwc(y),
                      nbt if pending else None)
@@ -157,7 +218,7 @@ class _BNActFn(torch.autograd.Function):
             wsrc = local if local is not None else coef
             dgamma = wsrc[0] if weight is not None and ctx.needs_input_grad[1] else None
             dbeta = wsrc[1] if ctx.needs_input_grad[2] else None
-            return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None, None
+            return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None, None, None
         C = x.size(1)
         xv, dyv = _nhwc(x), _nhwc(dy)
         yv = _nhwc(y) if y is not None else None
@@ -202,7 +263,7 @@ class _BNActFn(torch.autograd.Function):
         # views of the coefficient tensor (no copy kernels): autograd hands them to .grad
         dgamma = wsrc[0] if weight is not None and ctx.needs_input_grad[1] else None
         dbeta = wsrc[1] if ctx.needs_input_grad[2] else None
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 class BatchNormAct2d(nn.BatchNorm2d):
@@ -238,7 +299,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
         return None
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                residual_is_ancestor: bool = False, bn_stats=None, pool: Optional[nn.Module] = None) -> torch.Tensor:
+                residual_is_ancestor: bool = False, bn_stats=None, pool: Optional[nn.Module] = None,
+                defer: bool = False) -> torch.Tensor:
         """``residual_is_ancestor``: the caller guarantees ``x`` is computed from
         ``residual`` (ResNet identity shortcut), so this layer's backward runs before
         the residual producer's and the residual gradient can be folded into it.
@@ -246,7 +308,10 @@ class BatchNormAct2d(nn.BatchNorm2d):
         with x's partial sums (this layer then skips its own partial pass).
         ``pool``: a max-pool module applied to this layer's output -- returns
         ``pool(self(x))``, on the training path as ONE pass (BatchNorm + ReLU folded
-        into the pool kernel; the normalised activation is never materialised)."""
+        into the pool kernel; the normalised activation is never materialised).
+        ``defer``: the caller's only consumer of the output is a 1x1 conv that can apply
+        this layer's map itself (:class:`DeferredApply`); honoured on the fused training
+        path of a ReLU layer without residual or pool, else ignored."""
         geo = self._pool_geometry(pool, residual) if pool is not None else None
         if pool is not None and (geo is None or not fused_ok(x, residual)
                                  or not (self.training or not self.track_running_stats)):
@@ -268,13 +333,19 @@ class BatchNormAct2d(nn.BatchNorm2d):
                     if residual_is_ancestor and src is not None and not src.claimed and residual.requires_grad:
                         src.claimed, sink = True, src
                         residual = residual.detach()
+                pre = None
+                if defer and relu and residual is None and geo is None and defer_enabled():
+                    pre = DeferredApply()
+                    fold_stats["deferred"] += 1
                 y = _BNActFn.apply(
                     x, self.weight, self.bias, residual,
                     self.running_mean if track else None, self.running_var if track else None,
                     self.num_batches_tracked if track else None, momentum, float(self.eps), relu, self._group(),
-                    slot, sink, part, geo)
+                    slot, sink, part, geo, pre)
                 if slot is not None:
                     y._rla_fold = slot
+                if pre is not None:
+                    y._rla_pre = pre
                 return y
             if not torch.is_grad_enabled() or not (x.requires_grad or (self.weight is not None
                                                                           and self.weight.requires_grad)):

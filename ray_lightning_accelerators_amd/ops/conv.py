@@ -31,7 +31,7 @@ from torch import nn
 
 _choice: Dict[Tuple[str, int, int, int], str] = {}
 _timings: Dict[Tuple[str, int, int, int], Dict[str, float]] = {}
-stats = {"fast": 0, "fallback": 0, "bn_dgrad_fused": 0, "stem": 0}
+stats = {"fast": 0, "fallback": 0, "bn_dgrad_fused": 0, "stem": 0, "pre_applied": 0}
 
 _conv = torch.ops.aten.convolution
 _conv_bwd = torch.ops.aten.convolution_backward
@@ -108,19 +108,21 @@ def wgrad_ok(cin: int, cout: int) -> bool:
 
 
 def wgrad_hip(dy: torch.Tensor, x: torch.Tensor, kernel_size, stride, padding, splits: int = 0,
-              algo: int = 0) -> torch.Tensor:
+              algo: int = 0, pre_ss: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Weight gradient of an NHWC bf16 convolution on the MFMA kernel: ``dy`` [N, Cout,
     OH, OW] and ``x`` [N, Cin, H, W], both channels_last bf16; returns the fp32
     gradient [Cout, Cin, KH, KW] with channels_last strides (the kernel writes the
     [Cout, KH, KW, Cin] memory order directly).  ``algo`` 0: the 3x3 / stride-1 /
-    pad-1 halo kernel where it applies, else the generic one; 1: always generic."""
+    pad-1 halo kernel where it applies, else the generic one; 1: always generic.
+    ``pre_ss`` (1x1 / stride 1): ``x`` is a deferred BatchNorm + ReLU's input and the
+    kernel stages relu(x * scale + shift) (ops/bn.py DeferredApply)."""
     from . import require
 
     n, cin, h, w = x.shape
     cout, oh, ow = dy.size(1), dy.size(2), dy.size(3)
     kh, kw = kernel_size
     out = require().conv_wgrad(dy.permute(0, 2, 3, 1), x.permute(0, 2, 3, 1), n, h, w, cin, oh, ow, cout, kh, kw,
-                               stride[0], stride[1], padding[0], padding[1], splits, algo)
+                               stride[0], stride[1], padding[0], padding[1], splits, algo, pre_ss)
     return out.permute(0, 3, 1, 2)
 
 
@@ -258,15 +260,28 @@ def conv1x1_stats_ok(m: int, cin: int, cout: int) -> bool:
     return cin % 32 == 0 and cout % 64 == 0 and cout <= 4096 and os.environ.get("RLA_CONV1X1_STATS", "auto") != "off"
 
 
-def conv1x1_stats_hip(x: torch.Tensor, wb: torch.Tensor):
+def conv1x1_stats_hip(x: torch.Tensor, wb: torch.Tensor, pre=None):
     """``conv2d(x, wb)`` for a 1x1 / stride-1 layer on the MFMA kernel, plus the
     per-channel partial sums of its bf16 output: ``x`` [N, Cin, H, W] channels_last
-    bf16, ``wb`` [Cout, Cin] bf16.  Returns (y channels_last, part [rows, 2, Cout])."""
+    bf16, ``wb`` [Cout, Cin] bf16.  Returns (y channels_last, part [rows, 2, Cout]).
+    ``pre`` (ops/bn.py DeferredApply): ``x`` is that BatchNorm's input and the kernel
+    convolves relu(x * scale + shift) instead."""
     from . import require
 
     n, _, h, w = x.shape
-    y2, part = require().conv1x1_stats(_nhwc2d(x), wb)
+    if pre is not None:
+        y2, part = require().conv1x1_stats(_nhwc2d(x), wb, pre.st, pre.take_nbt())
+    else:
+        y2, part = require().conv1x1_stats(_nhwc2d(x), wb)
     return _from2d(y2, n, h, w), part
+
+
+def conv1x1_pre_ok(m: int, cin: int, cout: int) -> bool:
+    """Where a 1x1 conv applies a deferred BatchNorm + ReLU in its own kernels (forward
+    and weight gradient): K <= 128, the shapes whose forward runs on the in-tree kernel
+    anyway (profiles/r5_pair/rn50_graph.log ``fwd_st``; at K >= 256 the library GEMM +
+    the apply pass is faster)."""
+    return cin <= 128 and conv1x1_stats_ok(m, cin, cout) and wgrad_ok(cin, cout)
 
 
 def fuse_bn_dgrad_enabled() -> bool:
@@ -287,7 +302,7 @@ def _bn_partial(y: torch.Tensor) -> torch.Tensor:
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, shadow=None, fork=None, bn_stats=None, fuse_bn=False):
+    def forward(ctx, x, weight, shadow=None, fork=None, bn_stats=None, fuse_bn=False, pre=None):
         n, cin, h, w = x.shape
         cout = weight.size(0)
         # the arena's bf16 shadow (ops/shadow.py) when there is one: no cast kernel
@@ -295,6 +310,17 @@ class _Conv1x1Fn(torch.autograd.Function):
         x2 = _nhwc2d(x)
         key = (x2.size(0), cin, cout)
         w4 = wb.view(cout, cin, 1, 1)
+        ctx.pre_st = None
+        if pre is not None:
+            # x is a deferred BatchNorm + ReLU's input (ops/bn.py DeferredApply): the
+            # kernels apply its map to their operands; the caller checked conv1x1_pre_ok
+            y, part = conv1x1_stats_hip(x, wb, pre)
+            if bn_stats is not None:
+                bn_stats.part = part
+            ctx.pre_st = pre.st
+            ctx.save_for_backward(x, wb)
+            ctx.key, ctx.fork, ctx.fold = key, None, None
+            return y
         if bn_stats is not None and conv1x1_stats_ok(x2.size(0), cin, cout):
             # the next BatchNorm's statistics: in this GEMM's epilogue, or the library
             # forward + BN's own partial pass -- whichever is faster for the shape
@@ -339,6 +365,22 @@ class _Conv1x1Fn(torch.autograd.Function):
         be_d = be_w = None
         fork = ctx.fork if ctx.needs_input_grad[0] else None
         fold = ctx.fold
+        if ctx.pre_st is not None:
+            # deferred-BatchNorm input: the input gradient (w.r.t. the activation) does not
+            # read x; the weight gradient stages relu(x * scale + shift) in its kernel
+            if ctx.needs_input_grad[0]:
+                be_d = _pick("dgrad", ctx.key, {
+                    "gemm": lambda: torch.mm(dy2, wb),
+                    "miopen": lambda: _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                                [True, False, False])[0],
+                })
+                if be_d == "gemm":
+                    dx = _from2d(torch.mm(dy2, wb), n, h, w)
+                else:
+                    dx = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, False, False])[0]
+            if ctx.needs_input_grad[1]:
+                dw = wgrad_hip(dy, x, (1, 1), (1, 1), (0, 0), pre_ss=ctx.pre_st)
+            return dx, dw, None, None, None, None, None
         if fold is not None and fold.dres is not None and ctx.needs_input_grad[0]:
             # d = (dy . W + dres_next) * (x > 0) and its BatchNorm partial sums in one
             # kernel; the producer BatchNorm's backward takes d as its dy
@@ -373,7 +415,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         if be_d == "miopen" and be_w == "miopen" and fork is None:
             # both from MIOpen: one call (its host cost is tens of us per call)
             dx, dw = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, True, False])[:2]
-            return dx, dw.float(), None, None, None, None
+            return dx, dw.float(), None, None, None, None, None
         if be_d == "gemm":
             dx = _fork_dx(fork, lambda: _from2d(torch.mm(dy2, wb), n, h, w), None)
         elif be_d == "miopen":
@@ -386,7 +428,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         elif be_w == "miopen":
             dw = _conv_bwd(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
                            [False, True, False])[1].float()
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
 def fast_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
@@ -412,6 +454,21 @@ class Conv1x1NHWC(nn.Conv2d):
                 bn_stats: Optional[BNStats] = None) -> torch.Tensor:
         """``bn_stats``: the BatchNorm reading this output is training on batch
         statistics -- let this layer compute them where that is faster (BNStats)."""
+        pre = getattr(x, "_rla_pre", None)
+        if pre is not None:
+            # a deferred BatchNorm + ReLU output (ops/bn.py DeferredApply): applied in this
+            # conv's kernels where the shape allows, else materialised here
+            from .bn import materialize
+
+            if (fork is None and fast_ok(x, self) and _mode() != "off" and not pre.used
+                    and conv1x1_pre_ok(x.size(0) * x.size(2) * x.size(3), x.size(1), self.out_channels)):
+                pre.used = True
+                stats["fast"] += 1
+                stats["pre_applied"] += 1
+                from .shadow import bf16_weight
+
+                return _Conv1x1Fn.apply(x, self.weight, bf16_weight(self.weight), None, bn_stats, False, pre)
+            x = materialize(x)
         if torch.is_autocast_enabled("cuda") and x.is_cuda and x.dtype == torch.float32:
             x = x.to(torch.bfloat16)
         if fast_ok(x, self) and _mode() != "off":

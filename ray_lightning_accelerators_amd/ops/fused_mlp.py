@@ -202,9 +202,9 @@ def mlp3_buffers(L1: int, L2: int, B: int, device) -> Dict[str, torch.Tensor]:
     return {
         "dh1t": torch.zeros(L1 * bp, dtype=torch.bfloat16, device=device),
         "xring": torch.zeros(2 * W1_TILES * bp * 16, dtype=torch.bfloat16, device=device),
-        # 32.32 fixed point: integer atomics make the 49-way split-K sum order-independent;
-        # [slot][copy][Bp * L1] (see mlp3_h1_copies)
-        "h1pre": torch.zeros(2 * mlp3_h1_copies(L1) * bp * L1, dtype=torch.int64, device=device),
+        # 12.20 fixed point (int32): integer atomics make the 49-way split-K sum
+        # order-independent; [slot][copy][Bp * L1] (see mlp3_h1_copies)
+        "h1pre": torch.zeros(2 * mlp3_h1_copies(L1) * bp * L1, dtype=torch.int32, device=device),
         "act": torch.zeros((L1 + 2 * L2 + 16) * bp, dtype=torch.bfloat16, device=device),
         "yring": torch.full((2 * bp,), -1, dtype=torch.int32, device=device),
         # [0, 5) current state, [5, 10) the head's advanced copy (published by the tail),

@@ -131,6 +131,7 @@ def test_resnet_bottleneck_routes_stats(monkeypatch):
     y.float().sum().backward()
     assert calls["n"] == 3
     assert int(blk.bn1.num_batches_tracked) == int(blk.bn3.num_batches_tracked) == 1
+    assert int(blk.bn2.num_batches_tracked) == 1  # deferred apply: conv3's kernel counted it
     assert int(down[1].num_batches_tracked) == 1
     assert torch.isfinite(x.grad.float()).all()
 
@@ -228,3 +229,118 @@ def test_fused_bn_dgrad_guard_with_extra_consumer(monkeypatch):
     assert _rel(g1, g0) < 2e-2, _rel(g1, g0)
     for a, b in zip(p1, p0):
         assert _rel(a, b) < 3e-2, _rel(a, b)
+
+
+def _stats4(k, dev, seed):
+    """bn_finalize's [4, K] layout (mean, invstd, scale, shift) with random scale /
+    shift -- negative scales and shifts included, so the ReLU clips both ways."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    st = torch.randn(4, k, generator=g)
+    st[1] = st[1].abs() + 0.5
+    return st.to(dev).contiguous()
+
+
+def _apply(x, st):
+    """The materialised activation from the production apply kernel (bf16(relu(x * scale
+    + shift)))."""
+    from ray_lightning_accelerators_amd import ops
+
+    y = torch.empty_like(x)
+    ops.require().bn_apply(x, st[2].contiguous(), st[3].contiguous(), None, True, y)
+    return y
+
+
+@gpu
+@pytest.mark.parametrize("shape", [(2 * 56 * 56, 64, 256), (3 * 28 * 28, 128, 512), (1000, 64, 192), (77, 32, 64),
+                                   (300, 256, 128)])
+def test_conv1x1_pre_matches_materialized(shape):
+    """A deferred BatchNorm + ReLU applied inside the 1x1 forward (csrc/conv1x1.hip PRE)
+    == the same kernel on the activation materialised by the apply kernel: y and the
+    partial sums bitwise, and num_batches_tracked incremented once."""
+    from ray_lightning_accelerators_amd import ops
+
+    m, k, n = shape
+    torch.manual_seed(4)
+    dev = torch.device("cuda", 0)
+    x = torch.randn(m, k, device=dev).to(torch.bfloat16)
+    wb = (torch.randn(n, k, device=dev) / k ** 0.5).to(torch.bfloat16)
+    st = _stats4(k, dev, 5)
+    nbt = torch.zeros((), dtype=torch.int64, device=dev)
+    y1, p1 = ops.require().conv1x1_stats(x, wb, st, nbt)
+    y0, p0 = ops.require().conv1x1_stats(_apply(x, st), wb)
+    assert torch.equal(y1, y0)
+    assert torch.equal(p1, p0)
+    assert int(nbt) == 1
+    a = torch.relu(x.float() * st[2] + st[3]).to(torch.bfloat16).float()
+    assert _rel(y1, a @ wb.float().t()) < 8e-3
+
+
+@gpu
+@pytest.mark.parametrize("shape", [(2 * 28 * 28, 64, 256), (3 * 14 * 14, 128, 512), (500, 64, 64)])
+def test_wgrad_pre_matches_materialized(shape):
+    """The weight gradient staging relu(x * scale + shift) itself (csrc/conv_wgrad.hip
+    PRE) == the kernel on the materialised activation, bitwise (fp32 [Cout, Cin])."""
+    from ray_lightning_accelerators_amd import ops
+
+    m, cin, cout = shape
+    torch.manual_seed(6)
+    dev = torch.device("cuda", 0)
+    x = torch.randn(m, cin, device=dev).to(torch.bfloat16)
+    dy = torch.randn(m, cout, device=dev).to(torch.bfloat16)
+    st = _stats4(cin, dev, 7)
+    geo = (1, m, 1, cin, m, 1, cout, 1, 1, 1, 1, 0, 0)
+    g1 = ops.require().conv_wgrad(dy, x, *geo, 0, 0, st)
+    g0 = ops.require().conv_wgrad(dy, _apply(x, st), *geo, 0, 0)
+    assert torch.equal(g1, g0)
+    ref = dy.float().t() @ torch.relu(x.float() * st[2] + st[3]).to(torch.bfloat16).float()
+    assert _rel(g1.view(cout, cin), ref) < 1e-4
+
+
+@gpu
+@pytest.mark.parametrize("down", [False, True])
+def test_bottleneck_deferred_bn2_matches_applied(down, monkeypatch):
+    """A training Bottleneck with bn2's apply deferred into conv3 (RLA_BN_DEFER=1, the
+    default) == the same block with the apply pass (RLA_BN_DEFER=0): output, input
+    gradient, every parameter gradient and bn2's running statistics bitwise."""
+    from ray_lightning_accelerators_amd.models.resnet import Bottleneck
+    from ray_lightning_accelerators_amd.ops import bn as B
+    from ray_lightning_accelerators_amd.ops import conv as C
+    from ray_lightning_accelerators_amd.ops.bn import BatchNormAct2d
+    from torch import nn
+
+    monkeypatch.setenv("RLA_CONV1X1", "hip")  # one forward backend for both runs
+    monkeypatch.setenv("RLA_CONV_WGRAD", "hip")  # one weight-gradient backend for both runs
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(8)
+    cin = 64 if down else 256
+    ds = nn.Sequential(C.Conv1x1NHWC(64, 256), BatchNormAct2d(256, act=None)) if down else None
+    blk = Bottleneck(cin, 64, 1, ds, fused_bn=True).to(dev).to(memory_format=torch.channels_last)
+    x0 = torch.randn(2, cin, 20, 20, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    state = {k: v.clone() for k, v in blk.state_dict().items()}
+    outs = []
+    for defer in ("0", "1"):
+        monkeypatch.setenv("RLA_BN_DEFER", defer)
+        blk.load_state_dict(state)
+        blk.zero_grad(set_to_none=True)
+        n0, a0 = B.fold_stats["deferred"], C.stats["pre_applied"]
+        x = x0.clone().requires_grad_(True)
+        for _ in range(2):
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = blk(x)
+        y.float().square().mean().backward()
+        if defer == "1":
+            assert B.fold_stats["deferred"] - n0 == 2 and C.stats["pre_applied"] - a0 == 2
+        outs.append((y.detach().float(), x.grad.float(), [p.grad.detach().clone() for p in blk.parameters()],
+                     blk.bn2.running_mean.clone(), blk.bn2.running_var.clone(), int(blk.bn2.num_batches_tracked)))
+    (y0, g0, p0, m0, v0, n0), (y1, g1, p1, m1, v1, n1) = outs
+    assert torch.equal(y0, y1)
+    assert torch.equal(g0, g1)
+    for nm, a, b in zip([n for n, _ in blk.named_parameters()], p0, p1):
+        if nm == "conv2.weight":
+            # without a parameter arena conv2 is a plain autocast nn.Conv2d whose MIOpen
+            # weight gradient differs run to run at the 1e-7 level (split-K atomics):
+            # not bitwise even between two runs of the same mode
+            assert _rel(a, b.float()) < 1e-4, (nm, _rel(a, b.float()))
+        else:
+            assert torch.equal(a, b), nm
+    assert torch.equal(m0, m1) and torch.equal(v0, v1) and n0 == n1 == 2
