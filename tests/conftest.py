@@ -38,6 +38,7 @@ requires_gpu = pytest.mark.skipif(
 # pointer into memory it no longer owns (a stray asynchronous writer).  The report
 # names the test during which it happened and what was written.
 _CANARY = {"tensors": [], "prev": None}
+_MEMHIST = {"on": False}
 _CANARY_BYTE = 0x5A
 
 
@@ -138,6 +139,19 @@ def _device_canaries(request):
 
 
 def pytest_runtest_setup(item):
+    # RLA_MEMHIST=1 (diagnostic): the caching allocator records every device alloc / free
+    # with its Python stack from the first GPU test on, so a post-mortem can name the
+    # previous owners of a corrupted address range (tests/test_mlp3.py _alloc_history)
+    if os.environ.get("RLA_MEMHIST") == "1" and item.get_closest_marker("gpu") and not _MEMHIST["on"]:
+        try:
+            import torch
+
+            torch.cuda.memory._record_memory_history(enabled="all", context="all", stacks="python",
+                                                     max_entries=200000)
+            _MEMHIST["on"] = True
+        except Exception as e:  # noqa: BLE001 - a diagnostic must never fail a test
+            print(f"\nMEMHIST off: {e!r}"[:300], file=sys.stderr, flush=True)
+            _MEMHIST["on"] = True
     if os.environ.get("RLA_TEST_CLOCK") == "1":  # diagnostic: wall clock at each test start
         import time
 

@@ -512,6 +512,43 @@ def _session_facts(eng):
     return facts
 
 
+def _alloc_history(lo, hi, limit=12):
+    """Allocator history (RLA_MEMHIST=1, tests/conftest.py) of device addresses [lo, hi):
+    the segment holding them and the last alloc / free events of blocks overlapping
+    them, each with its innermost Python frames -- the previous owners of a corrupted
+    range."""
+    try:
+        return _alloc_history_impl(lo, hi, limit)
+    except Exception as e:  # noqa: BLE001 - diagnostics only
+        return {"error": repr(e)[:300]}
+
+
+def _alloc_history_impl(lo, hi, limit):
+    snap = torch.cuda.memory._snapshot()
+    out = {"segments": [], "events": []}
+    for seg in snap.get("segments", []):
+        a, n = seg["address"], seg["total_size"]
+        if a < hi and lo < a + n:
+            out["segments"].append({"address": hex(a), "size": n, "pool": str(seg.get("segment_pool_id")),
+                                    "stream": seg.get("stream"),
+                                    "frames": [f"{f['filename'].split('/')[-1]}:{f['line']} {f['name']}"
+                                               for f in (seg.get("frames") or [])[:6]]})
+    ev = []
+    for dev_trace in snap.get("device_traces", []):
+        for i, t in enumerate(dev_trace):
+            a, n = t.get("addr", 0), t.get("size", 0)
+            if a < hi and lo < a + max(n, 1):
+                ev.append((i, t))
+    for i, t in ev[-limit:]:
+        out["events"].append({"seq": i, "action": t.get("action"), "addr": hex(t.get("addr", 0)),
+                              "size": t.get("size"), "stream": t.get("stream"),
+                              "frames": [f"{f['filename'].split('/')[-1]}:{f['line']} {f['name']}"
+                                         for f in (t.get("frames") or [])
+                                         if "site-packages" not in f["filename"]][:8]})
+    out["n_events"] = len(ev)
+    return out
+
+
 def _fidelity_log(name, rows):
     import json
     import os
@@ -591,7 +628,26 @@ def _fidelity_run(eng, x, y, L1, L2, B, n_steps, world=1, autocast=False, make=N
 
             for name, t in (("p0", p0), ("m0", m0), ("g", g), ("params", eng.params), ("exp_avg", eng.exp_avg)):
                 dev_sum, host_sum, host2 = csum(t), csum(t.cpu()), csum(t.cpu())
-                dma[name] = {"device": dev_sum, "host": host_sum, "host_again": host2, "equal": dev_sum == host_sum}
+                # the device checksum again AFTER the copies: equal to the host's means the
+                # device content changed in between (an asynchronous writer); equal to the
+                # first means the copies returned data the device never held
+                dev_again = csum(t)
+                dma[name] = {"device": dev_sum, "host": host_sum, "host_again": host2, "device_again": dev_again,
+                             "equal": dev_sum == host_sum, "ptr": hex(t.data_ptr()), "bytes": t.numel() * 4}
+            # where p0 / g are not finite or are zero while the pre-step params are not: the
+            # corrupted ranges, on the device and in a host copy, with the allocator history
+            p0h = p0.cpu()
+            for name, t in (("p0", p0), ("g", g)):
+                bad_d = (~torch.isfinite(t)).nonzero().flatten()
+                if name == "p0":
+                    bad_d = torch.cat([bad_d, ((t == 0) & (eng.params != 0)).nonzero().flatten()]).unique()
+                if bad_d.numel():
+                    lo_i, hi_i = int(bad_d.min()), int(bad_d.max()) + 1
+                    dma[name]["corrupt_words"] = [lo_i, hi_i, int(bad_d.numel())]
+                    lo, hi = t.data_ptr() + 4 * lo_i, t.data_ptr() + 4 * hi_i
+                    dma[name]["alloc_history"] = _alloc_history(lo, hi)
+            dma["p0_host_nonfinite"] = int((~torch.isfinite(p0h)).sum())
+            dma["p0_host_zero_where_params_nonzero"] = int(((p0h == 0) & (eng.params.cpu() != 0)).sum())
             xs, xh = int(eng.x_u8.long().sum()), int(x.long().sum())
             dma["x_u8_h2d"] = {"device": xs, "host": xh, "equal": xs == xh}
             first_bad = {"step": step, "epoch": epoch, "cur": cur, "errs": errs, "dma": dma,
