@@ -755,8 +755,7 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int64_t N, int64_t H, int64_t W, int64_t 
     check_dev(*pre_ss, "pre_ss", at::kFloat);
     TORCH_CHECK(pre_ss->is_contiguous() && pre_ss->dim() == 2 && pre_ss->size(0) == 4 && pre_ss->size(1) == Cin,
                 "conv_wgrad: pre_ss must be [4, Cin] contiguous fp32");
-    TORCH_CHECK(KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && plan.kind == 0,
-                "conv_wgrad: pre_ss on 1x1 / stride-1 geometry only");
+    TORCH_CHECK(Cin <= 4096, "conv_wgrad: pre_ss with Cin <= 4096");
     pre = pre_ss->data_ptr<float>();
   }
   Tensor out = at::empty({Cout, KH, KW, Cin}, x.options().dtype(at::kFloat));
@@ -782,7 +781,8 @@ std::vector<int64_t> conv_wgrad_plan(int64_t N, int64_t H, int64_t W, int64_t Ci
 // flip: the input gradient -- x = dy, w = the forward weight [Cin][3][3][Cout]
 // stats: also the next BatchNorm's partial sums of bf16(y) -> {y, part [rows, 2, Cout]}
 std::vector<Tensor> conv3x3_impl(Tensor x, Tensor w, int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
-                                 bool flip, bool stats) {
+                                 bool flip, bool stats, optional<Tensor> pre_ss = {},
+                                 optional<Tensor> nbt_inc = {}) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda(), "conv3x3: GPU tensors");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "conv3x3: bf16 inputs");
   TORCH_CHECK(x.is_contiguous() && w.is_contiguous(), "conv3x3: contiguous NHWC / [Cout,3,3,Cin] memory");
@@ -807,13 +807,27 @@ std::vector<Tensor> conv3x3_impl(Tensor x, Tensor w, int64_t N, int64_t H, int64
   }
   TORCH_CHECK(rla::conv3x3_ok(g), "conv3x3: unsupported shape (Cin % 16, Cout % 64, halo tile size)");
   TORCH_CHECK(!(flip && stats), "conv3x3: statistics are a forward epilogue");
+  const float* pre = nullptr;
+  int64_t* nbt = nullptr;
+  if (pre_ss.has_value() && pre_ss->defined()) {
+    // a deferred BatchNorm + ReLU on x (the statistics forward only)
+    check_dev(*pre_ss, "pre_ss", at::kFloat);
+    TORCH_CHECK(stats && pre_ss->is_contiguous() && pre_ss->dim() == 2 && pre_ss->size(0) == 4 &&
+                    pre_ss->size(1) == Cin && rla::conv3x3_pre_ok(g),
+                "conv3x3: pre_ss must be [4, Cin] fp32 (Cin <= 512) on the statistics forward");
+    pre = pre_ss->data_ptr<float>();
+    if (nbt_inc.has_value() && nbt_inc->defined()) {
+      check_dev(*nbt_inc, "nbt_inc", at::kLong);
+      nbt = nbt_inc->data_ptr<int64_t>();
+    }
+  }
   Tensor y = at::empty({N, H, W, Cout}, x.options());
   Tensor part;
   if (stats) part = at::empty({g.wpb, 2, Cout}, x.options().dtype(at::kFloat));
   TORCH_CHECK(rla::launch_conv3x3(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                                   reinterpret_cast<const uint16_t*>(w.data_ptr()),
                                   reinterpret_cast<uint16_t*>(y.data_ptr()), g, flip, cur_stream(x),
-                                  stats ? part.data_ptr<float>() : nullptr),
+                                  stats ? part.data_ptr<float>() : nullptr, pre, nbt),
               "conv3x3: launch refused");
   if (stats) return {y, part};
   return {y};
@@ -823,8 +837,9 @@ Tensor conv3x3(Tensor x, Tensor w, int64_t N, int64_t H, int64_t W, int64_t Cin,
   return conv3x3_impl(x, w, N, H, W, Cin, Cout, flip, false)[0];
 }
 
-std::vector<Tensor> conv3x3_stats(Tensor x, Tensor w, int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout) {
-  return conv3x3_impl(x, w, N, H, W, Cin, Cout, false, true);
+std::vector<Tensor> conv3x3_stats(Tensor x, Tensor w, int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout,
+                                  optional<Tensor> pre_ss, optional<Tensor> nbt_inc) {
+  return conv3x3_impl(x, w, N, H, W, Cin, Cout, false, true, pre_ss, nbt_inc);
 }
 
 // ResNet stem forward: x [N, H, W, 3] NHWC bf16, w [64, 7, 7, 3] bf16 -> {y [N, OH, OW, 64]} or, with
@@ -962,7 +977,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("w"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"),
         py::arg("flip") = false);
   m.def("conv3x3_stats", &conv3x3_stats,
-        "3x3 / stride 1 / pad 1 forward + BatchNorm partial sums of its bf16 output -> (y, part [rows, 2, Cout])");
+        "3x3 / stride 1 / pad 1 forward + BatchNorm partial sums of its bf16 output -> (y, part [rows, 2, Cout])",
+        py::arg("x"), py::arg("w"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"),
+        py::arg("pre_ss") = py::none(), py::arg("nbt_inc") = py::none());
   m.def("conv3x3_supported", &conv3x3_supported, "shapes the 3x3 MFMA convolution covers");
   m.def("stem_fwd", &stem_fwd, "ResNet stem 7x7/s2 conv (3 -> 64) on MFMA [+ BatchNorm partial sums]");
   m.def("stem_supported", &stem_supported, "input shapes the stem kernel covers");

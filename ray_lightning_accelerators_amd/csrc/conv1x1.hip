@@ -193,15 +193,15 @@ __global__ __launch_bounds__(kC1Threads, 2) void conv1x1_stats_kernel(const uint
         const float4 s0 = *reinterpret_cast<const float4*>(sc), s1 = *reinterpret_cast<const float4*>(sc + 4);
         const float4 h0 = *reinterpret_cast<const float4*>(sc + kPreMaxK);
         const float4 h1 = *reinterpret_cast<const float4*>(sc + kPreMaxK + 4);
-        const float scl[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-        const float sft[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+        const f32x2 s2[4] = {{s0.x, s0.y}, {s0.z, s0.w}, {s1.x, s1.y}, {s1.z, s1.w}};
+        const f32x2 f2[4] = {{h0.x, h0.y}, {h0.z, h0.w}, {h1.x, h1.y}, {h1.z, h1.w}};
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < 2; ++j) {
+          u32x4 u = __builtin_bit_cast(u32x4, fb[j]);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float v = __builtin_fmaf((float)fb[j][e], scl[e], sft[e]);
-            fb[j][e] = (__bf16)(v > 0.f ? v : 0.f);
-          }
+          for (int wd = 0; wd < 4; ++wd) u[wd] = bn_relu_bf16x2(u[wd], s2[wd], f2[wd]);
+          fb[j] = __builtin_bit_cast(bf16x8, u);
+        }
       }
 #pragma unroll
       for (int t = 0; t < TNW; ++t)

@@ -120,18 +120,38 @@ struct CvSet {
 // (one per-lane base per pixel block, set per tile, instead of a multiply-add per
 // tap and block), and a stage's tile / chunk split is a shift.  Global loads take
 // 32-bit byte offsets from the SGPR base (saddr form: no 64-bit address math).
-template <int NX, bool FLIP, int JB, int DEPTH, int WC = 0, int CC = 0, bool ST = false>
+// PRE (round 6, forward only): x is the raw input of a deferred BatchNorm + ReLU (ResNet's
+// bn1 -> conv2, ops/bn.py DeferredApply): every in-image halo piece is staged as
+// bf16(relu(x * scale + shift)) -- bn_apply_kernel's exact expression -- on its way from
+// registers to LDS; the zero padding stays zero (the conv pads the ACTIVATION).  A
+// thread's pieces all hold channel half (tid & 1) of the stage's 16-channel chunk, so
+// each store reads 8 scales and 8 shifts from a per-workgroup LDS table.
+constexpr int kPreMaxC = 512;
+template <int NX, bool FLIP, int JB, int DEPTH, int WC = 0, int CC = 0, bool ST = false, bool PRE = false>
 __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __restrict__ x,
                                                              const uint16_t* __restrict__ w,
                                                              uint16_t* __restrict__ y, Conv3x3Geom g,
-                                                             float* __restrict__ part) {
+                                                             float* __restrict__ part,
+                                                             const float* __restrict__ pre_ss = nullptr,
+                                                             int64_t* __restrict__ nbt_inc = nullptr) {
   static_assert(!(ST && FLIP), "statistics are a forward epilogue");
+  static_assert(!(PRE && FLIP), "PRE is a forward variant");
   constexpr int XE = x_elems(NX, WC), BE = XE + kWElems;  // halo / whole buffer elements
   static_assert(2 * BE * 2 <= 160 * 1024, "two LDS buffers fit the CU's 160 KiB");
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * BE];
+  // [channel][scale, shift] interleaved: one 16-byte read covers a word's two channels
+  __shared__ __attribute__((aligned(16))) float pre_tab[PRE ? 2 * kPreMaxC : 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (WC) g.W = WC;
   if (CC) g.Cin = CC;
+  if constexpr (PRE) {
+    if (nbt_inc && blockIdx.x == 0 && tid == 0) nbt_inc[0] += 1;
+    for (int i = tid; i < g.Cin; i += kCvThreads) {
+      pre_tab[2 * i] = pre_ss[2 * g.Cin + i];
+      pre_tab[2 * i + 1] = pre_ss[3 * g.Cin + i];
+    }
+    // visible to every thread before the first store (the prologue's barrier follows it)
+  }
   const int WP = g.W + 2, HP = g.H + 2;
   const int RS = WC ? (WC + 2) * kRow + kHPad : WP * kRow;  // halo row stride (elements)
   // padded layout: LDS element offset of this thread's halo piece i (the same every chunk)
@@ -231,15 +251,32 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
 #pragma unroll
     for (int i = 0; i < kNW; ++i) st.w[i] = *reinterpret_cast<const u32x4*>(wc + (woff[i] + wstepb));
   };
-  auto store = [&](const CvSet<NX>& st, int buf) {
+  auto store = [&](const CvSet<NX>& st, int buf, int chunk) {
     __bf16* X = lds + buf * BE;
     __bf16* Wt = X + XE;
     const u32x4 z = {0u, 0u, 0u, 0u};
+    u32x4 xs[NX];
+#pragma unroll
+    for (int i = 0; i < NX; ++i) xs[i] = st.x[i];
+    if constexpr (PRE) {
+      // word by word (two channels), the coefficients read per word: the loop runs
+      // between MFMA stages with every accumulator and fragment register live, so it
+      // may hold only a few temporaries (16 coefficients at once spilled)
+      const float* t = pre_tab + 2 * (chunk * kKC + (tid & 1) * 8);
+#pragma unroll
+      for (int wd = 0; wd < 4; ++wd) {
+        const float4 c = *reinterpret_cast<const float4*>(t + 4 * wd);  // s0, f0, s1, f1
+        const f32x2 sc = {c.x, c.z}, sf = {c.y, c.w};
+#pragma unroll
+        for (int i = 0; i < NX; ++i) xs[i][wd] = bn_relu_bf16x2(xs[i][wd], sc, sf);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < NX; ++i) {  // p >= xpieces: a row past the image, never read
       const int p = tid + i * kCvThreads;
       const uint32_t off = WC ? xlds[WC ? i : 0] : (uint32_t)((p >> 1) * kRow + (p & 1) * 8);
-      *reinterpret_cast<u32x4*>(X + off) = (st.ok >> i) & 1u ? st.x[i] : z;
+      *reinterpret_cast<u32x4*>(X + off) = (st.ok >> i) & 1u ? xs[i] : z;
     }
 #pragma unroll
     for (int i = 0; i < kNW; ++i) {
@@ -407,7 +444,9 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
       zero();
     }
     compute(buf);
-    store(nxt, buf ^ 1);
+    int ncc = 0;
+    if constexpr (PRE) tile_of(it + 1, &ncc);  // the stored stage's chunk
+    store(nxt, buf ^ 1, ncc);
     __syncthreads();
     load(nxt, it + 1 + DEPTH);
     if (cc == nchunks - 1) epilogue(tile);
@@ -415,7 +454,8 @@ __global__ __launch_bounds__(kCvThreads) void conv3x3_kernel(const uint16_t* __r
   CvSet<NX> sets[DEPTH];
 #pragma unroll
   for (int d = 0; d < DEPTH; ++d) load(sets[d], d);
-  store(sets[0], 0);
+  if constexpr (PRE) __syncthreads();  // the coefficient table
+  store(sets[0], 0, 0);
   __syncthreads();
   load(sets[0], DEPTH);
   for (int it = 0; it < nst; it += DEPTH) {  // unrolled by DEPTH: the register sets stay static
@@ -517,63 +557,83 @@ bool conv3x3_ok(const Conv3x3Geom& g) {
 
 // the compile-time-shape instance (WC, CC) when the layer is one of them and its halo
 // needs exactly NX pieces per thread; false: use the run-time-shape kernel
-template <int NX, bool FLIP, int JB, int DEPTH, int WC, int CC, bool ST>
+struct C3Pre {
+  const float* ss;
+  int64_t* nbt;
+};
+
+template <int NX, bool FLIP, int JB, int DEPTH, int WC, int CC, bool ST, bool PRE>
+static void launch_one(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, hipStream_t st,
+                       dim3 grid, float* part, const C3Pre& pre) {
+  hipLaunchKernelGGL((conv3x3_kernel<NX, FLIP, JB, DEPTH, WC, CC, ST, PRE>), grid, dim3(kCvThreads), 0, st, x, w, y,
+                     g, part, pre.ss, pre.nbt);
+}
+
+template <int NX, bool FLIP, int JB, int DEPTH, int WC, int CC, bool ST, bool PRE>
 static bool launch_fixed(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, hipStream_t st,
-                         dim3 grid, float* part) {
+                         dim3 grid, float* part, const C3Pre& pre) {
   static const bool generic = getenv("RLA_CONV3X3_GENERIC") != nullptr;  // A/B switch: run-time-shape kernel
   if (generic || g.W != WC || g.Cin != CC || conv3x3_pieces_per_thread(g) > NX ||
       conv3x3_pieces_per_thread(g) < NX - 1)
     return false;
-  hipLaunchKernelGGL((conv3x3_kernel<NX, FLIP, JB, DEPTH, WC, CC, ST>), grid, dim3(kCvThreads), 0, st, x, w, y, g,
-                     part);
+  launch_one<NX, FLIP, JB, DEPTH, WC, CC, ST, PRE>(x, w, y, g, st, grid, part, pre);
   return true;
 }
 
-template <bool FLIP, int JB, int DEPTH, bool ST>
+template <bool FLIP, int JB, int DEPTH, bool ST, bool PRE>
 static void launch_nx(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, hipStream_t st,
-                      dim3 grid, float* part) {
-  const dim3 block(kCvThreads);
+                      dim3 grid, float* part, const C3Pre& pre) {
   // ResNet-50's stride-1 3x3 shapes (bottleneck conv2 forward; the input gradient of
-  // the same layers reads dy with the same width and channel count)
-  if constexpr (JB == 4) {
-    if (launch_fixed<7, FLIP, JB, DEPTH, 56, 64, ST>(x, w, y, g, st, grid, part)) return;
+  // the same layers reads dy with the same width and channel count).  Not with PRE:
+  // those instances already hold every VGPR and AGPR, the transform's temporaries
+  // spilled (732-1232 B of scratch per lane) -- PRE runs the run-time-shape kernel
+  if constexpr (PRE) {
+  } else if constexpr (JB == 4) {
+    if (launch_fixed<7, FLIP, JB, DEPTH, 56, 64, ST, PRE>(x, w, y, g, st, grid, part, pre)) return;
     // 28x28: a workgroup's range is one whole image (784 pixels = a 512 + a 272 tile)
-    if (launch_fixed<5, FLIP, JB, DEPTH, 28, 128, ST>(x, w, y, g, st, grid, part)) return;
+    if (launch_fixed<5, FLIP, JB, DEPTH, 28, 128, ST, PRE>(x, w, y, g, st, grid, part, pre)) return;
   } else {
-    if (launch_fixed<4, FLIP, JB, DEPTH, 28, 128, ST>(x, w, y, g, st, grid, part)) return;
-    if (launch_fixed<4, FLIP, JB, DEPTH, 14, 256, ST>(x, w, y, g, st, grid, part)) return;
-    if (launch_fixed<4, FLIP, JB, DEPTH, 7, 512, ST>(x, w, y, g, st, grid, part)) return;
+    if (launch_fixed<4, FLIP, JB, DEPTH, 28, 128, ST, PRE>(x, w, y, g, st, grid, part, pre)) return;
+    if (launch_fixed<4, FLIP, JB, DEPTH, 14, 256, ST, PRE>(x, w, y, g, st, grid, part, pre)) return;
+    if (launch_fixed<4, FLIP, JB, DEPTH, 7, 512, ST, PRE>(x, w, y, g, st, grid, part, pre)) return;
   }
   switch (conv3x3_pieces_per_thread(g)) {
     case 1: case 2: case 3: case 4:
-      hipLaunchKernelGGL((conv3x3_kernel<4, FLIP, JB, DEPTH, 0, 0, ST>), grid, block, 0, st, x, w, y, g, part);
+      launch_one<4, FLIP, JB, DEPTH, 0, 0, ST, PRE>(x, w, y, g, st, grid, part, pre);
       break;
     case 5:
-      hipLaunchKernelGGL((conv3x3_kernel<5, FLIP, JB, DEPTH, 0, 0, ST>), grid, block, 0, st, x, w, y, g, part);
+      launch_one<5, FLIP, JB, DEPTH, 0, 0, ST, PRE>(x, w, y, g, st, grid, part, pre);
       break;
     case 6:
-      hipLaunchKernelGGL((conv3x3_kernel<6, FLIP, JB, DEPTH, 0, 0, ST>), grid, block, 0, st, x, w, y, g, part);
+      launch_one<6, FLIP, JB, DEPTH, 0, 0, ST, PRE>(x, w, y, g, st, grid, part, pre);
       break;
     default:
-      hipLaunchKernelGGL((conv3x3_kernel<7, FLIP, JB, DEPTH, 0, 0, ST>), grid, block, 0, st, x, w, y, g, part);
+      launch_one<7, FLIP, JB, DEPTH, 0, 0, ST, PRE>(x, w, y, g, st, grid, part, pre);
       break;
   }
 }
 
+bool conv3x3_pre_ok(const Conv3x3Geom& g) { return conv3x3_ok(g) && g.Cin <= kPreMaxC; }
+
 bool launch_conv3x3(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, bool flip,
-                    hipStream_t st, float* part) {
-  if (!conv3x3_ok(g) || (flip && part)) return false;
+                    hipStream_t st, float* part, const float* pre_ss, int64_t* nbt_inc) {
+  if (!conv3x3_ok(g) || (flip && part) || (flip && pre_ss) || (pre_ss && !part) || (pre_ss && g.Cin > kPreMaxC))
+    return false;
   // persistent: one workgroup per (pixel range, output-channel block) -- one per CU
   const dim3 grid((unsigned)(g.wpb * (g.Cout / kTN)));
-  // 512-pixel tiles: twice the accumulators, so two register stages in flight
+  const C3Pre pre{pre_ss, nbt_inc};
+  // 512-pixel tiles: twice the accumulators, so two register stages in flight.  A
+  // deferred BatchNorm (pre_ss) comes with the statistics epilogue only (the ResNet path)
   if (g.tm == 512) {
-    if (flip) launch_nx<true, 4, 2, false>(x, w, y, g, st, grid, nullptr);
-    else if (part) launch_nx<false, 4, 2, true>(x, w, y, g, st, grid, part);
-    else launch_nx<false, 4, 2, false>(x, w, y, g, st, grid, nullptr);
+    if (flip) launch_nx<true, 4, 2, false, false>(x, w, y, g, st, grid, nullptr, pre);
+    else if (pre_ss) launch_nx<false, 4, 2, true, true>(x, w, y, g, st, grid, part, pre);
+    else if (part) launch_nx<false, 4, 2, true, false>(x, w, y, g, st, grid, part, pre);
+    else launch_nx<false, 4, 2, false, false>(x, w, y, g, st, grid, nullptr, pre);
   } else {
-    if (flip) launch_nx<true, 2, 4, false>(x, w, y, g, st, grid, nullptr);
-    else if (part) launch_nx<false, 2, 4, true>(x, w, y, g, st, grid, part);
-    else launch_nx<false, 2, 4, false>(x, w, y, g, st, grid, nullptr);
+    if (flip) launch_nx<true, 2, 4, false, false>(x, w, y, g, st, grid, nullptr, pre);
+    else if (pre_ss) launch_nx<false, 2, 4, true, true>(x, w, y, g, st, grid, part, pre);
+    else if (part) launch_nx<false, 2, 4, true, false>(x, w, y, g, st, grid, part, pre);
+    else launch_nx<false, 2, 4, false, false>(x, w, y, g, st, grid, nullptr, pre);
   }
   return true;
 }

@@ -75,19 +75,18 @@ __device__ __forceinline__ int64_t x_row(int64_t m, const WgradGeom& g, int r, i
   return (int64_t)((n * g.H + ih) * g.W + iw);
 }
 
-// PRE (1x1 / stride 1 only): x is the raw input of a deferred BatchNorm + ReLU
-// (ops/bn.py ``defer``; the forward conv applied it in its fragments, conv1x1.hip PRE):
-// each x chunk is staged as bf16(relu(x * scale + shift)) -- bn_apply_kernel's exact
-// expression -- so the gradient is bitwise the one of the materialised activation.
-// A thread's x chunks keep their channel columns across stages: 16 coefficients per
-// chunk in registers, loaded once.
+// PRE: x is the raw input of a deferred BatchNorm + ReLU (ops/bn.py DeferredApply; the
+// forward conv applied it to its operands, conv1x1.hip / conv3x3.hip PRE): each valid
+// x chunk is staged as bf16(relu(x * scale + shift)) -- bn_apply_kernel's exact
+// expression -- so the gradient is bitwise the one of the materialised activation;
+// zero-padding taps (GEN) stay zero.  A thread's x chunks keep their channel columns
+// across stages: 16 coefficients per chunk in registers, loaded once.
 template <int WA, int WB, bool GEN, int DEPTH = 2, bool PRE = false>
 __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t* __restrict__ dy,
                                                            const uint16_t* __restrict__ x, float* __restrict__ out,
                                                            WgradGeom g, int64_t M, int64_t rows_per_split,
                                                            int tiles_co, int tiles_ci, int splits,
                                                            const float* __restrict__ pre_ss = nullptr) {
-  static_assert(!(PRE && GEN), "PRE: 1x1 / stride-1 geometry");
   constexpr int NWT = WA * WB;          // wave tiles per workgroup tile
   constexpr int KS = 4 / NWT;           // waves sharing one wave tile (reduction split)
   constexpr int KB = KS == 4 ? 64 : 32;  // rows per stage: every wave gets >= 1 k-step of 16
@@ -181,13 +180,10 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const uint16_t* __res
       const int c = tid + i * kWgThreads, row = c / (TCI / 8), col = (c % (TCI / 8)) * 8;
       u32x4 v = st.b[i];
       if constexpr (PRE) {
-        bf16x8 h = __builtin_bit_cast(bf16x8, v);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float a = __builtin_fmaf((float)h[e], pre_sc[i][e], pre_sf[i][e]);
-          h[e] = (__bf16)(a > 0.f ? a : 0.f);
-        }
-        v = __builtin_bit_cast(u32x4, h);
+        for (int wd = 0; wd < 4; ++wd)
+          v[wd] = bn_relu_bf16x2(v[wd], (f32x2){pre_sc[i][2 * wd], pre_sc[i][2 * wd + 1]},
+                                 (f32x2){pre_sf[i][2 * wd], pre_sf[i][2 * wd + 1]});
       }
       *reinterpret_cast<u32x4*>(B + row * SB + col) = (st.ok >> (NA + i)) & 1u ? v : z;
     }
@@ -352,11 +348,13 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 // r (0..2) accumulates the three taps (r, 0..2) = 3 x 64x64 fp32 in AGPRs; wave 3
 // only helps load.  Rows outside the image (halo, p >= OW, rows past OH) are
 // zeros, so no tap needs a mask.
-template <int OWP>
+// PRE: as wgrad_kernel's (a deferred BatchNorm + ReLU on x, staged in-image only)
+template <int OWP, bool PRE = false>
 __global__ __launch_bounds__(kWgThreads) void wgrad3x3_kernel(const uint16_t* __restrict__ dy,
                                                               const uint16_t* __restrict__ x, float* __restrict__ out,
                                                               WgradGeom g, int stages_per_split, int tiles_co,
-                                                              int tiles_ci, int splits) {
+                                                              int tiles_ci, int splits,
+                                                              const float* __restrict__ pre_ss = nullptr) {
   constexpr int R = 64 / OWP, XP = OWP + 2, XROWS = (R + 2) * XP;
   constexpr int SA = 64 + kWgPad, SB = 64 + kWgPad;
   constexpr int NA = 64 * 8 / kWgThreads;                    // dy chunks per thread
@@ -410,6 +408,15 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_kernel(const uint16_t* __
       st.ok |= ok ? (1u << (NA + i)) : 0u;
     }
   };
+  // PRE: every x chunk of this thread holds channels ci0 + 8 (tid & 7) .. + 8
+  float pre_sc[PRE ? 8 : 1], pre_sf[PRE ? 8 : 1];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      pre_sc[e] = pre_ss[2 * g.Cin + ci0 + (tid & 7) * 8 + e];
+      pre_sf[e] = pre_ss[3 * g.Cin + ci0 + (tid & 7) * 8 + e];
+    }
+  }
   auto store = [&](const Set& st) {
     const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
@@ -420,7 +427,14 @@ __global__ __launch_bounds__(kWgThreads) void wgrad3x3_kernel(const uint16_t* __
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int c = tid + i * kWgThreads, ri = c >> 3, col = (c & 7) * 8;
-      *reinterpret_cast<u32x4*>(B + ri * SB + col) = (st.ok >> (NA + i)) & 1u ? st.b[i] : z;
+      u32x4 v = st.b[i];
+      if constexpr (PRE) {
+#pragma unroll
+        for (int wd = 0; wd < 4; ++wd)
+          v[wd] = bn_relu_bf16x2(v[wd], (f32x2){pre_sc[2 * wd], pre_sc[2 * wd + 1]},
+                                 (f32x2){pre_sf[2 * wd], pre_sf[2 * wd + 1]});
+      }
+      *reinterpret_cast<u32x4*>(B + ri * SB + col) = (st.ok >> (NA + i)) & 1u ? v : z;
     }
   };
 
@@ -520,7 +534,10 @@ void launch_tile(const uint16_t* dy, const uint16_t* x, float* out, const WgradG
   const int tco = g.Cout / (64 * WA), tci = g.Cin / (64 * WB);
   const int total = tco * tci * g.KH * g.KW * S;
   const dim3 grid((unsigned)((total + 7) / 8 * 8)), block(kWgThreads);
-  if (pre_ss)  // the binding admits PRE on 1x1 / stride-1 geometry only (gen == false)
+  if (pre_ss && gen)
+    hipLaunchKernelGGL((wgrad_kernel<WA, WB, true, 2, true>), grid, block, 0, st, dy, x, out, g, M, rps, tco, tci, S,
+                       pre_ss);
+  else if (pre_ss)
     hipLaunchKernelGGL((wgrad_kernel<WA, WB, false, 2, true>), grid, block, 0, st, dy, x, out, g, M, rps, tco, tci, S,
                        pre_ss);
   else if (gen)
@@ -614,12 +631,22 @@ void launch_wgrad(const uint16_t* dy, const uint16_t* x, float* out, float* part
     const int tco = g.Cout / 64, tci = g.Cin / 64, total = tco * tci * p.splits;
     const dim3 grid((unsigned)((total + 7) / 8 * 8)), block(kWgThreads);
     const int sps = (int)p.rows_per_split, owp = wgrad3x3_owp(g.OW);
+#define RLA_W3(O)                                                                                           \
+  do {                                                                                                      \
+    if (pre_ss)                                                                                             \
+      hipLaunchKernelGGL((wgrad3x3_kernel<O, true>), grid, block, 0, st, dy, x, dst, g, sps, tco, tci, p.splits, \
+                         pre_ss);                                                                           \
+    else                                                                                                    \
+      hipLaunchKernelGGL((wgrad3x3_kernel<O, false>), grid, block, 0, st, dy, x, dst, g, sps, tco, tci,      \
+                         p.splits);                                                                         \
+  } while (0)
     if (owp == 16)
-      hipLaunchKernelGGL(wgrad3x3_kernel<16>, grid, block, 0, st, dy, x, dst, g, sps, tco, tci, p.splits);
+      RLA_W3(16);
     else if (owp == 32)
-      hipLaunchKernelGGL(wgrad3x3_kernel<32>, grid, block, 0, st, dy, x, dst, g, sps, tco, tci, p.splits);
+      RLA_W3(32);
     else
-      hipLaunchKernelGGL(wgrad3x3_kernel<64>, grid, block, 0, st, dy, x, dst, g, sps, tco, tci, p.splits);
+      RLA_W3(64);
+#undef RLA_W3
   } else {
   const bool gen = !(g.KH == 1 && g.KW == 1 && g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0 && g.H == g.OH &&
                      g.W == g.OW);

@@ -323,8 +323,12 @@ bool conv3x3_ok(const Conv3x3Geom& g);
 // flip: input gradient -- x is dy [N, H, W, Cin], w the FORWARD weight [Cin][3][3][Cout]
 // (Cin = the forward's output channels), y is dx [N, H, W, Cout]
 // part (forward only, or null): BatchNorm partial sums of bf16(y), [g.wpb][2][Cout] fp32
+// pre_ss (forward with part only; [4, Cin] BatchNorm stats, Cin <= 512): x is a deferred
+// BatchNorm + ReLU's input, staged as bf16(relu(x * scale + shift)); nbt_inc += 1
+bool conv3x3_pre_ok(const Conv3x3Geom& g);
 bool launch_conv3x3(const uint16_t* x, const uint16_t* w, uint16_t* y, const Conv3x3Geom& g, bool flip,
-                    hipStream_t stream, float* part = nullptr);
+                    hipStream_t stream, float* part = nullptr, const float* pre_ss = nullptr,
+                    int64_t* nbt_inc = nullptr);
 
 // ResNet stem: 7x7 / stride 2 / pad 3 convolution, 3 -> 64 channels, NHWC bf16 (csrc/stem.hip);
 // part (or null): BatchNorm partial sums of bf16(y), [stem_grid(g)][2][64] fp32

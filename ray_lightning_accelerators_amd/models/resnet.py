@@ -81,19 +81,22 @@ class Bottleneck(nn.Module):
         return bn(conv(x, fork=fork) if fork is not None else conv(x), **kw)
 
     def forward(self, x):
-        # bn2's output feeds conv3 only: conv3 may apply bn2 + ReLU to its own operands
-        # (ops/bn.py DeferredApply), so that activation is never written
+        # bn2's output feeds conv3 only, bn1's conv2 only: the conv may apply the
+        # BatchNorm + ReLU to its own operands (ops/bn.py DeferredApply), so that
+        # activation is never written (bn1: stride-1 conv2, where the 3x3 kernel runs)
         defer = isinstance(self.conv3, Conv1x1NHWC)
+        defer1 = isinstance(self.conv2, ConvBF16) and tuple(self.conv2.stride) == (1, 1)
         if self.fused_bn and self.downsample is not None:
             # conv1 and the downsample conv both read x: their input gradients meet in
             # one tensor (ops.conv.GradFork) instead of an autograd add of two
             fork = GradFork()
             idt = self._conv_bn(self.downsample[0], self.downsample[1], x, fork=fork)
-            out = self._conv_bn(self.conv2, self.bn2, self._conv_bn(self.conv1, self.bn1, x, fork=fork), defer=defer)
+            out = self._conv_bn(self.conv2, self.bn2, self._conv_bn(self.conv1, self.bn1, x, fork=fork, defer=defer1),
+                                defer=defer)
             return self._conv_bn(self.conv3, self.bn3, out, residual=idt, residual_is_ancestor=False)
         idt = x if self.downsample is None else self.downsample(x)
         if self.fused_bn:
-            out = self._conv_bn(self.conv2, self.bn2, self._conv_bn(self.conv1, self.bn1, x), defer=defer)
+            out = self._conv_bn(self.conv2, self.bn2, self._conv_bn(self.conv1, self.bn1, x, defer=defer1), defer=defer)
             # identity shortcut: x is an ancestor of conv3's output, so bn3 may fold
             # its residual gradient into the previous block's bn3 backward (ops/bn.py)
             return self._conv_bn(self.conv3, self.bn3, out, residual=idt,

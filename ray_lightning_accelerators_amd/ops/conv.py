@@ -164,15 +164,43 @@ def conv3x3_hip(x: torch.Tensor, wb: torch.Tensor) -> torch.Tensor:
     return y.permute(0, 3, 1, 2)
 
 
-def conv3x3_stats_hip(x: torch.Tensor, wb: torch.Tensor):
+def conv3x3_stats_hip(x: torch.Tensor, wb: torch.Tensor, pre=None):
     """:func:`conv3x3_hip` plus the per-channel partial sums of its bf16 output from the
-    epilogue (csrc/conv3x3.hip ST): returns (y channels_last, part [rows, 2, Cout])."""
+    epilogue (csrc/conv3x3.hip ST): returns (y channels_last, part [rows, 2, Cout]).
+    ``pre`` (ops/bn.py DeferredApply): ``x`` is that BatchNorm's input and the kernel
+    convolves relu(x * scale + shift), with zero padding (csrc/conv3x3.hip PRE)."""
     from . import require
 
     n, cin, h, w = x.shape
     cout = wb.size(0)
-    y, part = require().conv3x3_stats(x.permute(0, 2, 3, 1), wb.permute(0, 2, 3, 1), n, h, w, cin, cout)
+    if pre is not None:
+        y, part = require().conv3x3_stats(x.permute(0, 2, 3, 1), wb.permute(0, 2, 3, 1), n, h, w, cin, cout,
+                                          pre.st, pre.take_nbt())
+    else:
+        y, part = require().conv3x3_stats(x.permute(0, 2, 3, 1), wb.permute(0, 2, 3, 1), n, h, w, cin, cout)
     return y.permute(0, 3, 1, 2), part
+
+
+class _TimingPre:
+    """A DeferredApply stand-in for timing candidates: same statistics, no
+    num_batches_tracked increment."""
+
+    __slots__ = ("st",)
+
+    def __init__(self, pre):
+        self.st = pre.st
+
+    def take_nbt(self):
+        return None
+
+
+def _applied(x: torch.Tensor, pre) -> torch.Tensor:
+    """relu(x * scale + shift) by the apply kernel (a timing candidate: no autograd)."""
+    from . import require
+
+    y = torch.empty_like(x, memory_format=torch.channels_last)
+    require().bn_apply(x.permute(0, 2, 3, 1), pre.st[2], pre.st[3], None, True, y.permute(0, 2, 3, 1))
+    return y
 
 
 def conv3x3_stats_enabled() -> bool:
@@ -486,7 +514,18 @@ class _ConvNHWCFn(torch.autograd.Function):
     device time.  The weight gradient reaches the fp32 master weight in fp32."""
 
     @staticmethod
-    def forward(ctx, x, weight, wb, stride, padding, fork=None, bn_stats=None):
+    def forward(ctx, x, weight, wb, stride, padding, fork=None, bn_stats=None, pre=None):
+        ctx.pre_st = None
+        if pre is not None:
+            # x is a deferred BatchNorm + ReLU's input (ops/bn.py DeferredApply): the
+            # forward stages the activation itself (conv_nhwc chose this path)
+            y, bn_stats.part = conv3x3_stats_hip(x, wb, pre)
+            ctx.pre_st = pre.st
+            ctx.c3 = True
+            ctx.save_for_backward(x, wb)
+            ctx.geo = (tuple(stride), tuple(padding))
+            ctx.fork = None
+            return y
         ctx.c3 = conv3x3_ok(x, wb, stride, padding)
         be = "miopen"
         if ctx.c3:
@@ -554,6 +593,31 @@ class _ConvNHWCFn(torch.autograd.Function):
 
             dx = _fork_dx(fork, None, acc)
             fork = None  # the input gradient is settled
+        if ctx.pre_st is not None:
+            # deferred-BatchNorm input: the weight gradient stages relu(x * scale + shift)
+            # (halo or generic MFMA kernel, csrc/conv_wgrad.hip PRE); the input gradient
+            # does not read x
+            cout, cin, kh, kw = wb.shape
+            if ctx.needs_input_grad[1]:
+                key = (x.size(0) * dy.size(2) * dy.size(3), cin, cout, kh, kw, stride[0], padding[0])
+                st = ctx.pre_st
+                bw = _pick("wgrad_kxk_pre", key, {
+                    "hip": lambda: wgrad_hip(dy, x, (kh, kw), stride, padding, pre_ss=st),
+                    "hip_gen": lambda: wgrad_hip(dy, x, (kh, kw), stride, padding, algo=1, pre_ss=st),
+                })
+                dw = wgrad_hip(dy, x, (kh, kw), stride, padding, algo=0 if bw == "hip" else 1, pre_ss=st)
+            if ctx.needs_input_grad[0]:
+                key = (x.size(0) * x.size(2) * x.size(3), cin, cout, 3, 3, 1, 1)
+                be_d = _pick("dgrad_kxk", key, {
+                    "miopen": lambda: _conv_bwd(dy, x, wb, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                                                [True, False, False])[0],
+                    "hip": lambda: conv3x3_dgrad_hip(dy, wb),
+                })
+                if be_d == "hip":
+                    dx = conv3x3_dgrad_hip(dy, wb)
+                else:
+                    dx = _conv_bwd(dy, x, wb, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False])[0]
+            return dx, dw, None, None, None, None, None, None
         if ctx.needs_input_grad[1]:
             cout, cin, kh, kw = wb.shape
             key = (x.size(0) * dy.size(2) * dy.size(3), cin, cout, kh, kw, stride[0], padding[0])
@@ -585,7 +649,7 @@ class _ConvNHWCFn(torch.autograd.Function):
             dxm, dw = _conv_bwd(dy, x, wb, None, list(stride), list(padding), [1, 1], False, [0, 0], 1, mask)[:2]
             if need_dx:
                 dx = _fork_dx(fork, lambda: dxm, None)
-            return dx, dw.float(), None, None, None, None, None
+            return dx, dw.float(), None, None, None, None, None, None
         if need_dx:
             dx = _fork_dx(fork, lambda: _conv_bwd(dy, x, wb, None, list(stride), list(padding), [1, 1], False,
                                                   [0, 0], 1, [True, False, False])[0], None)
@@ -593,7 +657,7 @@ class _ConvNHWCFn(torch.autograd.Function):
             dw = wgrad_hip(dy, x, (kh, kw), stride, padding)
         elif be == "hip_gen":
             dw = wgrad_hip(dy, x, (kh, kw), stride, padding, algo=1)
-        return dx, dw, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None
 
 
 @functools.lru_cache(maxsize=64)
@@ -678,5 +742,29 @@ def conv_nhwc(x: torch.Tensor, conv: nn.Conv2d, wb: torch.Tensor, fork: Optional
     """``conv(x)`` with the bf16 weight ``wb`` (the arena shadow), the weight gradient
     going to ``conv.weight`` in fp32 (``fork``: see :class:`GradFork`; ``bn_stats``:
     see :class:`BNStats`, filled only by the 3x3 stride-1 MFMA forward)."""
+    pre = getattr(x, "_rla_pre", None)
+    if pre is not None:
+        # a deferred BatchNorm + ReLU output (ops/bn.py DeferredApply): the 3x3 statistics
+        # forward stages the activation itself where that is faster than the apply pass +
+        # the regular kernel (timed per shape; the PRE kernel is the run-time-shape
+        # instance), else the activation is materialised here
+        from .bn import materialize
+
+        if (fork is None and bn_stats is not None and not pre.used and conv3x3_stats_enabled()
+                and x.size(1) <= 512 and conv3x3_ok(x, wb, conv.stride, conv.padding)):
+            key = (x.size(0) * x.size(2) * x.size(3), x.size(1), wb.size(0), 3, 3, 1, 1)
+            tp = _TimingPre(pre)
+            be = os.environ.get("RLA_CONV3X3_PRE", "auto")  # pre | apply | auto (timed)
+            if be not in ("pre", "apply"):
+                be = _pick("fwd_kxk_pre", key, {
+                    "pre": lambda: conv3x3_stats_hip(x, wb, tp),
+                    "apply": lambda: conv3x3_stats_hip(_applied(x, tp), wb),
+                })
+            if be == "pre":
+                pre.used = True
+                stats["fast"] += 1
+                stats["pre_applied"] += 1
+                return _ConvNHWCFn.apply(x, conv.weight, wb, conv.stride, conv.padding, None, bn_stats, pre)
+        x = materialize(x)
     stats["fast"] += 1
     return _ConvNHWCFn.apply(x, conv.weight, wb, conv.stride, conv.padding, fork, bn_stats)

@@ -71,6 +71,17 @@ class ConvBF16(nn.Conv2d):
         """``fork``: an ops.conv.GradFork shared with another consumer of ``x`` (fast path only).
         ``bn_stats``: an ops.conv.BNStats the 3x3 MFMA forward may fill (the next
         BatchNorm's batch statistics from its epilogue)."""
+        if getattr(x, "_rla_pre", None) is not None:
+            # a deferred BatchNorm + ReLU output (ops/bn.py DeferredApply): only conv_nhwc
+            # understands it -- every other path gets the materialised activation
+            from .conv import kxk_fast_ok
+            from .bn import materialize
+
+            wb = bf16_weight(self.weight)
+            if not (x.is_cuda and torch.is_autocast_enabled("cuda") and self.padding_mode == "zeros"
+                    and wb is not None and torch.is_grad_enabled() and self.weight.requires_grad
+                    and kxk_fast_ok(x, self)):
+                x = materialize(x)
         if x.is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16 \
                 and self.padding_mode == "zeros":
             wb = bf16_weight(self.weight)

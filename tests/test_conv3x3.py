@@ -278,3 +278,112 @@ def test_stem_wgrad_matches_fp32(shape):
     assert dw.shape == (64, 3, 7, 7) and dw.dtype == torch.float32
     assert dw.is_contiguous(memory_format=torch.channels_last)
     assert _rel(dw, w32.grad) < 1e-4, _rel(dw, w32.grad)
+
+
+def _stats4(c, dev, seed):
+    """bn_finalize's [4, C] layout with random scale / shift (both signs: the ReLU clips
+    either way)."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    st = torch.randn(4, c, generator=g)
+    st[1] = st[1].abs() + 0.5
+    return st.to(dev).contiguous()
+
+
+def _apply_nhwc(x, st):
+    from ray_lightning_accelerators_amd import ops
+
+    y = torch.empty_like(x)
+    ops.require().bn_apply(x, st[2].contiguous(), st[3].contiguous(), None, True, y)
+    return y
+
+
+@gpu
+@pytest.mark.parametrize("shape", SHAPES[:4] + SHAPES[-1:])
+def test_conv3x3_pre_matches_materialized(shape, tile_px):
+    """A deferred BatchNorm + ReLU staged by the 3x3 statistics forward (csrc/conv3x3.hip
+    PRE): y and the partial sums bitwise those of the kernel on the materialised
+    activation, the zero padding untouched (fp32 reference of conv(relu(x*s+b))), and
+    num_batches_tracked incremented once."""
+    from ray_lightning_accelerators_amd import ops
+
+    n, h, w, cin, cout = shape
+    torch.manual_seed(9)
+    dev = torch.device("cuda", 0)
+    x = torch.randn(n, h, w, cin, device=dev).to(torch.bfloat16)
+    wt = (torch.randn(cout, 3, 3, cin, device=dev) / (9 * cin) ** 0.5).to(torch.bfloat16)
+    st = _stats4(cin, dev, 10)
+    nbt = torch.zeros((), dtype=torch.int64, device=dev)
+    y1, p1 = ops.require().conv3x3_stats(x, wt, n, h, w, cin, cout, st, nbt)
+    a = _apply_nhwc(x, st)
+    y0, p0 = ops.require().conv3x3_stats(a, wt, n, h, w, cin, cout)
+    assert int(nbt) == 1
+    ref = F.conv2d(a.float().permute(0, 3, 1, 2), wt.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    assert _rel(y1, ref) < 8e-3, _rel(y1, ref)
+    # the PRE kernel is the run-time-shape instance; the materialised run may take a
+    # compile-time-shape one: the same MFMA order, so bitwise equal
+    assert torch.equal(y1, y0), float((y1.float() - y0.float()).abs().max())
+    assert torch.equal(p1, p0)
+
+
+@gpu
+@pytest.mark.parametrize("shape", [(2, 28, 28, 64, 64), (3, 14, 14, 128, 128), (2, 7, 7, 512, 512)])
+@pytest.mark.parametrize("algo", [0, 1])
+def test_wgrad3x3_pre_matches_materialized(shape, algo):
+    """The 3x3 weight gradient staging relu(x * scale + shift) itself (halo kernel,
+    algo 0; generic tap kernel, algo 1; csrc/conv_wgrad.hip PRE) == the same kernel on
+    the materialised activation, bitwise; padding taps stay zero."""
+    from ray_lightning_accelerators_amd import ops
+
+    n, h, w, cin, cout = shape
+    torch.manual_seed(11)
+    dev = torch.device("cuda", 0)
+    x = torch.randn(n, h, w, cin, device=dev).to(torch.bfloat16)
+    dy = torch.randn(n, h, w, cout, device=dev).to(torch.bfloat16)
+    st = _stats4(cin, dev, 12)
+    geo = (n, h, w, cin, h, w, cout, 3, 3, 1, 1, 1, 1)
+    g1 = ops.require().conv_wgrad(dy, x, *geo, 0, algo, st)
+    g0 = ops.require().conv_wgrad(dy, _apply_nhwc(x, st), *geo, 0, algo)
+    assert torch.equal(g1, g0)
+
+
+@gpu
+def test_resnet_block_bn1_deferred_into_conv2(monkeypatch):
+    """A training identity Bottleneck with a parameter arena (conv2 on the 3x3 kernel):
+    bn1 + ReLU deferred into conv2 (and bn2 into conv3) == the block with both apply
+    passes -- output, input gradient, every parameter gradient and bn1's running
+    statistics bitwise."""
+    from ray_lightning_accelerators_amd.models.resnet import Bottleneck
+    from ray_lightning_accelerators_amd.ops import bn as B
+    from ray_lightning_accelerators_amd.ops import conv as C
+    from ray_lightning_accelerators_amd.parallel.arena import ParamArena
+
+    monkeypatch.setenv("RLA_CONV1X1", "hip")
+    monkeypatch.setenv("RLA_CONV_WGRAD", "hip")
+    monkeypatch.setenv("RLA_CONV3X3_PRE", "pre")
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(13)
+    blk = Bottleneck(256, 64, 1, None, fused_bn=True).to(dev).to(memory_format=torch.channels_last)
+    arena = ParamArena(blk)
+    arena.enable_bf16_shadow(blk)
+    x0 = torch.randn(2, 256, 28, 28, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    state = {k: v.clone() for k, v in blk.state_dict().items()}
+    outs = []
+    for defer in ("0", "1"):
+        monkeypatch.setenv("RLA_BN_DEFER", defer)
+        blk.load_state_dict(state)
+        blk.zero_grad(set_to_none=True)
+        n0, a0 = B.fold_stats["deferred"], C.stats["pre_applied"]
+        x = x0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = blk(x)
+        y.float().square().mean().backward()
+        if defer == "1":
+            assert B.fold_stats["deferred"] - n0 == 2 and C.stats["pre_applied"] - a0 == 2
+        outs.append((y.detach().float(), x.grad.float(), [p.grad.detach().clone() for p in blk.parameters()],
+                     blk.bn1.running_mean.clone(), blk.bn1.running_var.clone(), int(blk.bn1.num_batches_tracked)))
+    (y0, g0, p0, m0, v0, n0), (y1, g1, p1, m1, v1, n1) = outs
+    assert torch.equal(y0, y1)
+    assert torch.equal(g0, g1)
+    for nm, a, b in zip([n for n, _ in blk.named_parameters()], p0, p1):
+        assert torch.equal(a, b), nm
+    assert torch.equal(m0, m1) and torch.equal(v0, v1) and n0 == n1 == 1
