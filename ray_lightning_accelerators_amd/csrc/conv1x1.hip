@@ -213,8 +213,8 @@ __global__ __launch_bounds__(kC1Threads, 2) void conv1x1_stats_kernel(const uint
 
   const int cw = nb + wn * 32 * TNW;  // wave's first channel
   // BWD: dy2 / yb / xb of a tile's [2 pixel blocks][2 channel halves] 16-byte chunks
-  u32x4 pre[3][2][2];
-  auto prefetch = [&](int ti) {
+  typedef u32x4 PreSet[3][2][2];
+  auto prefetch = [&](PreSet& pre, int ti) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       int64_t m = (int64_t)(t0 + ti) * 128 + wm * 64 + 32 * j + r;
@@ -232,7 +232,7 @@ __global__ __launch_bounds__(kC1Threads, 2) void conv1x1_stats_kernel(const uint
   // Stores: one v_permlane32_swap per dword of each channel-group pair (q, q + 1)
   // gives lane h channels 16p + 8h .. +8 -- one 16-byte store where the MFMA layout
   // gives two 8-byte ones (cdna_hip_programming.md, widened epilogue stores)
-  auto epilogue = [&](int ti) {
+  auto epilogue = [&](int ti, const PreSet& pre) {
     const int64_t m0 = (int64_t)(t0 + ti) * 128 + wm * 64 + r;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -300,15 +300,71 @@ __global__ __launch_bounds__(kC1Threads, 2) void conv1x1_stats_kernel(const uint
   }
 #pragma unroll
   for (int d = 0; d < NS - 1; ++d) issue(d);
-  for (int st = 0; st < nst; ++st) {
-    // stage st landed: the DMA issued after it (NS - 2 stages) may still fly;
-    // then every wave's part is in and every wave has finished reading buffer st - 1
-    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"((NS - 2) * kDma) : "memory");
-    issue(st + NS - 1);
-    const int ti = st / nch;
-    if (BWD && st == ti * nch) prefetch(ti);  // the tile's first stage
-    compute(st);
-    if (st - ti * nch == nch - 1) epilogue(ti);
+  if constexpr (!BWD) {
+    PreSet none;
+    for (int st = 0; st < nst; ++st) {
+      // stage st landed: the DMA issued after it (NS - 2 stages) may still fly;
+      // then every wave's part is in and every wave has finished reading buffer st - 1
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"((NS - 2) * kDma) : "memory");
+      issue(st + NS - 1);
+      const int ti = st / nch;
+      compute(st);
+      if (st - ti * nch == nch - 1) epilogue(ti, none);
+    }
+  } else {
+    // BWD (round 6): the epilogue operands of tile t + 1 are loaded at tile t's first
+    // stage into the other of two register sets (the tile loop is unrolled by two, so
+    // both sets stay in fixed registers).  Loaded at the tile's own first stage, as
+    // before, they were the youngest loads when the epilogue needed them, and the
+    // compiler's in-order wait for them also drained the DMA ring issued behind them
+    // -- and its conservative wait before re-filling the one set drained it again:
+    // the 401408 x 64 -> 256 layers ran at ~3.6 TB/s (profiles/r6_full).  The counted
+    // stage wait now also counts the 12 operand loads of every prefetch issued after
+    // the stage's DMA (vmcnt is 6 bits: capped at 63, which only waits longer).
+    constexpr int kPreLoads = 12;
+    auto wait_stage = [&](int st) {
+      int npf;  // prefetches issued after stage st's DMA
+      if (st < NS - 1) {
+        npf = 1 + (st >= 1 ? (st - 1) / nch + 1 : 0);  // the initial one + stages 0 .. st-1 starting a tile
+      } else {
+        const int lo = st - NS + 1, hi = st - 1;
+        npf = hi / nch - (lo >= 1 ? (lo - 1) / nch : -1);
+      }
+#define RLA_C1_WAIT(N)                                                                                     \
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(                            \
+                   (NS - 2) * kDma + (N) * kPreLoads > 63 ? 63 : (NS - 2) * kDma + (N) * kPreLoads)        \
+               : "memory")
+      switch (npf) {
+        case 0: RLA_C1_WAIT(0); break;
+        case 1: RLA_C1_WAIT(1); break;
+        case 2: RLA_C1_WAIT(2); break;
+        case 3: RLA_C1_WAIT(3); break;
+        default: RLA_C1_WAIT(4); break;
+      }
+#undef RLA_C1_WAIT
+    };
+    PreSet pa, pb;
+    prefetch(pa, 0);
+    int st = 0;
+    auto tile = [&](int ti, PreSet& cur, PreSet& nxt) {
+      // the first stage outside the chunk loop: the prefetch is then not inside a loop
+      // whose back-edge merge would make the compiler's waits for it conservative
+      wait_stage(st);
+      issue(st + NS - 1);
+      prefetch(nxt, ti + 1 < ntiles ? ti + 1 : ti);  // past the end: a harmless re-load
+      compute(st);
+      ++st;
+      for (int c = 1; c < nch; ++c, ++st) {
+        wait_stage(st);
+        issue(st + NS - 1);
+        compute(st);
+      }
+      epilogue(ti, cur);
+    };
+    for (int ti = 0; ti < ntiles; ti += 2) {
+      tile(ti, pa, pb);
+      if (ti + 1 < ntiles) tile(ti + 1, pb, pa);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup's LDS
 
