@@ -6,6 +6,7 @@ import os
 
 import pytest
 
+from test_mlp3 import test_mlp3_dp_loopback_grads_vs_fp32_autograd as _fidelity_dp
 from test_mlp3 import test_mlp3_one_launch_grads_vs_fp32_autograd as _fidelity
 
 _N = int(os.environ.get("RLA_FIDELITY_REPEAT", "0"))
@@ -16,3 +17,5 @@ _N = int(os.environ.get("RLA_FIDELITY_REPEAT", "0"))
 @pytest.mark.parametrize("rep", range(max(_N, 1)))
 def test_one_launch_fidelity_repeat(rep):
     _fidelity(128, 256)
+    if rep % 4 == 0:
+        _fidelity_dp("packed")
