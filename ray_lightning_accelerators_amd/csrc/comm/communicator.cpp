@@ -3,7 +3,11 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <stdexcept>
+#include <utility>
+#include <vector>
 
 namespace rla {
 namespace comm {
@@ -11,6 +15,40 @@ namespace {
 
 void hip_check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Uncached regions are never returned to the driver.  On this stack, once a
+// hipDeviceMallocUncached allocation has been freed, later ordinary allocations can
+// hold kernel writes that the copy engine never sees: scripts/probes/
+// uncached_reuse_probe.hip found stale device-to-host copies in 11,256 of 32,043
+// checks after such frees and in 0 of 32,820 with plain allocations instead
+// (profiles/r6_investigation/).  That was the round-5/6 "intermittent corrupted fresh
+// tensor" of the GPU suite: the MNIST data-parallel tests create and free these
+// regions, and the fidelity tests that follow them compare device and host copies.
+// A process-wide free list per (device, size) hands a destroyed communicator's
+// regions to the next one; the driver reclaims them at process exit.
+std::mutex g_uc_mu;
+std::map<std::pair<int, size_t>, std::vector<void*>> g_uc_free;
+
+void* uc_alloc(int device, size_t bytes, const char* what) {
+  {
+    std::lock_guard<std::mutex> g(g_uc_mu);
+    auto it = g_uc_free.find({device, bytes});
+    if (it != g_uc_free.end() && !it->second.empty()) {
+      void* p = it->second.back();
+      it->second.pop_back();
+      return p;
+    }
+  }
+  void* p = nullptr;
+  hip_check(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached), what);
+  return p;
+}
+
+void uc_release(int device, size_t bytes, void* p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> g(g_uc_mu);
+  g_uc_free[{device, bytes}].push_back(p);
 }
 
 ncclDataType_t to_nccl(DType d) {
@@ -63,10 +101,12 @@ Communicator::~Communicator() {
     if (aux_peers_[r] && aux_peers_[r] != aux_region_) hipIpcCloseMemHandle(aux_peers_[r]);
     if (ts_peers_[r] && ts_peers_[r] != ts_region_) hipIpcCloseMemHandle(ts_peers_[r]);
   }
-  if (ts_region_) hipFree(ts_region_);
+  // every kernel that used the regions has finished before they go to the next owner
+  if (ts_region_ || region_ || aux_region_) hipDeviceSynchronize();
+  uc_release(device_, ts_region_bytes_, ts_region_);
   if (ts_gen_) hipFree(ts_gen_);
-  if (region_) hipFree(region_);
-  if (aux_region_) hipFree(aux_region_);
+  uc_release(device_, region_bytes_, region_);
+  uc_release(device_, aux_region_bytes_, aux_region_);
   if (aux_gen_) hipFree(aux_gen_);
   if (gen_) hipFree(gen_);
   if (err_host_) hipHostFree(err_host_);
@@ -127,8 +167,8 @@ std::string Communicator::xgmi_handle(int64_t capacity_floats) {
   if (!region_) {
     slot_stride_ = (capacity_floats + 63) / 64 * 64;
     const int64_t bytes = xgmi_region_bytes(slot_stride_);
-    hip_check(hipExtMallocWithFlags(reinterpret_cast<void**>(&region_), (size_t)bytes, hipDeviceMallocUncached),
-              "hipExtMallocWithFlags(uncached)");
+    region_ = static_cast<char*>(uc_alloc(device_, (size_t)bytes, "hipExtMallocWithFlags(uncached)"));
+    region_bytes_ = (size_t)bytes;
     hip_check(hipMemset(region_, 0, (size_t)bytes), "hipMemset(region)");
     hip_check(hipMalloc(reinterpret_cast<void**>(&gen_), kXgmiMaxBlocks * sizeof(uint32_t)), "hipMalloc(gen)");
     hip_check(hipMemset(gen_, 0, kXgmiMaxBlocks * sizeof(uint32_t)), "hipMemset(gen)");
@@ -195,8 +235,8 @@ std::string Communicator::twoshot_handle(int64_t capacity_floats) {
     // chunk stride: a bucket of capacity_floats split W ways, rounded to 64 floats
     ts_stride_ = ((capacity_floats + world_ - 1) / world_ + 4 + 63) / 64 * 64;
     const int64_t bytes = twoshot_region_bytes(ts_stride_, world_);
-    hip_check(hipExtMallocWithFlags(reinterpret_cast<void**>(&ts_region_), (size_t)bytes, hipDeviceMallocUncached),
-              "hipExtMallocWithFlags(uncached two-shot)");
+    ts_region_ = static_cast<char*>(uc_alloc(device_, (size_t)bytes, "hipExtMallocWithFlags(uncached two-shot)"));
+    ts_region_bytes_ = (size_t)bytes;
     hip_check(hipMemset(ts_region_, 0, (size_t)bytes), "hipMemset(two-shot)");
     hip_check(hipMalloc(reinterpret_cast<void**>(&ts_gen_), kTwoShotMaxBlocks * sizeof(uint32_t)),
               "hipMalloc(two-shot gen)");
@@ -293,8 +333,8 @@ std::string Communicator::aux_handle(int64_t capacity_floats) {
   if (!aux_region_) {
     aux_stride_ = (capacity_floats + 63) / 64 * 64;
     const int64_t bytes = xgmi_region_bytes(aux_stride_);
-    hip_check(hipExtMallocWithFlags(reinterpret_cast<void**>(&aux_region_), (size_t)bytes, hipDeviceMallocUncached),
-              "hipExtMallocWithFlags(uncached aux)");
+    aux_region_ = static_cast<char*>(uc_alloc(device_, (size_t)bytes, "hipExtMallocWithFlags(uncached aux)"));
+    aux_region_bytes_ = (size_t)bytes;
     hip_check(hipMalloc(reinterpret_cast<void**>(&aux_gen_), kDpMaxBlocks * sizeof(uint32_t)), "hipMalloc(aux gen)");
     aux_rearm();
   }

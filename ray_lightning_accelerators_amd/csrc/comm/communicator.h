@@ -120,7 +120,8 @@ class Communicator {
   int rank_, world_, device_;
   ncclComm_t comm_ = nullptr;
   // xGMI
-  char* region_ = nullptr;                 // own region (uncached device memory)
+  char* region_ = nullptr;                 // own region (uncached device memory, pooled: uc_alloc)
+  size_t region_bytes_ = 0;
   char* peers_[kXgmiMaxRanks] = {};        // mapped regions (own included)
   bool xgmi_ready_ = false;
   int64_t slot_stride_ = 0;
@@ -130,6 +131,7 @@ class Communicator {
   int64_t spin_limit_ = int64_t(1) << 24;  // ~2-4 s of s_sleep polling
   // two-shot region
   char* ts_region_ = nullptr;
+  size_t ts_region_bytes_ = 0;
   char* ts_peers_[kXgmiMaxRanks] = {};
   uint32_t* ts_gen_ = nullptr;             // device: per-block generations
   int64_t ts_stride_ = 0;                  // chunk stride (fp32 elements)
@@ -138,6 +140,7 @@ class Communicator {
   int64_t twoshot_max_ = INT64_MAX;
   // auxiliary region
   char* aux_region_ = nullptr;
+  size_t aux_region_bytes_ = 0;
   char* aux_peers_[kXgmiMaxRanks] = {};
   uint32_t* aux_gen_ = nullptr;
   int64_t aux_stride_ = 0;

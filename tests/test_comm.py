@@ -697,3 +697,35 @@ def test_rccl_communicator_world1():
     torch.cuda.synchronize()
     assert torch.equal(t, torch.arange(10, device="cuda", dtype=torch.float32)) and torch.equal(out, t)
     assert c.error_state() == 0
+
+
+@gpu
+def test_communicator_churn_keeps_fresh_memory_coherent():
+    """Regression test for the round-5/6 intermittent corrupted-fresh-tensor failure:
+    freeing hipDeviceMallocUncached memory (the communicator's xGMI / aux regions) made
+    later ordinary allocations hold kernel writes the copy engine did not see
+    (scripts/probes/uncached_reuse_probe.hip).  The communicator now keeps its uncached
+    regions in a process-wide pool (csrc/comm/communicator.cpp uc_alloc): after many
+    communicators come and go -- as in the MNIST data-parallel tests -- every fresh
+    tensor written by a kernel reads the same through a kernel and through a
+    device-to-host copy."""
+    import gc
+
+    from ray_lightning_accelerators_amd.ops import fused_mlp
+    from ray_lightning_accelerators_amd.parallel.comm import native_comm_module
+
+    mod = native_comm_module()
+    dev = torch.device("cuda", 0)
+    bad = []
+    for i in range(60):
+        c = mod.Communicator(0, 1, 0)
+        c.aux_open([c.aux_handle(fused_mlp.mlp3_dp_capacity(32 * (1 + i % 4), 64))])
+        del c
+        gc.collect()
+        for n in (1 << 21, (1 << 21) + (1 << 18), 136074):
+            t = torch.arange(n, device=dev, dtype=torch.int32) * 3 + i  # written by a kernel
+            dev_sum = int(t.long().sum())
+            host_sum = int(t.cpu().long().sum())
+            if dev_sum != host_sum:
+                bad.append((i, n, dev_sum, host_sum))
+    assert not bad, bad[:4]
