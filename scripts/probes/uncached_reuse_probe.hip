@@ -13,9 +13,13 @@
 //   ./uncached_reuse_probe <seconds> [uncached_mb=8] [mode]
 //   mode 0: an uncached U allocated and freed every round; 1: plain hipMalloc U (control);
 //   2: one uncached U kept for the whole run (never freed), opened and closed through
-//   its IPC handle in this process every round; 3: one uncached U kept, no IPC (the pool)
+//   its IPC handle in this process every round; 3: one uncached U kept, no IPC (the pool);
+//   4: no U -- a world-1 RCCL communicator initialised, used once and destroyed every
+//   round (does ncclCommDestroy leave the same state behind?)
+// Build (mode 4 needs RCCL): ... -lrccl
 // Build: hipcc --offload-arch=gfx950 -O2 scripts/probes/uncached_reuse_probe.hip -o build/uncached_reuse_probe
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <chrono>
 #include <cstdio>
@@ -72,14 +76,27 @@ int main(int argc, char** argv) {
   if (mode >= 2) CK(hipExtMallocWithFlags(&keep, (size_t)ubytes, hipDeviceMallocUncached));
   long ipc_same = 0;
   while (now_s() < t_end) {
+    if (mode == 4) {
+      ncclUniqueId id;
+      ncclComm_t comm;
+      if (ncclGetUniqueId(&id) != ncclSuccess || ncclCommInitRank(&comm, 1, id, 0) != ncclSuccess) {
+        std::fprintf(stderr, "rccl init failed\n");
+        return 2;
+      }
+      if (ncclAllReduce(sink, sink, 4, ncclFloat32, ncclSum, comm, 0) != ncclSuccess) return 2;
+      CK(hipDeviceSynchronize());
+      ncclCommDestroy(comm);
+    }
     void* u = keep;
     if (mode == 0)
       CK(hipExtMallocWithFlags(&u, (size_t)ubytes, hipDeviceMallocUncached));
     else if (mode == 1)
       CK(hipMalloc(&u, (size_t)ubytes));
-    hipLaunchKernelGGL(fill_kernel, dim3(512), dim3(256), 0, 0, (unsigned*)u, ubytes / 4, 7u * seed);
-    hipLaunchKernelGGL(touch_kernel, dim3(512), dim3(256), 0, 0, (unsigned*)u, ubytes / 4, sink);
-    CK(hipDeviceSynchronize());
+    if (mode != 4) {
+      hipLaunchKernelGGL(fill_kernel, dim3(512), dim3(256), 0, 0, (unsigned*)u, ubytes / 4, 7u * seed);
+      hipLaunchKernelGGL(touch_kernel, dim3(512), dim3(256), 0, 0, (unsigned*)u, ubytes / 4, sink);
+      CK(hipDeviceSynchronize());
+    }
     if (mode == 2) {  // the communicator's loopback: its own region through its own IPC handle
       hipIpcMemHandle_t h;
       CK(hipIpcGetMemHandle(&h, u));
